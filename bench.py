@@ -1,0 +1,274 @@
+#!/usr/bin/env python
+"""Headline benchmark: edges/sec of GCN forward+backward on the 10M-edge
+synthetic graph, F = 128 (BASELINE.json `metric`, config 2).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+Workload: Erdos-Renyi, N = 1,000,000 nodes,
+5,000,000 random (s, d) pairs drawn with torch.Generator seed 0 (s first,
+then d), symmetrised to E = 10,000,000 directed edges (duplicates and rare
+self-pairs kept), N self-loops appended (data_procs/loop.py:13-17) ->
+nnz = 11,000,000.  X ~ N(0,1) seed 1; W glorot seed 2; b ~ U(-0.1, 0.1)
+seed 3; upstream gradient dY ~ N(0,1) seed 4.  Three GCN layers
+128 -> 128 -> 128 -> 128 (NodeModelAdditive deg_norm='sm', aggr='add',
+bias) with ReLU between layers.  One step = forward of all layers +
+backward to every weight and bias (no optimizer step, as the metric defines).
+
+    edges/s = E * L / t_step          (E = 10M graph edges, loops not counted)
+
+N > 1 GPUs (torch.distributed.run, one rank per GPU, RCCL): the same graph
+sharded by destination-node range (mgcn.dist); `value` is the whole job's
+edges/s, `scaling` "strong" (total work fixed).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "meta-gcn_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "edges/sec GCN fwd+bwd, 10M-edge synth graph F=128, at 1/2/4/8 MI355X"
+
+
+# ------------------------------------------------------------ workload
+def make_er_graph(n_nodes: int = 1_000_000, n_pairs: int = 5_000_000, seed: int = 0):
+    """Config-2 graph on the CPU: ([2, 2*n_pairs + n_nodes] int64, n_nodes)."""
+    g = torch.Generator().manual_seed(seed)
+    s = torch.randint(0, n_nodes, (n_pairs,), generator=g)
+    d = torch.randint(0, n_nodes, (n_pairs,), generator=g)
+    loops = torch.arange(n_nodes)
+    src = torch.cat([s, d, loops])
+    dst = torch.cat([d, s, loops])
+    return torch.stack([src, dst]), n_nodes
+
+
+def make_inputs(n_nodes: int, feat: int, layers: int):
+    gx = torch.Generator().manual_seed(1)
+    X = torch.randn(n_nodes, feat, generator=gx)
+    gw = torch.Generator().manual_seed(2)
+    gb = torch.Generator().manual_seed(3)
+    Ws, bs = [], []
+    for _ in range(layers):
+        a = (6.0 / (feat + feat)) ** 0.5
+        Ws.append(torch.rand(feat, feat, generator=gw) * (2 * a) - a)
+        bs.append(torch.rand(feat, generator=gb) * 0.2 - 0.1)
+    gy = torch.Generator().manual_seed(4)
+    dY = torch.randn(n_nodes, feat, generator=gy)
+    return X, Ws, bs, dY
+
+
+def spmm_bytes(n_rows: int, nnz: int, F: int) -> int:
+    """Algorithmic HBM bytes of one SpMM launch (SURVEY.md §8(d) B_spmm):
+    rowptr 8(N+1) + per slot (4 col + 4 weight + 4F gathered row) + 4NF out."""
+    return 8 * (n_rows + 1) + nnz * (8 + 4 * F) + 4 * n_rows * F
+
+
+# ------------------------------------------------------------ CPU baseline
+def cpu_baseline(ei_cpu, X, W, b, n_edges: int, reps: int = 3):
+    """The reference's op sequence on the host cores: oracle.torch_layer_reference
+    (matmul -> index_select -> mul(norm) -> scatter_add -> + b, autograd), one
+    middle layer (input requires grad) fwd+bwd, 1 warm-up + median of `reps`."""
+    from oracle import oracle as orc
+    threads = len(os.sched_getaffinity(0))
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit():
+        threads = min(threads, int(env))
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        x = X.clone().requires_grad_(True)
+        Wc = W.clone().requires_grad_(True)
+        bc = b.clone().requires_grad_(True)
+        dY = torch.randn(X.shape[0], W.shape[1], generator=torch.Generator().manual_seed(4))
+        times = []
+        for i in range(reps + 1):
+            t0 = time.perf_counter()
+            out = orc.torch_layer_reference(x, ei_cpu, Wc, bc, deg_norm="sm", aggr="add")
+            out.backward(dY)
+            t1 = time.perf_counter()
+            x.grad = Wc.grad = bc.grad = None
+            del out
+            if i > 0:
+                times.append(t1 - t0)
+        t = statistics.median(times)
+    finally:
+        torch.set_num_threads(prev)
+    return {"value": n_edges / t, "unit": "edges/s", "cores": threads, "kind": "port",
+            "sample": f"1 GCN layer fwd+bwd of config 2 (N=1M, E=10M+1M loops, F=128) in torch "
+                      f"CPU ops (oracle.torch_layer_reference), 1 warm-up + median of {reps}; "
+                      f"edge-layers/s (a 3-layer step = 3x this layer's time)",
+            "layer_s": t}
+
+
+# ------------------------------------------------------------ kernel timers
+class KernelTimer:
+    """HIP events around every SpMM launch, recorded on the launch stream
+    (mgcn.ops launches on torch's current stream)."""
+
+    def __init__(self):
+        self.events = {}
+
+    def __call__(self, name, start: bool):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        if start:
+            self.events.setdefault(name, []).append([ev, None])
+        else:
+            self.events[name][-1][1] = ev
+
+    def summary(self):
+        out = {}
+        for name, pairs in self.events.items():
+            ms = [a.elapsed_time(b) for a, b in pairs]
+            out[name] = {"launches": len(ms), "avg_ms": sum(ms) / len(ms)}
+        return out
+
+
+# ------------------------------------------------------------ main
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--nodes", type=int, default=1_000_000)
+    ap.add_argument("--pairs", type=int, default=5_000_000)
+    ap.add_argument("--feat", type=int, default=128)
+    ap.add_argument("--layers", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-timers", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run "
+                             "(one process per GPU)")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    import mgcn
+    from mgcn import ops
+    from mgcn.models import GCNLayer
+
+    F, L = args.feat, args.layers
+    ei_cpu, N = make_er_graph(args.nodes, args.pairs)
+    n_edges = 2 * args.pairs          # graph edges, self-loops not counted
+    nnz = ei_cpu.shape[1]
+    X, Ws, bs, dY = make_inputs(N, F, L)
+
+    if world > 1:
+        from mgcn.dist import ShardedGCN
+        model = ShardedGCN(ei_cpu, N, Ws, bs, device=dev)
+        run_step = model.step_fn(X, dY)
+    else:
+        layers = []
+        for i in range(L):
+            layer = GCNLayer(F, F, deg_norm='sm', aggr='add', bias=True,
+                             non_linear='relu' if i < L - 1 else 'none').to(dev)
+            nm = layer.gcn.node_models[0]
+            with torch.no_grad():
+                nm.weight_node.copy_(Ws[i])
+                nm.bias.copy_(bs[i])
+            layers.append(layer)
+        params = [p for layer in layers for p in layer.parameters()]
+        ei = ei_cpu.to(dev)
+        Xd = X.to(dev)
+        dYd = dY.to(dev)
+
+        def run_step():
+            for p in params:
+                p.grad = None
+            h = Xd
+            for layer in layers:
+                h = layer(h, ei)
+            h.backward(dYd)
+
+    # graph preparation (CSR views, degrees, norms) happens once, outside the
+    # timed region; reported separately
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run_step()
+    torch.cuda.synchronize()
+    prep_and_first_ms = (time.perf_counter() - t0) * 1e3
+
+    for _ in range(args.warmup):
+        run_step()
+    timer = None if args.no_kernel_timers else KernelTimer()
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    torch.cuda.synchronize()
+    barrier()
+    ops.set_kernel_timer(timer)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run_step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    ops.set_kernel_timer(None)
+    elapsed = t1 - t0
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    value = n_edges * L / (elapsed / args.steps)
+
+    result = {
+        "metric": METRIC, "value": value, "unit": "edges/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
+        "higher_is_better": True, "scaling": "strong" if world > 1 else "weak",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": "config2: Erdos-Renyi N=1M, E=10M (+1M self-loops), F=128, "
+                               "3-layer GCN (sm, add, bias, ReLU) fwd+bwd",
+                   "nodes": N, "edges": n_edges, "nnz": nnz, "feat": F, "layers": L,
+                   "global_batch": 1, "parallelism": f"dst-range x{world}" if world > 1
+                   else "single"},
+        "graph_prep_plus_first_step_ms": prep_and_first_ms,
+    }
+    if timer is not None:
+        ks = timer.summary()
+        rows_local = N // world
+        nnz_local = nnz // world
+        kern = {}
+        for name, s in ks.items():
+            if not name.startswith("spmm"):
+                continue
+            b = spmm_bytes(rows_local, nnz_local, F)
+            kern[name] = dict(s, bytes=b, gbs=b / (s["avg_ms"] * 1e-3) / 1e9)
+        dom = max(kern, key=lambda k: kern[k]["avg_ms"] * kern[k]["launches"])
+        a = kern[dom]["gbs"]
+        result["kernels"] = kern
+        result["roofline"] = {"bound": "hbm", "kernel": dom, "achieved": a, "peak": HBM_PEAK_GBS,
+                              "unit": "GB/s", "frac": a / HBM_PEAK_GBS, "traffic": None}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(ei_cpu, X, Ws[1], bs[1], n_edges)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

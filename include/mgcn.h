@@ -1,0 +1,195 @@
+/*
+ * mgcn.h -- C ABI of libmgcn.so, the MI355X (gfx950) engine behind the GCN
+ * neighbourhood aggregation  Y = reduce_{e: dst_e = i} w_e * H[src_e]  and its
+ * adjoint  dH = A^T dY.
+ *
+ * Plain C: pointers, sizes and a `void *stream` (a hipStream_t; NULL = the
+ * default stream).  No torch types.  Every buffer is BORROWED: the library
+ * never allocates or frees device memory; scratch space is passed in by the
+ * caller (see the *_workspace_bytes queries).  Every call returns 0 on
+ * success or an MGCN_E* code; mgcn_last_error() (thread-local) says why.
+ *
+ * Each entry point names the reference interface it replaces
+ * (paths relative to jzhou316/meta-gcn @ 2025-08-24):
+ *
+ *  - torch_scatter.scatter_{add,mean,max}(src, index, 0, out, dim_size, fill)
+ *      called at src/gcn_meta/models/common.py:56-59 on the gathered-and-scaled
+ *      edge tensor built at src/gcn_meta/models/gcn_base_models.py:209-224.
+ *      The reference materialises x_j = x[src] * norm  ([E, F]) and then
+ *      scatters it; mgcn_spmm_fwd fuses gather, scale, reduce, the
+ *      `out[out == fill] = 0` fix-up (common.py:63-64), the bias add
+ *      (gcn_base_models.py:240-241) and the layer ReLU
+ *      (gcn_model.py:196, kernel/gcn.py:26-28) and never materialises [E, F].
+ *  - the autograd adjoints of those ops (index_select -> index_add_,
+ *      mul -> mul, scatter -> gather / argmax routing): mgcn_spmm_bwd.
+ *  - NodeModelBase.degnorm_const (src/gcn_meta/models/gcn_base_models.py:65-146):
+ *      mgcn_degree_norm + mgcn_edge_norm.
+ *  - the per-forward graph bookkeeping of PyG (edge_index kept as COO and
+ *      re-scattered every call): mgcn_csr_build, run once per static graph.
+ */
+#ifndef MGCN_H
+#define MGCN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MGCN_ABI_VERSION 1
+
+/* return codes */
+#define MGCN_OK 0
+#define MGCN_EINVAL 1   /* bad argument (shape, alignment, null pointer)      */
+#define MGCN_EINDEX 2   /* an edge index is outside [0, n)                    */
+#define MGCN_EHIP 3     /* a HIP runtime call or kernel launch failed          */
+#define MGCN_EWORKSPACE 4 /* caller-provided workspace is too small            */
+
+/* reductions (common.py:54 `name in ['add', 'mean', 'max']`) */
+#define MGCN_REDUCE_SUM 0
+#define MGCN_REDUCE_MEAN 1
+#define MGCN_REDUCE_MAX 2
+
+/* degree normalisation methods (gcn_base_models.py:45 deg_norm) */
+#define MGCN_NORM_NONE 0
+#define MGCN_NORM_SM 1 /* symmetric:  deg^-1/2[src] * w * deg^-1/2[dst]  */
+#define MGCN_NORM_RW 2 /* random walk: deg^-1[src] * w                    */
+
+/* fill value of the 'max' reduction (common.py:57) */
+#define MGCN_MAX_FILL (-1e38f)
+
+int mgcn_abi_version(void);
+const char *mgcn_last_error(void);
+
+/* Tuning knobs (process-wide; default 0 = automatic):
+ *   "spmm_vec"    : cap the floats per lane of the SpMM gathers (1, 2, 4)
+ *   "spmm_unroll" : gathers in flight per lane group (4, 8 or 16)          */
+int mgcn_set_option(const char *name, int value);
+
+/* ------------------------------------------------------------------ graph */
+
+/* Bytes of scratch mgcn_csr_build needs for `nnz` edges over `n` rows. */
+size_t mgcn_csr_workspace_bytes(int64_t nnz, int64_t n);
+
+/*
+ * Build a CSR view of a COO edge list, grouping edges by `key` (pass
+ * edge_index[1] = dst for the forward view, edge_index[0] = src for the
+ * transposed view used by the backward pass).  Within a row the edges keep
+ * their original (COO) order -- the order in which the reference's CPU
+ * scatter_add / index_add_ accumulate -- so sums are reproduced bit for bit.
+ *
+ *   key[nnz], other[nnz] : int64 device arrays (rows of edge_index)
+ *   rowptr[n + 1]        : int64 out
+ *   col[nnz]             : int32 out, other[e] of each edge, row-grouped
+ *   eid[nnz]             : int32 out, original edge id e of each CSR slot
+ * Indices are validated: any key or other outside [0, n_key) / [0, n_other)
+ * returns MGCN_EINDEX (this call synchronises `stream` once to check).
+ * Replaces: COO edge_index consumed by index_select/scatter at
+ * gcn_base_models.py:211-237 on every forward.
+ */
+int mgcn_csr_build(const int64_t *key, const int64_t *other, int64_t nnz,
+                   int64_t n_key, int64_t n_other, int64_t *rowptr,
+                   int32_t *col, int32_t *eid, void *workspace,
+                   size_t workspace_bytes, void *stream);
+
+/*
+ * Node degrees and their inverse powers (gcn_base_models.py:117-135).
+ *   deg_in      : optional precomputed degrees [n] (the `deg` argument);
+ *                 when NULL the degree is the sum of edge weights (or the
+ *                 edge count) over the rows of the given CSR, which must be
+ *                 grouped by SOURCE node (gcn_base_models.py:124-126 sums
+ *                 over edge_index[0]); the sum runs in edge order.
+ *   edge_weight : optional [nnz] weights in COO order (indexed through eid).
+ *   method      : MGCN_NORM_SM -> dinv = 1/sqrt(deg), MGCN_NORM_RW -> 1/deg;
+ *                 +inf results become 0 (gcn_base_models.py:135).
+ *   deg_out     : [n] degree actually used (may alias deg_in)
+ *   dinv_out    : [n]
+ */
+int mgcn_degree_norm(int64_t n, const int64_t *rowptr_src, const int32_t *eid_src,
+                     const float *deg_in, const float *edge_weight, int method,
+                     float *deg_out, float *dinv_out, void *stream);
+
+/*
+ * Per-slot edge weights of a CSR view (gcn_base_models.py:137-142), stored in
+ * the CSR's own slot order so the SpMM streams them:
+ *   SM, no edge_weight : dinv[src] * dinv[dst]
+ *   SM, edge_weight    : (dinv[src] * ew) * dinv[dst]
+ *   RW, no edge_weight : dinv[src]   (the reference scales x rows before the
+ *                                     gather, :217-220; same products)
+ *   RW, edge_weight    : dinv[src] * ew
+ *   NONE, edge_weight  : ew          (PyG GraphConv/SAGEConv message weights)
+ * rows_are_dst = 1 for the forward (dst-grouped) view, 0 for the transposed.
+ */
+int mgcn_edge_norm(int64_t n_rows, int64_t nnz, const int64_t *rowptr, const int32_t *col,
+                   const int32_t *eid, int rows_are_dst, const float *dinv,
+                   const float *edge_weight, int method, float *w_out,
+                   void *stream);
+
+/* ------------------------------------------------------------ aggregation */
+
+/*
+ * Forward aggregation over a dst-grouped CSR (rows = destinations):
+ *   acc_i = reduce_{k in row i, in edge order} ( H[col_k, :] * w_k )
+ *   SUM : acc_i                   MEAN : acc_i / max(deg_i, 1)
+ *   MAX : max with fill -1e38, ties -> later edge; fill entries -> 0;
+ *         argmax[i, f] = eid of the winning edge, -1 where the output was fill
+ *   then  y = acc (+ bias[f]) ; if relu: y = y < 0 ? 0 : y
+ * w may be NULL (unweighted).  H rows have stride ldh floats, Y rows ldy.
+ * argmax: int32 [n_rows, F] (stride F), required for MAX, ignored otherwise.
+ * No floating-point contraction: products and sums are rounded separately,
+ * in edge order, exactly as the reference's mul + scatter_add sequence.
+ */
+int mgcn_spmm_fwd(int64_t n_rows, int32_t F, const int64_t *rowptr,
+                  const int32_t *col, const int32_t *eid, const float *w,
+                  const float *H, int64_t ldh, float *Y, int64_t ldy,
+                  int reduce, const float *bias, int relu, int32_t *argmax,
+                  void *stream);
+
+/*
+ * Adjoint aggregation over the transposed (src-grouped) CSR:
+ *   dH_s = sum_{k in row s, in edge order} ( g_k * w_k ) [* row_scale_s]
+ *   g_k  = dY[col_k, :]                         (SUM)
+ *        = dY[col_k, :] / cnt[col_k]            (MEAN; cnt = max(in-deg, 1))
+ *        = argmax[col_k, f] == eid_k ? dY : 0   (MAX)
+ * row_scale (nullable) is the RW post-scale dinv[src] (gcn_base_models.py:218).
+ * If accumulate != 0 the result is added to dH (dH += ...), else stored.
+ */
+int mgcn_spmm_bwd(int64_t n_rows, int32_t F, const int64_t *rowptr_t,
+                  const int32_t *col_t, const int32_t *eid_t, const float *w_t,
+                  const float *row_scale, const float *dY, int64_t lddy,
+                  float *dH, int64_t lddh, int reduce, const float *cnt,
+                  const int32_t *argmax, int accumulate, void *stream);
+
+/* ----------------------------------------------------------- elementwise */
+
+/* Bytes of scratch mgcn_relu_bwd_colsum needs. */
+size_t mgcn_colsum_workspace_bytes(int64_t n_rows, int32_t F);
+
+/*
+ * ReLU backward + bias gradient in one pass over [n_rows, F]:
+ *   dY = Z > 0 ? dZ : 0   (written only when relu != 0 and dY != NULL)
+ *   db[f] = sum_i dY[i, f] (when db != NULL; deterministic two-stage sum)
+ * Replaces autograd's threshold_backward + sum for `x + bias` then ReLU
+ * (gcn_base_models.py:240-241, gcn_model.py:196).
+ */
+int mgcn_relu_bwd_colsum(int64_t n_rows, int32_t F, const float *dZ,
+                         const float *Z, int relu, float *dY, float *db,
+                         void *workspace, size_t workspace_bytes,
+                         void *stream);
+
+/*
+ * Segment mean over contiguous node ranges (PyG global_mean_pool on a
+ * collated Batch, kernel/gcn.py:29; GCNModel pred_on='graph',
+ * gcn_model.py:112-123):  out[g, :] = sum_{i in [ptr[g], ptr[g+1])} x[i, :]
+ *                                     / max(ptr[g+1] - ptr[g], 1)
+ * summed in node order.
+ */
+int mgcn_segment_mean(int64_t n_seg, int32_t F, const int64_t *ptr,
+                      const float *x, int64_t ldx, float *out, int64_t ldo,
+                      void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MGCN_H */

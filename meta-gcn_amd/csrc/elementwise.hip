@@ -1,0 +1,183 @@
+// Dense epilogue passes around the aggregation (gfx950, HBM-bound).
+//
+//  * mgcn_relu_bwd_colsum: dY = Z > 0 ? dZ : 0 and db = column sums of dY in
+//    one read of dZ/Z (autograd's threshold_backward + the bias-gradient sum of
+//    `x + self.bias`, gcn_base_models.py:240-241 / gcn_model.py:196).
+//    Algorithmic bytes: 8 n F read + 4 n F written (relu) or 4 n F read.
+//    The column sum is two-stage and deterministic: block partials in a fixed
+//    row order, then one block folds the partials in block order.
+//  * mgcn_segment_mean: PyG global_mean_pool over a collated batch whose nodes
+//    are contiguous per graph (kernel/gcn.py:29), summed in node order.
+
+#include "mgcn_internal.h"
+
+namespace mgcn {
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kMaxPartialBlocks = 1024;
+
+// Block b owns rows b, b + gridDim.x, ... ; thread t owns columns
+// [c*T*4 + t_col*4, +4) for column chunk c, where T threads cover a row.
+template <int VEC>
+__global__ __launch_bounds__(kBlock) void relu_bwd_colsum_kernel(
+    int64_t n, int F, const float *__restrict__ dZ, const float *__restrict__ Z, int relu,
+    float *__restrict__ dY, float *__restrict__ partial /*[gridDim.x][F]*/, int T) {
+  __shared__ float red[kBlock * VEC];
+  const int R = kBlock / T;  // row slots per block iteration
+  const int t_col = threadIdx.x % T;
+  const int t_row = threadIdx.x / T;
+  for (int c0 = 0; c0 < F; c0 += T * VEC) {
+    const int f0 = c0 + t_col * VEC;
+    const bool f_ok = (t_row < R) && (f0 < F);
+    float acc[VEC];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) acc[j] = 0.0f;
+    if (f_ok) {
+      for (int64_t r = (int64_t)blockIdx.x * R + t_row; r < n; r += (int64_t)gridDim.x * R) {
+        const int64_t off = r * F + f0;
+        float g[VEC], z[VEC];
+        if constexpr (VEC == 4) {
+          const float4 a = *reinterpret_cast<const float4 *>(dZ + off);
+          g[0] = a.x; g[1] = a.y; g[2] = a.z; g[3] = a.w;
+          if (relu) {
+            const float4 b = *reinterpret_cast<const float4 *>(Z + off);
+            z[0] = b.x; z[1] = b.y; z[2] = b.z; z[3] = b.w;
+          }
+        } else {
+          g[0] = dZ[off];
+          if (relu) z[0] = Z[off];
+        }
+        if (relu) {
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) g[j] = (z[j] > 0.0f) ? g[j] : 0.0f;
+          if (dY != nullptr) {
+            if constexpr (VEC == 4)
+              *reinterpret_cast<float4 *>(dY + off) = make_float4(g[0], g[1], g[2], g[3]);
+            else
+              dY[off] = g[0];
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) acc[j] = __fadd_rn(acc[j], g[j]);
+      }
+    }
+    if (partial == nullptr) continue;
+    // fold the R row slots of this block (fixed order)
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) red[threadIdx.x * VEC + j] = acc[j];
+    __syncthreads();
+    if (t_row == 0 && f0 < F) {
+      float s[VEC];
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) s[j] = red[t_col * VEC + j];
+      for (int rr = 1; rr < R; ++rr)
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) s[j] = __fadd_rn(s[j], red[(rr * T + t_col) * VEC + j]);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) partial[(int64_t)blockIdx.x * F + f0 + j] = s[j];
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void colsum_finish_kernel(const float *__restrict__ partial,
+                                                               int nblk, int F,
+                                                               float *__restrict__ db) {
+  for (int f = blockIdx.x * blockDim.x + threadIdx.x; f < F; f += gridDim.x * blockDim.x) {
+    float s = 0.0f;
+    for (int b = 0; b < nblk; ++b) s = __fadd_rn(s, partial[(int64_t)b * F + f]);
+    db[f] = s;
+  }
+}
+
+// one wave per segment; lanes stride the features
+__global__ __launch_bounds__(kBlock) void segment_mean_kernel(int64_t n_seg, int F,
+                                                              const int64_t *__restrict__ ptr,
+                                                              const float *__restrict__ x,
+                                                              int64_t ldx, float *__restrict__ out,
+                                                              int64_t ldo) {
+  const int lane = threadIdx.x & 63;
+  const int64_t seg = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  if (seg >= n_seg) return;
+  const int64_t b = ptr[seg], e = ptr[seg + 1];
+  const float cnt = (float)((e - b) > 1 ? (e - b) : 1);
+  for (int f = lane; f < F; f += 64) {
+    float s = 0.0f;
+    for (int64_t i = b; i < e; ++i) s = __fadd_rn(s, x[i * ldx + f]);
+    out[seg * ldo + f] = __fdiv_rn(s, cnt);
+  }
+}
+
+int colsum_blocks(int64_t n) {
+  int64_t b = (n + 63) / 64;
+  if (b > kMaxPartialBlocks) b = kMaxPartialBlocks;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+}  // namespace
+}  // namespace mgcn
+
+using namespace mgcn;
+
+extern "C" size_t mgcn_colsum_workspace_bytes(int64_t n_rows, int32_t F) {
+  return align_up((size_t)colsum_blocks(n_rows) * (size_t)(F > 0 ? F : 1) * sizeof(float), 256);
+}
+
+extern "C" int mgcn_relu_bwd_colsum(int64_t n_rows, int32_t F, const float *dZ, const float *Z,
+                                    int relu, float *dY, float *db, void *workspace,
+                                    size_t workspace_bytes, void *stream) {
+  clear_error();
+  MGCN_REQUIRE(n_rows >= 0 && F >= 0, "mgcn_relu_bwd_colsum: negative size");
+  hipStream_t s = as_stream(stream);
+  if (F == 0) return MGCN_OK;
+  if (n_rows == 0) {
+    if (db) MGCN_HIP_TRY(hipMemsetAsync(db, 0, sizeof(float) * F, s));
+    return MGCN_OK;
+  }
+  MGCN_REQUIRE(dZ != nullptr, "mgcn_relu_bwd_colsum: dZ is null");
+  MGCN_REQUIRE(!relu || Z != nullptr, "mgcn_relu_bwd_colsum: relu needs Z");
+  const int nblk = colsum_blocks(n_rows);
+  float *partial = nullptr;
+  if (db != nullptr) {
+    const size_t need = mgcn_colsum_workspace_bytes(n_rows, F);
+    if (workspace == nullptr || workspace_bytes < need) {
+      set_error("mgcn_relu_bwd_colsum: workspace %zu < %zu", workspace_bytes, need);
+      return MGCN_EWORKSPACE;
+    }
+    partial = static_cast<float *>(workspace);
+  }
+  const bool v4 = (F % 4 == 0) && ((uintptr_t)dZ % 16 == 0) && (!relu || (uintptr_t)Z % 16 == 0) &&
+                  (dY == nullptr || (uintptr_t)dY % 16 == 0);
+  if (v4) {
+    int T = 1;
+    while (T < F / 4 && T < kBlock) T <<= 1;
+    hipLaunchKernelGGL(relu_bwd_colsum_kernel<4>, dim3(nblk), dim3(kBlock), 0, s, n_rows, F, dZ, Z,
+                       relu, dY, partial, T);
+  } else {
+    int T = 1;
+    while (T < F && T < kBlock) T <<= 1;
+    hipLaunchKernelGGL(relu_bwd_colsum_kernel<1>, dim3(nblk), dim3(kBlock), 0, s, n_rows, F, dZ, Z,
+                       relu, dY, partial, T);
+  }
+  if (int rc = check_launch("relu_bwd_colsum_kernel")) return rc;
+  if (db != nullptr) {
+    hipLaunchKernelGGL(colsum_finish_kernel, dim3((F + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
+                       partial, nblk, F, db);
+    return check_launch("colsum_finish_kernel");
+  }
+  return MGCN_OK;
+}
+
+extern "C" int mgcn_segment_mean(int64_t n_seg, int32_t F, const int64_t *ptr, const float *x,
+                                 int64_t ldx, float *out, int64_t ldo, void *stream) {
+  clear_error();
+  MGCN_REQUIRE(n_seg >= 0 && F >= 0, "mgcn_segment_mean: negative size");
+  if (n_seg == 0 || F == 0) return MGCN_OK;
+  MGCN_REQUIRE(ptr && x && out && ldx >= F && ldo >= F, "mgcn_segment_mean: bad arguments");
+  const int64_t blocks = (n_seg + (kBlock / 64) - 1) / (kBlock / 64);
+  hipLaunchKernelGGL(segment_mean_kernel, dim3((unsigned)blocks), dim3(kBlock), 0,
+                     as_stream(stream), n_seg, F, ptr, x, ldx, out, ldo);
+  return check_launch("segment_mean_kernel");
+}

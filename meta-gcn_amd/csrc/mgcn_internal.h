@@ -1,0 +1,58 @@
+// Internal helpers shared by the libmgcn translation units (not installed).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+
+#include "mgcn.h"
+
+namespace mgcn {
+
+void set_error(const char *fmt, ...);
+void clear_error();
+
+inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Check the last launch on this thread; record the HIP error string on failure.
+inline int check_launch(const char *what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("%s: %s", what, hipGetErrorString(e));
+    return MGCN_EHIP;
+  }
+  return MGCN_OK;
+}
+
+#define MGCN_HIP_TRY(call)                                                    \
+  do {                                                                        \
+    hipError_t _e = (call);                                                   \
+    if (_e != hipSuccess) {                                                   \
+      ::mgcn::set_error("%s failed: %s (%s:%d)", #call, hipGetErrorString(_e), \
+                        __FILE__, __LINE__);                                  \
+      return MGCN_EHIP;                                                       \
+    }                                                                         \
+  } while (0)
+
+#define MGCN_REQUIRE(cond, ...)       \
+  do {                                \
+    if (!(cond)) {                    \
+      ::mgcn::set_error(__VA_ARGS__); \
+      return MGCN_EINVAL;             \
+    }                                 \
+  } while (0)
+
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Grid sizing for grid-stride loops over memory-bound work: enough blocks to
+// fill 256 CUs several times over, capped (cdna_hip_programming.md G11).
+inline unsigned grid_for(int64_t work_items, int block) {
+  int64_t g = (work_items + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > 8192) g = 8192;
+  return static_cast<unsigned>(g);
+}
+
+}  // namespace mgcn

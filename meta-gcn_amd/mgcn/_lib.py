@@ -1,0 +1,126 @@
+"""ctypes binding of libmgcn.so (the C ABI declared in include/mgcn.h).
+
+The product path has exactly one implementation: the HIP kernels in this
+library.  If the library is missing, or a tensor is not on a HIP device, the
+call raises -- there is no CPU fallback anywhere in :mod:`mgcn`.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmgcn.so")
+
+# constants mirrored from include/mgcn.h
+ABI_VERSION = 1
+OK, EINVAL, EINDEX, EHIP, EWORKSPACE = 0, 1, 2, 3, 4
+REDUCE_SUM, REDUCE_MEAN, REDUCE_MAX = 0, 1, 2
+NORM_NONE, NORM_SM, NORM_RW = 0, 1, 2
+MAX_FILL = -1e38
+
+REDUCE_CODES = {"add": REDUCE_SUM, "sum": REDUCE_SUM, "mean": REDUCE_MEAN, "max": REDUCE_MAX}
+NORM_CODES = {None: NORM_NONE, "sm": NORM_SM, "rw": NORM_RW}
+
+_vp = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_i32 = ctypes.c_int32
+_int = ctypes.c_int
+_sz = ctypes.c_size_t
+
+# name -> (restype, argtypes); every symbol include/mgcn.h declares
+SIGNATURES = {
+    "mgcn_abi_version": (_int, []),
+    "mgcn_last_error": (ctypes.c_char_p, []),
+    "mgcn_set_option": (_int, [ctypes.c_char_p, _int]),
+    "mgcn_csr_workspace_bytes": (_sz, [_i64, _i64]),
+    "mgcn_csr_build": (_int, [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "mgcn_degree_norm": (_int, [_i64, _vp, _vp, _vp, _vp, _int, _vp, _vp, _vp]),
+    "mgcn_edge_norm": (_int, [_i64, _i64, _vp, _vp, _vp, _int, _vp, _vp, _int, _vp, _vp]),
+    "mgcn_spmm_fwd": (_int, [_i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _int, _vp,
+                             _int, _vp, _vp]),
+    "mgcn_spmm_bwd": (_int, [_i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _int,
+                             _vp, _vp, _int, _vp]),
+    "mgcn_colsum_workspace_bytes": (_sz, [_i64, _i32]),
+    "mgcn_relu_bwd_colsum": (_int, [_i64, _i32, _vp, _vp, _int, _vp, _vp, _vp, _sz, _vp]),
+    "mgcn_segment_mean": (_int, [_i64, _i32, _vp, _vp, _i64, _vp, _i64, _vp]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class MgcnError(RuntimeError):
+    """A libmgcn call failed (bad argument, bad index, HIP error)."""
+
+
+def load(path: str | None = None) -> ctypes.CDLL:
+    """Load libmgcn.so (after torch, so the HIP runtime torch already mapped
+    is the one the library binds to) and declare every C signature."""
+    global _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise MgcnError(
+                f"libmgcn.so not found at {p}: build it with "
+                "`make -C meta-gcn_amd/csrc` (or __graft_entry__.build()); "
+                "mgcn has no CPU fallback")
+        lib = ctypes.CDLL(p)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.mgcn_abi_version() != ABI_VERSION:
+            raise MgcnError(f"libmgcn ABI {lib.mgcn_abi_version()} != expected {ABI_VERSION}")
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != OK:
+        msg = load().mgcn_last_error().decode(errors="replace")
+        if rc == EINDEX:
+            raise IndexError(f"{what}: {msg}")
+        raise MgcnError(f"{what} failed (code {rc}): {msg}")
+
+
+def ptr(t: torch.Tensor | None):
+    """Raw device address of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def require_device(*tensors: torch.Tensor | None) -> torch.device:
+    """All tensors must live on one HIP device; returns it.  Raises for CPU
+    tensors: the engine is GPU-only and never falls back to a CPU path."""
+    dev = None
+    for t in tensors:
+        if t is None:
+            continue
+        if t.device.type != "cuda":
+            raise MgcnError(
+                f"mgcn kernels run on a HIP device only; got a tensor on {t.device} "
+                "(move the graph and features to 'cuda')")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise MgcnError(f"tensors on different devices: {dev} vs {t.device}")
+    if dev is None:
+        raise MgcnError("no tensor given")
+    return dev
+
+
+def stream_of(device: torch.device):
+    """The caller's current HIP stream on `device` (kernels launch there)."""
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def set_option(name: str, value: int) -> None:
+    check(load().mgcn_set_option(name.encode(), int(value)), f"mgcn_set_option({name})")

@@ -1,0 +1,227 @@
+"""Graph plans: the device-resident CSR views the aggregation kernels stream.
+
+A :class:`GraphPlan` is built once per static ``edge_index`` (libmgcn
+``mgcn_csr_build``) and holds
+
+* ``fwd``  -- edges grouped by destination ``edge_index[1]`` (rows = dst,
+  col = src): the forward SpMM walks one row per destination;
+* ``bwd``  -- edges grouped by source ``edge_index[0]`` (rows = src, col =
+  dst): the adjoint SpMM for ``dH = A^T dY`` and the out-degree of
+  ``degnorm_const`` (gcn_base_models.py:124-126 sums over ``edge_index[0]``);
+* ``in_cnt`` -- ``max(in-degree, 1)`` as float, torch_scatter 1.x's
+  ``count.clamp(min=1)`` of ``scatter_mean``.
+
+Within every row the edges keep their COO order, which is the order the
+reference's CPU ``scatter_add``/``index_add_`` accumulate in, so sums match bit
+for bit.  Normalisation weights (:class:`NormPlan`) hang off the plan, keyed by
+method / ``deg`` / ``edge_weight``.
+
+Plans are cached (``plan_for``), keyed by the identity of the ``edge_index``
+tensor (a weak reference, its ``_version`` counter and ``num_nodes``): the
+reference recomputes ``degnorm_const`` and re-scatters the COO list on every
+forward (gcn_base_models.py:215); graphs are static across layers and epochs,
+so this engine prepares them once.
+"""
+from __future__ import annotations
+
+import weakref
+from collections import OrderedDict
+from dataclasses import dataclass, field
+
+import torch
+
+from . import _lib as L
+
+
+@dataclass
+class CSRView:
+    """Edges grouped by one endpoint; ``col`` holds the other endpoint."""
+    rowptr: torch.Tensor  # int64 [n_rows + 1]
+    col: torch.Tensor     # int32 [nnz]
+    eid: torch.Tensor     # int32 [nnz] original COO edge id of each slot
+    n_rows: int
+    n_cols: int
+
+    @property
+    def nnz(self) -> int:
+        return int(self.col.numel())
+
+
+@dataclass
+class NormPlan:
+    """Per-slot weights of both views for one (method, deg, edge_weight)."""
+    method: int
+    w_fwd: torch.Tensor | None       # float [nnz] in fwd slot order (None: unweighted)
+    w_bwd: torch.Tensor | None       # float [nnz] in bwd slot order
+    row_scale_bwd: torch.Tensor | None  # RW without edge weights: dinv post-scale
+    deg: torch.Tensor | None
+    dinv: torch.Tensor | None
+
+
+@dataclass
+class GraphPlan:
+    num_nodes: int
+    nnz: int
+    device: torch.device
+    fwd: CSRView
+    bwd: CSRView
+    in_cnt: torch.Tensor  # float [num_nodes] = max(in-degree, 1)
+    norms: dict = field(default_factory=dict)
+    _key_refs: list = field(default_factory=list)
+
+    # ------------------------------------------------------------------ norms
+    def norm(self, method: str | None, deg: torch.Tensor | None = None,
+             edge_weight: torch.Tensor | None = None) -> NormPlan:
+        """Normalisation weights, as NodeModelBase.degnorm_const computes them
+        (gcn_base_models.py:65-146):
+
+        * ``edge_weight`` given -> the degree is recomputed from it and
+          ``deg`` is ignored (:102-110);
+        * else ``deg`` given -> used as is (:119-121);
+        * else ``deg`` = out-degree (edge count over ``edge_index[0]``, :117).
+        ``method`` None means unnormalised (``edge_weight`` then acts as a
+        plain message weight, PyG GraphConv/SAGEConv).
+        """
+        code = L.NORM_CODES[method]
+        if edge_weight is not None:
+            deg = None
+        key = (code, _tkey(deg), _tkey(edge_weight))
+        hit = self.norms.get(key)
+        if hit is not None and _alive(hit[1]):
+            return hit[0]
+        plan = _build_norm(self, code, deg, edge_weight)
+        self.norms[key] = (plan, [weakref.ref(_owner(t)) for t in (deg, edge_weight)
+                                  if t is not None])
+        if len(self.norms) > 8:
+            self.norms.pop(next(iter(self.norms)))
+        return plan
+
+
+def _tkey(t: torch.Tensor | None):
+    if t is None:
+        return None
+    return (t.data_ptr(), t._version, tuple(t.shape), tuple(t.stride()), t.dtype)
+
+
+def _owner(t: torch.Tensor) -> torch.Tensor:
+    # a view such as batch.x[:, 1] is a new Python object per call; its base
+    # outlives it, shares its version counter, and is what we keep a ref to
+    return t._base if t._base is not None else t
+
+
+def _alive(refs) -> bool:
+    return all(r() is not None for r in refs)
+
+
+def _f32(t: torch.Tensor | None, n: int, name: str, device) -> torch.Tensor | None:
+    if t is None:
+        return None
+    t = t.reshape(-1)
+    if t.numel() != n:
+        raise ValueError(f"{name} has {t.numel()} entries, expected {n}")
+    if t.device != device:
+        raise L.MgcnError(f"{name} is on {t.device}, graph is on {device}")
+    return t.to(torch.float32).contiguous()
+
+
+def build_view(key: torch.Tensor, other: torch.Tensor, n_key: int, n_other: int) -> CSRView:
+    """CSR over ``key`` (libmgcn ``mgcn_csr_build``); stable in COO order."""
+    lib = L.load()
+    dev = L.require_device(key, other)
+    key = key.to(torch.int64).contiguous()
+    other = other.to(torch.int64).contiguous()
+    nnz = int(key.numel())
+    rowptr = torch.empty(n_key + 1, dtype=torch.int64, device=dev)
+    col = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)[:nnz]
+    eid = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)[:nnz]
+    ws_bytes = int(lib.mgcn_csr_workspace_bytes(nnz, n_key))
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    with torch.cuda.device(dev):
+        rc = lib.mgcn_csr_build(L.ptr(key), L.ptr(other), nnz, n_key, n_other, L.ptr(rowptr),
+                                L.ptr(col), L.ptr(eid), L.ptr(ws), ws_bytes, L.stream_of(dev))
+    L.check(rc, "mgcn_csr_build")
+    return CSRView(rowptr=rowptr, col=col, eid=eid, n_rows=n_key, n_cols=n_other)
+
+
+def build_plan(edge_index: torch.Tensor, num_nodes: int) -> GraphPlan:
+    if edge_index.dim() != 2 or edge_index.size(0) != 2:
+        raise ValueError(f"edge_index must be [2, E], got {tuple(edge_index.shape)}")
+    dev = L.require_device(edge_index)
+    src, dst = edge_index[0], edge_index[1]
+    fwd = build_view(dst, src, num_nodes, num_nodes)
+    bwd = build_view(src, dst, num_nodes, num_nodes)
+    in_cnt = (fwd.rowptr[1:] - fwd.rowptr[:-1]).clamp_(min=1).to(torch.float32)
+    return GraphPlan(num_nodes=num_nodes, nnz=int(edge_index.size(1)), device=dev, fwd=fwd,
+                     bwd=bwd, in_cnt=in_cnt)
+
+
+def _build_norm(g: GraphPlan, code: int, deg, edge_weight) -> NormPlan:
+    lib = L.load()
+    dev = g.device
+    n = g.num_nodes
+    ew = _f32(edge_weight, g.nnz, "edge_weight", dev)
+    if code == L.NORM_NONE:
+        if ew is None:
+            return NormPlan(code, None, None, None, None, None)
+        dinv = None
+        dg = None
+    else:
+        deg_in = _f32(deg, n, "deg", dev)
+        dg = torch.empty(n, dtype=torch.float32, device=dev)
+        dinv = torch.empty(n, dtype=torch.float32, device=dev)
+        with torch.cuda.device(dev):
+            rc = lib.mgcn_degree_norm(n, L.ptr(g.bwd.rowptr), L.ptr(g.bwd.eid), L.ptr(deg_in),
+                                      L.ptr(ew), code, L.ptr(dg), L.ptr(dinv), L.stream_of(dev))
+        L.check(rc, "mgcn_degree_norm")
+    if code == L.NORM_RW and ew is None:
+        # x * dinv before the gather (gcn_base_models.py:217-220): the forward
+        # products are H[src] * dinv[src]; the adjoint post-scales by dinv[src].
+        w_fwd = _edge_norm(g.fwd, True, dinv, None, code)
+        return NormPlan(code, w_fwd, None, dinv, dg, dinv)
+    w_fwd = _edge_norm(g.fwd, True, dinv, ew, code)
+    w_bwd = _edge_norm(g.bwd, False, dinv, ew, code)
+    return NormPlan(code, w_fwd, w_bwd, None, dg, dinv)
+
+
+def _edge_norm(view: CSRView, rows_are_dst: bool, dinv, ew, code) -> torch.Tensor:
+    lib = L.load()
+    dev = view.rowptr.device
+    w = torch.empty(max(view.nnz, 1), dtype=torch.float32, device=dev)[:view.nnz]
+    with torch.cuda.device(dev):
+        rc = lib.mgcn_edge_norm(view.n_rows, view.nnz, L.ptr(view.rowptr), L.ptr(view.col),
+                                L.ptr(view.eid), int(rows_are_dst), L.ptr(dinv), L.ptr(ew), code,
+                                L.ptr(w), L.stream_of(dev))
+    L.check(rc, "mgcn_edge_norm")
+    return w
+
+
+# ------------------------------------------------------------------- cache
+_CACHE: "OrderedDict[tuple, tuple]" = OrderedDict()
+_CACHE_SIZE = 16
+
+
+def cache_key(edge_index: torch.Tensor, num_nodes: int) -> tuple:
+    return (edge_index.data_ptr(), edge_index._version, tuple(edge_index.shape),
+            edge_index.dtype, str(edge_index.device), int(num_nodes))
+
+
+def plan_for(edge_index: torch.Tensor, num_nodes: int) -> GraphPlan:
+    """Cached :func:`build_plan`.  An entry is valid only while the very
+    ``edge_index`` tensor it was built from is alive and unmodified."""
+    key = cache_key(edge_index, num_nodes)
+    hit = _CACHE.get(key)
+    if hit is not None:
+        ref, plan = hit
+        if ref() is edge_index:
+            _CACHE.move_to_end(key)
+            return plan
+        del _CACHE[key]
+    plan = build_plan(edge_index, num_nodes)
+    _CACHE[key] = (weakref.ref(edge_index), plan)
+    while len(_CACHE) > _CACHE_SIZE:
+        _CACHE.popitem(last=False)
+    return plan
+
+
+def clear_cache() -> None:
+    _CACHE.clear()

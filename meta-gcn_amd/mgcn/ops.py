@@ -1,0 +1,253 @@
+"""Autograd-aware aggregation ops on top of libmgcn.
+
+``aggregate`` is the fused replacement for the reference's message-passing
+core (src/gcn_meta/models/gcn_base_models.py:209-241 + common.py:37-66):
+
+    x_j = index_select(H, 0, src) * norm      # [E, F] materialised
+    y   = torch_scatter.scatter_{add,mean,max}(x_j, dst, dim_size=N)
+    y[y == -1e38] = 0                          # max only
+    y   = y + bias ; y = relu(y)               # layer epilogue
+
+Here it is one HIP kernel per direction (libmgcn ``mgcn_spmm_fwd`` /
+``mgcn_spmm_bwd``); the [E, F] tensor never exists.  Gradients follow the
+reference's autograd graph operation for operation (gather of dY, multiply by
+norm, index_add over sources in edge order; mean divides dY by the count;
+max routes through the saved argmax), so the adjoint is bit-identical too.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib as L
+from .graph import CSRView, GraphPlan, NormPlan, plan_for
+
+
+_TIMER = None  # optional callable(name, start: bool), e.g. bench.py's HIP-event timer
+
+
+def set_kernel_timer(timer) -> None:
+    """Install (or clear with None) a hook called right before and after each
+    libmgcn launch, on the launch stream -- used to time kernels with events."""
+    global _TIMER
+    _TIMER = timer
+
+
+def _contig_f32(t: torch.Tensor, name: str) -> torch.Tensor:
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name} must be float32 (the reference computes in fp32), got {t.dtype}")
+    if t.dim() != 2:
+        raise ValueError(f"{name} must be 2-D [N, F], got {tuple(t.shape)}")
+    if t.stride(1) != 1 or t.stride(0) < t.size(1):
+        t = t.contiguous()
+    return t
+
+
+def spmm_fwd(view: CSRView, w: torch.Tensor | None, H: torch.Tensor, reduce: int,
+             bias: torch.Tensor | None = None, relu: bool = False,
+             out: torch.Tensor | None = None):
+    """Y[view.n_rows, F] = epi(reduce_k H[col_k] * w_k); returns (Y, argmax)."""
+    lib = L.load()
+    H = _contig_f32(H, "H")
+    dev = L.require_device(H, view.rowptr, w, bias)
+    if H.size(0) != view.n_cols:
+        raise ValueError(f"H has {H.size(0)} rows, graph has {view.n_cols} source nodes")
+    F = H.size(1)
+    Y = out if out is not None else torch.empty(view.n_rows, F, dtype=torch.float32, device=dev)
+    argmax = None
+    if reduce == L.REDUCE_MAX:
+        argmax = torch.empty(view.n_rows, F, dtype=torch.int32, device=dev)
+    if bias is not None:
+        bias = bias.detach().to(torch.float32).contiguous()
+        if bias.numel() != F:
+            raise ValueError(f"bias has {bias.numel()} entries, expected {F}")
+    if _TIMER is not None:
+        _TIMER("spmm_fwd", True)
+    with torch.cuda.device(dev):
+        rc = lib.mgcn_spmm_fwd(view.n_rows, F, L.ptr(view.rowptr), L.ptr(view.col),
+                               L.ptr(view.eid), L.ptr(w), L.ptr(H), H.stride(0), L.ptr(Y),
+                               Y.stride(0), reduce, L.ptr(bias), int(bool(relu)), L.ptr(argmax),
+                               L.stream_of(dev))
+    if _TIMER is not None:
+        _TIMER("spmm_fwd", False)
+    L.check(rc, "mgcn_spmm_fwd")
+    return Y, argmax
+
+
+def spmm_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tensor | None,
+             dY: torch.Tensor, reduce: int, cnt: torch.Tensor | None = None,
+             argmax: torch.Tensor | None = None, out: torch.Tensor | None = None,
+             accumulate: bool = False) -> torch.Tensor:
+    """dH[view_t.n_rows, F] = sum_k g(dY[col_k]) * w_k  [* row_scale]."""
+    lib = L.load()
+    dY = _contig_f32(dY, "dY")
+    dev = L.require_device(dY, view_t.rowptr, w_t, row_scale)
+    F = dY.size(1)
+    dH = out if out is not None else torch.empty(view_t.n_rows, F, dtype=torch.float32,
+                                                 device=dev)
+    if _TIMER is not None:
+        _TIMER("spmm_bwd", True)
+    with torch.cuda.device(dev):
+        rc = lib.mgcn_spmm_bwd(view_t.n_rows, F, L.ptr(view_t.rowptr), L.ptr(view_t.col),
+                               L.ptr(view_t.eid), L.ptr(w_t), L.ptr(row_scale), L.ptr(dY),
+                               dY.stride(0), L.ptr(dH), dH.stride(0), reduce, L.ptr(cnt),
+                               L.ptr(argmax), int(bool(accumulate)), L.stream_of(dev))
+    if _TIMER is not None:
+        _TIMER("spmm_bwd", False)
+    L.check(rc, "mgcn_spmm_bwd")
+    return dH
+
+
+def relu_bwd_colsum(dZ: torch.Tensor, Z: torch.Tensor | None, relu: bool, want_db: bool):
+    """(dY, db): dY = Z > 0 ? dZ : 0 (dZ itself when not relu); db = sum_i dY."""
+    lib = L.load()
+    dZ = dZ.contiguous()
+    dev = L.require_device(dZ, Z)
+    n, F = dZ.shape
+    dY = torch.empty_like(dZ) if relu else dZ
+    db = torch.empty(F, dtype=torch.float32, device=dev) if want_db else None
+    if not relu and not want_db:
+        return dY, None
+    ws_bytes = int(lib.mgcn_colsum_workspace_bytes(n, F)) if want_db else 0
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev) if want_db else None
+    with torch.cuda.device(dev):
+        rc = lib.mgcn_relu_bwd_colsum(n, F, L.ptr(dZ), L.ptr(Z.contiguous() if relu else None),
+                                      int(bool(relu)), L.ptr(dY if relu else None), L.ptr(db),
+                                      L.ptr(ws), ws_bytes, L.stream_of(dev))
+    L.check(rc, "mgcn_relu_bwd_colsum")
+    return dY, db
+
+
+class _Aggregate(torch.autograd.Function):
+    """y = epi(A_norm (x) H) with bias and ReLU fused; see module docstring."""
+
+    @staticmethod
+    def forward(ctx, H, bias, plan: GraphPlan, norm: NormPlan, reduce: int, relu: bool):
+        Y, argmax = spmm_fwd(plan.fwd, norm.w_fwd, H, reduce, bias, relu)
+        ctx.plan, ctx.norm, ctx.reduce, ctx.relu = plan, norm, reduce, relu
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(Y if relu else None, argmax)
+        return Y
+
+    @staticmethod
+    def backward(ctx, dZ):
+        Y, argmax = ctx.saved_tensors
+        plan, norm = ctx.plan, ctx.norm
+        need_h = ctx.needs_input_grad[0]
+        need_b = ctx.has_bias and ctx.needs_input_grad[1]
+        dY, db = relu_bwd_colsum(dZ, Y, ctx.relu, need_b)
+        dH = None
+        if need_h:
+            dH = spmm_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, ctx.reduce,
+                          cnt=plan.in_cnt if ctx.reduce == L.REDUCE_MEAN else None,
+                          argmax=argmax)
+        return dH, db, None, None, None, None
+
+
+def aggregate(H: torch.Tensor, edge_index: torch.Tensor, aggr: str = "add",
+              deg_norm: str | None = None, deg: torch.Tensor | None = None,
+              edge_weight: torch.Tensor | None = None, bias: torch.Tensor | None = None,
+              relu: bool = False, num_nodes: int | None = None) -> torch.Tensor:
+    """Fused gather -> scale -> reduce -> (+bias) -> (ReLU) over ``edge_index``.
+
+    Semantics of NodeModelAdditive.forward after its matmul
+    (gcn_base_models.py:209-241): messages flow ``edge_index[0] -> [1]``;
+    ``deg_norm`` in {None, 'sm', 'rw'} as degnorm_const; ``aggr`` in
+    {'add', 'mean', 'max'} as common.scatter_.
+    """
+    if aggr not in L.REDUCE_CODES:
+        raise ValueError(f"aggr must be one of add/mean/max, got {aggr!r}")
+    if deg_norm not in L.NORM_CODES:
+        raise ValueError(f"deg_norm must be None, 'sm' or 'rw', got {deg_norm!r}")
+    n = H.size(0) if num_nodes is None else int(num_nodes)
+    plan = plan_for(edge_index, n)
+    norm = plan.norm(deg_norm, deg=deg, edge_weight=edge_weight)
+    return _Aggregate.apply(H, bias, plan, norm, L.REDUCE_CODES[aggr], bool(relu))
+
+
+def aggregate_plan(H: torch.Tensor, plan: GraphPlan, norm: NormPlan, aggr: str = "add",
+                   bias: torch.Tensor | None = None, relu: bool = False) -> torch.Tensor:
+    """:func:`aggregate` on an already-built plan (no cache lookup)."""
+    return _Aggregate.apply(H, bias, plan, norm, L.REDUCE_CODES[aggr], bool(relu))
+
+
+# ---------------------------------------------------------------- scatter_
+class _SegmentReduce(torch.autograd.Function):
+    """torch_scatter 1.x scatter_{add,mean,max}(src, index, 0, None, dim_size)
+    on an explicit [E, F] ``src`` (common.py:37-66), as a SpMM whose k-th slot
+    gathers src row eid_k; the adjoint gathers dY[index[e]] back per edge."""
+
+    @staticmethod
+    def forward(ctx, src, index, dim_size: int, reduce: int):
+        dev = L.require_device(src, index)
+        E = src.size(0)
+        from .graph import build_view
+        ids = torch.arange(E, dtype=torch.int64, device=dev)
+        view = build_view(index, ids, dim_size, E)
+        Y, argmax = spmm_fwd(view, None, src, reduce)
+        # adjoint view: one slot per edge e, pointing at row index[e]
+        view_t = CSRView(rowptr=torch.arange(E + 1, dtype=torch.int64, device=dev),
+                         col=index.to(torch.int32).contiguous(),
+                         eid=ids.to(torch.int32), n_rows=E, n_cols=dim_size)
+        cnt = (view.rowptr[1:] - view.rowptr[:-1]).clamp_(min=1).to(torch.float32)
+        ctx.view_t, ctx.reduce, ctx.cnt = view_t, reduce, cnt
+        ctx.save_for_backward(argmax)
+        return Y
+
+    @staticmethod
+    def backward(ctx, dY):
+        (argmax,) = ctx.saved_tensors
+        d_src = spmm_bwd(ctx.view_t, None, None, dY, ctx.reduce,
+                         cnt=ctx.cnt if ctx.reduce == L.REDUCE_MEAN else None, argmax=argmax)
+        return d_src, None, None, None
+
+
+def scatter_(name: str, src: torch.Tensor, index: torch.Tensor, dim_size: int | None = None,
+             out: torch.Tensor | None = None) -> torch.Tensor:
+    """Drop-in for src/gcn_meta/models/common.py:37-66 ``scatter_``.
+
+    'max' fills empty rows with -1e38 and then replaces exact fill values by 0
+    (:57, :63-64); 'mean' divides by ``max(count, 1)``.  ``out`` is accepted
+    for signature compatibility; like the reference's only caller (which
+    passes none) it must be None.
+    """
+    assert name in ["add", "mean", "max"]
+    if out is not None:
+        raise NotImplementedError("scatter_(out=...) is not supported; the reference never uses it")
+    if dim_size is None:
+        dim_size = int(index.max().item()) + 1 if index.numel() else 0
+    squeeze = src.dim() == 1
+    x = src.unsqueeze(1) if squeeze else src
+    y = _SegmentReduce.apply(x, index, int(dim_size), L.REDUCE_CODES[name])
+    return y.squeeze(1) if squeeze else y
+
+
+def segment_mean(x: torch.Tensor, ptr: torch.Tensor) -> torch.Tensor:
+    """Mean of contiguous row segments [ptr[g], ptr[g+1]) (global_mean_pool)."""
+    return _SegmentMean.apply(x, ptr)
+
+
+class _SegmentMean(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, ptr):
+        lib = L.load()
+        x = _contig_f32(x, "x")
+        ptr = ptr.to(torch.int64).contiguous()
+        dev = L.require_device(x, ptr)
+        G = ptr.numel() - 1
+        out = torch.empty(G, x.size(1), dtype=torch.float32, device=dev)
+        with torch.cuda.device(dev):
+            rc = lib.mgcn_segment_mean(G, x.size(1), L.ptr(ptr), L.ptr(x), x.stride(0), L.ptr(out),
+                                       out.stride(0), L.stream_of(dev))
+        L.check(rc, "mgcn_segment_mean")
+        ctx.save_for_backward(ptr)
+        ctx.n = x.size(0)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (ptr,) = ctx.saved_tensors
+        counts = (ptr[1:] - ptr[:-1])
+        seg = torch.repeat_interleave(torch.arange(counts.numel(), device=ptr.device), counts,
+                                      output_size=ctx.n)
+        scale = counts.clamp(min=1).to(dout.dtype)
+        return (dout / scale.unsqueeze(1))[seg], None

@@ -1,0 +1,228 @@
+"""GPU parity: libmgcn kernels (through the C ABI via mgcn) against the golden
+fixtures of the reference and against the C oracle.
+
+Bar (north_star): the aggregation is integer-indexed fp32 work done in the
+reference's exact operation order, so given the same H it must match BIT FOR
+BIT (np.testing.assert_array_equal).  Whole layers include a GEMM whose
+rounding differs between BLAS libraries: those compare with
+rtol = 1e-5 (forward) / 1e-4 (gradients) as stated per test.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_names, load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _t(a, dev, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    return t if dtype is None else t.to(dtype)
+
+
+def _meta(z):
+    m = [str(v) for v in z["meta"]]
+    return (None if m[0] == "none" else m[0]), m[1], bool(int(m[2])), bool(int(m[3])), \
+        bool(int(m[4]))
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+# ------------------------------------------------------------ fixtures
+@pytest.mark.parametrize("name", golden_names("aggr_"))
+def test_aggregate_matches_reference_bitwise(cuda, name):
+    import mgcn
+    z = load_golden(name)
+    deg_norm, aggr, bias, identity, relu = _meta(z)
+    x = _t(z["x"], cuda).requires_grad_(True)
+    ei = _t(z["edge_index"], cuda)
+    b = _t(z["b"], cuda).requires_grad_(True) if bias else None
+    deg = _t(z["deg"], cuda) if "deg" in z else None
+    ew = _t(z["edge_weight"], cuda) if "edge_weight" in z else None
+    y = mgcn.aggregate(x, ei, aggr=aggr, deg_norm=deg_norm, deg=deg, edge_weight=ew, bias=b,
+                       relu=relu)
+    np.testing.assert_array_equal(_np(y), z["y"])
+    y.backward(_t(z["dZ"], cuda))
+    np.testing.assert_array_equal(_np(x.grad), z["dx"])
+    if bias:
+        np.testing.assert_allclose(_np(b.grad), z["db"], rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("name", golden_names("layer_"))
+def test_node_model_additive_matches_reference(cuda, name):
+    from mgcn.models import NodeModelAdditive
+    z = load_golden(name)
+    deg_norm, aggr, bias, _, _ = _meta(z)
+    F = z["x"].shape[1]
+    m = NodeModelAdditive(F, F, deg_norm=deg_norm, aggr=aggr, bias=bias).to(cuda)
+    with torch.no_grad():
+        m.weight_node.copy_(_t(z["W"], cuda))
+        if bias:
+            m.bias.copy_(_t(z["b"], cuda))
+    x = _t(z["x"], cuda).requires_grad_(True)
+    y = m(x, _t(z["edge_index"], cuda))
+    np.testing.assert_allclose(_np(y), z["y"], rtol=1e-5, atol=1e-5)
+    y.backward(_t(z["dZ"], cuda))
+    np.testing.assert_allclose(_np(x.grad), z["dx"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(_np(m.weight_node.grad), z["dW"], rtol=1e-4, atol=1e-3)
+    if bias:
+        np.testing.assert_allclose(_np(m.bias.grad), z["db"], rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("name", golden_names("scatter_"))
+def test_scatter_matches_reference_bitwise(cuda, name):
+    import mgcn
+    z = load_golden(name)
+    op = str(z["meta"][0])
+    src = _t(z["src"], cuda).requires_grad_(True)
+    out = mgcn.scatter_(op, src, _t(z["index"], cuda), dim_size=z["out"].shape[0])
+    np.testing.assert_array_equal(_np(out), z["out"])
+    out.backward(_t(z["dY"], cuda))
+    np.testing.assert_array_equal(_np(src.grad), z["dsrc"])
+
+
+@pytest.mark.parametrize("name", golden_names("degnorm_"))
+def test_degnorm_const_matches_reference_bitwise(cuda, name):
+    from mgcn.models import NodeModelBase
+    z = load_golden(name)
+    method = str(z["meta"][0])
+    ei = _t(z["edge_index"], cuda)
+    deg = _t(z["deg"], cuda) if "deg" in z else None
+    ew = _t(z["edge_weight"], cuda) if "edge_weight" in z else None
+    norm = NodeModelBase.degnorm_const(ei, 300, deg, ew, method)
+    np.testing.assert_array_equal(_np(norm), z["norm"])
+
+
+def test_gcn_model_12_layer_botnet_matches_reference(cuda):
+    """Config 3 shape (run_botnet.sh:14): 12 layers F=32, residual_hop=1."""
+    from mgcn.models import GCNModel
+    z = load_golden("model12_botnet")
+    model = GCNModel(1, [32] * 12, 2, non_linear='relu', non_linear_layer_wise='relu',
+                     residual_hop=1, dropout=0.0, final_type='proj', pred_on='node',
+                     deg_norm='sm', aggr='add', bias=False).to(cuda)
+    sd = {k[2:]: _t(v, cuda) for k, v in z.items() if k.startswith("p_")}
+    model.load_state_dict(sd)
+    x = _t(z["x"], cuda)
+    out = model(x[:, 0:1], _t(z["edge_index"], cuda), deg_K=x[:, 1])
+    np.testing.assert_allclose(_np(out), z["out"], rtol=1e-4, atol=1e-4)
+    out.backward(_t(z["dout"], cuda))
+    for k, p in model.named_parameters():
+        ref = z["g_" + k]
+        scale = max(1.0, float(np.abs(ref).max()))
+        np.testing.assert_allclose(_np(p.grad), ref, rtol=1e-3, atol=1e-4 * scale, err_msg=k)
+
+
+# ------------------------------------------------- random graphs vs oracle
+def _graph(rng, N, E, loops=True, heavy=0):
+    s = rng.integers(0, N, E)
+    d = rng.integers(0, N, E)
+    if heavy:
+        d = np.concatenate([d, np.zeros(heavy, np.int64)])
+        s = np.concatenate([s, rng.integers(0, N, heavy)])
+    if loops:
+        s = np.concatenate([s, np.arange(N)])
+        d = np.concatenate([d, np.arange(N)])
+    return np.stack([s, d]).astype(np.int64)
+
+
+CASES = [
+    # N, E, F, deg_norm, aggr, relu, heavy
+    (20000, 200000, 128, "sm", "add", True, 0),
+    (20000, 200000, 64, "rw", "mean", False, 0),
+    (20000, 200000, 32, None, "max", False, 0),
+    (5000, 60000, 7, "sm", "max", True, 0),
+    (5000, 60000, 2, "rw", "add", False, 0),
+    (3000, 30000, 300, "sm", "mean", True, 0),
+    (3000, 30000, 128, "sm", "add", False, 12000),  # one destination of degree 12k
+    (3000, 30000, 1, "sm", "add", False, 0),
+]
+
+
+@pytest.mark.parametrize("N,E,F,deg_norm,aggr,relu,heavy", CASES)
+def test_random_graph_vs_oracle_bitwise(cuda, oracle, N, E, F, deg_norm, aggr, relu, heavy):
+    import mgcn
+    rng = np.random.default_rng(N + E + F)
+    ei = _graph(rng, N, E, heavy=heavy)
+    H = rng.standard_normal((N, F)).astype(np.float32)
+    b = rng.uniform(-0.5, 0.5, F).astype(np.float32)
+    dZ = rng.standard_normal((N, F)).astype(np.float32)
+    wf, wb, rs = oracle.edge_factors(ei, N, deg_norm)
+    y_ref, am = oracle.aggr_fwd(ei, H, wf, aggr, b, relu)
+    dH_ref, db_ref = oracle.aggr_bwd(ei, dZ, wb, rs, aggr, y_ref, relu, am, want_db=True)
+    Ht = _t(H, cuda).requires_grad_(True)
+    bt = _t(b, cuda).requires_grad_(True)
+    y = mgcn.aggregate(Ht, _t(ei, cuda), aggr=aggr, deg_norm=deg_norm, bias=bt, relu=relu)
+    np.testing.assert_array_equal(_np(y), y_ref)
+    y.backward(_t(dZ, cuda))
+    np.testing.assert_array_equal(_np(Ht.grad), dH_ref)
+    np.testing.assert_allclose(_np(bt.grad), db_ref, rtol=1e-4, atol=1e-3)
+
+
+def test_noncontiguous_and_strided_inputs(cuda, oracle):
+    import mgcn
+    rng = np.random.default_rng(7)
+    N, F = 2000, 64
+    ei = _graph(rng, N, 20000)
+    big = rng.standard_normal((N, 2 * F)).astype(np.float32)
+    H = big[:, ::2]
+    wf, _, _ = oracle.edge_factors(ei, N, "sm")
+    y_ref, _ = oracle.aggr_fwd(ei, H, wf, "add")
+    Ht = _t(big, cuda)[:, ::2]
+    y = mgcn.aggregate(Ht, _t(ei, cuda), aggr="add", deg_norm="sm")
+    np.testing.assert_array_equal(_np(y), y_ref)
+
+
+def test_empty_graph_and_isolated_nodes(cuda):
+    import mgcn
+    N, F = 17, 8
+    H = torch.randn(N, F, device=cuda)
+    ei = torch.zeros(2, 0, dtype=torch.long, device=cuda)
+    for aggr in ["add", "mean", "max"]:
+        y = mgcn.aggregate(H, ei, aggr=aggr, deg_norm="sm")
+        assert torch.equal(y, torch.zeros_like(y))
+
+
+def test_out_of_range_index_raises(cuda):
+    import mgcn
+    H = torch.randn(4, 8, device=cuda)
+    ei = torch.tensor([[0, 1], [2, 4]], device=cuda)
+    mgcn.clear_cache()
+    with pytest.raises(IndexError):
+        mgcn.aggregate(H, ei)
+
+
+def test_deterministic_repeat(cuda):
+    import mgcn
+    rng = np.random.default_rng(3)
+    ei = _t(_graph(rng, 10000, 100000), cuda)
+    H = torch.randn(10000, 128, device=cuda)
+    y1 = mgcn.aggregate(H, ei, deg_norm="sm")
+    y2 = mgcn.aggregate(H, ei, deg_norm="sm")
+    assert torch.equal(y1, y2)
+
+
+# --------------------------------------------- full size (config 2) properties
+@pytest.mark.slow
+def test_config2_full_size_forward_backward_bitwise(cuda, oracle):
+    """BASELINE config 2 (N = 1M, 10M symmetrised edges + 1M loops, F = 128):
+    the headline workload itself, forward and adjoint, bit for bit against
+    the C oracle (a few seconds of single-threaded CPU)."""
+    import mgcn
+    from bench import make_er_graph
+    ei, N = make_er_graph(1_000_000, 5_000_000)
+    eic = ei.to(cuda)
+    g = torch.Generator().manual_seed(1)
+    H = torch.randn(N, 128, generator=g)
+    dZ = torch.randn(N, 128, generator=g)
+    Ht = H.to(cuda).requires_grad_(True)
+    y = mgcn.aggregate(Ht, eic, deg_norm="sm", relu=True)
+    y.backward(dZ.to(cuda))
+    ein = ei.numpy()
+    wf, wb, rs = oracle.edge_factors(ein, N, "sm")
+    y_ref, _ = oracle.aggr_fwd(ein, H.numpy(), wf, "add", None, True)
+    np.testing.assert_array_equal(_np(y), y_ref)
+    dH_ref, _ = oracle.aggr_bwd(ein, dZ.numpy(), wb, rs, "add", y_ref, True, None)
+    np.testing.assert_array_equal(_np(Ht.grad), dH_ref)
