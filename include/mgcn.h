@@ -161,6 +161,22 @@ int mgcn_spmm_bwd(int64_t n_rows, int32_t F, const int64_t *rowptr_t,
                   float *dH, int64_t lddh, int reduce, const float *cnt,
                   const int32_t *argmax, int accumulate, void *stream);
 
+/* ------------------------------------------------------------------ dense */
+
+/* Bytes of scratch mgcn_gemm_tn needs. */
+size_t mgcn_gemm_tn_workspace_bytes(int64_t K, int32_t M, int32_t N);
+
+/*
+ * C[M, N] = A^T B (accumulate != 0: C += A^T B) for row-major A [K, M] (row
+ * stride lda) and B [K, N] (ldb), fp32 on v_mfma_f32_32x32x2_f32, K split over
+ * the chip with a deterministic fixed-order reduction of the partials.
+ * Replaces autograd's weight gradient of `torch.matmul(x, self.weight_node)`
+ * (gcn_base_models.py:201): dW = x^T dH with K = number of nodes.
+ */
+int mgcn_gemm_tn(int64_t K, int32_t M, int32_t N, const float *A, int64_t lda,
+                 const float *B, int64_t ldb, float *C, int64_t ldc, int accumulate,
+                 void *workspace, size_t workspace_bytes, void *stream);
+
 /* ----------------------------------------------------------- elementwise */
 
 /* Bytes of scratch mgcn_relu_bwd_colsum needs. */

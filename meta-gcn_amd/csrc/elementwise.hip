@@ -81,14 +81,23 @@ __global__ __launch_bounds__(kBlock) void relu_bwd_colsum_kernel(
   }
 }
 
+// db[f] = fold of the block partials: 4 interleaved groups of blocks, each in
+// block order, then the 4 group sums in order (deterministic).
 __global__ __launch_bounds__(kBlock) void colsum_finish_kernel(const float *__restrict__ partial,
                                                                int nblk, int F,
                                                                float *__restrict__ db) {
-  for (int f = blockIdx.x * blockDim.x + threadIdx.x; f < F; f += gridDim.x * blockDim.x) {
-    float s = 0.0f;
-    for (int b = 0; b < nblk; ++b) s = __fadd_rn(s, partial[(int64_t)b * F + f]);
-    db[f] = s;
-  }
+  __shared__ float red[4][64];
+  const int g = threadIdx.x >> 6;
+  const int f = blockIdx.x * 64 + (threadIdx.x & 63);
+  float s = 0.0f;
+  if (f < F)
+#pragma unroll 8
+    for (int b = g; b < nblk; b += 4) s = __fadd_rn(s, partial[(int64_t)b * F + f]);
+  red[g][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (g == 0 && f < F)
+    db[f] = __fadd_rn(__fadd_rn(red[0][threadIdx.x], red[1][threadIdx.x]),
+                      __fadd_rn(red[2][threadIdx.x], red[3][threadIdx.x]));
 }
 
 // one wave per segment; lanes stride the features
@@ -163,7 +172,7 @@ extern "C" int mgcn_relu_bwd_colsum(int64_t n_rows, int32_t F, const float *dZ, 
   }
   if (int rc = check_launch("relu_bwd_colsum_kernel")) return rc;
   if (db != nullptr) {
-    hipLaunchKernelGGL(colsum_finish_kernel, dim3((F + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
+    hipLaunchKernelGGL(colsum_finish_kernel, dim3((F + 63) / 64), dim3(kBlock), 0, s,
                        partial, nblk, F, db);
     return check_launch("colsum_finish_kernel");
   }

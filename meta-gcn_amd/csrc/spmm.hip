@@ -405,7 +405,7 @@ extern "C" int mgcn_spmm_fwd(int64_t n_rows, int32_t F, const int64_t *rowptr, c
   if (n_rows == 0 || F == 0) return MGCN_OK;
   MGCN_REQUIRE(rowptr && H && Y, "mgcn_spmm_fwd: null array");  // col may be NULL when nnz == 0
   MGCN_REQUIRE(ldh >= F && ldy >= F, "mgcn_spmm_fwd: leading dimension < F");
-  MGCN_REQUIRE(reduce != MGCN_REDUCE_MAX || (argmax != nullptr && eid != nullptr),
+  MGCN_REQUIRE(reduce != MGCN_REDUCE_MAX || argmax != nullptr,  // eid NULL only if nnz == 0
                "mgcn_spmm_fwd: MAX needs argmax and eid");
   SpmmArgs a{};
   a.n_rows = n_rows;
@@ -443,7 +443,7 @@ extern "C" int mgcn_spmm_bwd(int64_t n_rows, int32_t F, const int64_t *rowptr_t,
   MGCN_REQUIRE(rowptr_t && dY && dH, "mgcn_spmm_bwd: null array");  // col may be NULL when nnz == 0
   MGCN_REQUIRE(lddy >= F && lddh >= F, "mgcn_spmm_bwd: leading dimension < F");
   MGCN_REQUIRE(reduce != MGCN_REDUCE_MEAN || cnt != nullptr, "mgcn_spmm_bwd: MEAN needs cnt");
-  MGCN_REQUIRE(reduce != MGCN_REDUCE_MAX || (argmax != nullptr && eid_t != nullptr),
+  MGCN_REQUIRE(reduce != MGCN_REDUCE_MAX || argmax != nullptr,  // eid NULL only if nnz == 0
                "mgcn_spmm_bwd: MAX needs argmax and eid");
   SpmmArgs a{};
   a.n_rows = n_rows;

@@ -44,6 +44,9 @@ SIGNATURES = {
                              _int, _vp, _vp]),
     "mgcn_spmm_bwd": (_int, [_i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _int,
                              _vp, _vp, _int, _vp]),
+    "mgcn_gemm_tn_workspace_bytes": (_sz, [_i64, _i32, _i32]),
+    "mgcn_gemm_tn": (_int, [_i64, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _int, _vp, _sz,
+                            _vp]),
     "mgcn_colsum_workspace_bytes": (_sz, [_i64, _i32]),
     "mgcn_relu_bwd_colsum": (_int, [_i64, _i32, _vp, _vp, _int, _vp, _vp, _vp, _sz, _vp]),
     "mgcn_segment_mean": (_int, [_i64, _i32, _vp, _vp, _i64, _vp, _i64, _vp]),

@@ -26,7 +26,7 @@ from torch.nn.utils.rnn import pad_sequence
 
 from . import _lib as L
 from .graph import plan_for
-from .ops import aggregate_plan, scatter_  # noqa: F401  (re-exported)
+from .ops import aggregate_plan, linear, scatter_  # noqa: F401  (re-exported)
 
 
 # --------------------------------------------------------------- inits (PyG)
@@ -153,7 +153,7 @@ class NodeModelAdditive(NodeModelBase):
             raise NotImplementedError(
                 "edge_attr messages (gcn_base_models.py:204-227) are not supported by the "
                 "mgcn engine")
-        x = torch.matmul(x, self.weight_node)  # gcn_base_models.py:201
+        x = linear(x, self.weight_node)  # torch.matmul(x, W), gcn_base_models.py:201
         plan = plan_for(edge_index, x.size(0))
         # deg_norm None ignores edge_weight entirely (gcn_base_models.py:209-211)
         norm = plan.norm(self.deg_norm, deg=deg,

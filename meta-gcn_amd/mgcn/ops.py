@@ -117,6 +117,61 @@ def relu_bwd_colsum(dZ: torch.Tensor, Z: torch.Tensor | None, relu: bool, want_d
     return dY, db
 
 
+def gemm_tn(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor | None = None,
+            accumulate: bool = False) -> torch.Tensor:
+    """C = A^T B on fp32 MFMA with split-K (libmgcn ``mgcn_gemm_tn``)."""
+    lib = L.load()
+    A = _contig_f32(A, "A")
+    B = _contig_f32(B, "B")
+    dev = L.require_device(A, B)
+    K, M = A.shape
+    if B.size(0) != K:
+        raise ValueError(f"gemm_tn: A has {K} rows, B has {B.size(0)}")
+    N = B.size(1)
+    C = out if out is not None else torch.empty(M, N, dtype=torch.float32, device=dev)
+    ws_bytes = int(lib.mgcn_gemm_tn_workspace_bytes(K, M, N))
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    if _TIMER is not None:
+        _TIMER("gemm_tn", True)
+    with torch.cuda.device(dev):
+        rc = lib.mgcn_gemm_tn(K, M, N, L.ptr(A), A.stride(0), L.ptr(B), B.stride(0), L.ptr(C),
+                              C.stride(0), int(bool(accumulate)), L.ptr(ws), ws_bytes,
+                              L.stream_of(dev))
+    if _TIMER is not None:
+        _TIMER("gemm_tn", False)
+    L.check(rc, "mgcn_gemm_tn")
+    return C
+
+
+class _Linear(torch.autograd.Function):
+    """H = x @ W (gcn_base_models.py:201).  Forward and dX stay on
+    torch.matmul (hipBLASLt); dW = x^T dH, a K = num_nodes reduction that
+    hipBLASLt handles poorly, runs on libmgcn's split-K MFMA kernel."""
+
+    @staticmethod
+    def forward(ctx, x, W):
+        ctx.save_for_backward(x, W)
+        return torch.matmul(x, W)
+
+    @staticmethod
+    def backward(ctx, dH):
+        x, W = ctx.saved_tensors
+        dx = dW = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.matmul(dH, W.t())
+        if ctx.needs_input_grad[1]:
+            dW = gemm_tn(x, dH)
+        return dx, dW
+
+
+def linear(x: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
+    """``torch.matmul(x, W)`` with the libmgcn weight-gradient kernel."""
+    if x.dim() != 2 or x.dtype != torch.float32 or W.dtype != torch.float32 \
+            or x.device.type != "cuda":
+        return torch.matmul(x, W)
+    return _Linear.apply(x, W)
+
+
 class _Aggregate(torch.autograd.Function):
     """y = epi(A_norm (x) H) with bias and ReLU fused; see module docstring."""
 

@@ -1,0 +1,114 @@
+"""Destination-range sharding (mgcn.dist) under gloo, world size 2 and 4, on
+the CPU: sharded forward outputs must equal the single-process run bit for
+bit (every destination row is local, COO order kept) and so must the
+per-rank dH; replicated-parameter gradients (all-reduced partial sums) match
+within fp32 tolerance.  Local compute is the CPU test double in
+tests/cpu_backend.py; the GPU run of the same path uses libmgcn + RCCL."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _problem(N=300, pairs=1500, F=16, L=3, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    s = torch.randint(0, N, (pairs,), generator=g)
+    d = torch.randint(0, N, (pairs,), generator=g)
+    loops = torch.arange(N)
+    ei = torch.stack([torch.cat([s, d, loops]), torch.cat([d, s, loops])])
+    X = torch.randn(N, F, generator=g)
+    Ws = [torch.randn(F, F, generator=g) * 0.3 for _ in range(L)]
+    bs = [torch.randn(F, generator=g) * 0.1 for _ in range(L)]
+    dY = torch.randn(N, F, generator=g)
+    return ei, N, X, Ws, bs, dY
+
+
+def _run(rank, world, port, aggr, out_q):
+    sys.path[:0] = [os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "meta-gcn_amd"),
+                    HERE]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.set_num_threads(1)
+        from cpu_backend import CpuBackend
+        from mgcn.dist import ShardedGCN
+        ei, N, X, Ws, bs, dY = _problem()
+        m = ShardedGCN(ei, N, Ws, bs, device=torch.device("cpu"), aggr=aggr,
+                       backend=CpuBackend())
+        Xl = m.local_rows(X).requires_grad_(True)
+        out = m.forward(Xl)
+        out.backward(m.local_rows(dY))
+        from mgcn.dist import allreduce_grads
+        allreduce_grads(m.params())
+        res = {"rank": rank, "lo": m.shard.lo, "hi": m.shard.hi, "out": out.detach().numpy(),
+               "dX": Xl.grad.numpy(), "grads": [p.grad.numpy() for p in m.params()]}
+        out_q.put(res)
+    finally:
+        dist.destroy_process_group()
+
+
+def _launch(world, aggr):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_run, args=(r, world, port, aggr, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort(key=lambda r: r["rank"])
+    return res
+
+
+@pytest.mark.parametrize("world,aggr", [(2, "add"), (2, "mean"), (4, "add"), (2, "max")])
+def test_sharded_matches_single_process(world, aggr):
+    single = _launch(1, aggr)[0]
+    shards = _launch(world, aggr)
+    assert shards[0]["lo"] == 0 and shards[-1]["hi"] == single["out"].shape[0]
+    for r in shards:
+        lo, hi = r["lo"], r["hi"]
+        np.testing.assert_array_equal(r["out"], single["out"][lo:hi])   # forward: bitwise
+        np.testing.assert_array_equal(r["dX"], single["dX"][lo:hi])     # adjoint rows: bitwise
+        for g, g1 in zip(r["grads"], single["grads"]):                  # all-reduced partials
+            np.testing.assert_allclose(g, g1, rtol=1e-5, atol=1e-5)
+
+
+def test_single_process_double_matches_oracle(oracle):
+    """The CPU double (world 1) against the C oracle, one layer, W = I."""
+    sys.path.insert(0, HERE)
+    from cpu_backend import CpuBackend
+    from mgcn.dist import build_shard, sharded_aggregate
+    ei, N, X, Ws, bs, dY = _problem(L=1)
+    be = CpuBackend()
+    sh = build_shard(ei, N, "sm", backend=be)
+    x = X.clone().requires_grad_(True)
+    y = sharded_aggregate(x, sh, "add", bs[0], relu=True, backend=be)
+    y.backward(dY)
+    wf, wb, rs = oracle.edge_factors(ei.numpy(), N, "sm")
+    y_ref, _ = oracle.aggr_fwd(ei.numpy(), X.numpy(), wf, "add", bs[0].numpy(), True)
+    np.testing.assert_array_equal(y.detach().numpy(), y_ref)
+    dH, _ = oracle.aggr_bwd(ei.numpy(), dY.numpy(), wb, rs, "add", y_ref, True, None)
+    np.testing.assert_array_equal(x.grad.numpy(), dH)
+
+
+def test_partition_balances_edges():
+    from mgcn.dist import partition_nodes
+    rp = torch.tensor([0, 10, 10, 10, 50, 51, 60, 100])
+    b = partition_nodes(rp, 3)
+    assert b[0] == 0 and b[-1] == 7 and all(x <= y for x, y in zip(b, b[1:]))

@@ -226,3 +226,21 @@ def test_config2_full_size_forward_backward_bitwise(cuda, oracle):
     np.testing.assert_array_equal(_np(y), y_ref)
     dH_ref, _ = oracle.aggr_bwd(ein, dZ.numpy(), wb, rs, "add", y_ref, True, None)
     np.testing.assert_array_equal(_np(Ht.grad), dH_ref)
+
+
+# ----------------------------------------------------------------- dense
+@pytest.mark.parametrize("K,M,N", [(1_000_000, 128, 128), (4097, 128, 128), (3000, 7, 130),
+                                   (50, 32, 2), (0, 4, 4)])
+def test_gemm_tn_matches_fp64(cuda, K, M, N):
+    """dW = A^T B on fp32 MFMA (exact f32 products, f32 accumulation in a
+    different order than any BLAS): |err| <= 1e-5 * sum_k |a_k b_k| + 1e-6."""
+    from mgcn.ops import gemm_tn
+    g = torch.Generator(device=cuda).manual_seed(K + M)
+    A = torch.randn(K, M, device=cuda, generator=g)
+    B = torch.randn(K, N, device=cuda, generator=g)
+    C = gemm_tn(A, B)
+    ref = A.double().t() @ B.double()
+    bound = A.double().abs().t() @ B.double().abs()
+    assert ((C.double() - ref).abs() <= 1e-5 * bound + 1e-6).all()
+    C2 = gemm_tn(A, B)
+    assert torch.equal(C, C2)  # deterministic
