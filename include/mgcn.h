@@ -177,6 +177,25 @@ int mgcn_gemm_tn(int64_t K, int32_t M, int32_t N, const float *A, int64_t lda,
                  const float *B, int64_t ldb, float *C, int64_t ldc, int accumulate,
                  void *workspace, size_t workspace_bytes, void *stream);
 
+/* 1 if mgcn_gemm_nn handles this (K, N): K in {32, 64, 128}, 1 <= N <= 128. */
+int mgcn_gemm_nn_supported(int32_t K, int32_t N);
+/* Bytes of scratch mgcn_gemm_nn needs for its fused column sums. */
+size_t mgcn_gemm_nn_workspace_bytes(int64_t M, int32_t N);
+
+/*
+ * C[M, N] = A[M, K] . B[K, N] on v_mfma_f32_32x32x2_f32; A row-major (lda,
+ * 16-byte aligned rows), B addressed as B[k * sbk + n * sbn] (so W or W^T).
+ * Replaces `torch.matmul(x, self.weight_node)` (gcn_base_models.py:201) and
+ * its input gradient dX = dH W^T.  If Z != NULL the previous layer's ReLU
+ * backward and bias gradient are fused into the epilogue:
+ *   C = Z > 0 ? A.B : 0,  colsum[n] = sum_m C[m, n]  (deterministic)
+ * (gcn_model.py:196 + gcn_base_models.py:240-241 adjoints).
+ */
+int mgcn_gemm_nn(int64_t M, int32_t K, int32_t N, const float *A, int64_t lda,
+                 const float *B, int64_t sbk, int64_t sbn, float *C, int64_t ldc,
+                 const float *Z, int64_t ldz, float *colsum, void *workspace,
+                 size_t workspace_bytes, void *stream);
+
 /* ----------------------------------------------------------- elementwise */
 
 /* Bytes of scratch mgcn_relu_bwd_colsum needs. */

@@ -178,3 +178,243 @@ extern "C" int mgcn_gemm_tn(int64_t K, int32_t M, int32_t N, const float *A, int
                      partial, used, MN, N, C, ldc, accumulate);
   return check_launch("gemm_reduce_kernel");
 }
+
+// ---------------------------------------------------------------------------
+// mgcn_gemm_nn: C[M, N] = A[M, K] . B[K, N]   (tall-skinny: M = nodes, K, N = F)
+//
+// The forward transform H = X W (gcn_base_models.py:201) and the input
+// gradient dX = dH W^T of a layer (B = W^T through strides).  One workgroup
+// per 128-row tile of A; wave w owns output columns [32w, 32w + 32) and the
+// four 32-row M sub-tiles (4 accumulators of v_mfma_f32_32x32x2_f32).
+//   * the wave's 32-column slab of B stays in registers for the whole tile
+//     (K/2 floats per lane);
+//   * the A tile is staged once through LDS ([128][K + 4] floats: the +4 pad
+//     makes the ds_read_b128 fragment reads conflict-free) and read by all
+//     four waves;
+//   * K order inside the MFMA chain is permuted (lane half h takes
+//     k = s + h K/2) so one ds_read_b128 feeds four consecutive k-steps.
+// Epilogue modes:
+//   EPI_STORE  C = acc
+//   EPI_RELU   (the previous layer's ReLU backward fused into dX):
+//              C = Z > 0 ? acc : 0, and per-tile column sums of C written to
+//              colsum_partial[tile][N] (the bias gradient, folded in tile order
+//              by mgcn_colsum_finish -- deterministic).
+// Roofline: 2 M K N FLOP on 157 TF fp32 MFMA vs 4 M (K + N) bytes;
+// at K = N = 128 the MFMA side is the bound (0.21 ms vs 0.13 ms at 8 TB/s).
+
+namespace mgcn {
+namespace {
+
+constexpr int kNNRows = 128;  // rows of A per workgroup
+constexpr int EPI_STORE = 0, EPI_RELU = 1;
+
+template <int K, int EPI>
+__global__ __launch_bounds__(256, 2) void gemm_nn_kernel(
+    const float *__restrict__ A, int64_t lda, const float *__restrict__ B, int64_t sbk,
+    int64_t sbn, float *__restrict__ C, int64_t ldc, int64_t M, int N,
+    const float *__restrict__ Z, int64_t ldz, float *__restrict__ colsum_partial) {
+  constexpr int LDA = K + 4;
+  constexpr int KH = K / 2;  // k-steps per lane half
+  constexpr int V4_PER_ROW = K / 4;
+  constexpr int V4_PER_THREAD = kNNRows * V4_PER_ROW / 256;
+  // register prefetch of the next A tile, except where it would spill (the
+  // K = 128 ReLU epilogue needs those registers; the co-resident workgroup
+  // still overlaps its loads with this one's MFMAs)
+  constexpr bool kPrefetch = !(K == 128 && EPI == EPI_RELU);
+  __shared__ __attribute__((aligned(16))) float sA[kNNRows * LDA];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int h = lane >> 5, lc = lane & 31;
+  const int n = wave * 32 + lc;  // output column of this lane
+  const bool n_ok = n < N;
+  const int64_t n_tiles = (M + kNNRows - 1) / kNNRows;
+
+  // B slab of this wave's 32 columns: b[s] = B[k = s + h*KH][n] (whole kernel)
+  float b[KH];
+#pragma unroll
+  for (int s = 0; s < KH; ++s)
+    b[s] = n_ok ? B[(int64_t)(s + h * KH) * sbk + (int64_t)n * sbn] : 0.0f;
+
+  // register prefetch of one A tile: thread t holds float4 #(t + 256 i)
+  float4 pre[V4_PER_THREAD];
+  auto fetch = [&](int64_t tile) {
+    const int64_t m0 = tile * kNNRows;
+#pragma unroll
+    for (int i = 0; i < V4_PER_THREAD; ++i) {
+      const int idx = threadIdx.x + 256 * i;
+      const int r = idx / V4_PER_ROW, c4 = idx % V4_PER_ROW;
+      pre[i] = (m0 + r < M) ? *reinterpret_cast<const float4 *>(A + (m0 + r) * lda + c4 * 4)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  float csum = 0.0f;
+  int64_t tile = blockIdx.x;
+  if (kPrefetch && tile < n_tiles) fetch(tile);
+  for (; tile < n_tiles; tile += gridDim.x) {
+    const int64_t m0 = tile * kNNRows;
+    if (!kPrefetch) fetch(tile);
+    __syncthreads();  // previous tile's LDS reads are done
+#pragma unroll
+    for (int i = 0; i < V4_PER_THREAD; ++i) {
+      const int idx = threadIdx.x + 256 * i;
+      const int r = idx / V4_PER_ROW, c4 = idx % V4_PER_ROW;
+      *reinterpret_cast<float4 *>(&sA[r * LDA + c4 * 4]) = pre[i];
+    }
+    __syncthreads();
+    if (kPrefetch && tile + gridDim.x < n_tiles) fetch(tile + gridDim.x);  // overlaps MFMAs
+
+    f32x16 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
+#pragma unroll
+    for (int s4 = 0; s4 < KH; s4 += 4) {
+      float4 a4[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        a4[t] = *reinterpret_cast<const float4 *>(&sA[(t * 32 + lc) * LDA + h * KH + s4]);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[t].x, b[s4 + 0], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[t].y, b[s4 + 1], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[t].z, b[s4 + 2], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[t].w, b[s4 + 3], acc[t], 0, 0, 0);
+      }
+    }
+
+    // epilogue; C/D map: col = lane & 31 (-> n), row = (r&3) + 8 (r>>2) + 4 h.
+    // Full tiles take an unguarded path (guarded loads would serialise).
+    const bool full = (m0 + kNNRows <= M) && n_ok;
+    if (full) {
+      if constexpr (EPI == EPI_RELU) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          float zv[16];  // 16 independent loads in flight, then mask/store
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            zv[r] = Z[(m0 + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * ldz + n];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float v = (zv[r] > 0.0f) ? acc[t][r] : 0.0f;
+            csum = __fadd_rn(csum, v);
+            C[(m0 + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * ldc + n] = v;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            C[(m0 + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * ldc + n] = acc[t][r];
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int64_t row = m0 + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          if (row < M && n_ok) {
+            float v = acc[t][r];
+            if constexpr (EPI == EPI_RELU) {
+              v = (Z[row * ldz + n] > 0.0f) ? v : 0.0f;
+              csum = __fadd_rn(csum, v);
+            }
+            C[row * ldc + n] = v;
+          }
+        }
+    }
+  }
+  if constexpr (EPI == EPI_RELU) {
+    const float other = __shfl_xor(csum, 32, 64);
+    if (h == 0 && n_ok) colsum_partial[(int64_t)blockIdx.x * N + n] = __fadd_rn(csum, other);
+  }
+}
+
+int nn_grid(int64_t M) {
+  const int64_t tiles = (M + kNNRows - 1) / kNNRows;
+  return (int)(tiles < 512 ? (tiles > 0 ? tiles : 1) : 512);  // 2 persistent WGs per CU
+}
+
+template <int K>
+int launch_nn(int64_t M, int N, const float *A, int64_t lda, const float *B, int64_t sbk,
+              int64_t sbn, float *C, int64_t ldc, int epi, const float *Z, int64_t ldz,
+              float *partial, hipStream_t s) {
+  const unsigned blocks = (unsigned)nn_grid(M);
+  if (epi == EPI_RELU)
+    hipLaunchKernelGGL((gemm_nn_kernel<K, EPI_RELU>), dim3(blocks), dim3(256), 0, s, A, lda, B,
+                       sbk, sbn, C, ldc, M, N, Z, ldz, partial);
+  else
+    hipLaunchKernelGGL((gemm_nn_kernel<K, EPI_STORE>), dim3(blocks), dim3(256), 0, s, A, lda, B,
+                       sbk, sbn, C, ldc, M, N, Z, ldz, partial);
+  return check_launch("gemm_nn_kernel");
+}
+
+__global__ __launch_bounds__(256) void colsum_fold_kernel(const float *__restrict__ partial,
+                                                          int64_t nparts, int N,
+                                                          float *__restrict__ out) {
+  __shared__ float red[4][64];
+  const int g = threadIdx.x >> 6;
+  const int f = blockIdx.x * 64 + (threadIdx.x & 63);
+  float s = 0.0f;
+  if (f < N) {
+#pragma unroll 8
+    for (int64_t p = g; p < nparts; p += 4) s = __fadd_rn(s, partial[p * N + f]);
+  }
+  red[g][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (g == 0 && f < N)
+    out[f] = __fadd_rn(__fadd_rn(red[0][threadIdx.x], red[1][threadIdx.x]),
+                       __fadd_rn(red[2][threadIdx.x], red[3][threadIdx.x]));
+}
+
+}  // namespace
+}  // namespace mgcn
+
+extern "C" int mgcn_gemm_nn_supported(int32_t K, int32_t N) {
+  return (K == 32 || K == 64 || K == 128) && N >= 1 && N <= 128;
+}
+
+extern "C" size_t mgcn_gemm_nn_workspace_bytes(int64_t M, int32_t N) {
+  return align_up((size_t)nn_grid(M) * (size_t)(N > 0 ? N : 1) * 4, 256);
+}
+
+extern "C" int mgcn_gemm_nn(int64_t M, int32_t K, int32_t N, const float *A, int64_t lda,
+                            const float *B, int64_t sbk, int64_t sbn, float *C, int64_t ldc,
+                            const float *Z, int64_t ldz, float *colsum, void *workspace,
+                            size_t workspace_bytes, void *stream) {
+  clear_error();
+  MGCN_REQUIRE(M >= 0 && K >= 0 && N >= 0, "mgcn_gemm_nn: negative size");
+  MGCN_REQUIRE(mgcn_gemm_nn_supported(K, N), "mgcn_gemm_nn: unsupported K=%d N=%d", K, N);
+  hipStream_t s = as_stream(stream);
+  if (M == 0) {
+    if (colsum) MGCN_HIP_TRY(hipMemsetAsync(colsum, 0, sizeof(float) * N, s));
+    return MGCN_OK;
+  }
+  MGCN_REQUIRE(A && B && C && lda >= K && ldc >= N, "mgcn_gemm_nn: bad A/B/C");
+  MGCN_REQUIRE(lda % 4 == 0 && reinterpret_cast<uintptr_t>(A) % 16 == 0,
+               "mgcn_gemm_nn: A must be 16-byte aligned with lda % 4 == 0");
+  const int epi = (Z != nullptr) ? EPI_RELU : EPI_STORE;
+  MGCN_REQUIRE(epi == EPI_STORE || colsum != nullptr, "mgcn_gemm_nn: Z given without colsum");
+  float *partial = nullptr;
+  if (epi == EPI_RELU) {
+    const size_t need = mgcn_gemm_nn_workspace_bytes(M, N);
+    if (workspace == nullptr || workspace_bytes < need) {
+      set_error("mgcn_gemm_nn: workspace %zu < %zu", workspace_bytes, need);
+      return MGCN_EWORKSPACE;
+    }
+    partial = static_cast<float *>(workspace);
+  }
+  int rc;
+  if (K == 32)
+    rc = launch_nn<32>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, ldz, partial, s);
+  else if (K == 64)
+    rc = launch_nn<64>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, ldz, partial, s);
+  else
+    rc = launch_nn<128>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, ldz, partial, s);
+  if (rc || epi != EPI_RELU) return rc;
+  const int64_t parts = nn_grid(M);
+  hipLaunchKernelGGL(colsum_fold_kernel, dim3((N + 63) / 64), dim3(256), 0, s, partial, parts, N,
+                     colsum);
+  return check_launch("colsum_fold_kernel");
+}

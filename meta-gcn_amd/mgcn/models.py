@@ -26,7 +26,7 @@ from torch.nn.utils.rnn import pad_sequence
 
 from . import _lib as L
 from .graph import plan_for
-from .ops import aggregate_plan, linear, scatter_  # noqa: F401  (re-exported)
+from .ops import aggregate_plan, gcn_stack, linear, scatter_  # noqa: F401  (re-exported)
 
 
 # --------------------------------------------------------------- inits (PyG)
@@ -251,6 +251,7 @@ class GCNLayer(nn.Module):
                                   edge_gate=edge_gate, aggr=aggr, bias=bias,
                                   num_kernel=num_kernel, nodemodel=nodemodel, **kwargs)
         self.non_linear = activation(non_linear)
+        self.non_linear_name = non_linear
         self._relu = non_linear == 'relu'
 
     def reset_parameters(self):
@@ -263,6 +264,42 @@ class GCNLayer(nn.Module):
                                           relu=True)
         xo = self.gcn(x, edge_index_K, edge_attr_K, deg_K, edge_weight_K, **kwargs)
         return self.non_linear(xo)
+
+
+class GCNStack(nn.Module):
+    """A plain chain of GCNLayers (the config-2 model: 3 layers, ReLU between)
+    executed as ONE fused autograd node (:func:`mgcn.ops.gcn_stack`) whenever
+    every layer is a single additive kernel with the same deg_norm/aggr and a
+    'relu'/'none' activation; otherwise layer by layer.  Parameters live in
+    the GCNLayer modules (reference-compatible state_dict keys)."""
+
+    def __init__(self, layers):
+        super().__init__()
+        self.layers = nn.ModuleList(layers)
+
+    def _fusable(self):
+        nms = []
+        for layer in self.layers:
+            g = layer.gcn
+            if len(g.node_models) != 1 or layer.non_linear_name not in ('relu', 'none'):
+                return None
+            nms.append(g.node_models[0])
+        if len({(nm.deg_norm, nm.aggr) for nm in nms}) != 1:
+            return None
+        return nms
+
+    def forward(self, x, edge_index, deg=None, edge_weight=None):
+        nms = self._fusable()
+        if nms is None or x.device.type != "cuda":
+            for layer in self.layers:
+                x = layer(x, edge_index, None, deg, edge_weight)
+            return x
+        plan = plan_for(edge_index, x.size(0))
+        norm = plan.norm(nms[0].deg_norm, deg=deg,
+                         edge_weight=edge_weight if nms[0].deg_norm is not None else None)
+        relus = [layer.non_linear_name == 'relu' for layer in self.layers]
+        return gcn_stack(x, plan, norm, [nm.weight_node for nm in nms], [nm.bias for nm in nms],
+                         relus, nms[0].aggr)
 
 
 class GCNModel(nn.Module):
@@ -365,5 +402,5 @@ class GCNModel(nn.Module):
 
 
 __all__ = ["glorot", "zeros", "Identity", "activation", "scatter_", "NodeModelBase",
-           "NodeModelAdditive", "GCNMultiKernel", "GCNLayer", "GCNModel"]
+           "NodeModelAdditive", "GCNMultiKernel", "GCNLayer", "GCNStack", "GCNModel"]
 _ = L  # keep the binding imported so a missing library fails at import of ops

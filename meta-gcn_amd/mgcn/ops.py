@@ -143,22 +143,82 @@ def gemm_tn(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor | None = None,
     return C
 
 
+def gemm_nn_supported(K: int, N: int) -> bool:
+    return bool(L.load().mgcn_gemm_nn_supported(int(K), int(N)))
+
+
+def gemm_nn(A: torch.Tensor, W: torch.Tensor, transpose_w: bool = False,
+            Z: torch.Tensor | None = None):
+    """C = A @ W (or A @ W^T) on libmgcn's tall-skinny MFMA kernel
+    (``mgcn_gemm_nn``).  With ``Z``: C = Z > 0 ? A @ W^T : 0 and the column sums
+    of C are returned too (fused ReLU backward + bias gradient).  Returns
+    (C, colsum or None)."""
+    lib = L.load()
+    A = _contig_f32(A, "A")
+    if A.stride(0) % 4 or A.data_ptr() % 16:
+        A = A.contiguous()
+    W = W.detach()
+    dev = L.require_device(A, W, Z)
+    M, K = A.shape
+    if transpose_w:
+        N, Kw = W.shape
+        sbk, sbn = W.stride(1), W.stride(0)
+    else:
+        Kw, N = W.shape
+        sbk, sbn = W.stride(0), W.stride(1)
+    if Kw != K:
+        raise ValueError(f"gemm_nn: A is [{M}, {K}], W gives K = {Kw}")
+    C = torch.empty(M, N, dtype=torch.float32, device=dev)
+    colsum = ws = None
+    ws_bytes = 0
+    if Z is not None:
+        Z = _contig_f32(Z, "Z")
+        colsum = torch.empty(N, dtype=torch.float32, device=dev)
+        ws_bytes = int(lib.mgcn_gemm_nn_workspace_bytes(M, N))
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    if _TIMER is not None:
+        _TIMER("gemm_nn", True)
+    with torch.cuda.device(dev):
+        rc = lib.mgcn_gemm_nn(M, K, N, L.ptr(A), A.stride(0), L.ptr(W), sbk, sbn, L.ptr(C),
+                              C.stride(0), L.ptr(Z), Z.stride(0) if Z is not None else 0,
+                              L.ptr(colsum), L.ptr(ws), ws_bytes, L.stream_of(dev))
+    if _TIMER is not None:
+        _TIMER("gemm_nn", False)
+    L.check(rc, "mgcn_gemm_nn")
+    return C, colsum
+
+
+def _mm(x: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
+    """x @ W on libmgcn when the shape is supported, else hipBLASLt."""
+    if gemm_nn_supported(W.size(0), W.size(1)):
+        return gemm_nn(x, W)[0]
+    return torch.matmul(x, W.detach())
+
+
+def _mm_t(dH: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
+    """dH @ W^T."""
+    if gemm_nn_supported(W.size(1), W.size(0)):
+        return gemm_nn(dH, W, transpose_w=True)[0]
+    return torch.matmul(dH, W.detach().t())
+
+
 class _Linear(torch.autograd.Function):
-    """H = x @ W (gcn_base_models.py:201).  Forward and dX stay on
-    torch.matmul (hipBLASLt); dW = x^T dH, a K = num_nodes reduction that
-    hipBLASLt handles poorly, runs on libmgcn's split-K MFMA kernel."""
+    """H = x @ W (gcn_base_models.py:201) with all three products on libmgcn's
+    fp32 MFMA kernels: forward and dX on mgcn_gemm_nn (tall-skinny), dW =
+    x^T dH -- a K = num_nodes reduction -- on the split-K mgcn_gemm_tn."""
 
     @staticmethod
     def forward(ctx, x, W):
         ctx.save_for_backward(x, W)
-        return torch.matmul(x, W)
+        return _mm(x, W)
 
     @staticmethod
     def backward(ctx, dH):
         x, W = ctx.saved_tensors
         dx = dW = None
+        dH = dH.contiguous()
         if ctx.needs_input_grad[0]:
-            dx = torch.matmul(dH, W.t())
+            dx = _mm_t(dH, W)
         if ctx.needs_input_grad[1]:
             dW = gemm_tn(x, dH)
         return dx, dW
@@ -223,6 +283,80 @@ def aggregate_plan(H: torch.Tensor, plan: GraphPlan, norm: NormPlan, aggr: str =
                    bias: torch.Tensor | None = None, relu: bool = False) -> torch.Tensor:
     """:func:`aggregate` on an already-built plan (no cache lookup)."""
     return _Aggregate.apply(H, bias, plan, norm, L.REDUCE_CODES[aggr], bool(relu))
+
+
+class _GCNStack(torch.autograd.Function):
+    """A chain of GCN layers  Z_l = act_l(A_norm (Z_{l-1} W_l) + b_l)  as one
+    autograd node, so the backward can fuse across layer boundaries: the
+    ReLU mask and bias gradient of layer l-1 are computed in the epilogue of
+    layer l's dX GEMM (mgcn_gemm_nn with Z), instead of a separate pass.
+    Per layer: GEMM -> SpMM(+bias, ReLU) forward; SpMM^T, dW (split-K), dX
+    (+ fused ReLU/bias of the layer below) backward.  Same math and the same
+    per-edge summation order as the layer-by-layer modules."""
+
+    @staticmethod
+    def forward(ctx, x, plan, norm, reduce, relus, *params):
+        Ws, bs = params[0::2], params[1::2]
+        h = x
+        inputs, outs, args = [], [], []
+        for W, b, relu in zip(Ws, bs, relus):
+            inputs.append(h)
+            H = _mm(h, W)
+            h, am = spmm_fwd(plan.fwd, norm.w_fwd, H, reduce, b, relu)
+            outs.append(h)
+            args.append(am)
+        ctx.plan, ctx.norm, ctx.reduce, ctx.relus = plan, norm, reduce, relus
+        ctx.n_layers = len(Ws)
+        ctx.has_bias = [b is not None for b in bs]
+        ctx.save_for_backward(*inputs, *outs, *[a if a is not None else torch.empty(0)
+                                                for a in args], *Ws)
+        return h
+
+    @staticmethod
+    def backward(ctx, dZ):
+        n = ctx.n_layers
+        saved = ctx.saved_tensors
+        inputs, outs = saved[:n], saved[n:2 * n]
+        args, Ws = saved[2 * n:3 * n], saved[3 * n:4 * n]
+        plan, norm, reduce, relus = ctx.plan, ctx.norm, ctx.reduce, ctx.relus
+        gW = [None] * n
+        gb = [None] * n
+        top = n - 1
+        dY, db = relu_bwd_colsum(dZ.contiguous(), outs[top], relus[top], ctx.has_bias[top])
+        gb[top] = db
+        dx = None
+        for l in range(top, -1, -1):
+            am = args[l] if args[l].numel() else None
+            dH = spmm_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, reduce,
+                          cnt=plan.in_cnt if reduce == L.REDUCE_MEAN else None, argmax=am)
+            gW[l] = gemm_tn(inputs[l], dH)
+            W = Ws[l]
+            if l > 0:
+                fused = relus[l - 1] and gemm_nn_supported(W.size(1), W.size(0))
+                if fused:
+                    dY, db = gemm_nn(dH, W, transpose_w=True, Z=outs[l - 1])
+                    if not ctx.has_bias[l - 1]:
+                        db = None
+                else:
+                    dY, db = relu_bwd_colsum(_mm_t(dH, W), outs[l - 1], relus[l - 1],
+                                             ctx.has_bias[l - 1])
+                gb[l - 1] = db
+            elif ctx.needs_input_grad[0]:
+                dx = _mm_t(dH, W)
+        grads = []
+        for w, b in zip(gW, gb):
+            grads += [w, b]
+        return (dx, None, None, None, None, *grads)
+
+
+def gcn_stack(x: torch.Tensor, plan: GraphPlan, norm: NormPlan, Ws, bs, relus,
+              aggr: str = "add") -> torch.Tensor:
+    """Run len(Ws) fused GCN layers (see :class:`_GCNStack`)."""
+    params = []
+    for W, b in zip(Ws, bs):
+        params += [W, b]
+    return _GCNStack.apply(x, plan, norm, L.REDUCE_CODES[aggr], tuple(bool(r) for r in relus),
+                           *params)
 
 
 # ---------------------------------------------------------------- scatter_

@@ -244,3 +244,97 @@ def test_gemm_tn_matches_fp64(cuda, K, M, N):
     assert ((C.double() - ref).abs() <= 1e-5 * bound + 1e-6).all()
     C2 = gemm_tn(A, B)
     assert torch.equal(C, C2)  # deterministic
+
+
+@pytest.mark.parametrize("M,K,N,trans", [(1_000_000, 128, 128, False), (1_000_000, 128, 128, True),
+                                         (1000, 64, 100, False), (777, 32, 7, True), (1, 128, 128, False)])
+def test_gemm_nn_matches_fp64(cuda, M, K, N, trans):
+    from mgcn.ops import gemm_nn
+    g = torch.Generator(device=cuda).manual_seed(M + K + N)
+    A = torch.randn(M, K, device=cuda, generator=g)
+    W = torch.randn(N, K, device=cuda, generator=g) if trans else \
+        torch.randn(K, N, device=cuda, generator=g)
+    Wm = W.t() if trans else W
+    C, cs = gemm_nn(A, W, transpose_w=trans)
+    ref = A.double() @ Wm.double()
+    bound = A.double().abs() @ Wm.double().abs()
+    assert ((C.double() - ref).abs() <= 1e-5 * bound + 1e-6).all()
+    assert cs is None
+    # fused ReLU-backward epilogue: C = Z > 0 ? A W : 0, colsum = sum_m C
+    Z = torch.randn(M, N, device=cuda, generator=g)
+    C2, cs2 = gemm_nn(A, W, transpose_w=trans, Z=Z)
+    assert torch.equal(C2, torch.where(Z > 0, C, torch.zeros_like(C)))
+    ref_cs = C2.double().sum(0)
+    assert torch.allclose(cs2.double(), ref_cs, rtol=1e-4, atol=1e-3)
+
+
+def test_gcn_stack_identity_weights_bitwise_vs_oracle(cuda, oracle):
+    """3 fused layers with W = I: every layer's aggregation and the whole
+    adjoint chain (dx) are bit-exact against the oracle layer by layer."""
+    from mgcn.models import GCNLayer, GCNStack
+    rng = np.random.default_rng(11)
+    N, F = 6000, 128
+    ei = _graph(rng, N, 60000)
+    x = rng.standard_normal((N, F)).astype(np.float32)
+    dZ = rng.standard_normal((N, F)).astype(np.float32)
+    layers = [GCNLayer(F, F, deg_norm='sm', aggr='add', bias=True,
+                       non_linear='relu' if i < 2 else 'none').to(cuda) for i in range(3)]
+    bs = []
+    for layer in layers:
+        nm = layer.gcn.node_models[0]
+        with torch.no_grad():
+            nm.weight_node.copy_(torch.eye(F))
+            nm.bias.uniform_(-0.2, 0.2)
+        bs.append(nm.bias.detach().cpu().numpy())
+    stack = GCNStack(layers)
+    xt = _t(x, cuda).requires_grad_(True)
+    y = stack(xt, _t(ei, cuda))
+    y.backward(_t(dZ, cuda))
+    wf, wb, rs = oracle.edge_factors(ei, N, "sm")
+    hs = [x]
+    for i in range(3):
+        h, _ = oracle.aggr_fwd(ei, hs[-1], wf, "add", bs[i], relu=i < 2)
+        hs.append(h)
+    np.testing.assert_array_equal(_np(y), hs[-1])
+    g = dZ
+    dbs = []
+    for i in range(2, -1, -1):
+        g, db = oracle.aggr_bwd(ei, g, wb, rs, "add", hs[i + 1], relu=i < 2, want_db=True)
+        dbs.append(db)
+    np.testing.assert_array_equal(_np(xt.grad), g)
+    for layer, db in zip(layers[::-1], dbs):
+        np.testing.assert_allclose(_np(layer.gcn.node_models[0].bias.grad), db, rtol=1e-4,
+                                   atol=1e-3)
+
+
+def test_gcn_stack_matches_layer_by_layer(cuda):
+    """Fused stack == the same GCNLayers run one by one (forward and dW
+    bitwise: same kernels; db within fp32 summation-order tolerance)."""
+    from mgcn.models import GCNLayer, GCNStack
+    torch.manual_seed(0)
+    rng = np.random.default_rng(12)
+    N, F = 20000, 128
+    ei = _t(_graph(rng, N, 200000), cuda)
+    layers = [GCNLayer(F, F, deg_norm='sm', aggr='add', bias=True,
+                       non_linear='relu' if i < 2 else 'none').to(cuda) for i in range(3)]
+    for layer in layers:
+        with torch.no_grad():
+            layer.gcn.node_models[0].bias.uniform_(-0.1, 0.1)
+    x = torch.randn(N, F, device=cuda)
+    dZ = torch.randn(N, F, device=cuda)
+    stack = GCNStack(layers)
+    y1 = stack(x, ei)
+    y1.backward(dZ)
+    g1 = [p.grad.clone() for p in stack.parameters()]
+    for p in stack.parameters():
+        p.grad = None
+    h = x
+    for layer in layers:
+        h = layer(h, ei)
+    assert torch.equal(h, y1)
+    h.backward(dZ)
+    for (name, p), a in zip(stack.named_parameters(), g1):
+        if name.endswith("weight_node"):
+            assert torch.equal(p.grad, a), name
+        else:
+            torch.testing.assert_close(p.grad, a, rtol=1e-4, atol=1e-3)
