@@ -64,18 +64,24 @@ __global__ __launch_bounds__(256) void gemm_tn_partial_kernel(
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[t][s][r] = 0.0f;
 
-  for (int64_t k = kb; k < ke; k += 2 * kU) {
-    float a[kU][2], b[kU][2];
+  // operands for kU k-steps; the next group's loads are issued before the
+  // current group's MFMAs (register double buffer)
+  float a[kU][2], b[kU][2], na[kU][2], nb[kU][2];
+  auto load = [&](int64_t k, float (&x)[kU][2], float (&y)[kU][2]) {
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       const int64_t kr = k + 2 * u + lr;
       const bool okk = kr < ke;
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        a[u][t] = (okk && oka[t]) ? A[kr * lda + ia[t]] : 0.0f;
-        b[u][t] = (okk && okb[t]) ? B[kr * ldb + jb[t]] : 0.0f;
+        x[u][t] = (okk && oka[t]) ? A[kr * lda + ia[t]] : 0.0f;
+        y[u][t] = (okk && okb[t]) ? B[kr * ldb + jb[t]] : 0.0f;
       }
     }
+  };
+  if (kb < ke) load(kb, a, b);
+  for (int64_t k = kb; k < ke; k += 2 * kU) {
+    if (k + 2 * kU < ke) load(k + 2 * kU, na, nb);
 #pragma unroll
     for (int u = 0; u < kU; ++u)
 #pragma unroll
@@ -83,6 +89,13 @@ __global__ __launch_bounds__(256) void gemm_tn_partial_kernel(
 #pragma unroll
         for (int s = 0; s < 2; ++s)
           acc[t][s] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][t], b[u][s], acc[t][s], 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        a[u][t] = na[u][t];
+        b[u][t] = nb[u][t];
+      }
   }
 
   // partial slab [split][M][N]; C/D map: col = lane & 31,
@@ -126,8 +139,9 @@ __global__ __launch_bounds__(256) void gemm_reduce_kernel(const float *__restric
 }
 
 int gemm_splits(int64_t K, int tiles) {
-  // ~2048 workgroups in flight over 256 CUs, at least 64 rows of K per split
-  int64_t s = 2048 / (tiles > 0 ? tiles : 1);
+  // one resident round: 256 CUs x 3 workgroups (3 waves/SIMD at 134 VGPRs);
+  // at least 64 rows of K per split (partials: splits x 64 KB per tile)
+  int64_t s = 768 / (tiles > 0 ? tiles : 1);
   int64_t max_s = (K + 63) / 64;
   if (s > max_s) s = max_s;
   if (s < 1) s = 1;
@@ -220,7 +234,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nn_kernel(
   // register prefetch of the next A tile, except where it would spill (the
   // K = 128 ReLU epilogue needs those registers; the co-resident workgroup
   // still overlaps its loads with this one's MFMAs)
-  constexpr bool kPrefetch = !(K == 128 && EPI == EPI_RELU);
+  constexpr bool kPrefetch = true;
   __shared__ __attribute__((aligned(16))) float sA[kNNRows * LDA];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -263,59 +277,50 @@ __global__ __launch_bounds__(256, 2) void gemm_nn_kernel(
     __syncthreads();
     if (kPrefetch && tile + gridDim.x < n_tiles) fetch(tile + gridDim.x);  // overlaps MFMAs
 
-    f32x16 acc[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
-#pragma unroll
-    for (int s4 = 0; s4 < KH; s4 += 4) {
-      float4 a4[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-        a4[t] = *reinterpret_cast<const float4 *>(&sA[(t * 32 + lc) * LDA + h * KH + s4]);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[t].x, b[s4 + 0], acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[t].y, b[s4 + 1], acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[t].z, b[s4 + 2], acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[t].w, b[s4 + 3], acc[t], 0, 0, 0);
-      }
-    }
-
-    // epilogue; C/D map: col = lane & 31 (-> n), row = (r&3) + 8 (r>>2) + 4 h.
-    // Full tiles take an unguarded path (guarded loads would serialise).
+    // one 32-row subtile at a time: 16 accumulator registers, fragment reads
+    // double-buffered one step ahead, epilogue of subtile t overlapping the
+    // MFMAs of subtile t + 1.  C/D map: col = lane & 31 (-> n),
+    // row = (r & 3) + 8 (r >> 2) + 4 h.
     const bool full = (m0 + kNNRows <= M) && n_ok;
-    if (full) {
-      if constexpr (EPI == EPI_RELU) {
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          float zv[16];  // 16 independent loads in flight, then mask/store
+    for (int t = 0; t < 4; ++t) {
+      const float *arow = &sA[(t * 32 + lc) * LDA + h * KH];
+      f32x16 acc;
 #pragma unroll
-          for (int r = 0; r < 16; ++r)
-            zv[r] = Z[(m0 + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * ldz + n];
+      for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+      float4 cur = *reinterpret_cast<const float4 *>(arow);
+#pragma unroll
+      for (int s4 = 0; s4 < KH; s4 += 4) {
+        float4 nxt = cur;
+        if (s4 + 4 < KH) nxt = *reinterpret_cast<const float4 *>(arow + s4 + 4);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.x, b[s4 + 0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.y, b[s4 + 1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.z, b[s4 + 2], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.w, b[s4 + 3], acc, 0, 0, 0);
+        cur = nxt;
+      }
+      const int64_t rbase = m0 + t * 32 + 4 * h;
+      if (full) {  // unguarded: guarded loads would serialise (one wait per element)
+        if constexpr (EPI == EPI_RELU) {
+          float zv[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) zv[r] = Z[(rbase + (r & 3) + 8 * (r >> 2)) * ldz + n];
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const float v = (zv[r] > 0.0f) ? acc[t][r] : 0.0f;
+            const float v = (zv[r] > 0.0f) ? acc[r] : 0.0f;
             csum = __fadd_rn(csum, v);
-            C[(m0 + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * ldc + n] = v;
+            C[(rbase + (r & 3) + 8 * (r >> 2)) * ldc + n] = v;
           }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) C[(rbase + (r & 3) + 8 * (r >> 2)) * ldc + n] = acc[r];
         }
       } else {
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            C[(m0 + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * ldc + n] = acc[t][r];
-      }
-    } else {
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int64_t row = m0 + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          const int64_t row = rbase + (r & 3) + 8 * (r >> 2);
           if (row < M && n_ok) {
-            float v = acc[t][r];
+            float v = acc[r];
             if constexpr (EPI == EPI_RELU) {
               v = (Z[row * ldz + n] > 0.0f) ? v : 0.0f;
               csum = __fadd_rn(csum, v);
@@ -323,6 +328,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nn_kernel(
             C[row * ldc + n] = v;
           }
         }
+      }
     }
   }
   if constexpr (EPI == EPI_RELU) {

@@ -41,8 +41,27 @@ def main():
     ap.add_argument("--feat", type=int, default=128)
     ap.add_argument("--variants", action="store_true")
     ap.add_argument("--once", action="store_true", help="one fwd + one bwd launch (for PMC runs)")
+    ap.add_argument("--calibrate", action="store_true",
+                    help="known-byte launches for PMC calibration: a 2 GiB copy, and the SpMM "
+                         "on a 4M-node permutation graph (every 512-B row gathered exactly once)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
+    if args.calibrate:
+        src = torch.randn(512 * 1024 * 1024 // 1, device=dev)  # 2 GiB
+        dst = torch.empty_like(src)
+        dst.copy_(src)
+        del src, dst
+        Np = 4_000_000
+        perm = torch.randperm(Np, device=dev)
+        ei = torch.stack([perm, torch.arange(Np, device=dev)])
+        Hp = torch.randn(Np, 128, device=dev)
+        plan = plan_for(ei, Np)
+        ops.spmm_fwd(plan.fwd, None, Hp, 0)
+        torch.cuda.synchronize()
+        print(json.dumps({"copy_read_bytes": 2**31, "copy_write_bytes": 2**31,
+                          "perm_spmm_read_bytes": spmm_bytes(Np, Np, 128) - 4 * Np - 4 * Np * 128,
+                          "perm_spmm_write_bytes": 4 * Np * 128}))
+        return
     ei, N = make_er_graph()
     ei = ei.to(dev)
     F = args.feat
