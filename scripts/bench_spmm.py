@@ -89,6 +89,19 @@ def main():
                           "bwd_gbs": B / b_med / 1e6, "bytes": B}), flush=True)
     mgcn.set_option("spmm_vec", 0)
     mgcn.set_option("spmm_unroll", 8)
+    # feature-chunked passes: each pass gathers a column slice whose working
+    # set (N x chunk x 4 B) may stay resident in the 256 MiB Infinity Cache
+    Y = torch.empty(N, F, device=dev)
+    for chunks in (2, 4, 8):
+        w = F // chunks
+
+        def run(chunks=chunks, w=w):
+            for c in range(chunks):
+                ops.spmm_fwd(plan.fwd, norm.w_fwd, H[:, c * w:(c + 1) * w], 0,
+                             out=Y[:, c * w:(c + 1) * w])
+        f_med, f_min = time_it(run, args.reps)
+        print(json.dumps({"variant": f"chunks{chunks}", "fwd_ms": f_med, "fwd_min_ms": f_min,
+                          "fwd_gbs": B / f_med / 1e6}), flush=True)
 
 
 if __name__ == "__main__":

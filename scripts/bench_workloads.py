@@ -1,0 +1,109 @@
+"""Secondary workloads of BASELINE.json (parity/coverage cases, not the
+headline bench line):
+
+  config3: botnet-shaped node classification, 2 graphs x 143,107 nodes per
+           batch (bsz = 2, run_botnet.sh:14), 12-layer GCNModel F = 32,
+           residual_hop = 1, deg_norm 'sm', bias 0, final proj 32 -> 2,
+           CrossEntropy + Adam step (train_botnet.py:276-294).
+  config4: the config-2 graph with the GIN / SAGE / max aggregators: 3-layer
+           stacks of NodeModelAdditive(deg_norm=None, aggr=add|mean|max).
+
+    python scripts/bench_workloads.py --workload config3 [--steps 20]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "meta-gcn_amd")]
+import torch  # noqa: E402
+
+from bench import batch_graphs, make_botnet_graph, make_er_graph, make_inputs  # noqa: E402
+
+
+def timed(step, steps, warmup):
+    step()
+    torch.cuda.synchronize()
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+def config3(args, dev):
+    from mgcn.models import GCNModel
+    g1, n1, m1 = make_botnet_graph(seed=0)
+    g2, n2, m2 = make_botnet_graph(seed=1)
+    ei, N = batch_graphs([(g1, n1), (g2, n2)])
+    n_edges = ei.shape[1] - N
+    deg = torch.bincount(ei[0], minlength=N).float()
+    x = torch.stack([torch.ones(N), deg], 1).to(dev)
+    y = torch.cat([m1, m2]).long().to(dev)
+    ei = ei.to(dev)
+    torch.manual_seed(0)
+    model = GCNModel(1, [32] * 12, 2, non_linear='relu', non_linear_layer_wise='relu',
+                     residual_hop=1, dropout=0.0, final_type='proj', pred_on='node',
+                     deg_norm='sm', aggr='add', bias=False).to(dev)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=5e-4)
+    crit = torch.nn.CrossEntropyLoss()
+
+    def step():
+        opt.zero_grad()
+        out = model(x[:, 0].view(-1, 1), ei, deg_K=x[:, 1])
+        crit(out, y).backward()
+        opt.step()
+    t = timed(step, args.steps, args.warmup)
+    return {"workload": "config3 botnet-shaped 2x143,107 nodes, 12-layer GCNModel F=32 rh=1, "
+                        "CE + Adam", "nodes": N, "edges": n_edges, "max_in_degree":
+            int(torch.bincount(ei[1], minlength=N).max()), "ms_per_step": t * 1e3,
+            "edges_per_s": n_edges * 12 / t}
+
+
+def config4(args, dev):
+    from mgcn.models import GCNLayer, GCNStack
+    ei_cpu, N = make_er_graph()
+    ei = ei_cpu.to(dev)
+    n_edges = ei.shape[1] - N
+    X, Ws, bs, dY = make_inputs(N, 128, 3)
+    X, dY = X.to(dev), dY.to(dev)
+    res = {"workload": "config4 ER N=1M E=10M F=128, 3-layer stacks deg_norm=None", "edges": n_edges}
+    for aggr in ("add", "mean", "max"):
+        layers = []
+        for i in range(3):
+            layer = GCNLayer(128, 128, deg_norm=None, aggr=aggr, bias=True,
+                             non_linear='relu' if i < 2 else 'none').to(dev)
+            with torch.no_grad():
+                layer.gcn.node_models[0].weight_node.copy_(Ws[i])
+                layer.gcn.node_models[0].bias.copy_(bs[i])
+            layers.append(layer)
+        stack = GCNStack(layers)
+        params = list(stack.parameters())
+
+        def step():
+            for p in params:
+                p.grad = None
+            stack(X, ei).backward(dY)
+        t = timed(step, args.steps, args.warmup)
+        res[aggr] = {"ms_per_step": t * 1e3, "edges_per_s": n_edges * 3 / t}
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", choices=["config3", "config4"], required=True)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    fn = {"config3": config3, "config4": config4}[args.workload]
+    print(json.dumps(fn(args, dev)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
