@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define MGCN_ABI_VERSION 1
+#define MGCN_ABI_VERSION 2
 
 /* return codes */
 #define MGCN_OK 0
@@ -144,6 +144,7 @@ int mgcn_spmm_fwd(int64_t n_rows, int32_t F, const int64_t *rowptr,
                   const int32_t *col, const int32_t *eid, const float *w,
                   const float *H, int64_t ldh, float *Y, int64_t ldy,
                   int reduce, const float *bias, int relu, int32_t *argmax,
+                  const int32_t *heavy_rows, int64_t n_heavy, int64_t heavy_thr,
                   void *stream);
 
 /*
@@ -159,7 +160,21 @@ int mgcn_spmm_bwd(int64_t n_rows, int32_t F, const int64_t *rowptr_t,
                   const int32_t *col_t, const int32_t *eid_t, const float *w_t,
                   const float *row_scale, const float *dY, int64_t lddy,
                   float *dH, int64_t lddh, int reduce, const float *cnt,
-                  const int32_t *argmax, int accumulate, void *stream);
+                  const int32_t *argmax, int accumulate,
+                  const int32_t *heavy_rows, int64_t n_heavy, int64_t heavy_thr,
+                  void *stream);
+
+/*
+ * Degree skew (botnet graphs reach degree ~6k, config 3).  Rows with more
+ * than `thr` edges are listed once per plan by mgcn_heavy_rows (writes the
+ * row ids, returns their number in *n_out; synchronises `stream`; workspace
+ * >= 8 bytes) and passed to mgcn_spmm_fwd/bwd as (heavy_rows, n_heavy,
+ * heavy_thr): each such row then gets a whole workgroup that gathers a batch
+ * of its edges in parallel and folds them per feature in edge order (same
+ * bits), while the lane-group kernel skips it.  heavy_rows = NULL disables.
+ */
+int mgcn_heavy_rows(int64_t n_rows, const int64_t *rowptr, int64_t thr, int32_t *rows_out,
+                    int64_t *n_out, void *workspace, size_t workspace_bytes, void *stream);
 
 /* ------------------------------------------------------------------ dense */
 

@@ -113,6 +113,53 @@ __global__ __launch_bounds__(256) void gemm_tn_partial_kernel(
       }
 }
 
+// Small C (M, N <= 32: F = 32 layers and the 32 -> 2 projection of config 3):
+// one 32 x 32 MFMA tile per workgroup; the four waves take interleaved
+// k-steps of the split's K range (wave-level split-K) and their accumulators
+// are folded in wave order through LDS, then one slab per split.
+__global__ __launch_bounds__(256) void gemm_tn_small_kernel(
+    const float *__restrict__ A, int64_t lda, const float *__restrict__ B, int64_t ldb,
+    int64_t K, int M, int N, int64_t k_per_split, float *__restrict__ partial) {
+  constexpr int U = 8;
+  __shared__ float red[4][16][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int lr = lane >> 5, lc = lane & 31;
+  const int64_t kb = (int64_t)blockIdx.x * k_per_split;
+  const int64_t ke = (kb + k_per_split < K) ? kb + k_per_split : K;
+  const bool oka = lc < M, okb = lc < N;
+  const int ia = oka ? lc : 0, jb = okb ? lc : 0;
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+  // wave w takes k-steps w, w + 4, w + 8, ... (2 rows each)
+  for (int64_t k = kb + 2 * wave; k < ke; k += 2 * 4 * U) {
+    float a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t kr = k + 8 * u + lr;
+      const bool okk = kr < ke;
+      a[u] = (okk && oka) ? A[kr * lda + ia] : 0.0f;
+      b[u] = (okk && okb) ? B[kr * ldb + jb] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], b[u], acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) red[wave][r][lane] = acc[r];
+  __syncthreads();
+  if (wave == 0) {
+    float *slab = partial + (int64_t)blockIdx.x * M * N;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float v = __fadd_rn(__fadd_rn(red[0][r][lane], red[1][r][lane]),
+                                __fadd_rn(red[2][r][lane], red[3][r][lane]));
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * lr;
+      if (row < M && lc < N) slab[row * N + lc] = v;
+    }
+  }
+}
+
 // C[e] (+)= sum over splits of partial[split][e], in split order within each of
 // 4 interleaved groups, the groups then folded in order: deterministic.
 __global__ __launch_bounds__(256) void gemm_reduce_kernel(const float *__restrict__ partial,
@@ -184,9 +231,15 @@ extern "C" int mgcn_gemm_tn(int64_t K, int32_t M, int32_t N, const float *A, int
   kps = (kps + 2 * kU - 1) / (2 * kU) * (2 * kU);
   const int used = (int)((K + kps - 1) / kps);
   float *partial = static_cast<float *>(workspace);
-  hipLaunchKernelGGL(gemm_tn_partial_kernel, dim3(tiles_m * tiles_n, used), dim3(256), 0, s, A,
-                     lda, B, ldb, K, M, N, kps, tiles_n, partial);
-  if (int rc = check_launch("gemm_tn_partial_kernel")) return rc;
+  if (M <= 32 && N <= 32) {
+    hipLaunchKernelGGL(gemm_tn_small_kernel, dim3(used), dim3(256), 0, s, A, lda, B, ldb, K, M, N,
+                       kps, partial);
+    if (int rc = check_launch("gemm_tn_small_kernel")) return rc;
+  } else {
+    hipLaunchKernelGGL(gemm_tn_partial_kernel, dim3(tiles_m * tiles_n, used), dim3(256), 0, s, A,
+                       lda, B, ldb, K, M, N, kps, tiles_n, partial);
+    if (int rc = check_launch("gemm_tn_partial_kernel")) return rc;
+  }
   const int64_t MN = (int64_t)M * N;
   hipLaunchKernelGGL(gemm_reduce_kernel, dim3((unsigned)((MN + 63) / 64)), dim3(256), 0, s,
                      partial, used, MN, N, C, ldc, accumulate);
@@ -222,7 +275,10 @@ namespace {
 constexpr int kNNRows = 128;  // rows of A per workgroup
 constexpr int EPI_STORE = 0, EPI_RELU = 1;
 
-template <int K, int EPI>
+// NTP = 32-column tiles of N per workgroup (1, 2 or 4): wave w owns column
+// tile w % NTP and the 32-row subtiles t = w / NTP + j * (4 / NTP), so a small
+// N (F = 32 layers, config 3) still keeps all four waves busy.
+template <int K, int EPI, int NTP>
 __global__ __launch_bounds__(256, 2) void gemm_nn_kernel(
     const float *__restrict__ A, int64_t lda, const float *__restrict__ B, int64_t sbk,
     int64_t sbn, float *__restrict__ C, int64_t ldc, int64_t M, int N,
@@ -237,9 +293,11 @@ __global__ __launch_bounds__(256, 2) void gemm_nn_kernel(
   constexpr bool kPrefetch = true;
   __shared__ __attribute__((aligned(16))) float sA[kNNRows * LDA];
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
   const int h = lane >> 5, lc = lane & 31;
-  const int n = wave * 32 + lc;  // output column of this lane
+  constexpr int SUBS = 4 / NTP;  // waves sharing a column tile
+  const int mg = wave / NTP;     // first 32-row subtile of this wave
+  const int n = (wave % NTP) * 32 + lc;  // output column of this lane
   const bool n_ok = n < N;
   const int64_t n_tiles = (M + kNNRows - 1) / kNNRows;
 
@@ -283,7 +341,8 @@ __global__ __launch_bounds__(256, 2) void gemm_nn_kernel(
     // row = (r & 3) + 8 (r >> 2) + 4 h.
     const bool full = (m0 + kNNRows <= M) && n_ok;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
+    for (int j = 0; j < NTP; ++j) {
+      const int t = mg + j * SUBS;
       const float *arow = &sA[(t * 32 + lc) * LDA + h * KH];
       f32x16 acc;
 #pragma unroll
@@ -332,8 +391,16 @@ __global__ __launch_bounds__(256, 2) void gemm_nn_kernel(
     }
   }
   if constexpr (EPI == EPI_RELU) {
-    const float other = __shfl_xor(csum, 32, 64);
-    if (h == 0 && n_ok) colsum_partial[(int64_t)blockIdx.x * N + n] = __fadd_rn(csum, other);
+    // fold the waves that share a column tile, in subtile order (deterministic)
+    __shared__ float red[4][32];
+    const float both = __fadd_rn(csum, __shfl_xor(csum, 32, 64));
+    if (h == 0) red[wave][lc] = both;
+    __syncthreads();
+    if (wave < NTP && h == 0 && n_ok) {
+      float v = red[wave][lc];
+      for (int g = 1; g < SUBS; ++g) v = __fadd_rn(v, red[g * NTP + wave][lc]);
+      colsum_partial[(int64_t)blockIdx.x * N + n] = v;
+    }
   }
 }
 
@@ -347,12 +414,25 @@ int launch_nn(int64_t M, int N, const float *A, int64_t lda, const float *B, int
               int64_t sbn, float *C, int64_t ldc, int epi, const float *Z, int64_t ldz,
               float *partial, hipStream_t s) {
   const unsigned blocks = (unsigned)nn_grid(M);
-  if (epi == EPI_RELU)
-    hipLaunchKernelGGL((gemm_nn_kernel<K, EPI_RELU>), dim3(blocks), dim3(256), 0, s, A, lda, B,
-                       sbk, sbn, C, ldc, M, N, Z, ldz, partial);
-  else
-    hipLaunchKernelGGL((gemm_nn_kernel<K, EPI_STORE>), dim3(blocks), dim3(256), 0, s, A, lda, B,
-                       sbk, sbn, C, ldc, M, N, Z, ldz, partial);
+#define MGCN_NN(NTP_)                                                                          \
+  if (epi == EPI_RELU)                                                                        \
+    hipLaunchKernelGGL((gemm_nn_kernel<K, EPI_RELU, NTP_>), dim3(blocks), dim3(256), 0, s, A, \
+                       lda, B, sbk, sbn, C, ldc, M, N, Z, ldz, partial);                      \
+  else                                                                                        \
+    hipLaunchKernelGGL((gemm_nn_kernel<K, EPI_STORE, NTP_>), dim3(blocks), dim3(256), 0, s, A,\
+                       lda, B, sbk, sbn, C, ldc, M, N, Z, ldz, partial);
+  // NTP = 1 only where it compiles without spills (K = 32, N <= 32: the
+  // config-3 F = 32 layers); elsewhere idle column tiles are cheaper than spills
+  if constexpr (K == 32) {
+    if (N <= 32) {
+      MGCN_NN(1)
+    } else {
+      MGCN_NN(4)
+    }
+  } else {
+    MGCN_NN(4)
+  }
+#undef MGCN_NN
   return check_launch("gemm_nn_kernel");
 }
 

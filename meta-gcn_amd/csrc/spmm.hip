@@ -66,6 +66,9 @@ struct SpmmArgs {
   int mean;                // fwd: divide by max(deg,1)
   int relu;                // fwd
   int accumulate;          // bwd: Y += result
+  const int32_t *heavy_rows;  // rows with deg > heavy_thr, done by spmm_heavy_kernel
+  int64_t n_heavy;
+  int64_t heavy_thr;          // INT64_MAX: no heavy path
 };
 
 template <int V>
@@ -175,7 +178,9 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(const SpmmArgs a) {
     const int64_t row = wv * RPW + grp;
     const bool row_ok = row < a.n_rows;
     const int64_t beg = row_ok ? a.rowptr[row] : 0;
-    const int64_t deg = row_ok ? a.rowptr[row + 1] - beg : 0;
+    int64_t deg = row_ok ? a.rowptr[row + 1] - beg : 0;
+    const bool heavy = deg > a.heavy_thr;  // owned by spmm_heavy_kernel
+    if (heavy) deg = 0;
     const int64_t maxdeg = (RPW > 1) ? wave_max_over_groups<G>(deg) : deg;
 
     for (int c = 0; c < a.n_chunks; ++c) {
@@ -270,7 +275,7 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(const SpmmArgs a) {
         }
       }
 
-      if (!(row_ok && f_ok)) continue;
+      if (!(row_ok && f_ok) || heavy) continue;
       float *dst = a.Y + row * a.ldy + f0;
       if constexpr (kFwd) {
         const float inv_cnt = (float)(deg > 1 ? deg : 1);
@@ -306,6 +311,137 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(const SpmmArgs a) {
       }
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// Heavy rows (degree > heavy_thr; the botnet graphs reach ~6k, config 3):
+// one 256-thread workgroup per row.  The row's edges are taken in batches of
+// BE: phase A gathers BE source rows (a feature chunk of FC floats each) and
+// forms every product p[k][f] = g(X[col_k, f]) * w_k in parallel into LDS
+// (the multiplies are independent, so this is exactly the reference's
+// index_select * norm); phase B folds p[.][f] for each feature f sequentially
+// in edge order (FC threads, one chain per feature) -- the reference's
+// scatter_add order, bit for bit.  BE rows in flight per CU instead of U per
+// lane group: the row no longer serialises on HBM latency.
+template <int VEC, int MODE>
+__global__ __launch_bounds__(kBlock) void spmm_heavy_kernel(const SpmmArgs a, int FC, int BE) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float *P = smem;                                            // [BE][FC] products
+  int32_t *Eid = reinterpret_cast<int32_t *>(smem + BE * FC);  // [BE] per-edge metadata
+  int32_t *Col = Eid + BE;
+  float *Wt = reinterpret_cast<float *>(Col + BE);
+  float *Cnt = Wt + BE;
+  constexpr bool kFwd = (MODE == FWD_SUM || MODE == FWD_MAX);
+  constexpr bool kNeedEid = (MODE == FWD_MAX || MODE == BWD_MAX);
+  constexpr int kInFlight = 8;  // independent gathers per thread
+  const int t = threadIdx.x;
+  const int64_t row = a.heavy_rows[blockIdx.x];
+  const int64_t beg = a.rowptr[row];
+  const int64_t deg = a.rowptr[row + 1] - beg;
+  const bool has_w = a.w != nullptr;
+
+  for (int f0 = 0; f0 < a.F; f0 += FC) {
+    const int fc = (a.F - f0) < FC ? (a.F - f0) : FC;
+    const int nv = fc / VEC;  // vectors per row segment
+    float acc = (MODE == FWD_MAX) ? MGCN_MAX_FILL : 0.0f;
+    int32_t arg = -1;
+    for (int64_t e0 = 0; e0 < deg; e0 += BE) {
+      const int nb = (deg - e0) < BE ? (int)(deg - e0) : BE;
+      // phase A0: the batch's edge metadata -> LDS (coalesced)
+      for (int k = t; k < nb; k += kBlock) {
+        const int64_t slot = beg + e0 + k;
+        const int col = a.col[slot];
+        Col[k] = col;
+        Wt[k] = has_w ? a.w[slot] : 1.0f;
+        if constexpr (kNeedEid) Eid[k] = a.eid[slot];
+        if constexpr (MODE == BWD_MEAN) Cnt[k] = a.cnt[col];
+      }
+      __syncthreads();
+      // phase A1: kInFlight independent row-segment gathers per thread, then
+      // the products (one rounding each, as x_j * norm) -> LDS
+      const int total = nb * nv;
+      for (int base = t; base < total; base += kBlock * kInFlight) {
+        F32v<VEC> x[kInFlight];
+        I32v<VEC> am[kInFlight];
+#pragma unroll
+        for (int j = 0; j < kInFlight; ++j) {
+          const int idx = base + j * kBlock;
+          if (idx < total) {
+            const int k = idx / nv, c = idx - (idx / nv) * nv;
+            const int64_t off = (int64_t)Col[k] * a.ldx + f0 + c * VEC;
+            x[j] = load_f<VEC>(a.X + off);
+            if constexpr (MODE == BWD_MAX)
+              am[j] = load_i<VEC>(a.argmax_in + (int64_t)Col[k] * a.F + f0 + c * VEC);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < kInFlight; ++j) {
+          const int idx = base + j * kBlock;
+          if (idx < total) {
+            const int k = idx / nv, c = idx - (idx / nv) * nv;
+            const float w = Wt[k];
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) {
+              float v = x[j].v[q];
+              if constexpr (MODE == BWD_MAX) v = (am[j].v[q] == Eid[k]) ? v : 0.0f;
+              if constexpr (MODE == BWD_MEAN) v = __fdiv_rn(v, Cnt[k]);
+              P[k * FC + c * VEC + q] = __fmul_rn(v, w);
+            }
+          }
+        }
+      }
+      __syncthreads();
+      if (t < fc) {  // phase B: one sequential chain per feature
+        const float *pc = P + t;
+        if constexpr (MODE == FWD_MAX) {
+          for (int k = 0; k < nb; ++k) {
+            const float p = pc[k * FC];
+            if (p >= acc) {
+              acc = p;
+              arg = Eid[k];
+            }
+          }
+        } else {
+#pragma unroll 8
+          for (int k = 0; k < nb; ++k) acc = __fadd_rn(acc, pc[k * FC]);
+        }
+      }
+      __syncthreads();
+    }
+    if (t < fc) {
+      const int f = f0 + t;
+      float *dst = a.Y + row * a.ldy + f;
+      if constexpr (kFwd) {
+        float y = acc;
+        if constexpr (MODE == FWD_MAX) {
+          if (y == MGCN_MAX_FILL) {
+            y = 0.0f;
+            arg = -1;
+          }
+          a.argmax_out[row * a.F + f] = arg;
+        } else {
+          if (a.mean) y = __fdiv_rn(y, (float)(deg > 1 ? deg : 1));
+        }
+        if (a.bias != nullptr) y = __fadd_rn(y, a.bias[f]);
+        if (a.relu) y = (y < 0.0f) ? 0.0f : y;
+        *dst = y;
+      } else {
+        float v = acc;
+        if (a.row_scale != nullptr) v = __fmul_rn(v, a.row_scale[row]);
+        if (a.accumulate) v = __fadd_rn(*dst, v);
+        *dst = v;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void heavy_rows_kernel(int64_t n_rows,
+                                                            const int64_t *__restrict__ rowptr,
+                                                            int64_t thr, int32_t *__restrict__ out,
+                                                            unsigned long long *__restrict__ count) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n_rows;
+       r += (int64_t)gridDim.x * blockDim.x)
+    if (rowptr[r + 1] - rowptr[r] > thr) out[atomicAdd(count, 1ull)] = (int32_t)r;
 }
 
 int pick_vec(int32_t F, const void *p0, int64_t ld0, const void *p1, int64_t ld1) {
@@ -354,12 +490,35 @@ int launch_g(const SpmmArgs &a, hipStream_t stream) {
   return launch_one<VEC, 4, 4, MODE>(a, stream);
 }
 
+constexpr int kHeavyLdsBytes = 65536;  // products + edge ids per batch (default LDS limit)
+
+template <int VEC, int MODE>
+int launch_heavy(const SpmmArgs &a, hipStream_t stream) {
+  int FC = a.F < 128 ? a.F : 128;
+  FC = (FC + VEC - 1) / VEC * VEC;
+  const int BE = kHeavyLdsBytes / (4 * (FC + 4));  // products + 4 metadata words per edge
+  const size_t lds = sizeof(float) * (size_t)BE * (FC + 4);
+  hipLaunchKernelGGL((spmm_heavy_kernel<VEC, MODE>), dim3((unsigned)a.n_heavy), dim3(kBlock), lds,
+                     stream, a, FC, BE);
+  return check_launch("spmm_heavy_kernel");
+}
+
 template <int MODE>
 int launch_mode(SpmmArgs a, int vec, hipStream_t stream) {
   const int G_lanes_max = 64;
   const int per_chunk = G_lanes_max * vec;
   a.n_chunks = (a.F + per_chunk - 1) / per_chunk;
   if (a.n_chunks < 1) a.n_chunks = 1;
+  if (a.heavy_rows == nullptr || a.n_heavy <= 0) {
+    a.heavy_rows = nullptr;
+    a.n_heavy = 0;
+    a.heavy_thr = INT64_MAX;
+  } else {
+    int rc = vec == 4   ? launch_heavy<4, MODE>(a, stream)
+             : vec == 2 ? launch_heavy<2, MODE>(a, stream)
+                        : launch_heavy<1, MODE>(a, stream);
+    if (rc) return rc;
+  }
   if (vec == 4) return launch_g<4, MODE>(a, stream);
   if (vec == 2) return launch_g<2, MODE>(a, stream);
   return launch_g<1, MODE>(a, stream);
@@ -397,7 +556,8 @@ static int choose_vec(int32_t F, const void *p0, int64_t ld0, const void *p1, in
 extern "C" int mgcn_spmm_fwd(int64_t n_rows, int32_t F, const int64_t *rowptr, const int32_t *col,
                              const int32_t *eid, const float *w, const float *H, int64_t ldh,
                              float *Y, int64_t ldy, int reduce, const float *bias, int relu,
-                             int32_t *argmax, void *stream) {
+                             int32_t *argmax, const int32_t *heavy_rows, int64_t n_heavy,
+                             int64_t heavy_thr, void *stream) {
   clear_error();
   MGCN_REQUIRE(n_rows >= 0 && F >= 0, "mgcn_spmm_fwd: negative size");
   MGCN_REQUIRE(reduce == MGCN_REDUCE_SUM || reduce == MGCN_REDUCE_MEAN || reduce == MGCN_REDUCE_MAX,
@@ -420,6 +580,9 @@ extern "C" int mgcn_spmm_fwd(int64_t n_rows, int32_t F, const int64_t *rowptr, c
   a.ldy = ldy;
   a.bias = bias;
   a.argmax_out = argmax;
+  a.heavy_rows = heavy_rows;
+  a.n_heavy = n_heavy;
+  a.heavy_thr = heavy_thr;
   a.mean = reduce == MGCN_REDUCE_MEAN;
   a.relu = relu != 0;
   int vec = choose_vec(F, H, ldh, Y, ldy);
@@ -434,7 +597,8 @@ extern "C" int mgcn_spmm_bwd(int64_t n_rows, int32_t F, const int64_t *rowptr_t,
                              const int32_t *col_t, const int32_t *eid_t, const float *w_t,
                              const float *row_scale, const float *dY, int64_t lddy, float *dH,
                              int64_t lddh, int reduce, const float *cnt, const int32_t *argmax,
-                             int accumulate, void *stream) {
+                             int accumulate, const int32_t *heavy_rows, int64_t n_heavy,
+                             int64_t heavy_thr, void *stream) {
   clear_error();
   MGCN_REQUIRE(n_rows >= 0 && F >= 0, "mgcn_spmm_bwd: negative size");
   MGCN_REQUIRE(reduce == MGCN_REDUCE_SUM || reduce == MGCN_REDUCE_MEAN || reduce == MGCN_REDUCE_MAX,
@@ -460,10 +624,38 @@ extern "C" int mgcn_spmm_bwd(int64_t n_rows, int32_t F, const int64_t *rowptr_t,
   a.cnt = cnt;
   a.argmax_in = argmax;
   a.accumulate = accumulate != 0;
+  a.heavy_rows = heavy_rows;
+  a.n_heavy = n_heavy;
+  a.heavy_thr = heavy_thr;
   int vec = choose_vec(F, dY, lddy, dH, lddh);
   if (reduce == MGCN_REDUCE_MAX && reinterpret_cast<uintptr_t>(argmax) % (4 * vec)) vec = 1;
   hipStream_t s = as_stream(stream);
   if (reduce == MGCN_REDUCE_MAX) return launch_mode<BWD_MAX>(a, vec, s);
   if (reduce == MGCN_REDUCE_MEAN) return launch_mode<BWD_MEAN>(a, vec, s);
   return launch_mode<BWD_SUM>(a, vec, s);
+}
+
+extern "C" int mgcn_heavy_rows(int64_t n_rows, const int64_t *rowptr, int64_t thr, int32_t *rows_out,
+                               int64_t *n_out, void *workspace, size_t workspace_bytes,
+                               void *stream) {
+  clear_error();
+  MGCN_REQUIRE(n_rows >= 0 && thr >= 0 && n_out != nullptr, "mgcn_heavy_rows: bad arguments");
+  *n_out = 0;
+  if (n_rows == 0) return MGCN_OK;
+  MGCN_REQUIRE(rowptr && rows_out, "mgcn_heavy_rows: null array");
+  if (workspace == nullptr || workspace_bytes < sizeof(unsigned long long)) {
+    set_error("mgcn_heavy_rows: workspace needs %zu bytes", sizeof(unsigned long long));
+    return MGCN_EWORKSPACE;
+  }
+  hipStream_t s = as_stream(stream);
+  auto *count = static_cast<unsigned long long *>(workspace);
+  MGCN_HIP_TRY(hipMemsetAsync(count, 0, sizeof(*count), s));
+  hipLaunchKernelGGL(heavy_rows_kernel, dim3(grid_for(n_rows, kBlock)), dim3(kBlock), 0, s, n_rows,
+                     rowptr, thr, rows_out, count);
+  if (int rc = check_launch("heavy_rows_kernel")) return rc;
+  unsigned long long c = 0;
+  MGCN_HIP_TRY(hipMemcpyAsync(&c, count, sizeof(c), hipMemcpyDeviceToHost, s));
+  MGCN_HIP_TRY(hipStreamSynchronize(s));
+  *n_out = (int64_t)c;
+  return MGCN_OK;
 }

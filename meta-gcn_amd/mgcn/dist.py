@@ -49,6 +49,10 @@ class HipBackend:
     def norm(self, plan, method, deg=None, edge_weight=None):
         return plan.norm(method, deg=deg, edge_weight=edge_weight)
 
+    def finalize_view(self, view):
+        from .graph import find_heavy
+        return find_heavy(view)
+
     def spmm_fwd(self, *a, **k):
         from .ops import spmm_fwd
         return spmm_fwd(*a, **k)
@@ -109,7 +113,7 @@ def _remap(col: torch.Tensor, bounds: list, max_rows: int) -> torch.Tensor:
     return (c + owner * max_rows - b[owner]).to(torch.int32)
 
 
-def _slice_view(view: CSRView, lo: int, hi: int, bounds, max_rows, world) -> CSRView:
+def _slice_view(view: CSRView, lo: int, hi: int, bounds, max_rows, world):
     rp = view.rowptr[lo:hi + 1]
     beg = int(rp[0]) if hi >= lo else 0
     end = int(rp[-1])
@@ -136,6 +140,7 @@ def build_shard(edge_index: torch.Tensor, num_nodes: int, deg_norm="sm", deg=Non
     lo, hi = bounds[rank], bounds[rank + 1]
     fwd, fb, fe = _slice_view(plan.fwd, lo, hi, bounds, max_rows, world)
     bwd, bb, be = _slice_view(plan.bwd, lo, hi, bounds, max_rows, world)
+    fwd, bwd = backend.finalize_view(fwd), backend.finalize_view(bwd)
     w_fwd = None if norm.w_fwd is None else norm.w_fwd[fb:fe].contiguous()
     w_bwd = None if norm.w_bwd is None else norm.w_bwd[bb:be].contiguous()
     row_scale = None if norm.row_scale_bwd is None else norm.row_scale_bwd[lo:hi].contiguous()

@@ -33,6 +33,12 @@ import torch
 from . import _lib as L
 
 
+# Rows with more edges than this are aggregated by a whole workgroup
+# (libmgcn's heavy-row path, mgcn_heavy_rows); the lane-group kernel would
+# otherwise serialise on them (degree-skewed graphs, config 3).
+HEAVY_THRESHOLD = 128
+
+
 @dataclass
 class CSRView:
     """Edges grouped by one endpoint; ``col`` holds the other endpoint."""
@@ -41,10 +47,33 @@ class CSRView:
     eid: torch.Tensor     # int32 [nnz] original COO edge id of each slot
     n_rows: int
     n_cols: int
+    heavy: torch.Tensor | None = None  # int32 ids of rows with degree > heavy_thr
+    heavy_thr: int = HEAVY_THRESHOLD
 
     @property
     def nnz(self) -> int:
         return int(self.col.numel())
+
+    @property
+    def n_heavy(self) -> int:
+        return 0 if self.heavy is None else int(self.heavy.numel())
+
+
+def find_heavy(view: CSRView, thr: int = HEAVY_THRESHOLD) -> CSRView:
+    """Fill ``view.heavy`` with the rows whose degree exceeds ``thr``."""
+    import ctypes
+    lib = L.load()
+    dev = view.rowptr.device
+    rows = torch.empty(max(view.n_rows, 1), dtype=torch.int32, device=dev)
+    ws = torch.empty(8, dtype=torch.uint8, device=dev)
+    n = ctypes.c_int64(0)
+    with torch.cuda.device(dev):
+        rc = lib.mgcn_heavy_rows(view.n_rows, L.ptr(view.rowptr), int(thr), L.ptr(rows),
+                                 ctypes.byref(n), L.ptr(ws), 8, L.stream_of(dev))
+    L.check(rc, "mgcn_heavy_rows")
+    view.heavy = rows[:n.value].clone() if n.value > 0 else None
+    view.heavy_thr = int(thr)
+    return view
 
 
 @dataclass
@@ -140,7 +169,7 @@ def build_view(key: torch.Tensor, other: torch.Tensor, n_key: int, n_other: int)
         rc = lib.mgcn_csr_build(L.ptr(key), L.ptr(other), nnz, n_key, n_other, L.ptr(rowptr),
                                 L.ptr(col), L.ptr(eid), L.ptr(ws), ws_bytes, L.stream_of(dev))
     L.check(rc, "mgcn_csr_build")
-    return CSRView(rowptr=rowptr, col=col, eid=eid, n_rows=n_key, n_cols=n_other)
+    return find_heavy(CSRView(rowptr=rowptr, col=col, eid=eid, n_rows=n_key, n_cols=n_other))
 
 
 def build_plan(edge_index: torch.Tensor, num_nodes: int) -> GraphPlan:

@@ -26,7 +26,7 @@ from torch.nn.utils.rnn import pad_sequence
 
 from . import _lib as L
 from .graph import plan_for
-from .ops import aggregate_plan, gcn_stack, linear, scatter_  # noqa: F401  (re-exported)
+from .ops import aggregate_plan, gcn_stack, linear, linear_bias, scatter_  # noqa: F401
 
 
 # --------------------------------------------------------------- inits (PyG)
@@ -41,6 +41,15 @@ def zeros(tensor):
     """torch_geometric.nn.inits.zeros (gcn_base_models.py:197)."""
     if tensor is not None:
         tensor.data.fill_(0)
+
+
+class Linear(nn.Linear):
+    """torch.nn.Linear with identical parameters/state_dict, whose products run
+    on libmgcn (x W^T and dx on mgcn_gemm_nn, dW on the split-K mgcn_gemm_tn).
+    Used for GCNModel's residual and final projections (gcn_model.py:64-73)."""
+
+    def forward(self, input):
+        return linear_bias(input, self.weight, self.bias)
 
 
 # ------------------------------------------------------------- common.py
@@ -348,7 +357,7 @@ class GCNModel(nn.Module):
         self.dropout = nn.Dropout(dropout)
         if residual_hop is not None and residual_hop > 0:
             self.residuals = nn.ModuleList([
-                nn.Linear(self.enc_sizes[i], self.enc_sizes[j])
+                Linear(self.enc_sizes[i], self.enc_sizes[j])
                 for i, j in zip(range(0, len(self.enc_sizes), residual_hop),
                                 range(residual_hop, len(self.enc_sizes), residual_hop))])
             self.non_linear = activation(non_linear)
@@ -356,7 +365,7 @@ class GCNModel(nn.Module):
         if self.final_type == 'none':
             self.final = nn.Identity()
         elif self.final_type == 'proj':
-            self.final = nn.Linear(self.enc_sizes[-1], num_classes)
+            self.final = Linear(self.enc_sizes[-1], num_classes)
         else:
             raise ValueError
 
@@ -401,6 +410,6 @@ class GCNModel(nn.Module):
         return x
 
 
-__all__ = ["glorot", "zeros", "Identity", "activation", "scatter_", "NodeModelBase",
+__all__ = ["glorot", "zeros", "Identity", "activation", "scatter_", "Linear", "NodeModelBase",
            "NodeModelAdditive", "GCNMultiKernel", "GCNLayer", "GCNStack", "GCNModel"]
 _ = L  # keep the binding imported so a missing library fails at import of ops

@@ -66,7 +66,7 @@ def spmm_fwd(view: CSRView, w: torch.Tensor | None, H: torch.Tensor, reduce: int
         rc = lib.mgcn_spmm_fwd(view.n_rows, F, L.ptr(view.rowptr), L.ptr(view.col),
                                L.ptr(view.eid), L.ptr(w), L.ptr(H), H.stride(0), L.ptr(Y),
                                Y.stride(0), reduce, L.ptr(bias), int(bool(relu)), L.ptr(argmax),
-                               L.stream_of(dev))
+                               L.ptr(view.heavy), view.n_heavy, view.heavy_thr, L.stream_of(dev))
     if _TIMER is not None:
         _TIMER("spmm_fwd", False)
     L.check(rc, "mgcn_spmm_fwd")
@@ -90,7 +90,8 @@ def spmm_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tensor 
         rc = lib.mgcn_spmm_bwd(view_t.n_rows, F, L.ptr(view_t.rowptr), L.ptr(view_t.col),
                                L.ptr(view_t.eid), L.ptr(w_t), L.ptr(row_scale), L.ptr(dY),
                                dY.stride(0), L.ptr(dH), dH.stride(0), reduce, L.ptr(cnt),
-                               L.ptr(argmax), int(bool(accumulate)), L.stream_of(dev))
+                               L.ptr(argmax), int(bool(accumulate)), L.ptr(view_t.heavy),
+                               view_t.n_heavy, view_t.heavy_thr, L.stream_of(dev))
     if _TIMER is not None:
         _TIMER("spmm_bwd", False)
     L.check(rc, "mgcn_spmm_bwd")
@@ -222,6 +223,40 @@ class _Linear(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             dW = gemm_tn(x, dH)
         return dx, dW
+
+
+class _LinearBias(torch.autograd.Function):
+    """torch.nn.functional.linear(x, W, b) = x W^T + b with W [out, in] on the
+    libmgcn GEMMs (dW = dy^T x is the K = num_nodes reduction that hipBLASLt
+    runs at ~18 TFLOP/s: GCNModel's residual and final Linear layers,
+    gcn_model.py:64-73)."""
+
+    @staticmethod
+    def forward(ctx, x, W, b):
+        ctx.save_for_backward(x, W)
+        ctx.has_b = b is not None
+        y = _mm_t(x, W)
+        return y.add_(b.detach()) if b is not None else y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, W = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = dW = db = None
+        if ctx.needs_input_grad[0]:
+            dx = _mm(dy, W)
+        if ctx.needs_input_grad[1]:
+            dW = gemm_tn(dy, x)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = relu_bwd_colsum(dy, None, False, True)[1]
+        return dx, dW, db
+
+
+def linear_bias(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None) -> torch.Tensor:
+    """F.linear on libmgcn for 2-D fp32 HIP inputs (else torch's F.linear)."""
+    if x.dim() != 2 or x.dtype != torch.float32 or x.device.type != "cuda":
+        return torch.nn.functional.linear(x, W, b)
+    return _LinearBias.apply(x, W, b)
 
 
 def linear(x: torch.Tensor, W: torch.Tensor) -> torch.Tensor:

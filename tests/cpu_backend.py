@@ -56,6 +56,9 @@ class CpuBackend:
         return torch.repeat_interleave(torch.arange(view.n_rows),
                                        view.rowptr[1:] - view.rowptr[:-1])
 
+    def finalize_view(self, view):
+        return view
+
     def spmm_fwd(self, view, w, H, reduce, bias=None, relu=False):
         rows = self._rows(view)
         x = H[view.col.long()]

@@ -116,12 +116,15 @@ def test_gcn_model_12_layer_botnet_matches_reference(cuda):
 
 
 # ------------------------------------------------- random graphs vs oracle
-def _graph(rng, N, E, loops=True, heavy=0):
+def _graph(rng, N, E, loops=True, heavy=0, heavy_src=0):
     s = rng.integers(0, N, E)
     d = rng.integers(0, N, E)
-    if heavy:
-        d = np.concatenate([d, np.zeros(heavy, np.int64)])
+    if heavy:  # destinations 0..3 get `heavy` extra in-edges between them
+        d = np.concatenate([d, rng.integers(0, 4, heavy)])
         s = np.concatenate([s, rng.integers(0, N, heavy)])
+    if heavy_src:  # source 1 gets `heavy_src` extra out-edges
+        s = np.concatenate([s, np.ones(heavy_src, np.int64)])
+        d = np.concatenate([d, rng.integers(0, N, heavy_src)])
     if loops:
         s = np.concatenate([s, np.arange(N)])
         d = np.concatenate([d, np.arange(N)])
@@ -129,7 +132,7 @@ def _graph(rng, N, E, loops=True, heavy=0):
 
 
 CASES = [
-    # N, E, F, deg_norm, aggr, relu, heavy
+    # N, E, F, deg_norm, aggr, relu, heavy (extra in-edges on rows 0..3)
     (20000, 200000, 128, "sm", "add", True, 0),
     (20000, 200000, 64, "rw", "mean", False, 0),
     (20000, 200000, 32, None, "max", False, 0),
@@ -138,6 +141,10 @@ CASES = [
     (3000, 30000, 300, "sm", "mean", True, 0),
     (3000, 30000, 128, "sm", "add", False, 12000),  # one destination of degree 12k
     (3000, 30000, 1, "sm", "add", False, 0),
+    (3000, 30000, 32, "sm", "max", True, 9000),
+    (3000, 30000, 32, "rw", "mean", False, 7000),
+    (3000, 30000, 300, None, "max", False, 2000),
+    (3000, 30000, 7, "sm", "add", True, 1000),
 ]
 
 
@@ -145,7 +152,7 @@ CASES = [
 def test_random_graph_vs_oracle_bitwise(cuda, oracle, N, E, F, deg_norm, aggr, relu, heavy):
     import mgcn
     rng = np.random.default_rng(N + E + F)
-    ei = _graph(rng, N, E, heavy=heavy)
+    ei = _graph(rng, N, E, heavy=heavy, heavy_src=heavy // 2)
     H = rng.standard_normal((N, F)).astype(np.float32)
     b = rng.uniform(-0.5, 0.5, F).astype(np.float32)
     dZ = rng.standard_normal((N, F)).astype(np.float32)
@@ -230,7 +237,8 @@ def test_config2_full_size_forward_backward_bitwise(cuda, oracle):
 
 # ----------------------------------------------------------------- dense
 @pytest.mark.parametrize("K,M,N", [(1_000_000, 128, 128), (4097, 128, 128), (3000, 7, 130),
-                                   (50, 32, 2), (0, 4, 4)])
+                                   (50, 32, 2), (0, 4, 4), (286_214, 32, 32), (286_214, 2, 32),
+                                   (1001, 17, 5)])
 def test_gemm_tn_matches_fp64(cuda, K, M, N):
     """dW = A^T B on fp32 MFMA (exact f32 products, f32 accumulation in a
     different order than any BLAS): |err| <= 1e-5 * sum_k |a_k b_k| + 1e-6."""
@@ -247,7 +255,9 @@ def test_gemm_tn_matches_fp64(cuda, K, M, N):
 
 
 @pytest.mark.parametrize("M,K,N,trans", [(1_000_000, 128, 128, False), (1_000_000, 128, 128, True),
-                                         (1000, 64, 100, False), (777, 32, 7, True), (1, 128, 128, False)])
+                                         (1000, 64, 100, False), (777, 32, 7, True), (1, 128, 128, False),
+                                         (286_214, 32, 32, False), (286_214, 32, 32, True),
+                                         (5000, 32, 2, False), (3000, 64, 40, True)])
 def test_gemm_nn_matches_fp64(cuda, M, K, N, trans):
     from mgcn.ops import gemm_nn
     g = torch.Generator(device=cuda).manual_seed(M + K + N)
@@ -338,3 +348,42 @@ def test_gcn_stack_matches_layer_by_layer(cuda):
             assert torch.equal(p.grad, a), name
         else:
             torch.testing.assert_close(p.grad, a, rtol=1e-4, atol=1e-3)
+
+
+def test_heavy_rows_are_listed(cuda):
+    """Rows above the threshold get the workgroup path in both views."""
+    from mgcn.graph import HEAVY_THRESHOLD, plan_for
+    rng = np.random.default_rng(5)
+    ei = _t(_graph(rng, 2000, 10000, heavy=12 * HEAVY_THRESHOLD, heavy_src=2 * HEAVY_THRESHOLD),
+            cuda)
+    plan = plan_for(ei, 2000)
+    deg_in = (plan.fwd.rowptr[1:] - plan.fwd.rowptr[:-1])
+    deg_out = (plan.bwd.rowptr[1:] - plan.bwd.rowptr[:-1])
+    assert set(plan.fwd.heavy.tolist()) == set(torch.nonzero(deg_in > HEAVY_THRESHOLD)[:, 0].tolist())
+    assert set(plan.bwd.heavy.tolist()) == set(torch.nonzero(deg_out > HEAVY_THRESHOLD)[:, 0].tolist())
+    assert plan.bwd.n_heavy >= 1
+
+
+@pytest.mark.parametrize("M,fin,fout", [(286_214, 32, 32), (286_214, 32, 2), (5000, 7, 16)])
+def test_linear_matches_torch(cuda, M, fin, fout):
+    """mgcn.models.Linear (libmgcn GEMMs) == torch.nn.Linear within fp32 tolerance."""
+    from mgcn.models import Linear
+    torch.manual_seed(M + fin)
+    ref = torch.nn.Linear(fin, fout).to(cuda)
+    lin = Linear(fin, fout).to(cuda)
+    lin.load_state_dict(ref.state_dict())
+    x = torch.randn(M, fin, device=cuda)
+    x1 = x.clone().requires_grad_(True)
+    x2 = x.clone().requires_grad_(True)
+    dy = torch.randn(M, fout, device=cuda)
+    y1, y2 = lin(x1), ref(x2)
+    torch.testing.assert_close(y1, y2, rtol=1e-5, atol=1e-5)
+    y1.backward(dy)
+    y2.backward(dy)
+    torch.testing.assert_close(x1.grad, x2.grad, rtol=1e-5, atol=1e-5)
+    # dW, db sum over M = 286k rows: check against fp64 with a summation bound
+    ref_dw = dy.double().t() @ x.double()
+    bound = dy.double().abs().t() @ x.double().abs()
+    assert ((lin.weight.grad.double() - ref_dw).abs() <= 1e-5 * bound + 1e-6).all()
+    ref_db = dy.double().sum(0)
+    assert ((lin.bias.grad.double() - ref_db).abs() <= 1e-5 * dy.double().abs().sum(0) + 1e-6).all()
