@@ -64,7 +64,11 @@ const char *mgcn_last_error(void);
 
 /* Tuning knobs (process-wide; default 0 = automatic):
  *   "spmm_vec"    : cap the floats per lane of the SpMM gathers (1, 2, 4)
- *   "spmm_unroll" : gathers in flight per lane group (4, 8 or 16)          */
+ *   "spmm_unroll" : gathers in flight per lane group (4, 8 or 16)
+ *   "heavy_side_stream": 1 (default) runs the heavy-row launch on a side
+ *                   stream concurrently with the lane-group launch; 0 serial
+ *   "heavy_lds_kb": LDS per heavy-row workgroup, 16..160 (default 160)
+ *   "heavy_block" : threads per heavy-row workgroup, 256/512/1024 (1024)    */
 int mgcn_set_option(const char *name, int value);
 
 /* ------------------------------------------------------------------ graph */

@@ -30,6 +30,9 @@
 // issued back to back before any of them is consumed (U rows in flight per
 // group), then folded into the accumulator strictly in edge order.
 
+#include <algorithm>
+#include <vector>
+
 #include "mgcn_internal.h"
 
 namespace mgcn {
@@ -313,99 +316,240 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(const SpmmArgs a) {
   }
 }
 
+#ifdef MGCN_HEAVY_PROFILE
+// phase timestamps of workgroup 0 (scripts/prof_heavy.py): [role][batch][begin, end]
+// role 0: fold wave, 1: first producer wave, 2: last producer wave
+__device__ unsigned long long g_hprof[3][256][2];
+#define HPROF(role, b, which)                                              \
+  if (blockIdx.x == 0 && (b) < 256) g_hprof[role][b][which] = clock64();
+#else
+#define HPROF(role, b, which)
+#endif
+
 // ---------------------------------------------------------------------------
 // Heavy rows (degree > heavy_thr; the botnet graphs reach ~6k, config 3):
-// one 256-thread workgroup per row.  The row's edges are taken in batches of
-// BE: phase A gathers BE source rows (a feature chunk of FC floats each) and
-// forms every product p[k][f] = g(X[col_k, f]) * w_k in parallel into LDS
-// (the multiplies are independent, so this is exactly the reference's
-// index_select * norm); phase B folds p[.][f] for each feature f sequentially
-// in edge order (FC threads, one chain per feature) -- the reference's
-// scatter_add order, bit for bit.  BE rows in flight per CU instead of U per
-// lane group: the row no longer serialises on HBM latency.
-template <int VEC, int MODE>
-__global__ __launch_bounds__(kBlock) void spmm_heavy_kernel(const SpmmArgs a, int FC, int BE) {
+// one workgroup of HB threads per row, software-pipelined over batches of BE
+// edges with two LDS product buffers.  While the first ceil(FC/64) waves FOLD
+// batch b -- one sequential chain per feature, in edge order: the reference's
+// scatter_add order, bit for bit -- the remaining PRODUCER waves gather batch
+// b + 1 and form every product p[f][k] = g(X[col_k, f]) * w_k into the other
+// buffer (independent multiplies: exactly the reference's index_select *
+// norm).  One barrier per batch.
+//
+// Producers: thread (c, g) owns vector column c (VEC features) of the edge
+// quads g, g + dk, ...: the nv threads of one quad read consecutive 16-byte
+// pieces of each source row (coalesced), transpose the 4 x VEC block in
+// registers and store one ds_write_b128 per feature.  Products are
+// feature-major: feature f = c*VEC + q lives in row q*nv + c of stride BEp
+// (BEp/4 odd: the nv stores of one instruction hit distinct banks), so a
+// folding lane reads four consecutive edges per ds_read_b128 from an 8-deep
+// register ring.  Edge metadata travels one batch ahead through a 3-slot LDS
+// ring (fold: slot b, producers: slot b + 1, loads behind the gathers: slot
+// b + 2).  The launch runs on a side stream, concurrently with the lane-group
+// kernel (launch_mode).
+template <int VEC, int MODE, int HB>
+__global__ __launch_bounds__(HB) void spmm_heavy_kernel(const SpmmArgs a, int FC, int BE) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float *P = smem;                                            // [BE][FC] products
-  int32_t *Eid = reinterpret_cast<int32_t *>(smem + BE * FC);  // [BE] per-edge metadata
-  int32_t *Col = Eid + BE;
-  float *Wt = reinterpret_cast<float *>(Col + BE);
-  float *Cnt = Wt + BE;
   constexpr bool kFwd = (MODE == FWD_SUM || MODE == FWD_MAX);
   constexpr bool kNeedEid = (MODE == FWD_MAX || MODE == BWD_MAX);
-  constexpr int kInFlight = 8;  // independent gathers per thread
+  constexpr int kQ = HB >= 1024 ? (MODE == BWD_MAX ? 1 : 2) : 4;  // edge quads in flight / thread
+  constexpr int kEpt = 4;  // metadata entries per producer thread (BE <= kEpt * producers)
+  const int BEp = BE + 4;  // product row stride (BE % 16 == 0, so BEp / 4 is odd)
+  int32_t *ring = reinterpret_cast<int32_t *>(smem + 2 * FC * BEp);  // [3][4][BE]
+  auto ColR = [&](int b) { return ring + (b % 3) * 4 * BE; };
+  auto EidR = [&](int b) { return ColR(b) + BE; };
+  auto WtR = [&](int b) { return reinterpret_cast<float *>(ColR(b) + 2 * BE); };
+  auto CntR = [&](int b) { return reinterpret_cast<float *>(ColR(b) + 3 * BE); };
   const int t = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int64_t row = a.heavy_rows[blockIdx.x];
   const int64_t beg = a.rowptr[row];
   const int64_t deg = a.rowptr[row + 1] - beg;
   const bool has_w = a.w != nullptr;
+  const int nbatch = (int)((deg + BE - 1) / BE);
+  auto batch_len = [&](int b) {
+    const int64_t left = deg - (int64_t)b * BE;
+    return left < BE ? (int)left : BE;
+  };
 
   for (int f0 = 0; f0 < a.F; f0 += FC) {
     const int fc = (a.F - f0) < FC ? (a.F - f0) : FC;
-    const int nv = fc / VEC;  // vectors per row segment
+    const int nv = fc / VEC;                   // vectors per row segment
+    const int fold_waves = (fc + 63) / 64;     // 1 or 2
+    const int np = HB - 64 * fold_waves;       // producer threads
+    const int pt = t - 64 * fold_waves;        // producer index (< 0: folder)
+    const int dk = np / nv, npe = dk * nv;     // quad producers: npe threads
+    const int g_first = pt / nv, c_first = pt - (pt / nv) * nv;
+
+    int mcol[kEpt], meid[kEpt];
+    float mw[kEpt];
+    auto load_meta = [&](int b) {  // registers <- edges pt + np*i of batch b
+      if (b >= nbatch) return;
+      const int nb = batch_len(b);
+#pragma unroll
+      for (int i = 0; i < kEpt; ++i) {
+        const int k = pt + np * i;
+        if (k < nb) {
+          const int64_t slot = beg + (int64_t)b * BE + k;
+          mcol[i] = a.col[slot];
+          mw[i] = has_w ? a.w[slot] : 1.0f;
+          if constexpr (kNeedEid) meid[i] = a.eid[slot];
+        }
+      }
+    };
+    auto store_meta = [&](int b) {  // ring slot of batch b <- registers
+      if (b >= nbatch) return;
+      const int nb = batch_len(b);
+      int32_t *Col = ColR(b), *Eid = EidR(b);
+      float *Wt = WtR(b), *Cnt = CntR(b);
+#pragma unroll
+      for (int i = 0; i < kEpt; ++i) {
+        const int k = pt + np * i;
+        if (k < nb) {
+          Col[k] = mcol[i];
+          Wt[k] = mw[i];
+          if constexpr (kNeedEid) Eid[k] = meid[i];
+          if constexpr (MODE == BWD_MEAN) Cnt[k] = a.cnt[mcol[i]];
+        }
+      }
+    };
+    // products of batch b (metadata already in its ring slot); batch b + 1's
+    // metadata is loaded behind the first round of gathers
+    auto produce = [&](int b) {
+      float *P = smem + (b & 1) * FC * BEp + c_first * BEp;  // row q*nv + c: + q*nv*BEp
+      const int32_t *Col = ColR(b), *Eid = EidR(b);
+      const float *Wt = WtR(b), *Cnt = CntR(b);
+      const int nb = batch_len(b);
+      const int nq = (nb + 3) >> 2;
+      const float *xs = a.X + f0 + c_first * VEC;
+      bool first = true;
+      if (pt < npe) {
+        for (int g0 = g_first; g0 < nq; g0 += kQ * dk) {
+          F32v<VEC> x[kQ][4];
+          I32v<VEC> am[kQ][4];
+#pragma unroll
+          for (int u = 0; u < kQ; ++u) {
+            const int g = g0 + u * dk;
+            if (g < nq) {
+              const I32v<4> cols = load_i<4>(Col + 4 * g);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                if (4 * g + e < nb) {
+                  x[u][e] = load_f<VEC>(xs + (int64_t)cols.v[e] * a.ldx);
+                  if constexpr (MODE == BWD_MAX)
+                    am[u][e] = load_i<VEC>(a.argmax_in + (int64_t)cols.v[e] * a.F + f0 +
+                                           c_first * VEC);
+                }
+              }
+            }
+          }
+          if (first) load_meta(b + 1);
+          first = false;
+#pragma unroll
+          for (int u = 0; u < kQ; ++u) {
+            const int g = g0 + u * dk;
+            if (g < nq) {
+              const F32v<4> w = load_f<4>(Wt + 4 * g);
+              I32v<4> eid;
+              F32v<4> cnt;
+              if constexpr (MODE == BWD_MAX) eid = load_i<4>(Eid + 4 * g);
+              if constexpr (MODE == BWD_MEAN) cnt = load_f<4>(Cnt + 4 * g);
+              int off = 4 * g;
+              asm volatile("" : "+v"(off));  // keep per-quad store offsets out of registers
+#pragma unroll
+              for (int q = 0; q < VEC; ++q) {
+                F32v<4> o;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  float v = x[u][e].v[q];
+                  if constexpr (MODE == BWD_MAX) v = (am[u][e].v[q] == eid.v[e]) ? v : 0.0f;
+                  if constexpr (MODE == BWD_MEAN) v = __fdiv_rn(v, cnt.v[e]);
+                  o.v[e] = __fmul_rn(v, w.v[e]);
+                }
+                store_f<4>(P + q * nv * BEp + off, o);
+              }
+            }
+          }
+        }
+      }
+      if (first) load_meta(b + 1);
+      store_meta(b + 1);
+    };
+
     float acc = (MODE == FWD_MAX) ? MGCN_MAX_FILL : 0.0f;
     int32_t arg = -1;
-    for (int64_t e0 = 0; e0 < deg; e0 += BE) {
-      const int nb = (deg - e0) < BE ? (int)(deg - e0) : BE;
-      // phase A0: the batch's edge metadata -> LDS (coalesced)
-      for (int k = t; k < nb; k += kBlock) {
-        const int64_t slot = beg + e0 + k;
-        const int col = a.col[slot];
-        Col[k] = col;
-        Wt[k] = has_w ? a.w[slot] : 1.0f;
-        if constexpr (kNeedEid) Eid[k] = a.eid[slot];
-        if constexpr (MODE == BWD_MEAN) Cnt[k] = a.cnt[col];
-      }
-      __syncthreads();
-      // phase A1: kInFlight independent row-segment gathers per thread, then
-      // the products (one rounding each, as x_j * norm) -> LDS
-      const int total = nb * nv;
-      for (int base = t; base < total; base += kBlock * kInFlight) {
-        F32v<VEC> x[kInFlight];
-        I32v<VEC> am[kInFlight];
+    if (pt >= 0) {
+      load_meta(0);
+      store_meta(0);
+    }
+    __syncthreads();
+    if (pt >= 0 && nbatch > 0) produce(0);
+    __syncthreads();
+#ifdef MGCN_HEAVY_PROFILE
+    const int prole = t == 0 ? 0 : t == 64 * fold_waves ? 1 : t == HB - 64 ? 2 : -1;
+#endif
+    const int frow = (t % VEC) * nv + t / VEC;  // this folding lane's product row
+    for (int bi = 0; bi < nbatch; ++bi) {
+#ifdef MGCN_HEAVY_PROFILE
+      if (prole >= 0) HPROF(prole, bi, 0);
+#endif
+      if (wave < fold_waves) {
+        if (t < fc) {  // fold batch bi: one sequential chain per feature, edge order
+          const float *pr = smem + (bi & 1) * FC * BEp + frow * BEp;
+          const int nb = batch_len(bi);
+          const int n4 = nb >> 2;
+          if constexpr (MODE == FWD_MAX) {
+            const int32_t *Eid = EidR(bi);
+            for (int c4 = 0; c4 < n4; ++c4) {
+              const F32v<4> p = load_f<4>(pr + 4 * c4);
+              const I32v<4> e = load_i<4>(Eid + 4 * c4);
 #pragma unroll
-        for (int j = 0; j < kInFlight; ++j) {
-          const int idx = base + j * kBlock;
-          if (idx < total) {
-            const int k = idx / nv, c = idx - (idx / nv) * nv;
-            const int64_t off = (int64_t)Col[k] * a.ldx + f0 + c * VEC;
-            x[j] = load_f<VEC>(a.X + off);
-            if constexpr (MODE == BWD_MAX)
-              am[j] = load_i<VEC>(a.argmax_in + (int64_t)Col[k] * a.F + f0 + c * VEC);
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < kInFlight; ++j) {
-          const int idx = base + j * kBlock;
-          if (idx < total) {
-            const int k = idx / nv, c = idx - (idx / nv) * nv;
-            const float w = Wt[k];
-#pragma unroll
-            for (int q = 0; q < VEC; ++q) {
-              float v = x[j].v[q];
-              if constexpr (MODE == BWD_MAX) v = (am[j].v[q] == Eid[k]) ? v : 0.0f;
-              if constexpr (MODE == BWD_MEAN) v = __fdiv_rn(v, Cnt[k]);
-              P[k * FC + c * VEC + q] = __fmul_rn(v, w);
+              for (int q = 0; q < 4; ++q) {
+                if (p.v[q] >= acc) {
+                  acc = p.v[q];
+                  arg = e.v[q];
+                }
+              }
             }
-          }
-        }
-      }
-      __syncthreads();
-      if (t < fc) {  // phase B: one sequential chain per feature
-        const float *pc = P + t;
-        if constexpr (MODE == FWD_MAX) {
-          for (int k = 0; k < nb; ++k) {
-            const float p = pc[k * FC];
-            if (p >= acc) {
-              acc = p;
-              arg = Eid[k];
+            for (int k = 4 * n4; k < nb; ++k) {
+              if (pr[k] >= acc) {
+                acc = pr[k];
+                arg = Eid[k];
+              }
             }
+          } else {
+            // 8-deep ring of 4-edge reads; reads past nb (at most 32 floats)
+            // stay inside the LDS allocation and are never added
+            constexpr int kR = 8;
+            F32v<4> R[kR];
+#pragma unroll
+            for (int j = 0; j < kR; ++j) R[j] = load_f<4>(pr + 4 * j);
+            int c4 = 0;
+            for (; c4 + kR <= n4; c4 += kR) {
+#pragma unroll
+              for (int j = 0; j < kR; ++j) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc = __fadd_rn(acc, R[j].v[q]);
+                R[j] = load_f<4>(pr + 4 * (c4 + kR + j));
+                __builtin_amdgcn_sched_barrier(0);  // keep each refill behind its adds
+              }
+            }
+#pragma unroll
+            for (int j = 0; j < kR; ++j) {
+              if (c4 + j < n4) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc = __fadd_rn(acc, R[j].v[q]);
+              }
+            }
+            for (int k = 4 * n4; k < nb; ++k) acc = __fadd_rn(acc, pr[k]);
           }
-        } else {
-#pragma unroll 8
-          for (int k = 0; k < nb; ++k) acc = __fadd_rn(acc, pc[k * FC]);
         }
+      } else if (bi + 1 < nbatch) {
+        produce(bi + 1);
       }
+#ifdef MGCN_HEAVY_PROFILE
+      if (prole >= 0) HPROF(prole, bi, 1);
+#endif
       __syncthreads();
     }
     if (t < fc) {
@@ -432,6 +576,7 @@ __global__ __launch_bounds__(kBlock) void spmm_heavy_kernel(const SpmmArgs a, in
         *dst = v;
       }
     }
+    __syncthreads();  // buffers are reused by the next feature chunk
   }
 }
 
@@ -459,6 +604,7 @@ int pick_vec(int32_t F, const void *p0, int64_t ld0, const void *p1, int64_t ld1
 
 int g_force_vec = 0;  // tuning knobs (mgcn_set_option)
 int g_unroll = 8;
+int g_heavy_side = 1;  // heavy-row launch on a side stream (concurrent)
 
 template <int VEC, int G, int U, int MODE>
 int launch_one(const SpmmArgs &a, hipStream_t stream) {
@@ -490,17 +636,66 @@ int launch_g(const SpmmArgs &a, hipStream_t stream) {
   return launch_one<VEC, 4, 4, MODE>(a, stream);
 }
 
-constexpr int kHeavyLdsBytes = 65536;  // products + edge ids per batch (default LDS limit)
+// LDS per heavy workgroup (two product buffers + the metadata ring).  The
+// per-batch cost is one gather round trip, so bigger batches win while rows
+// are long: the default takes the whole 160 KB of a CU.
+int g_heavy_lds = 160 * 1024;
+
+template <int VEC, int MODE, int HB>
+int launch_heavy_hb(const SpmmArgs &a, hipStream_t stream) {
+  int FC = a.F < 128 ? a.F : 128;
+  FC = (FC + VEC - 1) / VEC * VEC;
+  const int producers = HB - 64 * ((FC + 63) / 64);
+  // 2 product buffers of FC x (BE + 4) floats + a 3-slot ring of 4 x BE words
+  int BE = (g_heavy_lds / 4 - 8 * FC) / (2 * FC + 12);
+  if (BE > 4 * producers) BE = 4 * producers;  // kEpt metadata entries per producer
+  BE &= ~15;
+  if (BE < 16) {
+    set_error("spmm heavy rows: heavy_lds_kb too small for F=%d", a.F);
+    return MGCN_EINVAL;
+  }
+  const size_t lds = sizeof(float) * ((size_t)2 * FC * (BE + 4) + (size_t)12 * BE);
+  static bool attr_set = false;  // one instantiation per (VEC, MODE)
+  if (!attr_set) {
+    MGCN_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(&spmm_heavy_kernel<VEC, MODE, HB>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((spmm_heavy_kernel<VEC, MODE, HB>), dim3((unsigned)a.n_heavy), dim3(HB), lds,
+                     stream, a, FC, BE);
+  return check_launch("spmm_heavy_kernel");
+}
+
+int g_heavy_block = 1024;
 
 template <int VEC, int MODE>
 int launch_heavy(const SpmmArgs &a, hipStream_t stream) {
-  int FC = a.F < 128 ? a.F : 128;
-  FC = (FC + VEC - 1) / VEC * VEC;
-  const int BE = kHeavyLdsBytes / (4 * (FC + 4));  // products + 4 metadata words per edge
-  const size_t lds = sizeof(float) * (size_t)BE * (FC + 4);
-  hipLaunchKernelGGL((spmm_heavy_kernel<VEC, MODE>), dim3((unsigned)a.n_heavy), dim3(kBlock), lds,
-                     stream, a, FC, BE);
-  return check_launch("spmm_heavy_kernel");
+  if (g_heavy_block == 256) return launch_heavy_hb<VEC, MODE, 256>(a, stream);
+  if (g_heavy_block == 512) return launch_heavy_hb<VEC, MODE, 512>(a, stream);
+  return launch_heavy_hb<VEC, MODE, 1024>(a, stream);
+}
+
+// Side stream per device for the heavy-row launch: fork from the caller's
+// stream with an event, join back with another (caller-visible ordering is
+// unchanged: everything after the call on `stream` waits for both launches).
+struct SideStream {
+  hipStream_t stream = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+
+int side_stream(SideStream **out) {
+  static thread_local SideStream per_dev[64];  // per host thread: events never shared
+  int dev = 0;
+  MGCN_HIP_TRY(hipGetDevice(&dev));
+  MGCN_REQUIRE(dev >= 0 && dev < 64, "side_stream: device id %d", dev);
+  SideStream &s = per_dev[dev];
+  if (s.stream == nullptr) {
+    MGCN_HIP_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+    MGCN_HIP_TRY(hipEventCreateWithFlags(&s.fork, hipEventDisableTiming));
+    MGCN_HIP_TRY(hipEventCreateWithFlags(&s.join, hipEventDisableTiming));
+  }
+  *out = &s;
+  return MGCN_OK;
 }
 
 template <int MODE>
@@ -513,11 +708,26 @@ int launch_mode(SpmmArgs a, int vec, hipStream_t stream) {
     a.heavy_rows = nullptr;
     a.n_heavy = 0;
     a.heavy_thr = INT64_MAX;
-  } else {
+  } else if (!g_heavy_side) {
     int rc = vec == 4   ? launch_heavy<4, MODE>(a, stream)
              : vec == 2 ? launch_heavy<2, MODE>(a, stream)
                         : launch_heavy<1, MODE>(a, stream);
     if (rc) return rc;
+  } else {
+    SideStream *side = nullptr;
+    if (int rc = side_stream(&side)) return rc;
+    MGCN_HIP_TRY(hipEventRecord(side->fork, stream));
+    MGCN_HIP_TRY(hipStreamWaitEvent(side->stream, side->fork, 0));
+    int rc = vec == 4   ? launch_heavy<4, MODE>(a, side->stream)
+             : vec == 2 ? launch_heavy<2, MODE>(a, side->stream)
+                        : launch_heavy<1, MODE>(a, side->stream);
+    if (rc) return rc;
+    MGCN_HIP_TRY(hipEventRecord(side->join, side->stream));
+    rc = vec == 4   ? launch_g<4, MODE>(a, stream)
+         : vec == 2 ? launch_g<2, MODE>(a, stream)
+                    : launch_g<1, MODE>(a, stream);
+    MGCN_HIP_TRY(hipStreamWaitEvent(stream, side->join, 0));
+    return rc;
   }
   if (vec == 4) return launch_g<4, MODE>(a, stream);
   if (vec == 2) return launch_g<2, MODE>(a, stream);
@@ -528,6 +738,14 @@ int launch_mode(SpmmArgs a, int vec, hipStream_t stream) {
 }  // namespace mgcn
 
 using namespace mgcn;
+
+#ifdef MGCN_HEAVY_PROFILE
+extern "C" int mgcn_debug_heavy_prof(unsigned long long *host) {
+  MGCN_HIP_TRY(hipDeviceSynchronize());
+  MGCN_HIP_TRY(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_hprof), sizeof(g_hprof)));
+  return MGCN_OK;
+}
+#endif
 
 extern "C" int mgcn_set_option(const char *name, int value) {
   clear_error();
@@ -541,6 +759,21 @@ extern "C" int mgcn_set_option(const char *name, int value) {
   if (n == "spmm_unroll") {
     MGCN_REQUIRE(value == 4 || value == 8 || value == 16, "spmm_unroll must be 4, 8 or 16");
     g_unroll = value;
+    return MGCN_OK;
+  }
+  if (n == "heavy_lds_kb") {
+    MGCN_REQUIRE(value >= 16 && value <= 160, "heavy_lds_kb must be in [16, 160]");
+    g_heavy_lds = value * 1024;
+    return MGCN_OK;
+  }
+  if (n == "heavy_block") {
+    MGCN_REQUIRE(value == 256 || value == 512 || value == 1024, "heavy_block must be 256, 512 or 1024");
+    g_heavy_block = value;
+    return MGCN_OK;
+  }
+  if (n == "heavy_side_stream") {
+    MGCN_REQUIRE(value == 0 || value == 1, "heavy_side_stream must be 0 or 1");
+    g_heavy_side = value;
     return MGCN_OK;
   }
   set_error("mgcn_set_option: unknown option '%s'", name);
@@ -657,5 +890,19 @@ extern "C" int mgcn_heavy_rows(int64_t n_rows, const int64_t *rowptr, int64_t th
   MGCN_HIP_TRY(hipMemcpyAsync(&c, count, sizeof(c), hipMemcpyDeviceToHost, s));
   MGCN_HIP_TRY(hipStreamSynchronize(s));
   *n_out = (int64_t)c;
+  if (c > 1) {  // heaviest first: the longest rows start first (prep-time, host sort)
+    std::vector<int32_t> rows(c);
+    std::vector<int64_t> rp(n_rows + 1);
+    MGCN_HIP_TRY(hipMemcpyAsync(rows.data(), rows_out, sizeof(int32_t) * c, hipMemcpyDeviceToHost, s));
+    MGCN_HIP_TRY(hipMemcpyAsync(rp.data(), rowptr, sizeof(int64_t) * (n_rows + 1),
+                                hipMemcpyDeviceToHost, s));
+    MGCN_HIP_TRY(hipStreamSynchronize(s));
+    std::stable_sort(rows.begin(), rows.end(), [&](int32_t x, int32_t y) {
+      const int64_t dx = rp[x + 1] - rp[x], dy = rp[y + 1] - rp[y];
+      return dx != dy ? dx > dy : x < y;
+    });
+    MGCN_HIP_TRY(hipMemcpyAsync(rows_out, rows.data(), sizeof(int32_t) * c, hipMemcpyHostToDevice, s));
+    MGCN_HIP_TRY(hipStreamSynchronize(s));
+  }
   return MGCN_OK;
 }

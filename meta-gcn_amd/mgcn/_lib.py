@@ -86,6 +86,13 @@ def load(path: str | None = None) -> ctypes.CDLL:
             fn.argtypes = args
         if lib.mgcn_abi_version() != ABI_VERSION:
             raise MgcnError(f"libmgcn ABI {lib.mgcn_abi_version()} != expected {ABI_VERSION}")
+        # tuning knobs from the environment: MGCN_OPTIONS="name=value,..."
+        for item in filter(None, os.environ.get("MGCN_OPTIONS", "").split(",")):
+            name, _, value = item.partition("=")
+            rc = lib.mgcn_set_option(name.strip().encode(), int(value))
+            if rc != OK:
+                raise MgcnError(f"MGCN_OPTIONS {item!r}: "
+                                f"{lib.mgcn_last_error().decode(errors='replace')}")
         if path is None:
             _lib = lib
         return lib
