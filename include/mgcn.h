@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define MGCN_ABI_VERSION 2
+#define MGCN_ABI_VERSION 3
 
 /* return codes */
 #define MGCN_OK 0
@@ -67,8 +67,11 @@ const char *mgcn_last_error(void);
  *   "spmm_unroll" : gathers in flight per lane group (4, 8 or 16)
  *   "heavy_side_stream": 1 (default) runs the heavy-row launch on a side
  *                   stream concurrently with the lane-group launch; 0 serial
- *   "heavy_lds_kb": LDS per heavy-row workgroup, 16..160 (default 160)
- *   "heavy_block" : threads per heavy-row workgroup, 256/512/1024 (1024)    */
+ *   "heavy_lds_kb": LDS per giant-row workgroup, 16..160 (default 160)
+ *   "heavy_block" : threads per giant-row workgroup, 256/512/1024 (1024)
+ *   "heavy_mid_lds_kb": LDS per (non-giant) heavy-row workgroup (default 40)
+ *   "heavy_giant_thr" : degree above which a heavy row is giant, read by
+ *                   mgcn_row_schedule (default 512)                        */
 int mgcn_set_option(const char *name, int value);
 
 /* ------------------------------------------------------------------ graph */
@@ -148,8 +151,7 @@ int mgcn_spmm_fwd(int64_t n_rows, int32_t F, const int64_t *rowptr,
                   const int32_t *col, const int32_t *eid, const float *w,
                   const float *H, int64_t ldh, float *Y, int64_t ldy,
                   int reduce, const float *bias, int relu, int32_t *argmax,
-                  const int32_t *heavy_rows, int64_t n_heavy, int64_t heavy_thr,
-                  void *stream);
+                  const int32_t *order, int64_t n_heavy, int64_t n_giant, void *stream);
 
 /*
  * Adjoint aggregation over the transposed (src-grouped) CSR:
@@ -165,20 +167,26 @@ int mgcn_spmm_bwd(int64_t n_rows, int32_t F, const int64_t *rowptr_t,
                   const float *row_scale, const float *dY, int64_t lddy,
                   float *dH, int64_t lddh, int reduce, const float *cnt,
                   const int32_t *argmax, int accumulate,
-                  const int32_t *heavy_rows, int64_t n_heavy, int64_t heavy_thr,
-                  void *stream);
+                  const int32_t *order, int64_t n_heavy, int64_t n_giant, void *stream);
 
 /*
- * Degree skew (botnet graphs reach degree ~6k, config 3).  Rows with more
- * than `thr` edges are listed once per plan by mgcn_heavy_rows (writes the
- * row ids, returns their number in *n_out; synchronises `stream`; workspace
- * >= 8 bytes) and passed to mgcn_spmm_fwd/bwd as (heavy_rows, n_heavy,
- * heavy_thr): each such row then gets a whole workgroup that gathers a batch
- * of its edges in parallel and folds them per feature in edge order (same
- * bits), while the lane-group kernel skips it.  heavy_rows = NULL disables.
+ * Row schedule (degree skew: the botnet graphs reach degree ~6k, config 3).
+ * mgcn_row_schedule writes every row id into order[n_rows], by degree,
+ * heaviest first (stable: equal degrees keep ascending ids), and returns
+ * n_heavy = #rows with degree > heavy_thr and n_giant = #those with degree >
+ * the "heavy_giant_thr" option; it synchronises `stream`.  Passed to
+ * mgcn_spmm_fwd/bwd as (order, n_heavy, n_giant): each heavy row gets a whole
+ * workgroup that gathers a batch of its edges in parallel and folds them per
+ * feature in edge order (same bits) -- giant rows a 1024-thread workgroup with
+ * the whole LDS of a CU on a side stream, the others a 256-thread one -- and
+ * the lane-group kernel takes order[n_heavy, n_rows) longest first, so the
+ * rows of one wave have similar degrees.  order = NULL: natural row order,
+ * no heavy path (n_heavy, n_giant ignored).
  */
-int mgcn_heavy_rows(int64_t n_rows, const int64_t *rowptr, int64_t thr, int32_t *rows_out,
-                    int64_t *n_out, void *workspace, size_t workspace_bytes, void *stream);
+size_t mgcn_row_schedule_workspace_bytes(int64_t n_rows);
+int mgcn_row_schedule(int64_t n_rows, const int64_t *rowptr, int64_t heavy_thr, int32_t *order,
+                      int64_t *n_heavy_out, int64_t *n_giant_out, void *workspace,
+                      size_t workspace_bytes, void *stream);
 
 /* ------------------------------------------------------------------ dense */
 

@@ -30,8 +30,7 @@
 // issued back to back before any of them is consumed (U rows in flight per
 // group), then folded into the accumulator strictly in edge order.
 
-#include <algorithm>
-#include <vector>
+#include <hipcub/hipcub.hpp>
 
 #include "mgcn_internal.h"
 
@@ -69,9 +68,14 @@ struct SpmmArgs {
   int mean;                // fwd: divide by max(deg,1)
   int relu;                // fwd
   int accumulate;          // bwd: Y += result
-  const int32_t *heavy_rows;  // rows with deg > heavy_thr, done by spmm_heavy_kernel
+  // row schedule (mgcn_row_schedule): rows by degree, heaviest first;
+  // order[0, n_heavy) go to spmm_heavy_kernel (the first n_giant of them as
+  // giant rows), order[n_heavy, n_rows) to the lane-group kernel in that
+  // order.  order == NULL: natural row order, no heavy path.
+  const int32_t *order;
   int64_t n_heavy;
-  int64_t heavy_thr;          // INT64_MAX: no heavy path
+  int64_t n_giant;
+  const int32_t *heavy_rows;  // per heavy launch: its slice of order
 };
 
 template <int V>
@@ -171,19 +175,20 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(const SpmmArgs a) {
   const int grp = lane / G;
   const int gbase = grp * G;
   const int wave_in_block = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t n_row_groups = (a.n_rows + RPW - 1) / RPW;
+  const int64_t n_work = a.order != nullptr ? a.n_rows - a.n_heavy : a.n_rows;
+  const int32_t *__restrict__ light = a.order != nullptr ? a.order + a.n_heavy : nullptr;
+  const int64_t n_row_groups = (n_work + RPW - 1) / RPW;
   const int64_t wave_stride = (int64_t)gridDim.x * kWaves;
   const float *__restrict__ X = a.X;
   const bool has_w = a.w != nullptr;
 
   for (int64_t wv = (int64_t)blockIdx.x * kWaves + wave_in_block; wv < n_row_groups;
        wv += wave_stride) {
-    const int64_t row = wv * RPW + grp;
-    const bool row_ok = row < a.n_rows;
+    const int64_t item = wv * RPW + grp;
+    const bool row_ok = item < n_work;
+    const int64_t row = !row_ok ? 0 : light != nullptr ? (int64_t)light[item] : item;
     const int64_t beg = row_ok ? a.rowptr[row] : 0;
-    int64_t deg = row_ok ? a.rowptr[row + 1] - beg : 0;
-    const bool heavy = deg > a.heavy_thr;  // owned by spmm_heavy_kernel
-    if (heavy) deg = 0;
+    const int64_t deg = row_ok ? a.rowptr[row + 1] - beg : 0;
     const int64_t maxdeg = (RPW > 1) ? wave_max_over_groups<G>(deg) : deg;
 
     for (int c = 0; c < a.n_chunks; ++c) {
@@ -278,7 +283,7 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(const SpmmArgs a) {
         }
       }
 
-      if (!(row_ok && f_ok) || heavy) continue;
+      if (!(row_ok && f_ok)) continue;
       float *dst = a.Y + row * a.ldy + f0;
       if constexpr (kFwd) {
         const float inv_cnt = (float)(deg > 1 ? deg : 1);
@@ -580,13 +585,22 @@ __global__ __launch_bounds__(HB) void spmm_heavy_kernel(const SpmmArgs a, int FC
   }
 }
 
-__global__ __launch_bounds__(kBlock) void heavy_rows_kernel(int64_t n_rows,
+__global__ __launch_bounds__(kBlock) void row_degree_kernel(int64_t n_rows,
                                                             const int64_t *__restrict__ rowptr,
-                                                            int64_t thr, int32_t *__restrict__ out,
+                                                            int64_t thr, int64_t giant_thr,
+                                                            int32_t *__restrict__ deg,
+                                                            int32_t *__restrict__ iota,
                                                             unsigned long long *__restrict__ count) {
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n_rows;
-       r += (int64_t)gridDim.x * blockDim.x)
-    if (rowptr[r + 1] - rowptr[r] > thr) out[atomicAdd(count, 1ull)] = (int32_t)r;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t d = rowptr[r + 1] - rowptr[r];
+    deg[r] = d < INT32_MAX ? (int32_t)d : INT32_MAX;
+    iota[r] = (int32_t)r;
+    if (d > thr) {
+      atomicAdd(&count[0], 1ull);
+      if (d > giant_thr) atomicAdd(&count[1], 1ull);
+    }
+  }
 }
 
 int pick_vec(int32_t F, const void *p0, int64_t ld0, const void *p1, int64_t ld1) {
@@ -637,42 +651,56 @@ int launch_g(const SpmmArgs &a, hipStream_t stream) {
 }
 
 // LDS per heavy workgroup (two product buffers + the metadata ring).  The
-// per-batch cost is one gather round trip, so bigger batches win while rows
-// are long: the default takes the whole 160 KB of a CU.
-int g_heavy_lds = 160 * 1024;
+// per-batch cost is about one gather round trip, so long rows want big
+// batches: a giant row's workgroup takes the whole 160 KB of a CU; the other
+// heavy rows (a few hundred edges) take little, so several share a CU.
+int g_heavy_lds = 160 * 1024;     // giant rows
+int g_heavy_mid_lds = 40 * 1024;  // other heavy rows
+int g_heavy_block = 1024;         // threads per giant-row workgroup
+int64_t g_giant_thr = 512;        // degree above which a heavy row is giant
 
 template <int VEC, int MODE, int HB>
-int launch_heavy_hb(const SpmmArgs &a, hipStream_t stream) {
+int launch_heavy_hb(SpmmArgs a, const int32_t *rows, int64_t n, int lds_budget,
+                    hipStream_t stream) {
+  if (n <= 0) return MGCN_OK;
+  a.heavy_rows = rows;
   int FC = a.F < 128 ? a.F : 128;
   FC = (FC + VEC - 1) / VEC * VEC;
   const int producers = HB - 64 * ((FC + 63) / 64);
   // 2 product buffers of FC x (BE + 4) floats + a 3-slot ring of 4 x BE words
-  int BE = (g_heavy_lds / 4 - 8 * FC) / (2 * FC + 12);
+  int BE = (lds_budget / 4 - 8 * FC) / (2 * FC + 12);
   if (BE > 4 * producers) BE = 4 * producers;  // kEpt metadata entries per producer
   BE &= ~15;
-  if (BE < 16) {
-    set_error("spmm heavy rows: heavy_lds_kb too small for F=%d", a.F);
-    return MGCN_EINVAL;
-  }
+  if (BE < 16) BE = 16;  // a small budget still gets one 16-edge batch (<= 21 KB)
   const size_t lds = sizeof(float) * ((size_t)2 * FC * (BE + 4) + (size_t)12 * BE);
-  static bool attr_set = false;  // one instantiation per (VEC, MODE)
+  static bool attr_set = false;  // one instantiation per (VEC, MODE, HB)
   if (!attr_set) {
     MGCN_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(&spmm_heavy_kernel<VEC, MODE, HB>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
-  hipLaunchKernelGGL((spmm_heavy_kernel<VEC, MODE, HB>), dim3((unsigned)a.n_heavy), dim3(HB), lds,
-                     stream, a, FC, BE);
+  hipLaunchKernelGGL((spmm_heavy_kernel<VEC, MODE, HB>), dim3((unsigned)n), dim3(HB), lds, stream,
+                     a, FC, BE);
   return check_launch("spmm_heavy_kernel");
 }
 
-int g_heavy_block = 1024;
-
 template <int VEC, int MODE>
-int launch_heavy(const SpmmArgs &a, hipStream_t stream) {
-  if (g_heavy_block == 256) return launch_heavy_hb<VEC, MODE, 256>(a, stream);
-  if (g_heavy_block == 512) return launch_heavy_hb<VEC, MODE, 512>(a, stream);
-  return launch_heavy_hb<VEC, MODE, 1024>(a, stream);
+int launch_heavy(const SpmmArgs &a, bool giant, hipStream_t stream) {
+  if (!giant)
+    return launch_heavy_hb<VEC, MODE, 256>(a, a.order + a.n_giant, a.n_heavy - a.n_giant,
+                                           g_heavy_mid_lds, stream);
+  if (g_heavy_block == 256)
+    return launch_heavy_hb<VEC, MODE, 256>(a, a.order, a.n_giant, g_heavy_lds, stream);
+  if (g_heavy_block == 512)
+    return launch_heavy_hb<VEC, MODE, 512>(a, a.order, a.n_giant, g_heavy_lds, stream);
+  return launch_heavy_hb<VEC, MODE, 1024>(a, a.order, a.n_giant, g_heavy_lds, stream);
+}
+
+template <int MODE>
+int launch_heavy_v(const SpmmArgs &a, int vec, bool giant, hipStream_t stream) {
+  if (vec == 4) return launch_heavy<4, MODE>(a, giant, stream);
+  if (vec == 2) return launch_heavy<2, MODE>(a, giant, stream);
+  return launch_heavy<1, MODE>(a, giant, stream);
 }
 
 // Side stream per device for the heavy-row launch: fork from the caller's
@@ -698,40 +726,39 @@ int side_stream(SideStream **out) {
   return MGCN_OK;
 }
 
+// Launch order: giant rows on the side stream (forked from `stream`, joined
+// back), then the other heavy rows and the lane-group kernel on `stream`; the
+// giant rows -- the critical path -- overlap everything else.
 template <int MODE>
 int launch_mode(SpmmArgs a, int vec, hipStream_t stream) {
   const int G_lanes_max = 64;
   const int per_chunk = G_lanes_max * vec;
   a.n_chunks = (a.F + per_chunk - 1) / per_chunk;
   if (a.n_chunks < 1) a.n_chunks = 1;
-  if (a.heavy_rows == nullptr || a.n_heavy <= 0) {
-    a.heavy_rows = nullptr;
+  if (a.order == nullptr) {
     a.n_heavy = 0;
-    a.heavy_thr = INT64_MAX;
-  } else if (!g_heavy_side) {
-    int rc = vec == 4   ? launch_heavy<4, MODE>(a, stream)
-             : vec == 2 ? launch_heavy<2, MODE>(a, stream)
-                        : launch_heavy<1, MODE>(a, stream);
-    if (rc) return rc;
-  } else {
-    SideStream *side = nullptr;
-    if (int rc = side_stream(&side)) return rc;
-    MGCN_HIP_TRY(hipEventRecord(side->fork, stream));
-    MGCN_HIP_TRY(hipStreamWaitEvent(side->stream, side->fork, 0));
-    int rc = vec == 4   ? launch_heavy<4, MODE>(a, side->stream)
-             : vec == 2 ? launch_heavy<2, MODE>(a, side->stream)
-                        : launch_heavy<1, MODE>(a, side->stream);
-    if (rc) return rc;
-    MGCN_HIP_TRY(hipEventRecord(side->join, side->stream));
+    a.n_giant = 0;
+  }
+  SideStream *side = nullptr;
+  if (a.n_giant > 0) {
+    if (g_heavy_side) {
+      if (int rc = side_stream(&side)) return rc;
+      MGCN_HIP_TRY(hipEventRecord(side->fork, stream));
+      MGCN_HIP_TRY(hipStreamWaitEvent(side->stream, side->fork, 0));
+      if (int rc = launch_heavy_v<MODE>(a, vec, true, side->stream)) return rc;
+      MGCN_HIP_TRY(hipEventRecord(side->join, side->stream));
+    } else if (int rc = launch_heavy_v<MODE>(a, vec, true, stream)) {
+      return rc;
+    }
+  }
+  int rc = a.n_heavy > a.n_giant ? launch_heavy_v<MODE>(a, vec, false, stream) : MGCN_OK;
+  if (rc == MGCN_OK) {
     rc = vec == 4   ? launch_g<4, MODE>(a, stream)
          : vec == 2 ? launch_g<2, MODE>(a, stream)
                     : launch_g<1, MODE>(a, stream);
-    MGCN_HIP_TRY(hipStreamWaitEvent(stream, side->join, 0));
-    return rc;
   }
-  if (vec == 4) return launch_g<4, MODE>(a, stream);
-  if (vec == 2) return launch_g<2, MODE>(a, stream);
-  return launch_g<1, MODE>(a, stream);
+  if (side != nullptr) MGCN_HIP_TRY(hipStreamWaitEvent(stream, side->join, 0));
+  return rc;
 }
 
 }  // namespace
@@ -771,6 +798,16 @@ extern "C" int mgcn_set_option(const char *name, int value) {
     g_heavy_block = value;
     return MGCN_OK;
   }
+  if (n == "heavy_mid_lds_kb") {
+    MGCN_REQUIRE(value >= 16 && value <= 160, "heavy_mid_lds_kb must be in [16, 160]");
+    g_heavy_mid_lds = value * 1024;
+    return MGCN_OK;
+  }
+  if (n == "heavy_giant_thr") {
+    MGCN_REQUIRE(value >= 0, "heavy_giant_thr must be >= 0");
+    g_giant_thr = value;
+    return MGCN_OK;
+  }
   if (n == "heavy_side_stream") {
     MGCN_REQUIRE(value == 0 || value == 1, "heavy_side_stream must be 0 or 1");
     g_heavy_side = value;
@@ -789,8 +826,8 @@ static int choose_vec(int32_t F, const void *p0, int64_t ld0, const void *p1, in
 extern "C" int mgcn_spmm_fwd(int64_t n_rows, int32_t F, const int64_t *rowptr, const int32_t *col,
                              const int32_t *eid, const float *w, const float *H, int64_t ldh,
                              float *Y, int64_t ldy, int reduce, const float *bias, int relu,
-                             int32_t *argmax, const int32_t *heavy_rows, int64_t n_heavy,
-                             int64_t heavy_thr, void *stream) {
+                             int32_t *argmax, const int32_t *order, int64_t n_heavy,
+                             int64_t n_giant, void *stream) {
   clear_error();
   MGCN_REQUIRE(n_rows >= 0 && F >= 0, "mgcn_spmm_fwd: negative size");
   MGCN_REQUIRE(reduce == MGCN_REDUCE_SUM || reduce == MGCN_REDUCE_MEAN || reduce == MGCN_REDUCE_MAX,
@@ -813,9 +850,11 @@ extern "C" int mgcn_spmm_fwd(int64_t n_rows, int32_t F, const int64_t *rowptr, c
   a.ldy = ldy;
   a.bias = bias;
   a.argmax_out = argmax;
-  a.heavy_rows = heavy_rows;
+  MGCN_REQUIRE(order == nullptr || (0 <= n_giant && n_giant <= n_heavy && n_heavy <= n_rows),
+               "spmm: need 0 <= n_giant <= n_heavy <= n_rows");
+  a.order = order;
   a.n_heavy = n_heavy;
-  a.heavy_thr = heavy_thr;
+  a.n_giant = n_giant;
   a.mean = reduce == MGCN_REDUCE_MEAN;
   a.relu = relu != 0;
   int vec = choose_vec(F, H, ldh, Y, ldy);
@@ -830,8 +869,8 @@ extern "C" int mgcn_spmm_bwd(int64_t n_rows, int32_t F, const int64_t *rowptr_t,
                              const int32_t *col_t, const int32_t *eid_t, const float *w_t,
                              const float *row_scale, const float *dY, int64_t lddy, float *dH,
                              int64_t lddh, int reduce, const float *cnt, const int32_t *argmax,
-                             int accumulate, const int32_t *heavy_rows, int64_t n_heavy,
-                             int64_t heavy_thr, void *stream) {
+                             int accumulate, const int32_t *order, int64_t n_heavy,
+                             int64_t n_giant, void *stream) {
   clear_error();
   MGCN_REQUIRE(n_rows >= 0 && F >= 0, "mgcn_spmm_bwd: negative size");
   MGCN_REQUIRE(reduce == MGCN_REDUCE_SUM || reduce == MGCN_REDUCE_MEAN || reduce == MGCN_REDUCE_MAX,
@@ -857,9 +896,11 @@ extern "C" int mgcn_spmm_bwd(int64_t n_rows, int32_t F, const int64_t *rowptr_t,
   a.cnt = cnt;
   a.argmax_in = argmax;
   a.accumulate = accumulate != 0;
-  a.heavy_rows = heavy_rows;
+  MGCN_REQUIRE(order == nullptr || (0 <= n_giant && n_giant <= n_heavy && n_heavy <= n_rows),
+               "spmm: need 0 <= n_giant <= n_heavy <= n_rows");
+  a.order = order;
   a.n_heavy = n_heavy;
-  a.heavy_thr = heavy_thr;
+  a.n_giant = n_giant;
   int vec = choose_vec(F, dY, lddy, dH, lddh);
   if (reduce == MGCN_REDUCE_MAX && reinterpret_cast<uintptr_t>(argmax) % (4 * vec)) vec = 1;
   hipStream_t s = as_stream(stream);
@@ -868,41 +909,66 @@ extern "C" int mgcn_spmm_bwd(int64_t n_rows, int32_t F, const int64_t *rowptr_t,
   return launch_mode<BWD_SUM>(a, vec, s);
 }
 
-extern "C" int mgcn_heavy_rows(int64_t n_rows, const int64_t *rowptr, int64_t thr, int32_t *rows_out,
-                               int64_t *n_out, void *workspace, size_t workspace_bytes,
-                               void *stream) {
+namespace {
+struct ScheduleScratch {
+  size_t deg, deg_sorted, iota, count, cub, total;
+};
+
+ScheduleScratch schedule_scratch(int64_t n_rows) {
+  ScheduleScratch s{};
+  const size_t b4 = align_up(static_cast<size_t>(n_rows > 0 ? n_rows : 1) * 4, 256);
+  size_t cub_bytes = 0;
+  (void)hipcub::DeviceRadixSort::SortPairsDescending(
+      nullptr, cub_bytes, (const int32_t *)nullptr, (int32_t *)nullptr, (const int32_t *)nullptr,
+      (int32_t *)nullptr, static_cast<int>(n_rows > 0 ? n_rows : 1), 0, 31, (hipStream_t)0);
+  s.deg = 0;
+  s.deg_sorted = b4;
+  s.iota = 2 * b4;
+  s.count = 3 * b4;
+  s.cub = s.count + 256;
+  s.total = s.cub + align_up(cub_bytes, 256);
+  return s;
+}
+}  // namespace
+
+extern "C" size_t mgcn_row_schedule_workspace_bytes(int64_t n_rows) {
+  return schedule_scratch(n_rows).total;
+}
+
+extern "C" int mgcn_row_schedule(int64_t n_rows, const int64_t *rowptr, int64_t heavy_thr,
+                                 int32_t *order, int64_t *n_heavy_out, int64_t *n_giant_out,
+                                 void *workspace, size_t workspace_bytes, void *stream) {
   clear_error();
-  MGCN_REQUIRE(n_rows >= 0 && thr >= 0 && n_out != nullptr, "mgcn_heavy_rows: bad arguments");
-  *n_out = 0;
+  MGCN_REQUIRE(n_rows >= 0 && n_rows < (int64_t(1) << 31) && heavy_thr >= 0 &&
+                   n_heavy_out != nullptr && n_giant_out != nullptr,
+               "mgcn_row_schedule: bad arguments");
+  *n_heavy_out = 0;
+  *n_giant_out = 0;
   if (n_rows == 0) return MGCN_OK;
-  MGCN_REQUIRE(rowptr && rows_out, "mgcn_heavy_rows: null array");
-  if (workspace == nullptr || workspace_bytes < sizeof(unsigned long long)) {
-    set_error("mgcn_heavy_rows: workspace needs %zu bytes", sizeof(unsigned long long));
+  MGCN_REQUIRE(rowptr && order, "mgcn_row_schedule: null array");
+  const ScheduleScratch s = schedule_scratch(n_rows);
+  if (workspace == nullptr || workspace_bytes < s.total) {
+    set_error("mgcn_row_schedule: workspace %zu bytes < required %zu", workspace_bytes, s.total);
     return MGCN_EWORKSPACE;
   }
-  hipStream_t s = as_stream(stream);
-  auto *count = static_cast<unsigned long long *>(workspace);
-  MGCN_HIP_TRY(hipMemsetAsync(count, 0, sizeof(*count), s));
-  hipLaunchKernelGGL(heavy_rows_kernel, dim3(grid_for(n_rows, kBlock)), dim3(kBlock), 0, s, n_rows,
-                     rowptr, thr, rows_out, count);
-  if (int rc = check_launch("heavy_rows_kernel")) return rc;
-  unsigned long long c = 0;
-  MGCN_HIP_TRY(hipMemcpyAsync(&c, count, sizeof(c), hipMemcpyDeviceToHost, s));
-  MGCN_HIP_TRY(hipStreamSynchronize(s));
-  *n_out = (int64_t)c;
-  if (c > 1) {  // heaviest first: the longest rows start first (prep-time, host sort)
-    std::vector<int32_t> rows(c);
-    std::vector<int64_t> rp(n_rows + 1);
-    MGCN_HIP_TRY(hipMemcpyAsync(rows.data(), rows_out, sizeof(int32_t) * c, hipMemcpyDeviceToHost, s));
-    MGCN_HIP_TRY(hipMemcpyAsync(rp.data(), rowptr, sizeof(int64_t) * (n_rows + 1),
-                                hipMemcpyDeviceToHost, s));
-    MGCN_HIP_TRY(hipStreamSynchronize(s));
-    std::stable_sort(rows.begin(), rows.end(), [&](int32_t x, int32_t y) {
-      const int64_t dx = rp[x + 1] - rp[x], dy = rp[y + 1] - rp[y];
-      return dx != dy ? dx > dy : x < y;
-    });
-    MGCN_HIP_TRY(hipMemcpyAsync(rows_out, rows.data(), sizeof(int32_t) * c, hipMemcpyHostToDevice, s));
-    MGCN_HIP_TRY(hipStreamSynchronize(s));
-  }
+  char *ws = static_cast<char *>(workspace);
+  int32_t *deg = reinterpret_cast<int32_t *>(ws + s.deg);
+  int32_t *deg_sorted = reinterpret_cast<int32_t *>(ws + s.deg_sorted);
+  int32_t *iota = reinterpret_cast<int32_t *>(ws + s.iota);
+  auto *count = reinterpret_cast<unsigned long long *>(ws + s.count);
+  size_t cub_bytes = s.total - s.cub;
+  hipStream_t st = as_stream(stream);
+  MGCN_HIP_TRY(hipMemsetAsync(count, 0, 2 * sizeof(unsigned long long), st));
+  hipLaunchKernelGGL(row_degree_kernel, dim3(grid_for(n_rows, kBlock)), dim3(kBlock), 0, st,
+                     n_rows, rowptr, heavy_thr, g_giant_thr, deg, iota, count);
+  if (int rc = check_launch("row_degree_kernel")) return rc;
+  // stable: equal degrees keep ascending row ids
+  MGCN_HIP_TRY(hipcub::DeviceRadixSort::SortPairsDescending(
+      ws + s.cub, cub_bytes, deg, deg_sorted, iota, order, static_cast<int>(n_rows), 0, 31, st));
+  unsigned long long c[2] = {0, 0};
+  MGCN_HIP_TRY(hipMemcpyAsync(c, count, sizeof(c), hipMemcpyDeviceToHost, st));
+  MGCN_HIP_TRY(hipStreamSynchronize(st));
+  *n_heavy_out = (int64_t)c[0];
+  *n_giant_out = (int64_t)c[1];
   return MGCN_OK;
 }

@@ -50,8 +50,8 @@ class HipBackend:
         return plan.norm(method, deg=deg, edge_weight=edge_weight)
 
     def finalize_view(self, view):
-        from .graph import find_heavy
-        return find_heavy(view)
+        from .graph import schedule_rows
+        return schedule_rows(view)
 
     def spmm_fwd(self, *a, **k):
         from .ops import spmm_fwd

@@ -34,8 +34,8 @@ from . import _lib as L
 
 
 # Rows with more edges than this are aggregated by a whole workgroup
-# (libmgcn's heavy-row path, mgcn_heavy_rows); the lane-group kernel would
-# otherwise serialise on them (degree-skewed graphs, config 3).
+# (libmgcn's heavy-row path); the lane-group kernel would otherwise
+# serialise on them (degree-skewed graphs, config 3).
 HEAVY_THRESHOLD = 128
 
 
@@ -47,7 +47,12 @@ class CSRView:
     eid: torch.Tensor     # int32 [nnz] original COO edge id of each slot
     n_rows: int
     n_cols: int
-    heavy: torch.Tensor | None = None  # int32 ids of rows with degree > heavy_thr
+    # row schedule (mgcn_row_schedule): row ids by degree, heaviest first;
+    # the first n_heavy (> heavy_thr edges) take the workgroup path, the
+    # first n_giant of those the giant launch.  None: natural order.
+    order: torch.Tensor | None = None
+    n_heavy: int = 0
+    n_giant: int = 0
     heavy_thr: int = HEAVY_THRESHOLD
 
     @property
@@ -55,25 +60,47 @@ class CSRView:
         return int(self.col.numel())
 
     @property
-    def n_heavy(self) -> int:
-        return 0 if self.heavy is None else int(self.heavy.numel())
+    def heavy(self) -> torch.Tensor | None:
+        """int32 ids of the heavy rows, heaviest first."""
+        return None if self.order is None or self.n_heavy == 0 else self.order[:self.n_heavy]
 
 
-def find_heavy(view: CSRView, thr: int = HEAVY_THRESHOLD) -> CSRView:
-    """Fill ``view.heavy`` with the rows whose degree exceeds ``thr``."""
+def schedule_rows(view: CSRView, thr: int = HEAVY_THRESHOLD) -> CSRView:
+    """Fill ``view.order`` / ``n_heavy`` / ``n_giant`` (mgcn_row_schedule).
+
+    The degree order pays on skewed graphs (waves of similar-degree rows,
+    longest first); on near-uniform ones (Erdos-Renyi, config 2) it only
+    scatters the row-pointer and edge-slot reads, so there the natural order
+    is kept (``order`` None): no heavy rows and max degree <= 4x mean + 8."""
     import ctypes
     lib = L.load()
     dev = view.rowptr.device
-    rows = torch.empty(max(view.n_rows, 1), dtype=torch.int32, device=dev)
-    ws = torch.empty(8, dtype=torch.uint8, device=dev)
-    n = ctypes.c_int64(0)
+    if view.n_rows == 0:
+        return view
+    order = torch.empty(view.n_rows, dtype=torch.int32, device=dev)
+    ws = torch.empty(lib.mgcn_row_schedule_workspace_bytes(view.n_rows), dtype=torch.uint8,
+                     device=dev)
+    n_heavy = ctypes.c_int64(0)
+    n_giant = ctypes.c_int64(0)
     with torch.cuda.device(dev):
-        rc = lib.mgcn_heavy_rows(view.n_rows, L.ptr(view.rowptr), int(thr), L.ptr(rows),
-                                 ctypes.byref(n), L.ptr(ws), 8, L.stream_of(dev))
-    L.check(rc, "mgcn_heavy_rows")
-    view.heavy = rows[:n.value].clone() if n.value > 0 else None
+        rc = lib.mgcn_row_schedule(view.n_rows, L.ptr(view.rowptr), int(thr), L.ptr(order),
+                                   ctypes.byref(n_heavy), ctypes.byref(n_giant), L.ptr(ws),
+                                   ws.numel(), L.stream_of(dev))
+    L.check(rc, "mgcn_row_schedule")
     view.heavy_thr = int(thr)
+    view.n_heavy = int(n_heavy.value)
+    view.n_giant = int(n_giant.value)
+    if view.n_heavy == 0:
+        top = int(order[0])
+        max_deg = int(view.rowptr[top + 1] - view.rowptr[top])
+        if max_deg <= 4 * view.nnz / view.n_rows + 8:
+            view.order, view.n_giant = None, 0
+            return view
+    view.order = order
     return view
+
+
+find_heavy = schedule_rows  # earlier name
 
 
 @dataclass
@@ -169,7 +196,7 @@ def build_view(key: torch.Tensor, other: torch.Tensor, n_key: int, n_other: int)
         rc = lib.mgcn_csr_build(L.ptr(key), L.ptr(other), nnz, n_key, n_other, L.ptr(rowptr),
                                 L.ptr(col), L.ptr(eid), L.ptr(ws), ws_bytes, L.stream_of(dev))
     L.check(rc, "mgcn_csr_build")
-    return find_heavy(CSRView(rowptr=rowptr, col=col, eid=eid, n_rows=n_key, n_cols=n_other))
+    return schedule_rows(CSRView(rowptr=rowptr, col=col, eid=eid, n_rows=n_key, n_cols=n_other))
 
 
 def build_plan(edge_index: torch.Tensor, num_nodes: int) -> GraphPlan:

@@ -66,7 +66,7 @@ def spmm_fwd(view: CSRView, w: torch.Tensor | None, H: torch.Tensor, reduce: int
         rc = lib.mgcn_spmm_fwd(view.n_rows, F, L.ptr(view.rowptr), L.ptr(view.col),
                                L.ptr(view.eid), L.ptr(w), L.ptr(H), H.stride(0), L.ptr(Y),
                                Y.stride(0), reduce, L.ptr(bias), int(bool(relu)), L.ptr(argmax),
-                               L.ptr(view.heavy), view.n_heavy, view.heavy_thr, L.stream_of(dev))
+                               L.ptr(view.order), view.n_heavy, view.n_giant, L.stream_of(dev))
     if _TIMER is not None:
         _TIMER("spmm_fwd", False)
     L.check(rc, "mgcn_spmm_fwd")
@@ -90,8 +90,8 @@ def spmm_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tensor 
         rc = lib.mgcn_spmm_bwd(view_t.n_rows, F, L.ptr(view_t.rowptr), L.ptr(view_t.col),
                                L.ptr(view_t.eid), L.ptr(w_t), L.ptr(row_scale), L.ptr(dY),
                                dY.stride(0), L.ptr(dH), dH.stride(0), reduce, L.ptr(cnt),
-                               L.ptr(argmax), int(bool(accumulate)), L.ptr(view_t.heavy),
-                               view_t.n_heavy, view_t.heavy_thr, L.stream_of(dev))
+                               L.ptr(argmax), int(bool(accumulate)), L.ptr(view_t.order),
+                               view_t.n_heavy, view_t.n_giant, L.stream_of(dev))
     if _TIMER is not None:
         _TIMER("spmm_bwd", False)
     L.check(rc, "mgcn_spmm_bwd")

@@ -145,6 +145,8 @@ CASES = [
     (3000, 30000, 32, "rw", "mean", False, 7000),
     (3000, 30000, 300, None, "max", False, 2000),
     (3000, 30000, 7, "sm", "add", True, 1000),
+    (5000, 20000, 32, "sm", "add", False, 300),  # skewed, no heavy row: degree order only
+    (5000, 20000, 16, None, "max", False, 300),
 ]
 
 
@@ -362,6 +364,47 @@ def test_heavy_rows_are_listed(cuda):
     assert set(plan.fwd.heavy.tolist()) == set(torch.nonzero(deg_in > HEAVY_THRESHOLD)[:, 0].tolist())
     assert set(plan.bwd.heavy.tolist()) == set(torch.nonzero(deg_out > HEAVY_THRESHOLD)[:, 0].tolist())
     assert plan.bwd.n_heavy >= 1
+
+
+HEAVY_CONFIGS = [
+    # libmgcn options for the heavy-row launches (read at plan time / launch)
+    {"heavy_giant_thr": 0},                      # every heavy row giant, 1024 threads
+    {"heavy_giant_thr": 1 << 40},                # none giant: 256-thread launch only
+    {"heavy_giant_thr": 0, "heavy_block": 256, "heavy_lds_kb": 16},  # many small batches
+    {"heavy_giant_thr": 0, "heavy_block": 512, "heavy_lds_kb": 24},
+    {"heavy_giant_thr": 600, "heavy_mid_lds_kb": 16, "heavy_side_stream": 0},
+]
+HEAVY_DEFAULTS = {"heavy_giant_thr": 512, "heavy_block": 1024, "heavy_lds_kb": 160,
+                  "heavy_mid_lds_kb": 40, "heavy_side_stream": 1}
+
+
+@pytest.mark.parametrize("cfg", HEAVY_CONFIGS)
+@pytest.mark.parametrize("F,aggr", [(32, "add"), (128, "mean"), (7, "max"), (64, "max")])
+def test_heavy_path_configurations_bitwise(cuda, oracle, cfg, F, aggr):
+    """Giant / mid heavy-row launches, block sizes and batch sizes all give
+    the reference's bits (fwd and adjoint, incl. ragged last batches)."""
+    import mgcn
+    rng = np.random.default_rng(F + len(aggr))
+    N = 3000
+    ei = _graph(rng, N, 30000, heavy=6000, heavy_src=2500)
+    H = rng.standard_normal((N, F)).astype(np.float32)
+    dZ = rng.standard_normal((N, F)).astype(np.float32)
+    wf, wb, rs = oracle.edge_factors(ei, N, "sm")
+    y_ref, am = oracle.aggr_fwd(ei, H, wf, aggr)
+    dH_ref, _ = oracle.aggr_bwd(ei, dZ, wb, rs, aggr, y_ref, False, am)
+    try:
+        for k, v in cfg.items():
+            mgcn.set_option(k, v)
+        mgcn.clear_cache()
+        Ht = _t(H, cuda).requires_grad_(True)
+        y = mgcn.aggregate(Ht, _t(ei, cuda), aggr=aggr, deg_norm="sm")
+        np.testing.assert_array_equal(_np(y), y_ref)
+        y.backward(_t(dZ, cuda))
+        np.testing.assert_array_equal(_np(Ht.grad), dH_ref)
+    finally:
+        for k, v in HEAVY_DEFAULTS.items():
+            mgcn.set_option(k, v)
+        mgcn.clear_cache()
 
 
 @pytest.mark.parametrize("M,fin,fout", [(286_214, 32, 32), (286_214, 32, 2), (5000, 7, 16)])
