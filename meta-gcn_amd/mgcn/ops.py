@@ -253,16 +253,19 @@ class _LinearBias(torch.autograd.Function):
 
 
 def linear_bias(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None) -> torch.Tensor:
-    """F.linear on libmgcn for 2-D fp32 HIP inputs (else torch's F.linear)."""
-    if x.dim() != 2 or x.dtype != torch.float32 or x.device.type != "cuda":
+    """F.linear on libmgcn for 2-D fp32 inputs (other ranks / dtypes: torch's
+    F.linear on the same HIP device).  CPU tensors raise: no CPU path."""
+    L.require_device(x, W, b)
+    if x.dim() != 2 or x.dtype != torch.float32:
         return torch.nn.functional.linear(x, W, b)
     return _LinearBias.apply(x, W, b)
 
 
 def linear(x: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
-    """``torch.matmul(x, W)`` with the libmgcn weight-gradient kernel."""
-    if x.dim() != 2 or x.dtype != torch.float32 or W.dtype != torch.float32 \
-            or x.device.type != "cuda":
+    """``torch.matmul(x, W)`` with the libmgcn weight-gradient kernel.  CPU
+    tensors raise: no CPU path."""
+    L.require_device(x, W)
+    if x.dim() != 2 or x.dtype != torch.float32 or W.dtype != torch.float32:
         return torch.matmul(x, W)
     return _Linear.apply(x, W)
 
