@@ -195,6 +195,72 @@ class KernelTimer:
 
 
 # ------------------------------------------------------------ main
+def build_stack(dev, ei_cpu, X, Ws, bs, dY):
+    """Single-GPU config-2 model (GCNStack of GCNLayers, the fused libmgcn
+    path) on one graph; returns (step, params).  The step is fwd + bwd to
+    every weight and bias against the fixed upstream gradient dY."""
+    from mgcn.models import GCNLayer, GCNStack
+    L = len(Ws)
+    F = Ws[0].shape[0]
+    layers = []
+    for i in range(L):
+        layer = GCNLayer(F, F, deg_norm='sm', aggr='add', bias=True,
+                         non_linear='relu' if i < L - 1 else 'none').to(dev)
+        nm = layer.gcn.node_models[0]
+        with torch.no_grad():
+            nm.weight_node.copy_(Ws[i])
+            nm.bias.copy_(bs[i])
+        layers.append(layer)
+    stack = GCNStack(layers)
+    params = list(stack.parameters())
+    ei = ei_cpu.to(dev)
+    Xd = X.to(dev)
+    dYd = dY.to(dev)
+
+    def step():
+        for p in params:
+            p.grad = None
+        stack(Xd, ei).backward(dYd)
+    return step, params
+
+
+def timed(run_step, steps, warmup, world, dev, timer=None):
+    """Graph prep + first step (untimed, reported), W warm-up steps, then
+    exactly K steps bracketed by barrier + device sync; max over ranks."""
+    from mgcn import ops
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    torch.cuda.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    run_step()
+    torch.cuda.synchronize()
+    prep_ms = (time.perf_counter() - t0) * 1e3
+    for _ in range(warmup):
+        run_step()
+    torch.cuda.synchronize()
+    barrier()
+    ops.set_kernel_timer(timer)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        run_step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    ops.set_kernel_timer(None)
+    elapsed = t1 - t0
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([elapsed, prep_ms], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, prep_ms = float(t[0]), float(t[1])
+    return elapsed, prep_ms
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -206,6 +272,12 @@ def main():
     ap.add_argument("--layers", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timers", action="store_true")
+    ap.add_argument("--mode", choices=["auto", "replica", "shard"], default="auto",
+                    help="N > 1: 'auto' measures data-parallel replicas (value, weak "
+                         "scaling) and the dst-range sharded graph (the 'sharded' field, "
+                         "strong scaling); 'replica' / 'shard' measure one of them")
+    ap.add_argument("--dist-backend", default="nccl", help=argparse.SUPPRESS)  # gloo: tests
+    ap.add_argument("--one-device", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -215,99 +287,88 @@ def main():
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run "
                              "(one process per GPU)")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    dev_index = 0 if args.one_device else local_rank
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
 
-    import mgcn
-    from mgcn import ops
-    from mgcn.models import GCNLayer, GCNStack
+    import mgcn  # noqa: F401
 
     F, L = args.feat, args.layers
-    ei_cpu, N = make_er_graph(args.nodes, args.pairs)
     n_edges = 2 * args.pairs          # graph edges, self-loops not counted
-    nnz = ei_cpu.shape[1]
-    X, Ws, bs, dY = make_inputs(N, F, L)
-
-    if world > 1:
+    X, Ws, bs, dY = make_inputs(args.nodes, F, L)
+    timer = None if args.no_kernel_timers else KernelTimer()
+    do_replica = world == 1 or args.mode in ("auto", "replica")
+    do_shard = world > 1 and args.mode in ("auto", "shard")
+    sharded = None
+    prep_ms = None
+    elapsed = None
+    N = args.nodes
+    if do_shard:
         from mgcn.dist import ShardedGCN
+        ei_cpu, N = make_er_graph(args.nodes, args.pairs)
         model = ShardedGCN(ei_cpu, N, Ws, bs, device=dev)
-        run_step = model.step_fn(X, dY)
-    else:
-        layers = []
-        for i in range(L):
-            layer = GCNLayer(F, F, deg_norm='sm', aggr='add', bias=True,
-                             non_linear='relu' if i < L - 1 else 'none').to(dev)
-            nm = layer.gcn.node_models[0]
-            with torch.no_grad():
-                nm.weight_node.copy_(Ws[i])
-                nm.bias.copy_(bs[i])
-            layers.append(layer)
-        stack = GCNStack(layers)
-        params = list(stack.parameters())
-        ei = ei_cpu.to(dev)
-        Xd = X.to(dev)
-        dYd = dY.to(dev)
+        nnz = ei_cpu.shape[1]
+        t_sh, prep_sh = timed(model.step_fn(X, dY), args.steps, args.warmup, world, dev,
+                              None if do_replica else timer)
+        sharded = {"value": n_edges * L / (t_sh / args.steps), "unit": "edges/s",
+                   "ms_per_step": t_sh / args.steps * 1e3, "scaling": "strong",
+                   "parallelism": f"dst-range x{world} (RCCL all-gathers of H and dY)",
+                   "workload": "config 2 (one 10M-edge graph) sharded by destination range",
+                   "graph_prep_plus_first_step_ms": prep_sh}
+        del model
+        torch.cuda.empty_cache()
+        if not do_replica:
+            elapsed, prep_ms = t_sh, prep_sh
+    if do_replica:
+        from mgcn.dist import allreduce_grads
+        # data-parallel replicas: rank r trains its own config-2 graph (seed r)
+        # with the shared weights; one bucketed gradient all-reduce per step
+        ei_cpu, N = make_er_graph(args.nodes, args.pairs, seed=rank)
+        nnz = ei_cpu.shape[1]
+        step, params = build_stack(dev, ei_cpu, X, Ws, bs, dY)
 
         def run_step():
-            for p in params:
-                p.grad = None
-            stack(Xd, ei).backward(dYd)
-
-    # graph preparation (CSR views, degrees, norms) happens once, outside the
-    # timed region; reported separately
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run_step()
-    torch.cuda.synchronize()
-    prep_and_first_ms = (time.perf_counter() - t0) * 1e3
-
-    for _ in range(args.warmup):
-        run_step()
-    timer = None if args.no_kernel_timers else KernelTimer()
-
-    def barrier():
-        if world > 1:
-            import torch.distributed as dist
-            dist.barrier()
-
-    torch.cuda.synchronize()
-    barrier()
-    ops.set_kernel_timer(timer)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        run_step()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    barrier()
-    ops.set_kernel_timer(None)
-    elapsed = t1 - t0
-    if world > 1:
-        import torch.distributed as dist
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+            step()
+            allreduce_grads(params)
+        elapsed, prep_ms = timed(run_step, args.steps, args.warmup, world, dev, timer)
     ms_per_step = elapsed / args.steps * 1e3
-    value = n_edges * L / (elapsed / args.steps)
+    if do_replica:
+        value = world * n_edges * L / (elapsed / args.steps)
+        scaling = "weak"
+        parallelism = f"dp{world}" if world > 1 else "single"
+        workload = ("config2: Erdos-Renyi N=1M, E=10M (+1M self-loops), F=128, 3-layer GCN "
+                    "(sm, add, bias, ReLU) fwd+bwd" + (
+                        f"; one graph per GPU (seed = rank), gradient all-reduce"
+                        if world > 1 else ""))
+    else:
+        value = sharded["value"]
+        scaling = "strong"
+        parallelism = f"dst-range x{world}"
+        workload = sharded["workload"]
 
     result = {
         "metric": METRIC, "value": value, "unit": "edges/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
-        "higher_is_better": True, "scaling": "strong" if world > 1 else "weak",
+        "higher_is_better": True, "scaling": scaling,
         "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": "config2: Erdos-Renyi N=1M, E=10M (+1M self-loops), F=128, "
-                               "3-layer GCN (sm, add, bias, ReLU) fwd+bwd",
-                   "nodes": N, "edges": n_edges, "nnz": nnz, "feat": F, "layers": L,
-                   "global_batch": 1, "parallelism": f"dst-range x{world}" if world > 1
-                   else "single"},
-        "graph_prep_plus_first_step_ms": prep_and_first_ms,
+        "config": {"workload": workload, "nodes": N, "edges": n_edges, "nnz": nnz, "feat": F,
+                   "layers": L, "global_batch": world if do_replica else 1,
+                   "parallelism": parallelism},
+        "graph_prep_plus_first_step_ms": prep_ms,
     }
+    if sharded is not None and do_replica:
+        result["sharded"] = sharded
     if timer is not None:
         ks = timer.summary()
-        rows_local = N // world
-        nnz_local = nnz // world
+        shard_only = not do_replica
+        rows_local = N // world if shard_only else N
+        nnz_local = nnz // world if shard_only else nnz
         kern = {}
         for name, s in ks.items():
             if name.startswith("spmm"):
@@ -320,7 +381,7 @@ def main():
                   key=lambda k: kern[k]["avg_ms"] * kern[k]["launches"])
         a = kern[dom]["gbs"]
         result["kernels"] = kern
-        traffic, src = pmc_traffic(dom, args, world)
+        traffic, src = pmc_traffic(dom, args, world if shard_only else 1)
         result["roofline"] = {"bound": "hbm", "kernel": dom, "achieved": a, "peak": HBM_PEAK_GBS,
                               "unit": "GB/s", "frac": a / HBM_PEAK_GBS, "traffic": traffic,
                               "traffic_source": src}
