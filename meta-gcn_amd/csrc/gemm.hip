@@ -250,190 +250,272 @@ extern "C" int mgcn_gemm_tn(int64_t K, int32_t M, int32_t N, const float *A, int
 // mgcn_gemm_nn: C[M, N] = A[M, K] . B[K, N]   (tall-skinny: M = nodes, K, N = F)
 //
 // The forward transform H = X W (gcn_base_models.py:201) and the input
-// gradient dX = dH W^T of a layer (B = W^T through strides).  One workgroup
-// per 128-row tile of A; wave w owns output columns [32w, 32w + 32) and the
-// four 32-row M sub-tiles (4 accumulators of v_mfma_f32_32x32x2_f32).
-//   * the wave's 32-column slab of B stays in registers for the whole tile
-//     (K/2 floats per lane);
-//   * the A tile is staged once through LDS ([128][K + 4] floats: the +4 pad
-//     makes the ds_read_b128 fragment reads conflict-free) and read by all
-//     four waves;
-//   * K order inside the MFMA chain is permuted (lane half h takes
-//     k = s + h K/2) so one ds_read_b128 feeds four consecutive k-steps.
+// gradient dX = dH W^T of a layer (B = W^T through strides).
+//   * B (at most 128 x 128) is staged ONCE per workgroup into LDS as B^T
+//     ([n][K + 4]), so a lane reads the 4 consecutive k of its column with one
+//     ds_read_b128 (K order inside the MFMA chain is permuted: lane half h
+//     takes k = m + h K/2, identically for A and B);
+//   * every wave streams its own 32-row subtiles of A straight from HBM into
+//     registers -- no LDS staging of A, no barriers, no re-reads: lane
+//     (h, r) reads row r's k-range [h K/2, h K/2 + K/2) as float4s;
+//   * A arrives in bursts of 8 float4 per lane (one 128-byte line), issued
+//     back to back so the line's 8 requests meet in L1, double-buffered in
+//     registers: the next burst loads while the current one feeds up to 128
+//     v_mfma_f32_32x32x2_f32;
+//   * persistent workgroups of 8 waves (grid = resident capacity).
 // Epilogue modes:
 //   EPI_STORE  C = acc
 //   EPI_RELU   (the previous layer's ReLU backward fused into dX):
-//              C = Z > 0 ? acc : 0, and per-tile column sums of C written to
-//              colsum_partial[tile][N] (the bias gradient, folded in tile order
-//              by mgcn_colsum_finish -- deterministic).
-// Roofline: 2 M K N FLOP on 157 TF fp32 MFMA vs 4 M (K + N) bytes;
-// at K = N = 128 the MFMA side is the bound (0.21 ms vs 0.13 ms at 8 TB/s).
+//              C = Z > 0 ? acc : 0, and per-workgroup column sums of C written
+//              to colsum_partial[workgroup][N] (the bias gradient, folded in
+//              workgroup order by colsum_fold_kernel -- deterministic).
+// Roofline: 2 M K N FLOP on 157 TF fp32 MFMA vs 4 M (K + N) bytes (+ 4 M N
+// for Z); at K = N = 128: 0.21 ms MFMA vs 0.13 ms (0.19 with Z) at 8 TB/s.
 
 namespace mgcn {
 namespace {
 
-constexpr int kNNRows = 128;  // rows of A per workgroup
+constexpr int kNNWaves = 8;  // waves per workgroup
+constexpr int kNNThreads = 64 * kNNWaves;
+constexpr int kNNMaxGrid = 1024;  // colsum partial slots
 constexpr int EPI_STORE = 0, EPI_RELU = 1;
 
-// NTP = 32-column tiles of N per workgroup (1, 2 or 4): wave w owns column
-// tile w % NTP and the 32-row subtiles t = w / NTP + j * (4 / NTP), so a small
-// N (F = 32 layers, config 3) still keeps all four waves busy.
-template <int K, int EPI, int NTP>
-__global__ __launch_bounds__(256, 2) void gemm_nn_kernel(
+template <int K, int NT, int EPI>
+__global__ __launch_bounds__(kNNThreads, 2) void gemm_nn_kernel(
     const float *__restrict__ A, int64_t lda, const float *__restrict__ B, int64_t sbk,
     int64_t sbn, float *__restrict__ C, int64_t ldc, int64_t M, int N,
     const float *__restrict__ Z, int64_t ldz, float *__restrict__ colsum_partial) {
-  constexpr int LDA = K + 4;
-  constexpr int KH = K / 2;  // k-steps per lane half
-  constexpr int V4_PER_ROW = K / 4;
-  constexpr int V4_PER_THREAD = kNNRows * V4_PER_ROW / 256;
-  // register prefetch of the next A tile, except where it would spill (the
-  // K = 128 ReLU epilogue needs those registers; the co-resident workgroup
-  // still overlaps its loads with this one's MFMAs)
-  constexpr bool kPrefetch = true;
-  __shared__ __attribute__((aligned(16))) float sA[kNNRows * LDA];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
+  constexpr int KH = K / 2;              // k per lane half
+  constexpr int S4 = KH / 4;             // float4 steps per 32-row subtile
+  constexpr int GS = (K == 32) ? 2 : 1;  // subtiles per unit (>= 8 steps per unit)
+  constexpr int S = GS * S4;             // float4 steps per unit
+  constexpr int LDB = K + 4;             // B^T row stride in LDS (floats)
+  __shared__ __attribute__((aligned(16))) float BT[NT * 32 * LDB];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 5, lc = lane & 31;
-  constexpr int SUBS = 4 / NTP;  // waves sharing a column tile
-  const int mg = wave / NTP;     // first 32-row subtile of this wave
-  const int n = (wave % NTP) * 32 + lc;  // output column of this lane
-  const bool n_ok = n < N;
-  const int64_t n_tiles = (M + kNNRows - 1) / kNNRows;
 
-  // B slab of this wave's 32 columns: b[s] = B[k = s + h*KH][n] (whole kernel)
-  float b[KH];
-#pragma unroll
-  for (int s = 0; s < KH; ++s)
-    b[s] = n_ok ? B[(int64_t)(s + h * KH) * sbk + (int64_t)n * sbn] : 0.0f;
+  // B^T into LDS, columns past N zero
+  for (int idx = tid; idx < NT * 32 * (K / 4); idx += kNNThreads) {
+    const int n = idx / (K / 4), k4 = (idx % (K / 4)) * 4;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (n < N) {
+      const float *bp = B + (int64_t)k4 * sbk + (int64_t)n * sbn;
+      v.x = bp[0];
+      v.y = bp[sbk];
+      v.z = bp[2 * sbk];
+      v.w = bp[3 * sbk];
+    }
+    *reinterpret_cast<float4 *>(&BT[n * LDB + k4]) = v;
+  }
+  __syncthreads();
 
-  // register prefetch of one A tile: thread t holds float4 #(t + 256 i)
-  float4 pre[V4_PER_THREAD];
-  auto fetch = [&](int64_t tile) {
-    const int64_t m0 = tile * kNNRows;
+  const int64_t n_sub = (M + 31) / 32;
+  const int64_t n_units = (n_sub + GS - 1) / GS;
+  const int64_t wstride = (int64_t)gridDim.x * kNNWaves;
+  // A is read in BURSTS of 8 float4 steps = one 128-byte line per lane,
+  // issued back to back (the 8 requests of a line meet in L1), into two
+  // register banks: burst t + 1 loads while burst t feeds the MFMAs.
+  constexpr int NB = S / 8;  // bursts per unit: 2 (K = 128) or 1 (K = 64; K = 32: 2 subtiles)
+  auto load_burst = [&](int64_t unit, int part, float4 (&bk)[8]) {
+    const float4 *rp[GS];
 #pragma unroll
-    for (int i = 0; i < V4_PER_THREAD; ++i) {
-      const int idx = threadIdx.x + 256 * i;
-      const int r = idx / V4_PER_ROW, c4 = idx % V4_PER_ROW;
-      pre[i] = (m0 + r < M) ? *reinterpret_cast<const float4 *>(A + (m0 + r) * lda + c4 * 4)
-                            : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int g = 0; g < GS; ++g) {
+      int64_t row = (unit * GS + g) * 32 + lc;
+      row = row < M ? row : M - 1;  // the tail's rows past M: loaded, never stored
+      rp[g] = reinterpret_cast<const float4 *>(A + row * lda + h * KH);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int st = part * 8 + i;
+      bk[i] = rp[st / S4][st % S4];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  const float *bt_lane = &BT[lc * LDB + h * KH];
+  float csum[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) csum[j] = 0.0f;
+  f32x16 acc[GS][NT];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int g = 0; g < GS; ++g)
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[g][j][r] = 0.0f;
+  };
+  auto compute_burst = [&](const float4 (&bk)[8], int part) {
+    float4 bcur[NT], bnxt[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+      bcur[j] = *reinterpret_cast<const float4 *>(bt_lane + j * 32 * LDB + 4 * ((part * 8) % S4));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int st = part * 8 + i;
+      const int sub = st / S4;
+      if (i + 1 < 8) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          bnxt[j] = *reinterpret_cast<const float4 *>(bt_lane + j * 32 * LDB + 4 * ((st + 1) % S4));
+      }
+      const float4 a = bk[i];
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        acc[sub][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, bcur[j].x, acc[sub][j], 0, 0, 0);
+        acc[sub][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, bcur[j].y, acc[sub][j], 0, 0, 0);
+        acc[sub][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, bcur[j].z, acc[sub][j], 0, 0, 0);
+        acc[sub][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, bcur[j].w, acc[sub][j], 0, 0, 0);
+      }
+#pragma unroll
+      for (int j = 0; j < NT; ++j) bcur[j] = bnxt[j];
     }
   };
-  float csum = 0.0f;
-  int64_t tile = blockIdx.x;
-  if (kPrefetch && tile < n_tiles) fetch(tile);
-  for (; tile < n_tiles; tile += gridDim.x) {
-    const int64_t m0 = tile * kNNRows;
-    if (!kPrefetch) fetch(tile);
-    __syncthreads();  // previous tile's LDS reads are done
+  // epilogue; C/D map: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 h.
+  // Addresses = lane pointer + wave-uniform row offset; full subtiles store
+  // unguarded, the M tail per element.
+  auto epilogue = [&](int64_t unit) {
 #pragma unroll
-    for (int i = 0; i < V4_PER_THREAD; ++i) {
-      const int idx = threadIdx.x + 256 * i;
-      const int r = idx / V4_PER_ROW, c4 = idx % V4_PER_ROW;
-      *reinterpret_cast<float4 *>(&sA[r * LDA + c4 * 4]) = pre[i];
-    }
-    __syncthreads();
-    if (kPrefetch && tile + gridDim.x < n_tiles) fetch(tile + gridDim.x);  // overlaps MFMAs
-
-    // one 32-row subtile at a time: 16 accumulator registers, fragment reads
-    // double-buffered one step ahead, epilogue of subtile t overlapping the
-    // MFMAs of subtile t + 1.  C/D map: col = lane & 31 (-> n),
-    // row = (r & 3) + 8 (r >> 2) + 4 h.
-    const bool full = (m0 + kNNRows <= M) && n_ok;
+    for (int g = 0; g < GS; ++g) {
+      const int64_t r0 = (unit * GS + g) * 32;
+      const bool rows_full = r0 + 32 <= M;  // wave-uniform
 #pragma unroll
-    for (int j = 0; j < NTP; ++j) {
-      const int t = mg + j * SUBS;
-      const float *arow = &sA[(t * 32 + lc) * LDA + h * KH];
-      f32x16 acc;
+      for (int j = 0; j < NT; ++j) {
+        const int n = j * 32 + lc;
+        const bool n_ok = n < N;
+        float *cp = C + (r0 + 4 * h) * ldc + n;
+        const float *zp = (EPI == EPI_RELU) ? Z + (r0 + 4 * h) * ldz + n : nullptr;
+        if (rows_full) {
+          if constexpr (EPI == EPI_RELU) {
+            float zv[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-      float4 cur = *reinterpret_cast<const float4 *>(arow);
+            for (int r = 0; r < 16; ++r) zv[r] = n_ok ? zp[((r & 3) + 8 * (r >> 2)) * ldz] : 0.0f;
 #pragma unroll
-      for (int s4 = 0; s4 < KH; s4 += 4) {
-        float4 nxt = cur;
-        if (s4 + 4 < KH) nxt = *reinterpret_cast<const float4 *>(arow + s4 + 4);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.x, b[s4 + 0], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.y, b[s4 + 1], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.z, b[s4 + 2], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.w, b[s4 + 3], acc, 0, 0, 0);
-        cur = nxt;
-      }
-      const int64_t rbase = m0 + t * 32 + 4 * h;
-      if (full) {  // unguarded: guarded loads would serialise (one wait per element)
-        if constexpr (EPI == EPI_RELU) {
-          float zv[16];
+            for (int r = 0; r < 16; ++r) {
+              const float v = (zv[r] > 0.0f) ? acc[g][j][r] : 0.0f;
+              if (n_ok) {
+                csum[j] = __fadd_rn(csum[j], v);
+                cp[((r & 3) + 8 * (r >> 2)) * ldc] = v;
+              }
+            }
+          } else {
+            if (n_ok) {
 #pragma unroll
-          for (int r = 0; r < 16; ++r) zv[r] = Z[(rbase + (r & 3) + 8 * (r >> 2)) * ldz + n];
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const float v = (zv[r] > 0.0f) ? acc[r] : 0.0f;
-            csum = __fadd_rn(csum, v);
-            C[(rbase + (r & 3) + 8 * (r >> 2)) * ldc + n] = v;
+              for (int r = 0; r < 16; ++r) cp[((r & 3) + 8 * (r >> 2)) * ldc] = acc[g][j][r];
+            }
           }
         } else {
 #pragma unroll
-          for (int r = 0; r < 16; ++r) C[(rbase + (r & 3) + 8 * (r >> 2)) * ldc + n] = acc[r];
-        }
-      } else {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int64_t row = rbase + (r & 3) + 8 * (r >> 2);
-          if (row < M && n_ok) {
-            float v = acc[r];
-            if constexpr (EPI == EPI_RELU) {
-              v = (Z[row * ldz + n] > 0.0f) ? v : 0.0f;
-              csum = __fadd_rn(csum, v);
+          for (int r = 0; r < 16; ++r) {
+            const int rr = (r & 3) + 8 * (r >> 2);
+            if (n_ok && r0 + 4 * h + rr < M) {
+              float v = acc[g][j][r];
+              if constexpr (EPI == EPI_RELU) {
+                v = (zp[rr * ldz] > 0.0f) ? v : 0.0f;
+                csum[j] = __fadd_rn(csum[j], v);
+              }
+              cp[rr * ldc] = v;
             }
-            C[row * ldc + n] = v;
           }
         }
       }
     }
+  };
+
+  float4 bank0[8], bank1[8];
+  int64_t u = (int64_t)blockIdx.x * kNNWaves + wave;
+  if (u < n_units) load_burst(u, 0, bank0);
+  if constexpr (NB == 2) {
+    for (; u < n_units; u += wstride) {
+      const int64_t un = (u + wstride < n_units) ? u + wstride : u;  // last: harmless reload
+      zero_acc();
+      load_burst(u, 1, bank1);
+      compute_burst(bank0, 0);
+      load_burst(un, 0, bank0);
+      compute_burst(bank1, 1);
+      epilogue(u);
+    }
+  } else {
+    for (; u < n_units; u += 2 * wstride) {
+      const int64_t u1 = u + wstride;
+      load_burst(u1 < n_units ? u1 : u, 0, bank1);
+      zero_acc();
+      compute_burst(bank0, 0);
+      epilogue(u);
+      if (u1 >= n_units) break;
+      const int64_t u2 = u + 2 * wstride;
+      load_burst(u2 < n_units ? u2 : u1, 0, bank0);
+      zero_acc();
+      compute_burst(bank1, 0);
+      epilogue(u1);
+    }
   }
   if constexpr (EPI == EPI_RELU) {
-    // fold the waves that share a column tile, in subtile order (deterministic)
-    __shared__ float red[4][32];
-    const float both = __fadd_rn(csum, __shfl_xor(csum, 32, 64));
-    if (h == 0) red[wave][lc] = both;
+    // fold the lane halves, then the waves in wave order (deterministic)
+    __syncthreads();  // BT is free
+    float *red = BT;  // [kNNWaves][NT * 32]
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const float both = __fadd_rn(csum[j], __shfl_xor(csum[j], 32, 64));
+      if (h == 0) red[wave * NT * 32 + j * 32 + lc] = both;
+    }
     __syncthreads();
-    if (wave < NTP && h == 0 && n_ok) {
-      float v = red[wave][lc];
-      for (int g = 1; g < SUBS; ++g) v = __fadd_rn(v, red[g * NTP + wave][lc]);
+    for (int n = tid; n < N; n += kNNThreads) {
+      float v = red[n];
+      for (int w = 1; w < kNNWaves; ++w) v = __fadd_rn(v, red[w * NT * 32 + n]);
       colsum_partial[(int64_t)blockIdx.x * N + n] = v;
     }
   }
 }
 
-int nn_grid(int64_t M) {
-  const int64_t tiles = (M + kNNRows - 1) / kNNRows;
-  return (int)(tiles < 512 ? (tiles > 0 ? tiles : 1) : 512);  // 2 persistent WGs per CU
+template <int K, int NT, int EPI>
+int nn_blocks(int64_t M) {
+  // resident capacity of this instantiation (queried once), capped by work
+  static int per_cu = 0;
+  if (per_cu == 0) {
+    int b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gemm_nn_kernel<K, NT, EPI>, kNNThreads,
+                                                     0) != hipSuccess || b < 1)
+      b = 1;
+    per_cu = b;
+  }
+  constexpr int GS = (K == 32) ? 2 : 1;
+  const int64_t units = ((M + 31) / 32 + GS - 1) / GS;
+  int64_t g = (units + kNNWaves - 1) / kNNWaves;
+  const int64_t cap = 256LL * per_cu;
+  if (g > cap) g = cap;
+  if (g > kNNMaxGrid) g = kNNMaxGrid;
+  return (int)(g > 0 ? g : 1);
+}
+
+template <int K, int NT>
+int launch_nn_nt(int64_t M, int N, const float *A, int64_t lda, const float *B, int64_t sbk,
+                 int64_t sbn, float *C, int64_t ldc, int epi, const float *Z, int64_t ldz,
+                 float *partial, int *grid_out, hipStream_t s) {
+  if (epi == EPI_RELU) {
+    const int g = nn_blocks<K, NT, EPI_RELU>(M);
+    hipLaunchKernelGGL((gemm_nn_kernel<K, NT, EPI_RELU>), dim3(g), dim3(kNNThreads), 0, s, A,
+                       lda, B, sbk, sbn, C, ldc, M, N, Z, ldz, partial);
+    *grid_out = g;
+  } else {
+    const int g = nn_blocks<K, NT, EPI_STORE>(M);
+    hipLaunchKernelGGL((gemm_nn_kernel<K, NT, EPI_STORE>), dim3(g), dim3(kNNThreads), 0, s, A,
+                       lda, B, sbk, sbn, C, ldc, M, N, Z, ldz, partial);
+    *grid_out = g;
+  }
+  return check_launch("gemm_nn_kernel");
 }
 
 template <int K>
 int launch_nn(int64_t M, int N, const float *A, int64_t lda, const float *B, int64_t sbk,
               int64_t sbn, float *C, int64_t ldc, int epi, const float *Z, int64_t ldz,
-              float *partial, hipStream_t s) {
-  const unsigned blocks = (unsigned)nn_grid(M);
-#define MGCN_NN(NTP_)                                                                          \
-  if (epi == EPI_RELU)                                                                        \
-    hipLaunchKernelGGL((gemm_nn_kernel<K, EPI_RELU, NTP_>), dim3(blocks), dim3(256), 0, s, A, \
-                       lda, B, sbk, sbn, C, ldc, M, N, Z, ldz, partial);                      \
-  else                                                                                        \
-    hipLaunchKernelGGL((gemm_nn_kernel<K, EPI_STORE, NTP_>), dim3(blocks), dim3(256), 0, s, A,\
-                       lda, B, sbk, sbn, C, ldc, M, N, Z, ldz, partial);
-  // NTP = 1 only where it compiles without spills (K = 32, N <= 32: the
-  // config-3 F = 32 layers); elsewhere idle column tiles are cheaper than spills
-  if constexpr (K == 32) {
-    if (N <= 32) {
-      MGCN_NN(1)
-    } else {
-      MGCN_NN(4)
-    }
-  } else {
-    MGCN_NN(4)
-  }
-#undef MGCN_NN
-  return check_launch("gemm_nn_kernel");
+              float *partial, int *grid_out, hipStream_t s) {
+  const int nt = (N + 31) / 32;
+  if (nt == 1) return launch_nn_nt<K, 1>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, ldz, partial, grid_out, s);
+  if (nt == 2) return launch_nn_nt<K, 2>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, ldz, partial, grid_out, s);
+  if (nt == 3) return launch_nn_nt<K, 3>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, ldz, partial, grid_out, s);
+  return launch_nn_nt<K, 4>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, ldz, partial, grid_out, s);
 }
 
 __global__ __launch_bounds__(256) void colsum_fold_kernel(const float *__restrict__ partial,
@@ -462,7 +544,8 @@ extern "C" int mgcn_gemm_nn_supported(int32_t K, int32_t N) {
 }
 
 extern "C" size_t mgcn_gemm_nn_workspace_bytes(int64_t M, int32_t N) {
-  return align_up((size_t)nn_grid(M) * (size_t)(N > 0 ? N : 1) * 4, 256);
+  (void)M;
+  return align_up((size_t)kNNMaxGrid * (size_t)(N > 0 ? N : 1) * 4, 256);
 }
 
 extern "C" int mgcn_gemm_nn(int64_t M, int32_t K, int32_t N, const float *A, int64_t lda,
@@ -492,15 +575,15 @@ extern "C" int mgcn_gemm_nn(int64_t M, int32_t K, int32_t N, const float *A, int
     partial = static_cast<float *>(workspace);
   }
   int rc;
+  int grid = 0;
   if (K == 32)
-    rc = launch_nn<32>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, ldz, partial, s);
+    rc = launch_nn<32>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, ldz, partial, &grid, s);
   else if (K == 64)
-    rc = launch_nn<64>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, ldz, partial, s);
+    rc = launch_nn<64>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, ldz, partial, &grid, s);
   else
-    rc = launch_nn<128>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, ldz, partial, s);
+    rc = launch_nn<128>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, ldz, partial, &grid, s);
   if (rc || epi != EPI_RELU) return rc;
-  const int64_t parts = nn_grid(M);
-  hipLaunchKernelGGL(colsum_fold_kernel, dim3((N + 63) / 64), dim3(256), 0, s, partial, parts, N,
-                     colsum);
+  hipLaunchKernelGGL(colsum_fold_kernel, dim3((N + 63) / 64), dim3(256), 0, s, partial,
+                     (int64_t)grid, N, colsum);
   return check_launch("colsum_fold_kernel");
 }
