@@ -71,7 +71,9 @@ const char *mgcn_last_error(void);
  *   "heavy_block" : threads per giant-row workgroup, 256/512/1024 (1024)
  *   "heavy_mid_lds_kb": LDS per (non-giant) heavy-row workgroup (default 40)
  *   "heavy_giant_thr" : degree above which a heavy row is giant, read by
- *                   mgcn_row_schedule (default 512)                        */
+ *                   mgcn_row_schedule (default 512)
+ *   "gemm_tn_variant": LDS-staged dW kernel chunk depth (M, N multiples of
+ *                   128): 0 = 64 rows (default), 1 = 32, 2 = 16             */
 int mgcn_set_option(const char *name, int value);
 
 /* ------------------------------------------------------------------ graph */

@@ -113,6 +113,117 @@ __global__ __launch_bounds__(256) void gemm_tn_partial_kernel(
       }
 }
 
+// LDS-staged variant for M, N multiples of 128 (the F = 128 layers).  The
+// per-lane dword loads of gemm_tn_partial_kernel are fragment-shaped (every
+// wave-instruction 2 x 128 B) and keep the texture-address path busy at full
+// MFMA rate; here each 32-row chunk of both operands moves in 1-KiB
+// global_load_lds_dwordx4 instructions (2 rows of 512 B, lane-linear image)
+// into one of two LDS buffers, and the MFMA fragments come from LDS with
+// ds_read_b32.  One barrier per chunk; the next chunk's loads are issued
+// right after it, so they run under the current chunk's MFMAs (2 BK per
+// wave).  K order inside a chunk is permuted (lane half h takes rows
+// h BK/2 .. (h + 1) BK/2 - 1): the same products per output, summed in a
+// different order.
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+template <int BK, int WPS>
+__global__ __launch_bounds__(256, WPS) void gemm_tn_lds_kernel(
+    const float *__restrict__ A, int64_t lda, const float *__restrict__ B, int64_t ldb,
+    int64_t K, int M, int N, int64_t k_per_split, int tiles_n, float *__restrict__ partial) {
+  constexpr int kTnChunkFloats = BK * kTile;  // one operand's chunk image
+  constexpr int HS = BK / 2;                  // k-steps per chunk
+  __shared__ __attribute__((aligned(16))) float lds[2][2][kTnChunkFloats];  // [buf][A/B]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wi = wave >> 1, wj = wave & 1;
+  const int tile_m = blockIdx.x / tiles_n, tile_n = blockIdx.x % tiles_n;
+  const int64_t kb = (int64_t)blockIdx.y * k_per_split;
+  const int64_t ke = (kb + k_per_split < K) ? kb + k_per_split : K;
+  const int h = lane >> 5, lc = lane & 31;
+  // glds source: lane -> row pair half (lane >> 5), 4 floats at column 4 (lane & 31)
+  const int g_row = lane >> 5, g_col = (lane & 31) * 4;
+  const float *a_src = A + (int64_t)tile_m * kTile + g_col;
+  const float *b_src = B + (int64_t)tile_n * kTile + g_col;
+
+  auto issue = [&](int64_t k0, int buf) {
+    // wave w moves row pairs w, w + 4, ... of both operands
+#pragma unroll
+    for (int q = 0; q < BK / 8; ++q) {
+      const int pair = wave + 4 * q;
+      int64_t row = k0 + 2 * pair + g_row;
+      row = row < K ? row : K - 1;  // past the end: a valid row, masked in compute
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a_src + row * lda),
+                                       (lds_void_t *)(&lds[buf][0][pair * 2 * kTile]), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(b_src + row * ldb),
+                                       (lds_void_t *)(&lds[buf][1][pair * 2 * kTile]), 16, 0, 0);
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][s][r] = 0.0f;
+
+  auto compute = [&](int buf, int valid) {  // valid: rows of this chunk below ke
+    const float *la = &lds[buf][0][wi * 64 + lc];
+    const float *lb = &lds[buf][1][wj * 64 + lc];
+    float a[2], b[2], na[2], nb[2];
+    auto frag = [&](int m, float (&x)[2], float (&y)[2]) {
+      const int k = m + HS * h;
+      const bool ok = k < valid;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        x[t] = ok ? la[k * kTile + 32 * t] : 0.0f;
+        y[t] = ok ? lb[k * kTile + 32 * t] : 0.0f;
+      }
+    };
+    frag(0, a, b);
+#pragma unroll
+    for (int m = 0; m < HS; ++m) {
+      if (m + 1 < HS) frag(m + 1, na, nb);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+          acc[t][s2] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[t], b[s2], acc[t][s2], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        a[t] = na[t];
+        b[t] = nb[t];
+      }
+    }
+  };
+
+  const int64_t nchunks = (ke - kb + BK - 1) / BK;
+  if (nchunks > 0) issue(kb, 0);
+  for (int64_t c = 0; c < nchunks; ++c) {
+    const int64_t k0 = kb + c * BK;
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's loads of chunk c have landed
+    __syncthreads();                // everyone's have; buffer (c + 1) & 1 is free
+    if (c + 1 < nchunks) issue(k0 + BK, (int)((c + 1) & 1));
+    const int64_t left = ke - k0;
+    if (left >= BK)
+      compute((int)(c & 1), BK);
+    else
+      compute((int)(c & 1), (int)left);
+  }
+
+  float *slab = partial + (int64_t)blockIdx.y * M * N;
+  const int i0 = tile_m * kTile + wi * 64, j0 = tile_n * kTile + wj * 64;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = i0 + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        slab[(int64_t)row * N + j0 + s2 * 32 + lc] = acc[t][s2][r];
+      }
+}
+
 // Small C (M, N <= 32: F = 32 layers and the 32 -> 2 projection of config 3):
 // one 32 x 32 MFMA tile per workgroup; the four waves take interleaved
 // k-steps of the split's K range (wave-level split-K) and their accumulators
@@ -185,10 +296,20 @@ __global__ __launch_bounds__(256) void gemm_reduce_kernel(const float *__restric
   }
 }
 
-int gemm_splits(int64_t K, int tiles) {
-  // one resident round: 256 CUs x 3 workgroups (3 waves/SIMD at 134 VGPRs);
-  // at least 64 rows of K per split (partials: splits x 64 KB per tile)
-  int64_t s = 768 / (tiles > 0 ? tiles : 1);
+bool tn_lds(int M, int N) { return M % kTile == 0 && N % kTile == 0; }
+
+// LDS-staged dW variants (mgcn_set_option "gemm_tn_variant"; measured at
+// K = 1M, M = N = 128: 0.321 / 0.335 / 0.337 ms): 0 = BK 64, one workgroup
+// per CU; 1 = BK 32, two; 2 = BK 16, three
+int g_tn_lds_variant = 0;
+int tn_lds_wgs() { return g_tn_lds_variant == 1 ? 2 : g_tn_lds_variant == 2 ? 3 : 1; }
+
+int gemm_splits(int64_t K, int M, int N) {
+  // one resident round: 256 CUs x 3 workgroups (3 waves/SIMD at 134 VGPRs),
+  // or x 2 for the LDS-staged kernel (64 KB of LDS each); at least 64 rows of
+  // K per split (partials: splits x 64 KB per tile)
+  const int tiles = ((M + kTile - 1) / kTile) * ((N + kTile - 1) / kTile);
+  int64_t s = (tn_lds(M, N) ? 256 * tn_lds_wgs() : 768) / (tiles > 0 ? tiles : 1);
   int64_t max_s = (K + 63) / 64;
   if (s > max_s) s = max_s;
   if (s < 1) s = 1;
@@ -196,13 +317,19 @@ int gemm_splits(int64_t K, int tiles) {
 }
 
 }  // namespace
+
+int gemm_set_tn_variant(int value) {
+  if (value < 0 || value > 2) return MGCN_EINVAL;
+  g_tn_lds_variant = value;
+  return MGCN_OK;
+}
+
 }  // namespace mgcn
 
 using namespace mgcn;
 
 extern "C" size_t mgcn_gemm_tn_workspace_bytes(int64_t K, int32_t M, int32_t N) {
-  const int tiles = ((M + kTile - 1) / kTile) * ((N + kTile - 1) / kTile);
-  return align_up((size_t)gemm_splits(K, tiles) * (size_t)M * (size_t)N * sizeof(float), 256);
+  return align_up((size_t)gemm_splits(K, M, N) * (size_t)M * (size_t)N * sizeof(float), 256);
 }
 
 extern "C" int mgcn_gemm_tn(int64_t K, int32_t M, int32_t N, const float *A, int64_t lda,
@@ -221,20 +348,33 @@ extern "C" int mgcn_gemm_tn(int64_t K, int32_t M, int32_t N, const float *A, int
   }
   MGCN_REQUIRE(A && B && lda >= M && ldb >= N, "mgcn_gemm_tn: bad A/B");
   const int tiles_m = (M + kTile - 1) / kTile, tiles_n = (N + kTile - 1) / kTile;
-  const int splits = gemm_splits(K, tiles_m * tiles_n);
+  const int splits = gemm_splits(K, M, N);
   const size_t need = mgcn_gemm_tn_workspace_bytes(K, M, N);
   if (workspace == nullptr || workspace_bytes < need) {
     set_error("mgcn_gemm_tn: workspace %zu < %zu", workspace_bytes, need);
     return MGCN_EWORKSPACE;
   }
   int64_t kps = (K + splits - 1) / splits;
-  kps = (kps + 2 * kU - 1) / (2 * kU) * (2 * kU);
+  kps = (kps + 63) / 64 * 64;  // whole chunks of every variant (and whole kU groups)
   const int used = (int)((K + kps - 1) / kps);
   float *partial = static_cast<float *>(workspace);
   if (M <= 32 && N <= 32) {
     hipLaunchKernelGGL(gemm_tn_small_kernel, dim3(used), dim3(256), 0, s, A, lda, B, ldb, K, M, N,
                        kps, partial);
     if (int rc = check_launch("gemm_tn_small_kernel")) return rc;
+  } else if (tn_lds(M, N) && reinterpret_cast<uintptr_t>(A) % 16 == 0 &&
+             reinterpret_cast<uintptr_t>(B) % 16 == 0 && lda % 4 == 0 && ldb % 4 == 0) {
+    const dim3 grid(tiles_m * tiles_n, used);
+    if (g_tn_lds_variant == 1)
+      hipLaunchKernelGGL((gemm_tn_lds_kernel<32, 2>), grid, dim3(256), 0, s, A, lda, B, ldb, K, M,
+                         N, kps, tiles_n, partial);
+    else if (g_tn_lds_variant == 2)
+      hipLaunchKernelGGL((gemm_tn_lds_kernel<16, 3>), grid, dim3(256), 0, s, A, lda, B, ldb, K, M,
+                         N, kps, tiles_n, partial);
+    else
+      hipLaunchKernelGGL((gemm_tn_lds_kernel<64, 1>), grid, dim3(256), 0, s, A, lda, B, ldb, K, M,
+                         N, kps, tiles_n, partial);
+    if (int rc = check_launch("gemm_tn_lds_kernel")) return rc;
   } else {
     hipLaunchKernelGGL(gemm_tn_partial_kernel, dim3(tiles_m * tiles_n, used), dim3(256), 0, s, A,
                        lda, B, ldb, K, M, N, kps, tiles_n, partial);

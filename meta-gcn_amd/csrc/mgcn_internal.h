@@ -55,4 +55,7 @@ inline unsigned grid_for(int64_t work_items, int block) {
   return static_cast<unsigned>(g);
 }
 
+// mgcn_set_option("gemm_tn_variant") -> gemm.hip
+int gemm_set_tn_variant(int value);
+
 }  // namespace mgcn

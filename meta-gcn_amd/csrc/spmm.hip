@@ -808,6 +808,10 @@ extern "C" int mgcn_set_option(const char *name, int value) {
     g_giant_thr = value;
     return MGCN_OK;
   }
+  if (n == "gemm_tn_variant") {
+    MGCN_REQUIRE(value >= 0 && value <= 2, "gemm_tn_variant must be 0, 1 or 2");
+    return gemm_set_tn_variant(value);
+  }
   if (n == "heavy_side_stream") {
     MGCN_REQUIRE(value == 0 || value == 1, "heavy_side_stream must be 0 or 1");
     g_heavy_side = value;
