@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define MGCN_ABI_VERSION 3
+#define MGCN_ABI_VERSION 4
 
 /* return codes */
 #define MGCN_OK 0
@@ -145,7 +145,9 @@ int mgcn_edge_norm(int64_t n_rows, int64_t nnz, const int64_t *rowptr, const int
  *         argmax[i, f] = eid of the winning edge, -1 where the output was fill
  *   then  y = acc (+ bias[f]) ; if relu: y = y < 0 ? 0 : y
  * w may be NULL (unweighted).  H rows have stride ldh floats, Y rows ldy.
- * argmax: int32 [n_rows, F] (stride F), required for MAX, ignored otherwise.
+ * argmax: int32 [n_rows, F] (stride F) for MAX, ignored otherwise; and/or
+ * win_mask (see mgcn_max_mask): MAX also writes every edge's winner bits at
+ * its slot (argmax may then be NULL).
  * No floating-point contraction: products and sums are rounded separately,
  * in edge order, exactly as the reference's mul + scatter_add sequence.
  */
@@ -153,14 +155,16 @@ int mgcn_spmm_fwd(int64_t n_rows, int32_t F, const int64_t *rowptr,
                   const int32_t *col, const int32_t *eid, const float *w,
                   const float *H, int64_t ldh, float *Y, int64_t ldy,
                   int reduce, const float *bias, int relu, int32_t *argmax,
-                  const int32_t *order, int64_t n_heavy, int64_t n_giant, void *stream);
+                  uint32_t *win_mask, const int32_t *order, int64_t n_heavy,
+                  int64_t n_giant, void *stream);
 
 /*
  * Adjoint aggregation over the transposed (src-grouped) CSR:
  *   dH_s = sum_{k in row s, in edge order} ( g_k * w_k ) [* row_scale_s]
  *   g_k  = dY[col_k, :]                         (SUM)
  *        = dY[col_k, :] / cnt[col_k]            (MEAN; cnt = max(in-deg, 1))
- *        = argmax[col_k, f] == eid_k ? dY : 0   (MAX)
+ *        = argmax[col_k, f] == eid_k ? dY : 0   (MAX; or bit f of the edge's
+ *                       win_mask word, found through slot_map = mgcn_slot_map)
  * row_scale (nullable) is the RW post-scale dinv[src] (gcn_base_models.py:218).
  * If accumulate != 0 the result is added to dH (dH += ...), else stored.
  */
@@ -168,7 +172,8 @@ int mgcn_spmm_bwd(int64_t n_rows, int32_t F, const int64_t *rowptr_t,
                   const int32_t *col_t, const int32_t *eid_t, const float *w_t,
                   const float *row_scale, const float *dY, int64_t lddy,
                   float *dH, int64_t lddh, int reduce, const float *cnt,
-                  const int32_t *argmax, int accumulate,
+                  const int32_t *argmax, const uint32_t *win_mask,
+                  const int32_t *slot_map, int accumulate,
                   const int32_t *order, int64_t n_heavy, int64_t n_giant, void *stream);
 
 /*
@@ -189,6 +194,25 @@ size_t mgcn_row_schedule_workspace_bytes(int64_t n_rows);
 int mgcn_row_schedule(int64_t n_rows, const int64_t *rowptr, int64_t heavy_thr, int32_t *order,
                       int64_t *n_heavy_out, int64_t *n_giant_out, void *workspace,
                       size_t workspace_bytes, void *stream);
+
+/*
+ * Max aggregation adjoint without the per-edge argmax gather (config 4 max).
+ * mgcn_max_mask: from the forward's argmax [n_rows, F], for every fwd row d
+ * and edge slot k of it, bit f of win_mask[k * ceil(F/32) + f/32] =
+ * (argmax[d, f] == eid[k]) -- the edges each output feature came from (16 B
+ * per edge at F = 128); mgcn_spmm_fwd writes the same bits itself when given
+ * win_mask.  mgcn_slot_map: slot_map[j] = the fwd slot of the edge in bwd
+ * slot j (eid / eid_t of the two views; workspace
+ * mgcn_slot_map_workspace_bytes).  mgcn_spmm_bwd(MAX, win_mask, slot_map)
+ * then reads one word per edge, issued with the dY gather instead of after a
+ * 4F-byte argmax row.  Same routing as argmax (torch_scatter 1.x scatter_max
+ * backward), same bits.
+ */
+size_t mgcn_slot_map_workspace_bytes(int64_t nnz);
+int mgcn_slot_map(int64_t nnz, const int32_t *eid, const int32_t *eid_t, int32_t *slot_map,
+                  void *workspace, size_t workspace_bytes, void *stream);
+int mgcn_max_mask(int64_t n_rows, int32_t F, const int64_t *rowptr, const int32_t *eid,
+                  const int32_t *argmax, uint32_t *win_mask, void *stream);
 
 /* ------------------------------------------------------------------ dense */
 

@@ -45,7 +45,8 @@ enum Mode : int {
   FWD_MAX = 1,
   BWD_SUM = 2,
   BWD_MEAN = 3,
-  BWD_MAX = 4,
+  BWD_MAX = 4,   // routed through argmax rows
+  BWD_MAXM = 5,  // routed through per-slot winner bits (win_mask)
 };
 
 struct SpmmArgs {
@@ -64,7 +65,10 @@ struct SpmmArgs {
   const float *row_scale;  // bwd RW post-scale, nullable
   const float *cnt;        // bwd MEAN: max(in-degree,1) per gathered row
   int32_t *argmax_out;     // fwd MAX
-  const int32_t *argmax_in;  // bwd MAX
+  const int32_t *argmax_in;  // bwd MAX (argmax routing), or:
+  const uint32_t *win_mask;  // bwd MAXM: winner bits per fwd slot ([nnz][ceil(F/32)])
+  const int32_t *slot_map;   // bwd MAXM: the fwd slot of every bwd slot
+  uint32_t *win_mask_out;    // fwd MAX (optional): winner bits of every fwd slot
   int mean;                // fwd: divide by max(deg,1)
   int relu;                // fwd
   int accumulate;          // bwd: Y += result
@@ -211,6 +215,7 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(const SpmmArgs a) {
           mc = a.col[beg + my];
           if (has_w) mw = a.w[beg + my];
           if constexpr (kNeedEid) me = a.eid[beg + my];
+          if constexpr (MODE == BWD_MAXM) me = a.slot_map[beg + my];  // fwd slot of this edge
           if constexpr (MODE == BWD_MEAN) mcnt = a.cnt[mc];
         }
         const int64_t rem = deg - e0;
@@ -229,12 +234,25 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(const SpmmArgs a) {
             const int kk = k & (G - 1);
             const int ck = bcast_i<G>(mc, gbase, kk);
             wk[u] = bcast_f<G>(mw, gbase, kk);
-            ek[u] = kNeedEid ? bcast_i<G>(me, gbase, kk) : 0;
+            ek[u] = (kNeedEid || MODE == BWD_MAXM) ? bcast_i<G>(me, gbase, kk) : 0;
             float cntk = 1.0f;
             if constexpr (MODE == BWD_MEAN) cntk = bcast_f<G>(mcnt, gbase, kk);
             ok[u] = (k < nb) && f_ok;
             const float *src = X + (int64_t)ck * a.ldx + f0;
-            if constexpr (MODE == BWD_MAX) {
+            if constexpr (MODE == BWD_MAXM) {
+              // dY row and the edge's winner bits (at its fwd slot) are loaded
+              // together -- no load waits on a test -- then selected
+#pragma unroll
+              for (int j = 0; j < VEC; ++j) xv[u].v[j] = 0.0f;
+              if (ok[u]) {
+                const int64_t W = (a.F + 31) >> 5;
+                const uint32_t word = a.win_mask[(int64_t)ek[u] * W + (f0 >> 5)];
+                const F32v<VEC> g = load_f<VEC>(src);
+                const uint32_t bits = word >> (f0 & 31);
+#pragma unroll
+                for (int j = 0; j < VEC; ++j) xv[u].v[j] = ((bits >> j) & 1u) ? g.v[j] : 0.0f;
+              }
+            } else if constexpr (MODE == BWD_MAX) {
               // route dY only through the (d, f) entries whose argmax is this edge
 #pragma unroll
               for (int j = 0; j < VEC; ++j) xv[u].v[j] = 0.0f;
@@ -283,6 +301,38 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(const SpmmArgs a) {
         }
       }
 
+      if constexpr (MODE == FWD_MAX) {
+        if (a.win_mask_out != nullptr) {
+          // winner bits of every edge of this row, at its own (fwd) slot: a
+          // second pass over the row's edge ids; each 32-bit word is OR-ed
+          // over its lanes (all lanes of the group take part)
+          int32_t winner[VEC];
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) winner[j] = (acc.v[j] == MGCN_MAX_FILL) ? -1 : arg.v[j];
+          const int64_t W = (a.F + 31) >> 5;
+          constexpr int LW = (32 / VEC) < G ? (32 / VEC) : G;  // lanes per word in a group
+          for (int64_t e0 = 0; e0 < maxdeg; e0 += G) {
+            const int64_t my = e0 + gl;
+            int32_t me = -1;
+            if (my < deg) me = a.eid[beg + my];
+            const int64_t rem = deg - e0;
+            const int nb = rem <= 0 ? 0 : (rem < G ? (int)rem : G);
+            const int64_t remw = maxdeg - e0;
+            const int nbmax = remw < G ? (int)remw : G;  // wave-uniform
+            for (int k = 0; k < nbmax; ++k) {
+              const int32_t ek = bcast_i<G>(me, gbase, k);
+              uint32_t v = 0;
+#pragma unroll
+              for (int j = 0; j < VEC; ++j) v |= (winner[j] == ek ? 1u : 0u) << j;
+              v <<= (f0 & 31);
+#pragma unroll
+              for (int off = 1; off < LW; off <<= 1) v |= __shfl_xor(v, off, 64);
+              if (k < nb && f_ok && (f0 & 31) == 0)
+                a.win_mask_out[(beg + e0 + k) * W + (f0 >> 5)] = v;
+            }
+          }
+        }
+      }
       if (!(row_ok && f_ok)) continue;
       float *dst = a.Y + row * a.ldy + f0;
       if constexpr (kFwd) {
@@ -303,7 +353,9 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(const SpmmArgs a) {
           acc.v[j] = y;
         }
         store_f<VEC>(dst, acc);
-        if constexpr (MODE == FWD_MAX) store_i<VEC>(a.argmax_out + row * a.F + f0, arg);
+        if constexpr (MODE == FWD_MAX) {
+          if (a.argmax_out != nullptr) store_i<VEC>(a.argmax_out + row * a.F + f0, arg);
+        }
       } else {
         if (a.row_scale != nullptr) {
           const float s = a.row_scale[row];
@@ -357,7 +409,8 @@ __global__ __launch_bounds__(HB) void spmm_heavy_kernel(const SpmmArgs a, int FC
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr bool kFwd = (MODE == FWD_SUM || MODE == FWD_MAX);
   constexpr bool kNeedEid = (MODE == FWD_MAX || MODE == BWD_MAX);
-  constexpr int kQ = HB >= 1024 ? (MODE == BWD_MAX ? 1 : 2) : 4;  // edge quads in flight / thread
+  constexpr bool kMaxBwd = (MODE == BWD_MAX || MODE == BWD_MAXM);
+  constexpr int kQ = HB >= 1024 ? (kMaxBwd ? 1 : 2) : 4;  // edge quads in flight / thread
   constexpr int kEpt = 4;  // metadata entries per producer thread (BE <= kEpt * producers)
   const int BEp = BE + 4;  // product row stride (BE % 16 == 0, so BEp / 4 is odd)
   int32_t *ring = reinterpret_cast<int32_t *>(smem + 2 * FC * BEp);  // [3][4][BE]
@@ -399,6 +452,7 @@ __global__ __launch_bounds__(HB) void spmm_heavy_kernel(const SpmmArgs a, int FC
           mcol[i] = a.col[slot];
           mw[i] = has_w ? a.w[slot] : 1.0f;
           if constexpr (kNeedEid) meid[i] = a.eid[slot];
+          if constexpr (MODE == BWD_MAXM) meid[i] = a.slot_map[slot];  // fwd slot
         }
       }
     };
@@ -413,7 +467,7 @@ __global__ __launch_bounds__(HB) void spmm_heavy_kernel(const SpmmArgs a, int FC
         if (k < nb) {
           Col[k] = mcol[i];
           Wt[k] = mw[i];
-          if constexpr (kNeedEid) Eid[k] = meid[i];
+          if constexpr (kNeedEid || MODE == BWD_MAXM) Eid[k] = meid[i];
           if constexpr (MODE == BWD_MEAN) Cnt[k] = a.cnt[mcol[i]];
         }
       }
@@ -441,9 +495,19 @@ __global__ __launch_bounds__(HB) void spmm_heavy_kernel(const SpmmArgs a, int FC
               for (int e = 0; e < 4; ++e) {
                 if (4 * g + e < nb) {
                   x[u][e] = load_f<VEC>(xs + (int64_t)cols.v[e] * a.ldx);
-                  if constexpr (MODE == BWD_MAX)
-                    am[u][e] = load_i<VEC>(a.argmax_in + (int64_t)cols.v[e] * a.F + f0 +
-                                           c_first * VEC);
+                  if constexpr (kMaxBwd) {
+                    if constexpr (MODE == BWD_MAXM) {  // winner flags of this edge (1 / 0)
+                      const int64_t W = (a.F + 31) >> 5;
+                      const int f = f0 + c_first * VEC;
+                      const int32_t fslot = Eid[4 * g + e];  // ring holds the fwd slot
+                      const uint32_t bits = a.win_mask[(int64_t)fslot * W + (f >> 5)] >> (f & 31);
+#pragma unroll
+                      for (int q = 0; q < VEC; ++q) am[u][e].v[q] = (bits >> q) & 1u;
+                    } else {
+                      am[u][e] = load_i<VEC>(a.argmax_in + (int64_t)cols.v[e] * a.F + f0 +
+                                             c_first * VEC);
+                    }
+                  }
                 }
               }
             }
@@ -457,7 +521,11 @@ __global__ __launch_bounds__(HB) void spmm_heavy_kernel(const SpmmArgs a, int FC
               const F32v<4> w = load_f<4>(Wt + 4 * g);
               I32v<4> eid;
               F32v<4> cnt;
-              if constexpr (MODE == BWD_MAX) eid = load_i<4>(Eid + 4 * g);
+              if constexpr (MODE == BWD_MAXM) {
+                eid.v[0] = eid.v[1] = eid.v[2] = eid.v[3] = 1;  // flags: 1 = winner
+              } else if constexpr (MODE == BWD_MAX) {
+                eid = load_i<4>(Eid + 4 * g);
+              }
               if constexpr (MODE == BWD_MEAN) cnt = load_f<4>(Cnt + 4 * g);
               int off = 4 * g;
               asm volatile("" : "+v"(off));  // keep per-quad store offsets out of registers
@@ -467,7 +535,7 @@ __global__ __launch_bounds__(HB) void spmm_heavy_kernel(const SpmmArgs a, int FC
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                   float v = x[u][e].v[q];
-                  if constexpr (MODE == BWD_MAX) v = (am[u][e].v[q] == eid.v[e]) ? v : 0.0f;
+                  if constexpr (kMaxBwd) v = (am[u][e].v[q] == eid.v[e]) ? v : 0.0f;
                   if constexpr (MODE == BWD_MEAN) v = __fdiv_rn(v, cnt.v[e]);
                   o.v[e] = __fmul_rn(v, w.v[e]);
                 }
@@ -567,7 +635,7 @@ __global__ __launch_bounds__(HB) void spmm_heavy_kernel(const SpmmArgs a, int FC
             y = 0.0f;
             arg = -1;
           }
-          a.argmax_out[row * a.F + f] = arg;
+          if (a.argmax_out != nullptr) a.argmax_out[row * a.F + f] = arg;
         } else {
           if (a.mean) y = __fdiv_rn(y, (float)(deg > 1 ? deg : 1));
         }
@@ -579,6 +647,33 @@ __global__ __launch_bounds__(HB) void spmm_heavy_kernel(const SpmmArgs a, int FC
         if (a.row_scale != nullptr) v = __fmul_rn(v, a.row_scale[row]);
         if (a.accumulate) v = __fadd_rn(*dst, v);
         *dst = v;
+      }
+    }
+    if constexpr (MODE == FWD_MAX) {
+      if (a.win_mask_out != nullptr) {
+        // winner bits of every edge of the row: the chunk's winners go to
+        // LDS, then every wave takes edges k = wave, wave + HB/64, ... and
+        // forms each 64-feature slice with one ballot
+        int32_t *win_lds = reinterpret_cast<int32_t *>(smem);  // buffers are free here
+        if (t < fc) win_lds[t] = (acc == MGCN_MAX_FILL) ? -1 : arg;
+        __syncthreads();
+        const int64_t W = (a.F + 31) >> 5;
+        const int lane = t & 63;
+        int32_t wv[2];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) wv[r] = (64 * r + lane < fc) ? win_lds[64 * r + lane] : -1;
+        for (int64_t k = wave; k < deg; k += HB / 64) {
+          const int32_t ek = a.eid[beg + k];
+          const int64_t sk = beg + k;  // own fwd slot
+#pragma unroll
+          for (int r = 0; r < 2; ++r) {
+            if (64 * r >= fc) break;
+            const uint64_t bal = __ballot(wv[r] == ek);
+            const int fb = f0 + 64 * r;  // 32-aligned (FC is 128 or F)
+            if (lane == 0) a.win_mask_out[sk * W + (fb >> 5)] = (uint32_t)bal;
+            if (lane == 32 && fb + 32 < a.F) a.win_mask_out[sk * W + (fb >> 5) + 1] = (uint32_t)(bal >> 32);
+          }
+        }
       }
     }
     __syncthreads();  // buffers are reused by the next feature chunk
@@ -599,6 +694,68 @@ __global__ __launch_bounds__(kBlock) void row_degree_kernel(int64_t n_rows,
     if (d > thr) {
       atomicAdd(&count[0], 1ull);
       if (d > giant_thr) atomicAdd(&count[1], 1ull);
+    }
+  }
+}
+
+// mgcn_slot_map: inverse permutation of the fwd view's edge ids, then the
+// fwd slot of every bwd slot.
+__global__ __launch_bounds__(kBlock) void invert_eid_kernel(int64_t nnz,
+                                                             const int32_t *__restrict__ eid_t,
+                                                             int32_t *__restrict__ inv) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < nnz;
+       j += (int64_t)gridDim.x * blockDim.x)
+    inv[eid_t[j]] = (int32_t)j;
+}
+
+__global__ __launch_bounds__(kBlock) void slot_map_kernel(int64_t nnz,
+                                                           const int32_t *__restrict__ eid,
+                                                           const int32_t *__restrict__ inv,
+                                                           int32_t *__restrict__ slot_map) {
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < nnz;
+       k += (int64_t)gridDim.x * blockDim.x)
+    slot_map[k] = inv[eid[k]];
+}
+
+// mgcn_max_mask: for every fwd row d and edge k of it, the features f whose
+// argmax[d, f] is that edge, as bits at win_mask[k][f / 32].  A 32-lane group per (row, 128-feature chunk), 4
+// features per lane: argmax of row d is read once (coalesced), the row's
+// (eid, slot) pairs lane-parallel and broadcast; each 32-bit word is OR-ed
+// over its 8 lanes by shuffles, and the 4 word lanes store an edge's 16 B.
+__global__ __launch_bounds__(kBlock) void max_mask_kernel(int64_t n_rows, int32_t F,
+                                                          const int64_t *__restrict__ rowptr,
+                                                          const int32_t *__restrict__ eid,
+                                                          const int32_t *__restrict__ argmax,
+                                                          uint32_t *__restrict__ win_mask) {
+  const int gl = threadIdx.x & 31;
+  const int nchunk = (F + 127) >> 7;
+  const int W = (F + 31) >> 5;
+  const int64_t groups = n_rows * nchunk;
+  const int64_t gstride = (int64_t)gridDim.x * (kBlock / 32);
+  for (int64_t gid = (int64_t)blockIdx.x * (kBlock / 32) + (threadIdx.x >> 5); gid < groups;
+       gid += gstride) {
+    const int64_t d = gid / nchunk;
+    const int c = (int)(gid - d * nchunk);
+    const int f0 = c * 128 + 4 * gl;
+    int32_t am[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) am[j] = (f0 + j < F) ? argmax[d * F + f0 + j] : -1;
+    const int64_t beg = rowptr[d], end = rowptr[d + 1];
+    for (int64_t e0 = beg; e0 < end; e0 += 32) {
+      const int64_t my = e0 + gl;
+      const int32_t me = my < end ? eid[my] : -1;
+      const int nb = (end - e0) < 32 ? (int)(end - e0) : 32;
+      for (int k = 0; k < nb; ++k) {
+        const int32_t ek = __shfl(me, k, 32);
+        uint32_t v = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v |= (am[j] == ek ? 1u : 0u) << j;
+        v <<= 4 * (gl & 7);
+        v |= __shfl_xor(v, 1, 32);
+        v |= __shfl_xor(v, 2, 32);
+        v |= __shfl_xor(v, 4, 32);
+        if ((gl & 7) == 0 && f0 < F) win_mask[(e0 + k) * W + (f0 >> 5)] = v;
+      }
     }
   }
 }
@@ -830,8 +987,8 @@ static int choose_vec(int32_t F, const void *p0, int64_t ld0, const void *p1, in
 extern "C" int mgcn_spmm_fwd(int64_t n_rows, int32_t F, const int64_t *rowptr, const int32_t *col,
                              const int32_t *eid, const float *w, const float *H, int64_t ldh,
                              float *Y, int64_t ldy, int reduce, const float *bias, int relu,
-                             int32_t *argmax, const int32_t *order, int64_t n_heavy,
-                             int64_t n_giant, void *stream) {
+                             int32_t *argmax, uint32_t *win_mask, const int32_t *order,
+                             int64_t n_heavy, int64_t n_giant, void *stream) {
   clear_error();
   MGCN_REQUIRE(n_rows >= 0 && F >= 0, "mgcn_spmm_fwd: negative size");
   MGCN_REQUIRE(reduce == MGCN_REDUCE_SUM || reduce == MGCN_REDUCE_MEAN || reduce == MGCN_REDUCE_MAX,
@@ -839,8 +996,8 @@ extern "C" int mgcn_spmm_fwd(int64_t n_rows, int32_t F, const int64_t *rowptr, c
   if (n_rows == 0 || F == 0) return MGCN_OK;
   MGCN_REQUIRE(rowptr && H && Y, "mgcn_spmm_fwd: null array");  // col may be NULL when nnz == 0
   MGCN_REQUIRE(ldh >= F && ldy >= F, "mgcn_spmm_fwd: leading dimension < F");
-  MGCN_REQUIRE(reduce != MGCN_REDUCE_MAX || argmax != nullptr,  // eid NULL only if nnz == 0
-               "mgcn_spmm_fwd: MAX needs argmax and eid");
+  MGCN_REQUIRE(reduce != MGCN_REDUCE_MAX || argmax != nullptr || win_mask != nullptr,
+               "mgcn_spmm_fwd: MAX needs argmax and/or win_mask (+ eid)");
   SpmmArgs a{};
   a.n_rows = n_rows;
   a.F = F;
@@ -854,6 +1011,7 @@ extern "C" int mgcn_spmm_fwd(int64_t n_rows, int32_t F, const int64_t *rowptr, c
   a.ldy = ldy;
   a.bias = bias;
   a.argmax_out = argmax;
+  a.win_mask_out = reduce == MGCN_REDUCE_MAX ? win_mask : nullptr;
   MGCN_REQUIRE(order == nullptr || (0 <= n_giant && n_giant <= n_heavy && n_heavy <= n_rows),
                "spmm: need 0 <= n_giant <= n_heavy <= n_rows");
   a.order = order;
@@ -862,7 +1020,9 @@ extern "C" int mgcn_spmm_fwd(int64_t n_rows, int32_t F, const int64_t *rowptr, c
   a.mean = reduce == MGCN_REDUCE_MEAN;
   a.relu = relu != 0;
   int vec = choose_vec(F, H, ldh, Y, ldy);
-  if (reduce == MGCN_REDUCE_MAX && reinterpret_cast<uintptr_t>(argmax) % (4 * vec)) vec = 1;
+  if (reduce == MGCN_REDUCE_MAX && argmax != nullptr &&
+      reinterpret_cast<uintptr_t>(argmax) % (4 * vec))
+    vec = 1;
   if (bias != nullptr && reinterpret_cast<uintptr_t>(bias) % 4) return MGCN_EINVAL;
   hipStream_t s = as_stream(stream);
   if (reduce == MGCN_REDUCE_MAX) return launch_mode<FWD_MAX>(a, vec, s);
@@ -873,8 +1033,9 @@ extern "C" int mgcn_spmm_bwd(int64_t n_rows, int32_t F, const int64_t *rowptr_t,
                              const int32_t *col_t, const int32_t *eid_t, const float *w_t,
                              const float *row_scale, const float *dY, int64_t lddy, float *dH,
                              int64_t lddh, int reduce, const float *cnt, const int32_t *argmax,
-                             int accumulate, const int32_t *order, int64_t n_heavy,
-                             int64_t n_giant, void *stream) {
+                             const uint32_t *win_mask, const int32_t *slot_map, int accumulate,
+                             const int32_t *order, int64_t n_heavy, int64_t n_giant,
+                             void *stream) {
   clear_error();
   MGCN_REQUIRE(n_rows >= 0 && F >= 0, "mgcn_spmm_bwd: negative size");
   MGCN_REQUIRE(reduce == MGCN_REDUCE_SUM || reduce == MGCN_REDUCE_MEAN || reduce == MGCN_REDUCE_MAX,
@@ -883,8 +1044,10 @@ extern "C" int mgcn_spmm_bwd(int64_t n_rows, int32_t F, const int64_t *rowptr_t,
   MGCN_REQUIRE(rowptr_t && dY && dH, "mgcn_spmm_bwd: null array");  // col may be NULL when nnz == 0
   MGCN_REQUIRE(lddy >= F && lddh >= F, "mgcn_spmm_bwd: leading dimension < F");
   MGCN_REQUIRE(reduce != MGCN_REDUCE_MEAN || cnt != nullptr, "mgcn_spmm_bwd: MEAN needs cnt");
-  MGCN_REQUIRE(reduce != MGCN_REDUCE_MAX || argmax != nullptr,  // eid NULL only if nnz == 0
-               "mgcn_spmm_bwd: MAX needs argmax and eid");
+  MGCN_REQUIRE(reduce != MGCN_REDUCE_MAX || argmax != nullptr || win_mask != nullptr,
+               "mgcn_spmm_bwd: MAX needs argmax (+ eid) or win_mask (+ slot_map)");
+  MGCN_REQUIRE(win_mask == nullptr || slot_map != nullptr || reduce != MGCN_REDUCE_MAX,
+               "mgcn_spmm_bwd: win_mask needs slot_map");
   SpmmArgs a{};
   a.n_rows = n_rows;
   a.F = F;
@@ -899,6 +1062,8 @@ extern "C" int mgcn_spmm_bwd(int64_t n_rows, int32_t F, const int64_t *rowptr_t,
   a.row_scale = row_scale;
   a.cnt = cnt;
   a.argmax_in = argmax;
+  a.win_mask = reduce == MGCN_REDUCE_MAX ? win_mask : nullptr;
+  a.slot_map = slot_map;
   a.accumulate = accumulate != 0;
   MGCN_REQUIRE(order == nullptr || (0 <= n_giant && n_giant <= n_heavy && n_heavy <= n_rows),
                "spmm: need 0 <= n_giant <= n_heavy <= n_rows");
@@ -906,9 +1071,12 @@ extern "C" int mgcn_spmm_bwd(int64_t n_rows, int32_t F, const int64_t *rowptr_t,
   a.n_heavy = n_heavy;
   a.n_giant = n_giant;
   int vec = choose_vec(F, dY, lddy, dH, lddh);
-  if (reduce == MGCN_REDUCE_MAX && reinterpret_cast<uintptr_t>(argmax) % (4 * vec)) vec = 1;
+  if (reduce == MGCN_REDUCE_MAX && a.win_mask == nullptr &&
+      reinterpret_cast<uintptr_t>(argmax) % (4 * vec))
+    vec = 1;
   hipStream_t s = as_stream(stream);
-  if (reduce == MGCN_REDUCE_MAX) return launch_mode<BWD_MAX>(a, vec, s);
+  if (reduce == MGCN_REDUCE_MAX)
+    return a.win_mask != nullptr ? launch_mode<BWD_MAXM>(a, vec, s) : launch_mode<BWD_MAX>(a, vec, s);
   if (reduce == MGCN_REDUCE_MEAN) return launch_mode<BWD_MEAN>(a, vec, s);
   return launch_mode<BWD_SUM>(a, vec, s);
 }
@@ -975,4 +1143,44 @@ extern "C" int mgcn_row_schedule(int64_t n_rows, const int64_t *rowptr, int64_t 
   *n_heavy_out = (int64_t)c[0];
   *n_giant_out = (int64_t)c[1];
   return MGCN_OK;
+}
+
+extern "C" size_t mgcn_slot_map_workspace_bytes(int64_t nnz) {
+  return align_up((size_t)(nnz > 0 ? nnz : 1) * sizeof(int32_t), 256);
+}
+
+extern "C" int mgcn_slot_map(int64_t nnz, const int32_t *eid, const int32_t *eid_t,
+                             int32_t *slot_map, void *workspace, size_t workspace_bytes,
+                             void *stream) {  // slot_map[j] = fwd slot of bwd slot j
+  clear_error();
+  MGCN_REQUIRE(nnz >= 0, "mgcn_slot_map: negative nnz");
+  if (nnz == 0) return MGCN_OK;
+  MGCN_REQUIRE(eid && eid_t && slot_map, "mgcn_slot_map: null array");
+  if (workspace == nullptr || workspace_bytes < mgcn_slot_map_workspace_bytes(nnz)) {
+    set_error("mgcn_slot_map: workspace %zu < %zu", workspace_bytes,
+              mgcn_slot_map_workspace_bytes(nnz));
+    return MGCN_EWORKSPACE;
+  }
+  hipStream_t s = as_stream(stream);
+  int32_t *inv = static_cast<int32_t *>(workspace);
+  hipLaunchKernelGGL(invert_eid_kernel, dim3(grid_for(nnz, kBlock)), dim3(kBlock), 0, s, nnz,
+                     eid, inv);
+  if (int rc = check_launch("invert_eid_kernel")) return rc;
+  hipLaunchKernelGGL(slot_map_kernel, dim3(grid_for(nnz, kBlock)), dim3(kBlock), 0, s, nnz, eid_t,
+                     inv, slot_map);
+  return check_launch("slot_map_kernel");
+}
+
+extern "C" int mgcn_max_mask(int64_t n_rows, int32_t F, const int64_t *rowptr,
+                             const int32_t *eid, const int32_t *argmax, uint32_t *win_mask,
+                             void *stream) {
+  clear_error();
+  MGCN_REQUIRE(n_rows >= 0 && F >= 0, "mgcn_max_mask: negative size");
+  if (n_rows == 0 || F == 0) return MGCN_OK;
+  MGCN_REQUIRE(rowptr && argmax, "mgcn_max_mask: null array");  // eid/slot_map/mask: nnz > 0
+  hipStream_t s = as_stream(stream);
+  const int64_t threads = n_rows * ((F + 127) / 128) * 32;
+  hipLaunchKernelGGL(max_mask_kernel, dim3(grid_for(threads, kBlock)), dim3(kBlock), 0, s, n_rows,
+                     F, rowptr, eid, argmax, win_mask);
+  return check_launch("max_mask_kernel");
 }

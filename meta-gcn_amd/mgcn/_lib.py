@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmgcn.so")
 
 # constants mirrored from include/mgcn.h
-ABI_VERSION = 3
+ABI_VERSION = 4
 OK, EINVAL, EINDEX, EHIP, EWORKSPACE = 0, 1, 2, 3, 4
 REDUCE_SUM, REDUCE_MEAN, REDUCE_MAX = 0, 1, 2
 NORM_NONE, NORM_SM, NORM_RW = 0, 1, 2
@@ -41,9 +41,12 @@ SIGNATURES = {
     "mgcn_degree_norm": (_int, [_i64, _vp, _vp, _vp, _vp, _int, _vp, _vp, _vp]),
     "mgcn_edge_norm": (_int, [_i64, _i64, _vp, _vp, _vp, _int, _vp, _vp, _int, _vp, _vp]),
     "mgcn_spmm_fwd": (_int, [_i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _int, _vp,
-                             _int, _vp, _vp, _i64, _i64, _vp]),
+                             _int, _vp, _vp, _vp, _i64, _i64, _vp]),
     "mgcn_spmm_bwd": (_int, [_i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _int,
-                             _vp, _vp, _int, _vp, _i64, _i64, _vp]),
+                             _vp, _vp, _vp, _vp, _int, _vp, _i64, _i64, _vp]),
+    "mgcn_slot_map_workspace_bytes": (_sz, [_i64]),
+    "mgcn_slot_map": (_int, [_i64, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "mgcn_max_mask": (_int, [_i64, _i32, _vp, _vp, _vp, _vp, _vp]),
     "mgcn_row_schedule_workspace_bytes": (_sz, [_i64]),
     "mgcn_row_schedule": (_int, [_i64, _vp, _i64, _vp, ctypes.POINTER(ctypes.c_int64),
                                  ctypes.POINTER(ctypes.c_int64), _vp, _sz, _vp]),

@@ -124,6 +124,23 @@ class GraphPlan:
     in_cnt: torch.Tensor  # float [num_nodes] = max(in-degree, 1)
     norms: dict = field(default_factory=dict)
     _key_refs: list = field(default_factory=list)
+    _slot_map: torch.Tensor | None = None
+
+    def slot_map(self) -> torch.Tensor:
+        """int32 [nnz]: the fwd-view slot of every bwd-view slot (mgcn_slot_map),
+        built on first use (max aggregation)."""
+        if self._slot_map is None:
+            lib = L.load()
+            dev = self.device
+            out = torch.empty(max(self.nnz, 1), dtype=torch.int32, device=dev)
+            ws = torch.empty(int(lib.mgcn_slot_map_workspace_bytes(self.nnz)), dtype=torch.uint8,
+                             device=dev)
+            with torch.cuda.device(dev):
+                rc = lib.mgcn_slot_map(self.nnz, L.ptr(self.fwd.eid), L.ptr(self.bwd.eid),
+                                       L.ptr(out), L.ptr(ws), ws.numel(), L.stream_of(dev))
+            L.check(rc, "mgcn_slot_map")
+            self._slot_map = out
+        return self._slot_map
 
     # ------------------------------------------------------------------ norms
     def norm(self, method: str | None, deg: torch.Tensor | None = None,

@@ -44,8 +44,12 @@ def _contig_f32(t: torch.Tensor, name: str) -> torch.Tensor:
 
 def spmm_fwd(view: CSRView, w: torch.Tensor | None, H: torch.Tensor, reduce: int,
              bias: torch.Tensor | None = None, relu: bool = False,
-             out: torch.Tensor | None = None):
-    """Y[view.n_rows, F] = epi(reduce_k H[col_k] * w_k); returns (Y, argmax)."""
+             out: torch.Tensor | None = None, mask_plan: GraphPlan | None = None):
+    """Y[view.n_rows, F] = epi(reduce_k H[col_k] * w_k); returns (Y, argmax).
+
+    Max with ``mask_plan`` (the plan ``view`` belongs to): instead of argmax
+    the kernel writes every edge's winner bits at its slot (int32
+    [nnz, ceil(F/32)] bit patterns), returned in argmax's place."""
     lib = L.load()
     H = _contig_f32(H, "H")
     dev = L.require_device(H, view.rowptr, w, bias)
@@ -53,9 +57,13 @@ def spmm_fwd(view: CSRView, w: torch.Tensor | None, H: torch.Tensor, reduce: int
         raise ValueError(f"H has {H.size(0)} rows, graph has {view.n_cols} source nodes")
     F = H.size(1)
     Y = out if out is not None else torch.empty(view.n_rows, F, dtype=torch.float32, device=dev)
-    argmax = None
+    argmax = mask = None
     if reduce == L.REDUCE_MAX:
-        argmax = torch.empty(view.n_rows, F, dtype=torch.int32, device=dev)
+        if mask_plan is not None:
+            mask = torch.empty(max(mask_plan.nnz, 1), (F + 31) // 32, dtype=torch.int32,
+                               device=dev)
+        else:
+            argmax = torch.empty(view.n_rows, F, dtype=torch.int32, device=dev)
     if bias is not None:
         bias = bias.detach().to(torch.float32).contiguous()
         if bias.numel() != F:
@@ -66,17 +74,19 @@ def spmm_fwd(view: CSRView, w: torch.Tensor | None, H: torch.Tensor, reduce: int
         rc = lib.mgcn_spmm_fwd(view.n_rows, F, L.ptr(view.rowptr), L.ptr(view.col),
                                L.ptr(view.eid), L.ptr(w), L.ptr(H), H.stride(0), L.ptr(Y),
                                Y.stride(0), reduce, L.ptr(bias), int(bool(relu)), L.ptr(argmax),
-                               L.ptr(view.order), view.n_heavy, view.n_giant, L.stream_of(dev))
+                               L.ptr(mask), L.ptr(view.order), view.n_heavy,
+                               view.n_giant, L.stream_of(dev))
     if _TIMER is not None:
         _TIMER("spmm_fwd", False)
     L.check(rc, "mgcn_spmm_fwd")
-    return Y, argmax
+    return Y, (mask if mask is not None else argmax)
 
 
 def spmm_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tensor | None,
              dY: torch.Tensor, reduce: int, cnt: torch.Tensor | None = None,
              argmax: torch.Tensor | None = None, out: torch.Tensor | None = None,
-             accumulate: bool = False) -> torch.Tensor:
+             accumulate: bool = False, win_mask: torch.Tensor | None = None,
+             slot_map: torch.Tensor | None = None) -> torch.Tensor:
     """dH[view_t.n_rows, F] = sum_k g(dY[col_k]) * w_k  [* row_scale]."""
     lib = L.load()
     dY = _contig_f32(dY, "dY")
@@ -90,7 +100,9 @@ def spmm_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tensor 
         rc = lib.mgcn_spmm_bwd(view_t.n_rows, F, L.ptr(view_t.rowptr), L.ptr(view_t.col),
                                L.ptr(view_t.eid), L.ptr(w_t), L.ptr(row_scale), L.ptr(dY),
                                dY.stride(0), L.ptr(dH), dH.stride(0), reduce, L.ptr(cnt),
-                               L.ptr(argmax), int(bool(accumulate)), L.ptr(view_t.order),
+                               L.ptr(argmax), L.ptr(win_mask), L.ptr(slot_map),
+                               int(bool(accumulate)),
+                               L.ptr(view_t.order),
                                view_t.n_heavy, view_t.n_giant, L.stream_of(dev))
     if _TIMER is not None:
         _TIMER("spmm_bwd", False)
@@ -270,20 +282,36 @@ def linear(x: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
     return _Linear.apply(x, W)
 
 
+def max_mask(plan: GraphPlan, argmax: torch.Tensor) -> torch.Tensor:
+    """Winner bits of every edge at its fwd slot (mgcn_max_mask): int32
+    [nnz, ceil(F/32)] (bit patterns), replacing argmax in the backward."""
+    lib = L.load()
+    F = argmax.size(1)
+    W = (F + 31) // 32
+    dev = argmax.device
+    mask = torch.empty(max(plan.nnz, 1), W, dtype=torch.int32, device=dev)
+    with torch.cuda.device(dev):
+        rc = lib.mgcn_max_mask(plan.fwd.n_rows, F, L.ptr(plan.fwd.rowptr), L.ptr(plan.fwd.eid),
+                               L.ptr(argmax), L.ptr(mask), L.stream_of(dev))
+    L.check(rc, "mgcn_max_mask")
+    return mask
+
+
 class _Aggregate(torch.autograd.Function):
-    """y = epi(A_norm (x) H) with bias and ReLU fused; see module docstring."""
+    """y = epi(A_norm (x) H) with bias and ReLU fused; see module docstring.
+    Max saves the per-edge winner bits (max_mask), not the argmax rows."""
 
     @staticmethod
     def forward(ctx, H, bias, plan: GraphPlan, norm: NormPlan, reduce: int, relu: bool):
-        Y, argmax = spmm_fwd(plan.fwd, norm.w_fwd, H, reduce, bias, relu)
+        Y, mask = spmm_fwd(plan.fwd, norm.w_fwd, H, reduce, bias, relu, mask_plan=plan)
         ctx.plan, ctx.norm, ctx.reduce, ctx.relu = plan, norm, reduce, relu
         ctx.has_bias = bias is not None
-        ctx.save_for_backward(Y if relu else None, argmax)
+        ctx.save_for_backward(Y if relu else None, mask)  # max: winner bits per edge
         return Y
 
     @staticmethod
     def backward(ctx, dZ):
-        Y, argmax = ctx.saved_tensors
+        Y, mask = ctx.saved_tensors
         plan, norm = ctx.plan, ctx.norm
         need_h = ctx.needs_input_grad[0]
         need_b = ctx.has_bias and ctx.needs_input_grad[1]
@@ -292,7 +320,7 @@ class _Aggregate(torch.autograd.Function):
         if need_h:
             dH = spmm_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, ctx.reduce,
                           cnt=plan.in_cnt if ctx.reduce == L.REDUCE_MEAN else None,
-                          argmax=argmax)
+                          win_mask=mask, slot_map=plan.slot_map() if mask is not None else None)
         return dH, db, None, None, None, None
 
 
@@ -340,9 +368,9 @@ class _GCNStack(torch.autograd.Function):
         for W, b, relu in zip(Ws, bs, relus):
             inputs.append(h)
             H = _mm(h, W)
-            h, am = spmm_fwd(plan.fwd, norm.w_fwd, H, reduce, b, relu)
+            h, am = spmm_fwd(plan.fwd, norm.w_fwd, H, reduce, b, relu, mask_plan=plan)
             outs.append(h)
-            args.append(am)
+            args.append(am)  # max: winner bits per edge (adjoint slot order)
         ctx.plan, ctx.norm, ctx.reduce, ctx.relus = plan, norm, reduce, relus
         ctx.n_layers = len(Ws)
         ctx.has_bias = [b is not None for b in bs]
@@ -366,7 +394,8 @@ class _GCNStack(torch.autograd.Function):
         for l in range(top, -1, -1):
             am = args[l] if args[l].numel() else None
             dH = spmm_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, reduce,
-                          cnt=plan.in_cnt if reduce == L.REDUCE_MEAN else None, argmax=am)
+                          cnt=plan.in_cnt if reduce == L.REDUCE_MEAN else None, win_mask=am,
+                          slot_map=plan.slot_map() if am is not None else None)
             gW[l] = gemm_tn(inputs[l], dH)
             W = Ws[l]
             if l > 0:

@@ -366,6 +366,34 @@ def test_heavy_rows_are_listed(cuda):
     assert plan.bwd.n_heavy >= 1
 
 
+@pytest.mark.parametrize("F", [128, 7, 300])
+def test_max_adjoint_mask_equals_argmax_routing(cuda, oracle, F):
+    """mgcn_max_mask + win_mask adjoint == the argmax-routed adjoint, bit for
+    bit (light and heavy rows, ragged words), and == the oracle."""
+    from mgcn import ops
+    from mgcn.graph import plan_for
+    rng = np.random.default_rng(F)
+    N = 3000
+    ei = _graph(rng, N, 30000, heavy=3000, heavy_src=2000)
+    H = rng.standard_normal((N, F)).astype(np.float32)
+    dZ = rng.standard_normal((N, F)).astype(np.float32)
+    wf, wb, rs = oracle.edge_factors(ei, N, None)
+    y_ref, am_ref = oracle.aggr_fwd(ei, H, wf, "max")
+    dH_ref, _ = oracle.aggr_bwd(ei, dZ, wb, rs, "max", y_ref, False, am_ref)
+    plan = plan_for(_t(ei, cuda), N)
+    Y, argmax = ops.spmm_fwd(plan.fwd, None, _t(H, cuda), 2)
+    mask = ops.max_mask(plan, argmax)
+    d_arg = ops.spmm_bwd(plan.bwd, None, None, _t(dZ, cuda), 2, argmax=argmax)
+    d_mask = ops.spmm_bwd(plan.bwd, None, None, _t(dZ, cuda), 2, win_mask=mask,
+                          slot_map=plan.slot_map())
+    assert torch.equal(d_arg, d_mask)
+    np.testing.assert_array_equal(_np(d_mask), dH_ref)
+    # the forward kernels (lane-group and heavy rows) write the same bits directly
+    Y2, fused = ops.spmm_fwd(plan.fwd, None, _t(H, cuda), 2, mask_plan=plan)
+    assert torch.equal(Y2, Y)
+    assert torch.equal(fused, mask)
+
+
 HEAVY_CONFIGS = [
     # libmgcn options for the heavy-row launches (read at plan time / launch)
     {"heavy_giant_thr": 0},                      # every heavy row giant, 1024 threads
