@@ -242,12 +242,14 @@ size_t mgcn_gemm_nn_workspace_bytes(int64_t M, int32_t N);
  * its input gradient dX = dH W^T.  If Z != NULL the previous layer's ReLU
  * backward and bias gradient are fused into the epilogue:
  *   C = Z > 0 ? A.B : 0,  colsum[n] = sum_m C[m, n]  (deterministic)
- * (gcn_model.py:196 + gcn_base_models.py:240-241 adjoints).
+ * (gcn_model.py:196 + gcn_base_models.py:240-241 adjoints); with row_div
+ * (mean aggregation, = max(in-degree, 1)) C is stored divided by it, the
+ * column sums stay undivided.
  */
 int mgcn_gemm_nn(int64_t M, int32_t K, int32_t N, const float *A, int64_t lda,
                  const float *B, int64_t sbk, int64_t sbn, float *C, int64_t ldc,
-                 const float *Z, int64_t ldz, float *colsum, void *workspace,
-                 size_t workspace_bytes, void *stream);
+                 const float *Z, int64_t ldz, const float *row_div, float *colsum,
+                 void *workspace, size_t workspace_bytes, void *stream);
 
 /* ----------------------------------------------------------- elementwise */
 
@@ -256,14 +258,17 @@ size_t mgcn_colsum_workspace_bytes(int64_t n_rows, int32_t F);
 
 /*
  * ReLU backward + bias gradient in one pass over [n_rows, F]:
- *   dY = Z > 0 ? dZ : 0   (written only when relu != 0 and dY != NULL)
- *   db[f] = sum_i dY[i, f] (when db != NULL; deterministic two-stage sum)
+ *   dY = Z > 0 ? dZ : 0   (written only when relu != 0 or row_div != NULL,
+ *                          and dY != NULL; divided by row_div[i] when given:
+ *                          the mean aggregation's 1/count, applied once per
+ *                          row instead of once per edge in the adjoint)
+ *   db[f] = sum_i dY[i, f] (undivided; when db != NULL; deterministic)
  * Replaces autograd's threshold_backward + sum for `x + bias` then ReLU
  * (gcn_base_models.py:240-241, gcn_model.py:196).
  */
 int mgcn_relu_bwd_colsum(int64_t n_rows, int32_t F, const float *dZ,
-                         const float *Z, int relu, float *dY, float *db,
-                         void *workspace, size_t workspace_bytes,
+                         const float *Z, int relu, const float *row_div, float *dY,
+                         float *db, void *workspace, size_t workspace_bytes,
                          void *stream);
 
 /*

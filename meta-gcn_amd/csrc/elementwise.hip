@@ -22,7 +22,8 @@ constexpr int kMaxPartialBlocks = 1024;
 template <int VEC>
 __global__ __launch_bounds__(kBlock) void relu_bwd_colsum_kernel(
     int64_t n, int F, const float *__restrict__ dZ, const float *__restrict__ Z, int relu,
-    float *__restrict__ dY, float *__restrict__ partial /*[gridDim.x][F]*/, int T) {
+    const float *__restrict__ row_div, float *__restrict__ dY,
+    float *__restrict__ partial /*[gridDim.x][F]*/, int T) {
   __shared__ float red[kBlock * VEC];
   const int R = kBlock / T;  // row slots per block iteration
   const int t_col = threadIdx.x % T;
@@ -51,12 +52,15 @@ __global__ __launch_bounds__(kBlock) void relu_bwd_colsum_kernel(
         if (relu) {
 #pragma unroll
           for (int j = 0; j < VEC; ++j) g[j] = (z[j] > 0.0f) ? g[j] : 0.0f;
-          if (dY != nullptr) {
-            if constexpr (VEC == 4)
-              *reinterpret_cast<float4 *>(dY + off) = make_float4(g[0], g[1], g[2], g[3]);
-            else
-              dY[off] = g[0];
-          }
+        }
+        if ((relu || row_div != nullptr) && dY != nullptr) {
+          float o[VEC];  // mean aggregation: rows pre-divided by their count
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) o[j] = row_div != nullptr ? __fdiv_rn(g[j], row_div[r]) : g[j];
+          if constexpr (VEC == 4)
+            *reinterpret_cast<float4 *>(dY + off) = make_float4(o[0], o[1], o[2], o[3]);
+          else
+            dY[off] = o[0];
         }
 #pragma unroll
         for (int j = 0; j < VEC; ++j) acc[j] = __fadd_rn(acc[j], g[j]);
@@ -135,8 +139,8 @@ extern "C" size_t mgcn_colsum_workspace_bytes(int64_t n_rows, int32_t F) {
 }
 
 extern "C" int mgcn_relu_bwd_colsum(int64_t n_rows, int32_t F, const float *dZ, const float *Z,
-                                    int relu, float *dY, float *db, void *workspace,
-                                    size_t workspace_bytes, void *stream) {
+                                    int relu, const float *row_div, float *dY, float *db,
+                                    void *workspace, size_t workspace_bytes, void *stream) {
   clear_error();
   MGCN_REQUIRE(n_rows >= 0 && F >= 0, "mgcn_relu_bwd_colsum: negative size");
   hipStream_t s = as_stream(stream);
@@ -163,12 +167,12 @@ extern "C" int mgcn_relu_bwd_colsum(int64_t n_rows, int32_t F, const float *dZ, 
     int T = 1;
     while (T < F / 4 && T < kBlock) T <<= 1;
     hipLaunchKernelGGL(relu_bwd_colsum_kernel<4>, dim3(nblk), dim3(kBlock), 0, s, n_rows, F, dZ, Z,
-                       relu, dY, partial, T);
+                       relu, row_div, dY, partial, T);
   } else {
     int T = 1;
     while (T < F && T < kBlock) T <<= 1;
     hipLaunchKernelGGL(relu_bwd_colsum_kernel<1>, dim3(nblk), dim3(kBlock), 0, s, n_rows, F, dZ, Z,
-                       relu, dY, partial, T);
+                       relu, row_div, dY, partial, T);
   }
   if (int rc = check_launch("relu_bwd_colsum_kernel")) return rc;
   if (db != nullptr) {

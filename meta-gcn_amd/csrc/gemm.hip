@@ -418,13 +418,14 @@ namespace {
 constexpr int kNNWaves = 8;  // waves per workgroup
 constexpr int kNNThreads = 64 * kNNWaves;
 constexpr int kNNMaxGrid = 1024;  // colsum partial slots
-constexpr int EPI_STORE = 0, EPI_RELU = 1;
+constexpr int EPI_STORE = 0, EPI_RELU = 1, EPI_RELU_DIV = 2;  // DIV: C stored / row_div
 
 template <int K, int NT, int EPI>
 __global__ __launch_bounds__(kNNThreads, 2) void gemm_nn_kernel(
     const float *__restrict__ A, int64_t lda, const float *__restrict__ B, int64_t sbk,
     int64_t sbn, float *__restrict__ C, int64_t ldc, int64_t M, int N,
-    const float *__restrict__ Z, int64_t ldz, float *__restrict__ colsum_partial) {
+    const float *__restrict__ Z, int64_t ldz, const float *__restrict__ row_div,
+    float *__restrict__ colsum_partial) {
   constexpr int KH = K / 2;              // k per lane half
   constexpr int S4 = KH / 4;             // float4 steps per 32-row subtile
   constexpr int GS = (K == 32) ? 2 : 1;  // subtiles per unit (>= 8 steps per unit)
@@ -525,9 +526,9 @@ __global__ __launch_bounds__(kNNThreads, 2) void gemm_nn_kernel(
         const int n = j * 32 + lc;
         const bool n_ok = n < N;
         float *cp = C + (r0 + 4 * h) * ldc + n;
-        const float *zp = (EPI == EPI_RELU) ? Z + (r0 + 4 * h) * ldz + n : nullptr;
+        const float *zp = (EPI != EPI_STORE) ? Z + (r0 + 4 * h) * ldz + n : nullptr;
         if (rows_full) {
-          if constexpr (EPI == EPI_RELU) {
+          if constexpr (EPI != EPI_STORE) {
             float zv[16];
 #pragma unroll
             for (int r = 0; r < 16; ++r) zv[r] = n_ok ? zp[((r & 3) + 8 * (r >> 2)) * ldz] : 0.0f;
@@ -535,8 +536,12 @@ __global__ __launch_bounds__(kNNThreads, 2) void gemm_nn_kernel(
             for (int r = 0; r < 16; ++r) {
               const float v = (zv[r] > 0.0f) ? acc[g][j][r] : 0.0f;
               if (n_ok) {
-                csum[j] = __fadd_rn(csum[j], v);
-                cp[((r & 3) + 8 * (r >> 2)) * ldc] = v;
+                csum[j] = __fadd_rn(csum[j], v);  // bias gradient: undivided
+                const int rr = (r & 3) + 8 * (r >> 2);
+                if constexpr (EPI == EPI_RELU_DIV)
+                  cp[rr * ldc] = __fdiv_rn(v, row_div[r0 + 4 * h + rr]);
+                else
+                  cp[rr * ldc] = v;
               }
             }
           } else {
@@ -551,9 +556,10 @@ __global__ __launch_bounds__(kNNThreads, 2) void gemm_nn_kernel(
             const int rr = (r & 3) + 8 * (r >> 2);
             if (n_ok && r0 + 4 * h + rr < M) {
               float v = acc[g][j][r];
-              if constexpr (EPI == EPI_RELU) {
+              if constexpr (EPI != EPI_STORE) {
                 v = (zp[rr * ldz] > 0.0f) ? v : 0.0f;
                 csum[j] = __fadd_rn(csum[j], v);
+                if constexpr (EPI == EPI_RELU_DIV) v = __fdiv_rn(v, row_div[r0 + 4 * h + rr]);
               }
               cp[rr * ldc] = v;
             }
@@ -591,7 +597,7 @@ __global__ __launch_bounds__(kNNThreads, 2) void gemm_nn_kernel(
       epilogue(u1);
     }
   }
-  if constexpr (EPI == EPI_RELU) {
+  if constexpr (EPI != EPI_STORE) {
     // fold the lane halves, then the waves in wave order (deterministic)
     __syncthreads();  // BT is free
     float *red = BT;  // [kNNWaves][NT * 32]
@@ -632,16 +638,21 @@ int nn_blocks(int64_t M) {
 template <int K, int NT>
 int launch_nn_nt(int64_t M, int N, const float *A, int64_t lda, const float *B, int64_t sbk,
                  int64_t sbn, float *C, int64_t ldc, int epi, const float *Z, int64_t ldz,
-                 float *partial, int *grid_out, hipStream_t s) {
-  if (epi == EPI_RELU) {
+                 const float *row_div, float *partial, int *grid_out, hipStream_t s) {
+  if (epi == EPI_RELU_DIV) {
+    const int g = nn_blocks<K, NT, EPI_RELU_DIV>(M);
+    hipLaunchKernelGGL((gemm_nn_kernel<K, NT, EPI_RELU_DIV>), dim3(g), dim3(kNNThreads), 0, s, A,
+                       lda, B, sbk, sbn, C, ldc, M, N, Z, ldz, row_div, partial);
+    *grid_out = g;
+  } else if (epi == EPI_RELU) {
     const int g = nn_blocks<K, NT, EPI_RELU>(M);
     hipLaunchKernelGGL((gemm_nn_kernel<K, NT, EPI_RELU>), dim3(g), dim3(kNNThreads), 0, s, A,
-                       lda, B, sbk, sbn, C, ldc, M, N, Z, ldz, partial);
+                       lda, B, sbk, sbn, C, ldc, M, N, Z, ldz, row_div, partial);
     *grid_out = g;
   } else {
     const int g = nn_blocks<K, NT, EPI_STORE>(M);
     hipLaunchKernelGGL((gemm_nn_kernel<K, NT, EPI_STORE>), dim3(g), dim3(kNNThreads), 0, s, A,
-                       lda, B, sbk, sbn, C, ldc, M, N, Z, ldz, partial);
+                       lda, B, sbk, sbn, C, ldc, M, N, Z, ldz, row_div, partial);
     *grid_out = g;
   }
   return check_launch("gemm_nn_kernel");
@@ -650,12 +661,15 @@ int launch_nn_nt(int64_t M, int N, const float *A, int64_t lda, const float *B, 
 template <int K>
 int launch_nn(int64_t M, int N, const float *A, int64_t lda, const float *B, int64_t sbk,
               int64_t sbn, float *C, int64_t ldc, int epi, const float *Z, int64_t ldz,
-              float *partial, int *grid_out, hipStream_t s) {
+              const float *rd, float *partial, int *grid_out, hipStream_t s) {
   const int nt = (N + 31) / 32;
-  if (nt == 1) return launch_nn_nt<K, 1>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, ldz, partial, grid_out, s);
-  if (nt == 2) return launch_nn_nt<K, 2>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, ldz, partial, grid_out, s);
-  if (nt == 3) return launch_nn_nt<K, 3>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, ldz, partial, grid_out, s);
-  return launch_nn_nt<K, 4>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, ldz, partial, grid_out, s);
+  if (nt == 1)
+    return launch_nn_nt<K, 1>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, ldz, rd, partial, grid_out, s);
+  if (nt == 2)
+    return launch_nn_nt<K, 2>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, ldz, rd, partial, grid_out, s);
+  if (nt == 3)
+    return launch_nn_nt<K, 3>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, ldz, rd, partial, grid_out, s);
+  return launch_nn_nt<K, 4>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, ldz, rd, partial, grid_out, s);
 }
 
 __global__ __launch_bounds__(256) void colsum_fold_kernel(const float *__restrict__ partial,
@@ -690,8 +704,8 @@ extern "C" size_t mgcn_gemm_nn_workspace_bytes(int64_t M, int32_t N) {
 
 extern "C" int mgcn_gemm_nn(int64_t M, int32_t K, int32_t N, const float *A, int64_t lda,
                             const float *B, int64_t sbk, int64_t sbn, float *C, int64_t ldc,
-                            const float *Z, int64_t ldz, float *colsum, void *workspace,
-                            size_t workspace_bytes, void *stream) {
+                            const float *Z, int64_t ldz, const float *row_div, float *colsum,
+                            void *workspace, size_t workspace_bytes, void *stream) {
   clear_error();
   MGCN_REQUIRE(M >= 0 && K >= 0 && N >= 0, "mgcn_gemm_nn: negative size");
   MGCN_REQUIRE(mgcn_gemm_nn_supported(K, N), "mgcn_gemm_nn: unsupported K=%d N=%d", K, N);
@@ -703,10 +717,11 @@ extern "C" int mgcn_gemm_nn(int64_t M, int32_t K, int32_t N, const float *A, int
   MGCN_REQUIRE(A && B && C && lda >= K && ldc >= N, "mgcn_gemm_nn: bad A/B/C");
   MGCN_REQUIRE(lda % 4 == 0 && reinterpret_cast<uintptr_t>(A) % 16 == 0,
                "mgcn_gemm_nn: A must be 16-byte aligned with lda % 4 == 0");
-  const int epi = (Z != nullptr) ? EPI_RELU : EPI_STORE;
+  const int epi = Z == nullptr ? EPI_STORE : row_div != nullptr ? EPI_RELU_DIV : EPI_RELU;
   MGCN_REQUIRE(epi == EPI_STORE || colsum != nullptr, "mgcn_gemm_nn: Z given without colsum");
+  MGCN_REQUIRE(row_div == nullptr || Z != nullptr, "mgcn_gemm_nn: row_div needs Z");
   float *partial = nullptr;
-  if (epi == EPI_RELU) {
+  if (epi != EPI_STORE) {
     const size_t need = mgcn_gemm_nn_workspace_bytes(M, N);
     if (workspace == nullptr || workspace_bytes < need) {
       set_error("mgcn_gemm_nn: workspace %zu < %zu", workspace_bytes, need);
@@ -717,12 +732,12 @@ extern "C" int mgcn_gemm_nn(int64_t M, int32_t K, int32_t N, const float *A, int
   int rc;
   int grid = 0;
   if (K == 32)
-    rc = launch_nn<32>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, ldz, partial, &grid, s);
+    rc = launch_nn<32>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, ldz, row_div, partial, &grid, s);
   else if (K == 64)
-    rc = launch_nn<64>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, ldz, partial, &grid, s);
+    rc = launch_nn<64>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, ldz, row_div, partial, &grid, s);
   else
-    rc = launch_nn<128>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, ldz, partial, &grid, s);
-  if (rc || epi != EPI_RELU) return rc;
+    rc = launch_nn<128>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, ldz, row_div, partial, &grid, s);
+  if (rc || epi == EPI_STORE) return rc;
   hipLaunchKernelGGL(colsum_fold_kernel, dim3((N + 63) / 64), dim3(256), 0, s, partial,
                      (int64_t)grid, N, colsum);
   return check_launch("colsum_fold_kernel");

@@ -56,9 +56,9 @@ SIGNATURES = {
     "mgcn_gemm_nn_supported": (_int, [_i32, _i32]),
     "mgcn_gemm_nn_workspace_bytes": (_sz, [_i64, _i32]),
     "mgcn_gemm_nn": (_int, [_i64, _i32, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _i64, _vp, _i64,
-                            _vp, _vp, _sz, _vp]),
+                            _vp, _vp, _vp, _sz, _vp]),
     "mgcn_colsum_workspace_bytes": (_sz, [_i64, _i32]),
-    "mgcn_relu_bwd_colsum": (_int, [_i64, _i32, _vp, _vp, _int, _vp, _vp, _vp, _sz, _vp]),
+    "mgcn_relu_bwd_colsum": (_int, [_i64, _i32, _vp, _vp, _int, _vp, _vp, _vp, _vp, _sz, _vp]),
     "mgcn_segment_mean": (_int, [_i64, _i32, _vp, _vp, _i64, _vp, _i64, _vp]),
 }
 

@@ -110,21 +110,26 @@ def spmm_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tensor 
     return dH
 
 
-def relu_bwd_colsum(dZ: torch.Tensor, Z: torch.Tensor | None, relu: bool, want_db: bool):
-    """(dY, db): dY = Z > 0 ? dZ : 0 (dZ itself when not relu); db = sum_i dY."""
+def relu_bwd_colsum(dZ: torch.Tensor, Z: torch.Tensor | None, relu: bool, want_db: bool,
+                    row_div: torch.Tensor | None = None):
+    """(dY, db): dY = Z > 0 ? dZ : 0 (dZ itself when not relu), divided by
+    ``row_div`` per row when given (mean aggregation); db = sum_i of the
+    undivided dY."""
     lib = L.load()
     dZ = dZ.contiguous()
-    dev = L.require_device(dZ, Z)
+    dev = L.require_device(dZ, Z, row_div)
     n, F = dZ.shape
-    dY = torch.empty_like(dZ) if relu else dZ
+    write = relu or row_div is not None
+    dY = torch.empty_like(dZ) if write else dZ
     db = torch.empty(F, dtype=torch.float32, device=dev) if want_db else None
-    if not relu and not want_db:
+    if not write and not want_db:
         return dY, None
     ws_bytes = int(lib.mgcn_colsum_workspace_bytes(n, F)) if want_db else 0
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev) if want_db else None
     with torch.cuda.device(dev):
         rc = lib.mgcn_relu_bwd_colsum(n, F, L.ptr(dZ), L.ptr(Z.contiguous() if relu else None),
-                                      int(bool(relu)), L.ptr(dY if relu else None), L.ptr(db),
+                                      int(bool(relu)), L.ptr(row_div), L.ptr(dY if write else None),
+                                      L.ptr(db),
                                       L.ptr(ws), ws_bytes, L.stream_of(dev))
     L.check(rc, "mgcn_relu_bwd_colsum")
     return dY, db
@@ -161,7 +166,7 @@ def gemm_nn_supported(K: int, N: int) -> bool:
 
 
 def gemm_nn(A: torch.Tensor, W: torch.Tensor, transpose_w: bool = False,
-            Z: torch.Tensor | None = None):
+            Z: torch.Tensor | None = None, row_div: torch.Tensor | None = None):
     """C = A @ W (or A @ W^T) on libmgcn's tall-skinny MFMA kernel
     (``mgcn_gemm_nn``).  With ``Z``: C = Z > 0 ? A @ W^T : 0 and the column sums
     of C are returned too (fused ReLU backward + bias gradient).  Returns
@@ -194,7 +199,8 @@ def gemm_nn(A: torch.Tensor, W: torch.Tensor, transpose_w: bool = False,
     with torch.cuda.device(dev):
         rc = lib.mgcn_gemm_nn(M, K, N, L.ptr(A), A.stride(0), L.ptr(W), sbk, sbn, L.ptr(C),
                               C.stride(0), L.ptr(Z), Z.stride(0) if Z is not None else 0,
-                              L.ptr(colsum), L.ptr(ws), ws_bytes, L.stream_of(dev))
+                              L.ptr(row_div), L.ptr(colsum), L.ptr(ws), ws_bytes,
+                              L.stream_of(dev))
     if _TIMER is not None:
         _TIMER("gemm_nn", False)
     L.check(rc, "mgcn_gemm_nn")
@@ -315,12 +321,16 @@ class _Aggregate(torch.autograd.Function):
         plan, norm = ctx.plan, ctx.norm
         need_h = ctx.needs_input_grad[0]
         need_b = ctx.has_bias and ctx.needs_input_grad[1]
-        dY, db = relu_bwd_colsum(dZ, Y, ctx.relu, need_b)
+        mean = ctx.reduce == L.REDUCE_MEAN
+        # mean: dY rows divided by their count once here (bitwise the same as
+        # dividing every gathered copy), so the adjoint is a plain sum
+        dY, db = relu_bwd_colsum(dZ, Y, ctx.relu, need_b,
+                                 row_div=plan.in_cnt if (mean and need_h) else None)
         dH = None
         if need_h:
-            dH = spmm_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, ctx.reduce,
-                          cnt=plan.in_cnt if ctx.reduce == L.REDUCE_MEAN else None,
-                          win_mask=mask, slot_map=plan.slot_map() if mask is not None else None)
+            dH = spmm_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY,
+                          L.REDUCE_SUM if mean else ctx.reduce, win_mask=mask,
+                          slot_map=plan.slot_map() if mask is not None else None)
         return dH, db, None, None, None, None
 
 
@@ -388,25 +398,30 @@ class _GCNStack(torch.autograd.Function):
         gW = [None] * n
         gb = [None] * n
         top = n - 1
-        dY, db = relu_bwd_colsum(dZ.contiguous(), outs[top], relus[top], ctx.has_bias[top])
+        # mean: every layer's dY is produced divided by the row counts (fused
+        # into relu_bwd_colsum / the dX GEMM epilogue); the adjoint is a sum
+        mean = reduce == L.REDUCE_MEAN
+        rd = plan.in_cnt if mean else None
+        adj = L.REDUCE_SUM if mean else reduce
+        dY, db = relu_bwd_colsum(dZ.contiguous(), outs[top], relus[top], ctx.has_bias[top],
+                                 row_div=rd)
         gb[top] = db
         dx = None
         for l in range(top, -1, -1):
             am = args[l] if args[l].numel() else None
-            dH = spmm_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, reduce,
-                          cnt=plan.in_cnt if reduce == L.REDUCE_MEAN else None, win_mask=am,
+            dH = spmm_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, adj, win_mask=am,
                           slot_map=plan.slot_map() if am is not None else None)
             gW[l] = gemm_tn(inputs[l], dH)
             W = Ws[l]
             if l > 0:
                 fused = relus[l - 1] and gemm_nn_supported(W.size(1), W.size(0))
                 if fused:
-                    dY, db = gemm_nn(dH, W, transpose_w=True, Z=outs[l - 1])
+                    dY, db = gemm_nn(dH, W, transpose_w=True, Z=outs[l - 1], row_div=rd)
                     if not ctx.has_bias[l - 1]:
                         db = None
                 else:
                     dY, db = relu_bwd_colsum(_mm_t(dH, W), outs[l - 1], relus[l - 1],
-                                             ctx.has_bias[l - 1])
+                                             ctx.has_bias[l - 1], row_div=rd)
                 gb[l - 1] = db
             elif ctx.needs_input_grad[0]:
                 dx = _mm_t(dH, W)
