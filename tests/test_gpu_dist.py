@@ -1,0 +1,87 @@
+"""The destination-range sharded path (mgcn.dist) on the GPU with libmgcn:
+two ranks sharing cuda:0 (collectives over gloo, which carries HIP tensors;
+the 8-GPU runs use RCCL through the same code) against the same model run as
+one rank.  Forward rows and dX rows must be bitwise equal (every destination
+row's edges are local and in COO order); all-reduced weight/bias gradients
+within fp32 tolerance.  Covers add / mean / max (argmax all-gather)."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _problem(N=3000, pairs=15000, F=32, L=3, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    s = torch.randint(0, N, (pairs,), generator=g)
+    d = torch.randint(0, N, (pairs,), generator=g)
+    loops = torch.arange(N)
+    ei = torch.stack([torch.cat([s, d, loops]), torch.cat([d, s, loops])])
+    X = torch.randn(N, F, generator=g)
+    Ws = [torch.randn(F, F, generator=g) * 0.3 for _ in range(L)]
+    bs = [torch.randn(F, generator=g) * 0.1 for _ in range(L)]
+    dY = torch.randn(N, F, generator=g)
+    return ei, N, X, Ws, bs, dY
+
+
+def _run(rank, world, port, aggr, out_q):
+    sys.path[:0] = [os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "meta-gcn_amd")]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        from mgcn.dist import ShardedGCN, allreduce_grads
+        ei, N, X, Ws, bs, dY = _problem()
+        m = ShardedGCN(ei, N, Ws, bs, device=dev, aggr=aggr)
+        Xl = m.local_rows(X).requires_grad_(True)
+        out = m.forward(Xl)
+        out.backward(m.local_rows(dY))
+        allreduce_grads(m.params())
+        torch.cuda.synchronize()
+        out_q.put({"rank": rank, "lo": m.shard.lo, "hi": m.shard.hi,
+                   "out": out.detach().cpu().numpy(), "dX": Xl.grad.cpu().numpy(),
+                   "grads": [p.grad.cpu().numpy() for p in m.params()]})
+    finally:
+        dist.destroy_process_group()
+
+
+def _launch(world, aggr):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_run, args=(r, world, port, aggr, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    return sorted(res, key=lambda r: r["rank"])
+
+
+@pytest.mark.parametrize("aggr", ["add", "mean", "max"])
+def test_sharded_gpu_matches_one_rank(cuda, aggr):
+    single = _launch(1, aggr)[0]
+    shards = _launch(2, aggr)
+    assert shards[0]["lo"] == 0 and shards[-1]["hi"] == single["out"].shape[0]
+    for r in shards:
+        lo, hi = r["lo"], r["hi"]
+        np.testing.assert_array_equal(r["out"], single["out"][lo:hi])
+        np.testing.assert_array_equal(r["dX"], single["dX"][lo:hi])
+        for g, g1 in zip(r["grads"], single["grads"]):  # re-associated partial sums
+            np.testing.assert_allclose(g, g1, rtol=1e-5, atol=1e-5 * np.abs(g1).max())
