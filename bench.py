@@ -52,34 +52,10 @@ def make_er_graph(n_nodes: int = 1_000_000, n_pairs: int = 5_000_000, seed: int 
     return torch.stack([src, dst]), n_nodes
 
 
-def make_botnet_graph(n_nodes: int = 143_107, bg_edges: int = 350_000, max_deg: int = 5_900,
-                      p2p_nodes: int = 10_000, p2p_edges: int = 49_566, seed: int = 0):
-    """Config-3 stand-in (the botnet HDF5 data is not in the reference tree):
-    one graph of n_nodes with a heavy-tailed (Chung-Lu, power-law exponent
-    ~2.1) background whose largest expected degree is max_deg
-    (botnet_plot.ipynb:460 shows 5.9k), plus a p2p overlay of p2p_edges
-    random edges among p2p_nodes bots (hard_attn_evil_edge.ipynb:203),
-    symmetrised, self-loops appended (data_procs/loop.py).  Returns
-    (edge_index, n_nodes, bot_mask)."""
-    g = torch.Generator().manual_seed(seed)
-    rank = torch.arange(1, n_nodes + 1, dtype=torch.float64)
-    w = rank.pow(-1.0 / 1.1)
-    w = w / w.sum()
-    # expected degree of node i ~ 2 * bg_edges * w_i; clamp the head at max_deg
-    w = torch.minimum(w, torch.full_like(w, max_deg / (2.0 * bg_edges)))
-    perm = torch.randperm(n_nodes, generator=g)
-    w = w[perm]
-    s = torch.multinomial(w, bg_edges, replacement=True, generator=g)
-    d = torch.multinomial(w, bg_edges, replacement=True, generator=g)
-    bots = torch.randperm(n_nodes, generator=g)[:p2p_nodes]
-    ps = bots[torch.randint(0, p2p_nodes, (p2p_edges,), generator=g)]
-    pd = bots[torch.randint(0, p2p_nodes, (p2p_edges,), generator=g)]
-    s, d = torch.cat([s, ps]), torch.cat([d, pd])
-    loops = torch.arange(n_nodes)
-    ei = torch.stack([torch.cat([s, d, loops]), torch.cat([d, s, loops])])
-    mask = torch.zeros(n_nodes, dtype=torch.bool)
-    mask[bots] = True
-    return ei, n_nodes, mask
+def make_botnet_graph(*args, **kw):
+    """Config-3 graph generator (mgcn.botnet.make_botnet_graph)."""
+    from mgcn.botnet import make_botnet_graph as make
+    return make(*args, **kw)
 
 
 def batch_graphs(graphs):
