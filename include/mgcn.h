@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define MGCN_ABI_VERSION 4
+#define MGCN_ABI_VERSION 5
 
 /* return codes */
 #define MGCN_OK 0
@@ -73,7 +73,12 @@ const char *mgcn_last_error(void);
  *   "heavy_giant_thr" : degree above which a heavy row is giant, read by
  *                   mgcn_row_schedule (default 512)
  *   "gemm_tn_variant": LDS-staged dW kernel chunk depth (M, N multiples of
- *                   128): 0 = 64 rows (default), 1 = 32, 2 = 16             */
+ *                   128): 0 = 64 rows (default), 1 = 32, 2 = 16
+ *   "gemm_precision": product arithmetic of mgcn_gemm_nn / mgcn_gemm_tn:
+ *                   1 = bf16x6 (default; fp32 operands split exactly into
+ *                   three bf16 terms, six products on bf16 MFMA, fp32
+ *                   accumulate -- fp32-level error), 0 = f32
+ *                   MFMA (v_mfma_f32_32x32x2_f32)                          */
 int mgcn_set_option(const char *name, int value);
 
 /* ------------------------------------------------------------------ graph */
@@ -148,6 +153,9 @@ int mgcn_edge_norm(int64_t n_rows, int64_t nnz, const int64_t *rowptr, const int
  * argmax: int32 [n_rows, F] (stride F) for MAX, ignored otherwise; and/or
  * win_mask (see mgcn_max_mask): MAX also writes every edge's winner bits at
  * its slot (argmax may then be NULL).
+ * relu_mask (nullable; needs relu and F <= 128): uint32 [n_rows][4], bit b
+ * of word v set iff y[i, 4 b + v] > 0 -- the ReLU mask mgcn_gemm_nn's dX
+ * epilogue reads (16 B per row instead of the 4F-byte Z row).
  * No floating-point contraction: products and sums are rounded separately,
  * in edge order, exactly as the reference's mul + scatter_add sequence.
  */
@@ -155,8 +163,13 @@ int mgcn_spmm_fwd(int64_t n_rows, int32_t F, const int64_t *rowptr,
                   const int32_t *col, const int32_t *eid, const float *w,
                   const float *H, int64_t ldh, float *Y, int64_t ldy,
                   int reduce, const float *bias, int relu, int32_t *argmax,
-                  uint32_t *win_mask, const int32_t *order, int64_t n_heavy,
-                  int64_t n_giant, void *stream);
+                  uint32_t *win_mask, uint32_t *relu_mask, const int32_t *order,
+                  int64_t n_heavy, int64_t n_giant, void *stream);
+
+/* The ReLU mask of rows Z (layout as mgcn_spmm_fwd's relu_mask; F <= 128),
+ * for callers whose Z was not produced by mgcn_spmm_fwd. */
+int mgcn_relu_mask(int64_t n_rows, int32_t F, const float *Z, int64_t ldz,
+                   uint32_t *relu_mask, void *stream);
 
 /*
  * Adjoint aggregation over the transposed (src-grouped) CSR:
@@ -221,7 +234,7 @@ size_t mgcn_gemm_tn_workspace_bytes(int64_t K, int32_t M, int32_t N);
 
 /*
  * C[M, N] = A^T B (accumulate != 0: C += A^T B) for row-major A [K, M] (row
- * stride lda) and B [K, N] (ldb), fp32 on v_mfma_f32_32x32x2_f32, K split over
+ * stride lda) and B [K, N] (ldb), fp32 on MFMA (gemm_precision), K split over
  * the chip with a deterministic fixed-order reduction of the partials.
  * Replaces autograd's weight gradient of `torch.matmul(x, self.weight_node)`
  * (gcn_base_models.py:201): dW = x^T dH with K = number of nodes.
@@ -236,11 +249,13 @@ int mgcn_gemm_nn_supported(int32_t K, int32_t N);
 size_t mgcn_gemm_nn_workspace_bytes(int64_t M, int32_t N);
 
 /*
- * C[M, N] = A[M, K] . B[K, N] on v_mfma_f32_32x32x2_f32; A row-major (lda,
- * 16-byte aligned rows), B addressed as B[k * sbk + n * sbn] (so W or W^T).
- * Replaces `torch.matmul(x, self.weight_node)` (gcn_base_models.py:201) and
- * its input gradient dX = dH W^T.  If Z != NULL the previous layer's ReLU
- * backward and bias gradient are fused into the epilogue:
+ * C[M, N] = A[M, K] . B[K, N] on MFMA (gemm_precision: bf16x6 or f32); A
+ * row-major (lda, 16-byte aligned rows), B addressed as B[k * sbk + n * sbn]
+ * (so W or W^T).  Replaces `torch.matmul(x, self.weight_node)`
+ * (gcn_base_models.py:201) and its input gradient dX = dH W^T.  If relu_mask
+ * != NULL (mgcn_spmm_fwd / mgcn_relu_mask layout, the previous layer's
+ * output Z > 0) the ReLU backward and bias gradient are fused into the
+ * epilogue:
  *   C = Z > 0 ? A.B : 0,  colsum[n] = sum_m C[m, n]  (deterministic)
  * (gcn_model.py:196 + gcn_base_models.py:240-241 adjoints); with row_div
  * (mean aggregation, = max(in-degree, 1)) C is stored divided by it, the
@@ -248,7 +263,7 @@ size_t mgcn_gemm_nn_workspace_bytes(int64_t M, int32_t N);
  */
 int mgcn_gemm_nn(int64_t M, int32_t K, int32_t N, const float *A, int64_t lda,
                  const float *B, int64_t sbk, int64_t sbn, float *C, int64_t ldc,
-                 const float *Z, int64_t ldz, const float *row_div, float *colsum,
+                 const uint32_t *relu_mask, const float *row_div, float *colsum,
                  void *workspace, size_t workspace_bytes, void *stream);
 
 /* ----------------------------------------------------------- elementwise */

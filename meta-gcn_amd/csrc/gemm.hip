@@ -126,6 +126,199 @@ __global__ __launch_bounds__(256) void gemm_tn_partial_kernel(
 // different order.
 typedef __attribute__((address_space(3))) void lds_void_t;
 
+// ---------------------------------------------------------------------------
+// bf16x6 product arithmetic (mgcn_set_option "gemm_precision" 1): every fp32
+// operand split exactly-rounded into three bf16 terms x = hi + mid + lo (RNE
+// at each step; x - hi and r - mid are exact, |mid| <= 2^-9 |x|, |lo| <=
+// 2^-18 |x|, |x - (hi + mid + lo)| <= 2^-27 |x|) and the six products whose
+// magnitude reaches 2^-18 (hh, hm, mh, mm, hl, lh) summed on
+// v_mfma_f32_32x32x16_bf16 (16x the f32 MFMA rate) into one fp32
+// accumulator.  Dropped terms (ml, lm, ll) are below 2^-27 of |a b|; the
+// accumulator takes 6 K / 16 roundings per output against K for the f32
+// form.  Error vs fp64: scripts/bench_gemm.py, tests/test_gpu_parity.py.
+constexpr int PREC_F32 = 0, PREC_BF16X6 = 1;
+int g_gemm_precision = PREC_BF16X6;
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// bf16 pair (one VGPR) -> the two floats it holds (exact)
+__device__ __forceinline__ f32x2 widen_bf16x2(uint32_t p) {
+  return f32x2{__uint_as_float(p << 16), __uint_as_float(p & 0xffff0000u)};
+}
+
+// one pair of floats -> its hi / mid / lo bf16 pairs (v_cvt_pk_bf16_f32, RNE)
+__device__ __forceinline__ void split3_pair(f32x2 x, uint32_t &hi, uint32_t &mid, uint32_t &lo) {
+  hi = __builtin_bit_cast(uint32_t, __builtin_convertvector(x, bf16x2));
+  const f32x2 r = x - widen_bf16x2(hi);  // exact (Sterbenz)
+  mid = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, bf16x2));
+  lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(r - widen_bf16x2(mid), bf16x2));
+}
+
+__device__ __forceinline__ void split3_bf16(const float (&x)[8], bf16x8 &hi, bf16x8 &mid,
+                                            bf16x8 &lo) {
+  uint32_t h[4], m[4], l[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) split3_pair(f32x2{x[2 * p], x[2 * p + 1]}, h[p], m[p], l[p]);
+  hi = __builtin_bit_cast(bf16x8, h);
+  mid = __builtin_bit_cast(bf16x8, m);
+  lo = __builtin_bit_cast(bf16x8, l);
+}
+
+// six-product bf16 MFMA chain on one accumulator, smallest terms first
+__device__ __forceinline__ f32x16 mfma_x6(const bf16x8 &ah, const bf16x8 &am, const bf16x8 &al,
+                                          const bf16x8 &bh, const bf16x8 &bm, const bf16x8 &bl,
+                                          f32x16 c) {
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, c, 0, 0, 0);
+}
+
+
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16_t;
+
+// dW for M, N multiples of 128 in bf16x6.  Per chunk of 16 k-rows, each
+// thread loads 2 float4 of each operand (coalesced 512-B rows), splits them
+// and writes the three bf16 terms into [k][128] images (256-B rows, 16-B
+// chunks XOR-swizzled: chunk ch of row r at ch ^ ((r & 3) << 2 | (r >> 2) & 3)),
+// from which every MFMA fragment (8 consecutive k of one column) is two
+// ds_read_b64_tr_b16 (each 16-lane group transposes a 4-row x 16-column
+// block; conflict-free on this swizzle).  The next chunk's loads are in
+// flight in registers while the current chunk's 24 MFMAs per wave run.
+constexpr int kTnX6Rows = 16;                       // k-rows per chunk
+constexpr int kTnX6Img = kTnX6Rows * 256;           // bytes per term image
+__device__ __forceinline__ int tn_x6_off(int row, int ch) {
+  return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+__global__ __launch_bounds__(256, 3) void gemm_tn_x6_kernel(
+    const float *__restrict__ A, int64_t lda, const float *__restrict__ B, int64_t ldb,
+    int64_t K, int M, int N, int64_t k_per_split, int tiles_n, float *__restrict__ partial) {
+  // images: [operand A/B][term hi/mid/lo] x kTnX6Img bytes
+  __shared__ __attribute__((aligned(16))) char lds[6 * kTnX6Img];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wi = wave >> 1, wj = wave & 1;
+  const int tile_m = blockIdx.x / tiles_n, tile_n = blockIdx.x % tiles_n;
+  const int64_t kb = (int64_t)blockIdx.y * k_per_split;
+  const int64_t ke = (kb + k_per_split < K) ? kb + k_per_split : K;
+  const int h = lane >> 5, lc = lane & 31;
+
+  // staging: thread -> float4 items tid and tid + 256 of a [16][32] float4 chunk
+  const float *a_base = A + (int64_t)tile_m * kTile;
+  const float *b_base = B + (int64_t)tile_n * kTile;
+  float4 ra[2], rb[2];
+  auto load_chunk = [&](int64_t k0) {
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int f = tid + 256 * m;
+      const int64_t row = k0 + (f >> 5);
+      const bool ok = row < ke;
+      const int64_t rr = ok ? row : kb;  // a valid row, zeroed below
+      const float4 va = *reinterpret_cast<const float4 *>(a_base + rr * lda + 4 * (f & 31));
+      const float4 vb = *reinterpret_cast<const float4 *>(b_base + rr * ldb + 4 * (f & 31));
+      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+      ra[m] = ok ? va : z;
+      rb[m] = ok ? vb : z;
+    }
+  };
+  auto store_chunk = [&]() {
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int f = tid + 256 * m;
+      const int row = f >> 5, c4 = f & 31;
+      const int off = tn_x6_off(row, c4 >> 1) + 8 * (c4 & 1);
+#pragma unroll
+      for (int op = 0; op < 2; ++op) {
+        const float4 v = op ? rb[m] : ra[m];
+        uint32_t hi[2], mid[2], lo[2];
+        split3_pair(f32x2{v.x, v.y}, hi[0], mid[0], lo[0]);
+        split3_pair(f32x2{v.z, v.w}, hi[1], mid[1], lo[1]);
+        char *img = lds + op * 3 * kTnX6Img + off;
+        *reinterpret_cast<uint2 *>(img) = make_uint2(hi[0], hi[1]);
+        *reinterpret_cast<uint2 *>(img + kTnX6Img) = make_uint2(mid[0], mid[1]);
+        *reinterpret_cast<uint2 *>(img + 2 * kTnX6Img) = make_uint2(lo[0], lo[1]);
+      }
+    }
+  };
+
+  // fragment addresses: lane = 16 g + 4 q + p reads rows 8 h + q (+ 4) and
+  // chunk (col0 >> 3) + 2 (g & 1) + (p >> 1), half p & 1
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  auto frag_off = [&](int col0, int second) {
+    const int row = 8 * h + q + 4 * second;
+    return tn_x6_off(row, (col0 >> 3) + 2 * (g & 1) + (p >> 1)) + 8 * (p & 1);
+  };
+  int offa[2][2], offb[2][2];  // [tile][read]
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      offa[t][r] = frag_off(wi * 64 + 32 * t, r);
+      offb[t][r] = 3 * kTnX6Img + frag_off(wj * 64 + 32 * t, r);
+    }
+  auto read8 = [&](const int (&o)[2], int term) {
+    const v4i16 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_v4i16_t *)(lds + o[0] + term * kTnX6Img));
+    const v4i16 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_v4i16_t *)(lds + o[1] + term * kTnX6Img));
+    const short y[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+    return __builtin_bit_cast(bf16x8, y);
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][s2][r] = 0.0f;
+
+  const int64_t nchunks = (ke - kb + kTnX6Rows - 1) / kTnX6Rows;
+  if (nchunks > 0) load_chunk(kb);
+  for (int64_t c = 0; c < nchunks; ++c) {
+    __syncthreads();  // the previous chunk's fragments are read
+    store_chunk();
+    if (c + 1 < nchunks) load_chunk(kb + (c + 1) * kTnX6Rows);
+    __syncthreads();
+    bf16x8 fa[2][3], fb[2][3];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int term = 0; term < 3; ++term) {
+        fa[t][term] = read8(offa[t], term);
+        fb[t][term] = read8(offb[t], term);
+      }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+        acc[t][s2] = mfma_x6(fa[t][0], fa[t][1], fa[t][2], fb[s2][0], fb[s2][1], fb[s2][2],
+                             acc[t][s2]);
+  }
+
+  float *slab = partial + (int64_t)blockIdx.y * M * N;
+  const int i0 = tile_m * kTile + wi * 64, j0 = tile_n * kTile + wj * 64;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = i0 + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        slab[(int64_t)row * N + j0 + s2 * 32 + lc] = acc[t][s2][r];
+      }
+}
+
+
+
 template <int BK, int WPS>
 __global__ __launch_bounds__(256, WPS) void gemm_tn_lds_kernel(
     const float *__restrict__ A, int64_t lda, const float *__restrict__ B, int64_t ldb,
@@ -309,7 +502,8 @@ int gemm_splits(int64_t K, int M, int N) {
   // or x 2 for the LDS-staged kernel (64 KB of LDS each); at least 64 rows of
   // K per split (partials: splits x 64 KB per tile)
   const int tiles = ((M + kTile - 1) / kTile) * ((N + kTile - 1) / kTile);
-  int64_t s = (tn_lds(M, N) ? 256 * tn_lds_wgs() : 768) / (tiles > 0 ? tiles : 1);
+  const int per_cu = !tn_lds(M, N) ? 3 : g_gemm_precision == PREC_BF16X6 ? 3 : tn_lds_wgs();
+  int64_t s = 256 * per_cu / (tiles > 0 ? tiles : 1);
   int64_t max_s = (K + 63) / 64;
   if (s > max_s) s = max_s;
   if (s < 1) s = 1;
@@ -365,7 +559,10 @@ extern "C" int mgcn_gemm_tn(int64_t K, int32_t M, int32_t N, const float *A, int
   } else if (tn_lds(M, N) && reinterpret_cast<uintptr_t>(A) % 16 == 0 &&
              reinterpret_cast<uintptr_t>(B) % 16 == 0 && lda % 4 == 0 && ldb % 4 == 0) {
     const dim3 grid(tiles_m * tiles_n, used);
-    if (g_tn_lds_variant == 1)
+    if (g_gemm_precision == PREC_BF16X6)
+      hipLaunchKernelGGL(gemm_tn_x6_kernel, grid, dim3(256), 0, s, A, lda, B, ldb, K, M, N, kps,
+                         tiles_n, partial);
+    else if (g_tn_lds_variant == 1)
       hipLaunchKernelGGL((gemm_tn_lds_kernel<32, 2>), grid, dim3(256), 0, s, A, lda, B, ldb, K, M,
                          N, kps, tiles_n, partial);
     else if (g_tn_lds_variant == 2)
@@ -374,7 +571,7 @@ extern "C" int mgcn_gemm_tn(int64_t K, int32_t M, int32_t N, const float *A, int
     else
       hipLaunchKernelGGL((gemm_tn_lds_kernel<64, 1>), grid, dim3(256), 0, s, A, lda, B, ldb, K, M,
                          N, kps, tiles_n, partial);
-    if (int rc = check_launch("gemm_tn_lds_kernel")) return rc;
+    if (int rc = check_launch("gemm_tn_lds/x6_kernel")) return rc;
   } else {
     hipLaunchKernelGGL(gemm_tn_partial_kernel, dim3(tiles_m * tiles_n, used), dim3(256), 0, s, A,
                        lda, B, ldb, K, M, N, kps, tiles_n, partial);
@@ -420,35 +617,59 @@ constexpr int kNNThreads = 64 * kNNWaves;
 constexpr int kNNMaxGrid = 1024;  // colsum partial slots
 constexpr int EPI_STORE = 0, EPI_RELU = 1, EPI_RELU_DIV = 2;  // DIV: C stored / row_div
 
-template <int K, int NT, int EPI>
-__global__ __launch_bounds__(kNNThreads, 2) void gemm_nn_kernel(
+template <int K, int NT, int P>
+constexpr int nn_lds_bytes() {
+  return P == PREC_BF16X6 ? 3 * NT * 32 * (K + 8) * 2 : NT * 32 * (K + 4) * 4;
+}
+
+template <int K, int NT, int EPI, int P>
+__global__ __launch_bounds__(kNNThreads, P == PREC_BF16X6 ? 1 : 2) void gemm_nn_kernel(
     const float *__restrict__ A, int64_t lda, const float *__restrict__ B, int64_t sbk,
     int64_t sbn, float *__restrict__ C, int64_t ldc, int64_t M, int N,
-    const float *__restrict__ Z, int64_t ldz, const float *__restrict__ row_div,
+    const uint32_t *__restrict__ relu_mask, const float *__restrict__ row_div,
     float *__restrict__ colsum_partial) {
   constexpr int KH = K / 2;              // k per lane half
   constexpr int S4 = KH / 4;             // float4 steps per 32-row subtile
   constexpr int GS = (K == 32) ? 2 : 1;  // subtiles per unit (>= 8 steps per unit)
   constexpr int S = GS * S4;             // float4 steps per unit
-  constexpr int LDB = K + 4;             // B^T row stride in LDS (floats)
-  __shared__ __attribute__((aligned(16))) float BT[NT * 32 * LDB];
+  constexpr int LDB = K + 4;             // f32: B^T row stride in LDS (floats)
+  constexpr int LDK = K + 8;             // bf16x6: split-B^T row stride (bf16)
+  __shared__ __attribute__((aligned(16))) char smem[nn_lds_bytes<K, NT, P>()];
+  float *BT = reinterpret_cast<float *>(smem);    // f32: [n][LDB]
+  __bf16 *BS = reinterpret_cast<__bf16 *>(smem);  // bf16x6: [term][n][LDK]
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 5, lc = lane & 31;
 
-  // B^T into LDS, columns past N zero
-  for (int idx = tid; idx < NT * 32 * (K / 4); idx += kNNThreads) {
-    const int n = idx / (K / 4), k4 = (idx % (K / 4)) * 4;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (n < N) {
-      const float *bp = B + (int64_t)k4 * sbk + (int64_t)n * sbn;
-      v.x = bp[0];
-      v.y = bp[sbk];
-      v.z = bp[2 * sbk];
-      v.w = bp[3 * sbk];
+  if constexpr (P == PREC_BF16X6) {
+    // B^T split into its three bf16 terms, 8 k per item; columns past N zero
+    for (int idx = tid; idx < NT * 32 * (K / 8); idx += kNNThreads) {
+      const int n = idx / (K / 8), k8 = (idx % (K / 8)) * 8;
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        v[j] = (n < N) ? B[(int64_t)(k8 + j) * sbk + (int64_t)n * sbn] : 0.0f;
+      bf16x8 th, tm, tl;
+      split3_bf16(v, th, tm, tl);
+      *reinterpret_cast<bf16x8 *>(&BS[(0 * NT * 32 + n) * LDK + k8]) = th;
+      *reinterpret_cast<bf16x8 *>(&BS[(1 * NT * 32 + n) * LDK + k8]) = tm;
+      *reinterpret_cast<bf16x8 *>(&BS[(2 * NT * 32 + n) * LDK + k8]) = tl;
     }
-    *reinterpret_cast<float4 *>(&BT[n * LDB + k4]) = v;
+  } else {
+    // B^T into LDS, columns past N zero
+    for (int idx = tid; idx < NT * 32 * (K / 4); idx += kNNThreads) {
+      const int n = idx / (K / 4), k4 = (idx % (K / 4)) * 4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (n < N) {
+        const float *bp = B + (int64_t)k4 * sbk + (int64_t)n * sbn;
+        v.x = bp[0];
+        v.y = bp[sbk];
+        v.z = bp[2 * sbk];
+        v.w = bp[3 * sbk];
+      }
+      *reinterpret_cast<float4 *>(&BT[n * LDB + k4]) = v;
+    }
   }
   __syncthreads();
 
@@ -470,7 +691,11 @@ __global__ __launch_bounds__(kNNThreads, 2) void gemm_nn_kernel(
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int st = part * 8 + i;
+#ifdef X6_NOLOAD
+      bk[i] = make_float4((float)st, (float)i, 1.0f, (float)rp[0][0].x * 0.0f);
+#else
       bk[i] = rp[st / S4][st % S4];
+#endif
     }
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -487,7 +712,71 @@ __global__ __launch_bounds__(kNNThreads, 2) void gemm_nn_kernel(
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[g][j][r] = 0.0f;
   };
+  // bf16x6: lane (h, lc) fragment of k-step ks covers k = h KH + 8 ks + j
+  // (j = 0..7) of A row lc and of B^T row j * 32 + lc: two float4 of the
+  // burst, one ds_read_b128 per term and column tile.
+  const __bf16 *bs_lane = &BS[lc * LDK + h * KH];
+  // Software pipeline over the burst's 4 k-steps x NT column tiles: the next
+  // tile's three B fragments (ds_read_b128) and the next k-step's A split
+  // (VALU) are issued before the current tile's six MFMAs, double-buffered
+  // in registers, so LDS latency and split work hide under the MFMA chain.
+  auto compute_burst_x6 = [&](const float4 (&bk)[8], int part) {
+    constexpr int STEPS = 4;  // k-steps per burst (8 float4)
+    uint32_t ah[2][4], am[2][4], al[2][4];
+    bf16x8 bh[2], bm[2], bl[2];
+    auto split_pair = [&](int i, int p, int slot) {  // pair p of k-step i
+      const float4 v = bk[2 * i + (p >> 1)];
+      const f32x2 x = (p & 1) ? f32x2{v.z, v.w} : f32x2{v.x, v.y};
+      split3_pair(x, ah[slot][p], am[slot][p], al[slot][p]);
+    };
+    auto load_b = [&](int i, int j, int slot) {
+      const int ks = ((part * 8 + 2 * i) % S4) / 2;
+      const __bf16 *bp = bs_lane + j * 32 * LDK + 8 * ks;
+      bh[slot] = *reinterpret_cast<const bf16x8 *>(bp);
+      bm[slot] = *reinterpret_cast<const bf16x8 *>(bp + NT * 32 * LDK);
+      bl[slot] = *reinterpret_cast<const bf16x8 *>(bp + 2 * NT * 32 * LDK);
+    };
+    load_b(0, 0, 0);
+#pragma unroll
+    for (int p = 0; p < 4; ++p) split_pair(0, p, 0);
+#pragma unroll
+    for (int i = 0; i < STEPS; ++i) {
+      const int sub = (part * 8 + 2 * i) / S4;
+      const bf16x8 xh = __builtin_bit_cast(bf16x8, ah[i & 1]);
+      const bf16x8 xm = __builtin_bit_cast(bf16x8, am[i & 1]);
+      const bf16x8 xl = __builtin_bit_cast(bf16x8, al[i & 1]);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int t = i * NT + j;
+        // next tile's fragments and a share of the next k-step's split,
+        // interleaved with this tile's six MFMAs (MFMA, DS read, 2 VALU, ...)
+        if (t + 1 < STEPS * NT) load_b((t + 1) / NT, (t + 1) % NT, (t + 1) & 1);
+        if (i + 1 < STEPS) {
+#pragma unroll
+          for (int p = 0; p < 4; ++p)
+            if (p % NT == j) split_pair(i + 1, p, (i + 1) & 1);
+        }
+#ifdef X6_NOMFMA
+        acc[sub][j][0] += (float)xh[0] + (float)bh[t & 1][1] + (float)bm[t & 1][2] +
+                          (float)bl[t & 1][3] + (float)xm[4] + (float)xl[5];
+#else
+        acc[sub][j] = mfma_x6(xh, xm, xl, bh[t & 1], bm[t & 1], bl[t & 1], acc[sub][j]);
+#endif
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+          if (q < 3) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+          __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
   auto compute_burst = [&](const float4 (&bk)[8], int part) {
+    if constexpr (P == PREC_BF16X6) {
+      compute_burst_x6(bk, part);
+      return;
+    }
     float4 bcur[NT], bnxt[NT];
 #pragma unroll
     for (int j = 0; j < NT; ++j)
@@ -513,6 +802,22 @@ __global__ __launch_bounds__(kNNThreads, 2) void gemm_nn_kernel(
       for (int j = 0; j < NT; ++j) bcur[j] = bnxt[j];
     }
   };
+  // ReLU mask words of the unit's rows (EPI_RELU*): column n = 32 j + lc is
+  // bit 8 j + (lc >> 2) of word lc & 3, so a lane needs one word per row --
+  // 16 per subtile, loaded when the unit starts (in flight under the MFMAs)
+  uint32_t mword[GS][16];
+  auto load_mask = [&](int64_t unit) {
+    if constexpr (EPI != EPI_STORE) {
+#pragma unroll
+      for (int g = 0; g < GS; ++g)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          int64_t row = (unit * GS + g) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          row = row < M ? row : M - 1;
+          mword[g][r] = relu_mask[row * 4 + (lc & 3)];
+        }
+    }
+  };
   // epilogue; C/D map: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 h.
   // Addresses = lane pointer + wave-uniform row offset; full subtiles store
   // unguarded, the M tail per element.
@@ -525,16 +830,13 @@ __global__ __launch_bounds__(kNNThreads, 2) void gemm_nn_kernel(
       for (int j = 0; j < NT; ++j) {
         const int n = j * 32 + lc;
         const bool n_ok = n < N;
+        const int bit = 8 * j + (lc >> 2);
         float *cp = C + (r0 + 4 * h) * ldc + n;
-        const float *zp = (EPI != EPI_STORE) ? Z + (r0 + 4 * h) * ldz + n : nullptr;
         if (rows_full) {
           if constexpr (EPI != EPI_STORE) {
-            float zv[16];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) zv[r] = n_ok ? zp[((r & 3) + 8 * (r >> 2)) * ldz] : 0.0f;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-              const float v = (zv[r] > 0.0f) ? acc[g][j][r] : 0.0f;
+              const float v = ((mword[g][r] >> bit) & 1u) ? acc[g][j][r] : 0.0f;
               if (n_ok) {
                 csum[j] = __fadd_rn(csum[j], v);  // bias gradient: undivided
                 const int rr = (r & 3) + 8 * (r >> 2);
@@ -557,7 +859,7 @@ __global__ __launch_bounds__(kNNThreads, 2) void gemm_nn_kernel(
             if (n_ok && r0 + 4 * h + rr < M) {
               float v = acc[g][j][r];
               if constexpr (EPI != EPI_STORE) {
-                v = (zp[rr * ldz] > 0.0f) ? v : 0.0f;
+                v = ((mword[g][r] >> bit) & 1u) ? v : 0.0f;
                 csum[j] = __fadd_rn(csum[j], v);
                 if constexpr (EPI == EPI_RELU_DIV) v = __fdiv_rn(v, row_div[r0 + 4 * h + rr]);
               }
@@ -576,6 +878,7 @@ __global__ __launch_bounds__(kNNThreads, 2) void gemm_nn_kernel(
     for (; u < n_units; u += wstride) {
       const int64_t un = (u + wstride < n_units) ? u + wstride : u;  // last: harmless reload
       zero_acc();
+      load_mask(u);
       load_burst(u, 1, bank1);
       compute_burst(bank0, 0);
       load_burst(un, 0, bank0);
@@ -587,12 +890,14 @@ __global__ __launch_bounds__(kNNThreads, 2) void gemm_nn_kernel(
       const int64_t u1 = u + wstride;
       load_burst(u1 < n_units ? u1 : u, 0, bank1);
       zero_acc();
+      load_mask(u);
       compute_burst(bank0, 0);
       epilogue(u);
       if (u1 >= n_units) break;
       const int64_t u2 = u + 2 * wstride;
       load_burst(u2 < n_units ? u2 : u1, 0, bank0);
       zero_acc();
+      load_mask(u1);
       compute_burst(bank1, 0);
       epilogue(u1);
     }
@@ -615,13 +920,13 @@ __global__ __launch_bounds__(kNNThreads, 2) void gemm_nn_kernel(
   }
 }
 
-template <int K, int NT, int EPI>
+template <int K, int NT, int EPI, int P>
 int nn_blocks(int64_t M) {
   // resident capacity of this instantiation (queried once), capped by work
   static int per_cu = 0;
   if (per_cu == 0) {
     int b = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gemm_nn_kernel<K, NT, EPI>, kNNThreads,
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gemm_nn_kernel<K, NT, EPI, P>, kNNThreads,
                                                      0) != hipSuccess || b < 1)
       b = 1;
     per_cu = b;
@@ -635,41 +940,55 @@ int nn_blocks(int64_t M) {
   return (int)(g > 0 ? g : 1);
 }
 
-template <int K, int NT>
-int launch_nn_nt(int64_t M, int N, const float *A, int64_t lda, const float *B, int64_t sbk,
-                 int64_t sbn, float *C, int64_t ldc, int epi, const float *Z, int64_t ldz,
-                 const float *row_div, float *partial, int *grid_out, hipStream_t s) {
-  if (epi == EPI_RELU_DIV) {
-    const int g = nn_blocks<K, NT, EPI_RELU_DIV>(M);
-    hipLaunchKernelGGL((gemm_nn_kernel<K, NT, EPI_RELU_DIV>), dim3(g), dim3(kNNThreads), 0, s, A,
-                       lda, B, sbk, sbn, C, ldc, M, N, Z, ldz, row_div, partial);
-    *grid_out = g;
-  } else if (epi == EPI_RELU) {
-    const int g = nn_blocks<K, NT, EPI_RELU>(M);
-    hipLaunchKernelGGL((gemm_nn_kernel<K, NT, EPI_RELU>), dim3(g), dim3(kNNThreads), 0, s, A,
-                       lda, B, sbk, sbn, C, ldc, M, N, Z, ldz, row_div, partial);
-    *grid_out = g;
-  } else {
-    const int g = nn_blocks<K, NT, EPI_STORE>(M);
-    hipLaunchKernelGGL((gemm_nn_kernel<K, NT, EPI_STORE>), dim3(g), dim3(kNNThreads), 0, s, A,
-                       lda, B, sbk, sbn, C, ldc, M, N, Z, ldz, row_div, partial);
-    *grid_out = g;
-  }
+
+template <int K, int NT, int EPI, int P>
+int launch_nn_epi(int64_t M, int N, const float *A, int64_t lda, const float *B, int64_t sbk,
+                  int64_t sbn, float *C, int64_t ldc, const uint32_t *mask,
+                  const float *row_div, float *partial, int *grid_out, hipStream_t s) {
+  const int g = nn_blocks<K, NT, EPI, P>(M);
+  hipLaunchKernelGGL((gemm_nn_kernel<K, NT, EPI, P>), dim3(g), dim3(kNNThreads), 0, s, A, lda, B,
+                     sbk, sbn, C, ldc, M, N, mask, row_div, partial);
+  *grid_out = g;
   return check_launch("gemm_nn_kernel");
+}
+
+template <int K, int NT, int P>
+int launch_nn_nt(int64_t M, int N, const float *A, int64_t lda, const float *B, int64_t sbk,
+                 int64_t sbn, float *C, int64_t ldc, int epi, const uint32_t *Z,
+                 const float *rd, float *partial, int *grid_out, hipStream_t s) {
+  if (epi == EPI_RELU_DIV)
+    return launch_nn_epi<K, NT, EPI_RELU_DIV, P>(M, N, A, lda, B, sbk, sbn, C, ldc, Z, rd,
+                                                 partial, grid_out, s);
+  if (epi == EPI_RELU)
+    return launch_nn_epi<K, NT, EPI_RELU, P>(M, N, A, lda, B, sbk, sbn, C, ldc, Z, rd, partial,
+                                             grid_out, s);
+  return launch_nn_epi<K, NT, EPI_STORE, P>(M, N, A, lda, B, sbk, sbn, C, ldc, Z, rd, partial,
+                                            grid_out, s);
+}
+
+template <int K, int P>
+int launch_nn_p(int64_t M, int N, const float *A, int64_t lda, const float *B, int64_t sbk,
+                int64_t sbn, float *C, int64_t ldc, int epi, const uint32_t *Z,
+                const float *rd, float *partial, int *grid_out, hipStream_t s) {
+  const int nt = (N + 31) / 32;
+  if (nt == 1)
+    return launch_nn_nt<K, 1, P>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, rd, partial, grid_out, s);
+  if (nt == 2)
+    return launch_nn_nt<K, 2, P>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, rd, partial, grid_out, s);
+  if (nt == 3)
+    return launch_nn_nt<K, 3, P>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, rd, partial, grid_out, s);
+  return launch_nn_nt<K, 4, P>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, rd, partial, grid_out, s);
 }
 
 template <int K>
 int launch_nn(int64_t M, int N, const float *A, int64_t lda, const float *B, int64_t sbk,
-              int64_t sbn, float *C, int64_t ldc, int epi, const float *Z, int64_t ldz,
+              int64_t sbn, float *C, int64_t ldc, int epi, const uint32_t *Z,
               const float *rd, float *partial, int *grid_out, hipStream_t s) {
-  const int nt = (N + 31) / 32;
-  if (nt == 1)
-    return launch_nn_nt<K, 1>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, ldz, rd, partial, grid_out, s);
-  if (nt == 2)
-    return launch_nn_nt<K, 2>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, ldz, rd, partial, grid_out, s);
-  if (nt == 3)
-    return launch_nn_nt<K, 3>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, ldz, rd, partial, grid_out, s);
-  return launch_nn_nt<K, 4>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, ldz, rd, partial, grid_out, s);
+  if (g_gemm_precision == PREC_BF16X6)
+    return launch_nn_p<K, PREC_BF16X6>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, rd, partial,
+                                       grid_out, s);
+  return launch_nn_p<K, PREC_F32>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, rd, partial,
+                                  grid_out, s);
 }
 
 __global__ __launch_bounds__(256) void colsum_fold_kernel(const float *__restrict__ partial,
@@ -691,6 +1010,13 @@ __global__ __launch_bounds__(256) void colsum_fold_kernel(const float *__restric
 }
 
 }  // namespace
+
+int gemm_set_precision(int value) {
+  if (value != PREC_F32 && value != PREC_BF16X6) return MGCN_EINVAL;
+  g_gemm_precision = value;
+  return MGCN_OK;
+}
+
 }  // namespace mgcn
 
 extern "C" int mgcn_gemm_nn_supported(int32_t K, int32_t N) {
@@ -704,7 +1030,7 @@ extern "C" size_t mgcn_gemm_nn_workspace_bytes(int64_t M, int32_t N) {
 
 extern "C" int mgcn_gemm_nn(int64_t M, int32_t K, int32_t N, const float *A, int64_t lda,
                             const float *B, int64_t sbk, int64_t sbn, float *C, int64_t ldc,
-                            const float *Z, int64_t ldz, const float *row_div, float *colsum,
+                            const uint32_t *relu_mask, const float *row_div, float *colsum,
                             void *workspace, size_t workspace_bytes, void *stream) {
   clear_error();
   MGCN_REQUIRE(M >= 0 && K >= 0 && N >= 0, "mgcn_gemm_nn: negative size");
@@ -717,9 +1043,9 @@ extern "C" int mgcn_gemm_nn(int64_t M, int32_t K, int32_t N, const float *A, int
   MGCN_REQUIRE(A && B && C && lda >= K && ldc >= N, "mgcn_gemm_nn: bad A/B/C");
   MGCN_REQUIRE(lda % 4 == 0 && reinterpret_cast<uintptr_t>(A) % 16 == 0,
                "mgcn_gemm_nn: A must be 16-byte aligned with lda % 4 == 0");
-  const int epi = Z == nullptr ? EPI_STORE : row_div != nullptr ? EPI_RELU_DIV : EPI_RELU;
-  MGCN_REQUIRE(epi == EPI_STORE || colsum != nullptr, "mgcn_gemm_nn: Z given without colsum");
-  MGCN_REQUIRE(row_div == nullptr || Z != nullptr, "mgcn_gemm_nn: row_div needs Z");
+  const int epi = relu_mask == nullptr ? EPI_STORE : row_div != nullptr ? EPI_RELU_DIV : EPI_RELU;
+  MGCN_REQUIRE(epi == EPI_STORE || colsum != nullptr, "mgcn_gemm_nn: relu_mask given without colsum");
+  MGCN_REQUIRE(row_div == nullptr || relu_mask != nullptr, "mgcn_gemm_nn: row_div needs relu_mask");
   float *partial = nullptr;
   if (epi != EPI_STORE) {
     const size_t need = mgcn_gemm_nn_workspace_bytes(M, N);
@@ -732,11 +1058,11 @@ extern "C" int mgcn_gemm_nn(int64_t M, int32_t K, int32_t N, const float *A, int
   int rc;
   int grid = 0;
   if (K == 32)
-    rc = launch_nn<32>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, ldz, row_div, partial, &grid, s);
+    rc = launch_nn<32>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, relu_mask, row_div, partial, &grid, s);
   else if (K == 64)
-    rc = launch_nn<64>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, ldz, row_div, partial, &grid, s);
+    rc = launch_nn<64>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, relu_mask, row_div, partial, &grid, s);
   else
-    rc = launch_nn<128>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, ldz, row_div, partial, &grid, s);
+    rc = launch_nn<128>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, relu_mask, row_div, partial, &grid, s);
   if (rc || epi == EPI_STORE) return rc;
   hipLaunchKernelGGL(colsum_fold_kernel, dim3((N + 63) / 64), dim3(256), 0, s, partial,
                      (int64_t)grid, N, colsum);

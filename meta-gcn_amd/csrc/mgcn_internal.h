@@ -57,5 +57,6 @@ inline unsigned grid_for(int64_t work_items, int block) {
 
 // mgcn_set_option("gemm_tn_variant") -> gemm.hip
 int gemm_set_tn_variant(int value);
+int gemm_set_precision(int value);
 
 }  // namespace mgcn

@@ -69,6 +69,8 @@ struct SpmmArgs {
   const uint32_t *win_mask;  // bwd MAXM: winner bits per fwd slot ([nnz][ceil(F/32)])
   const int32_t *slot_map;   // bwd MAXM: the fwd slot of every bwd slot
   uint32_t *win_mask_out;    // fwd MAX (optional): winner bits of every fwd slot
+  uint32_t *relu_mask;       // fwd (optional, F <= 128): Y > 0 bits per row, 4 words,
+                             // bit b of word v <=> Y[row][4 b + v] > 0
   int mean;                // fwd: divide by max(deg,1)
   int relu;                // fwd
   int accumulate;          // bwd: Y += result
@@ -353,6 +355,17 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(const SpmmArgs a) {
           acc.v[j] = y;
         }
         store_f<VEC>(dst, acc);
+        if constexpr (VEC == 4 && G == 32) {
+          // ReLU mask for the dX GEMM epilogue: lane gl holds features 4 gl + j,
+          // so word j of the row is the group's 32 bits of one ballot
+          if (a.relu_mask != nullptr) {
+            uint32_t mw[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) mw[j] = (uint32_t)(__ballot(acc.v[j] > 0.0f) >> gbase);
+            if (gl == 0)
+              *reinterpret_cast<uint4 *>(a.relu_mask + row * 4) = make_uint4(mw[0], mw[1], mw[2], mw[3]);
+          }
+        }
         if constexpr (MODE == FWD_MAX) {
           if (a.argmax_out != nullptr) store_i<VEC>(a.argmax_out + row * a.F + f0, arg);
         }
@@ -773,6 +786,36 @@ int pick_vec(int32_t F, const void *p0, int64_t ld0, const void *p1, int64_t ld1
   return 1;
 }
 
+// ReLU mask of rows of Y (F <= 128; layout as SpmmArgs::relu_mask): two
+// rows per wave, lane gl of a row's 32 holds features 4 gl .. 4 gl + 3.
+// rows == NULL: rows 0 .. n - 1, else rows[0 .. n).
+__global__ __launch_bounds__(256) void relu_mask_kernel(int64_t n, int F, const float *__restrict__ Y,
+                                                        int64_t ldy, const int32_t *__restrict__ rows,
+                                                        uint32_t *__restrict__ mask) {
+  const int lane = threadIdx.x & 63;
+  const int gl = lane & 31, gbase = lane & 32;
+  const int64_t item = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+  const bool ok = item < n;
+  const int64_t row = !ok ? 0 : rows != nullptr ? (int64_t)rows[item] : item;
+  uint32_t mw[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int f = 4 * gl + j;
+    const bool pos = ok && f < F && Y[row * ldy + f] > 0.0f;
+    mw[j] = (uint32_t)(__ballot(pos) >> gbase);
+  }
+  if (ok && gl == 0) *reinterpret_cast<uint4 *>(mask + row * 4) = make_uint4(mw[0], mw[1], mw[2], mw[3]);
+}
+
+int launch_relu_mask(int64_t n, int F, const float *Y, int64_t ldy, const int32_t *rows,
+                     uint32_t *mask, hipStream_t stream) {
+  if (n <= 0) return MGCN_OK;
+  const int64_t blocks = (n + 7) / 8;
+  hipLaunchKernelGGL(relu_mask_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, n, F, Y, ldy,
+                     rows, mask);
+  return check_launch("relu_mask_kernel");
+}
+
 int g_force_vec = 0;  // tuning knobs (mgcn_set_option)
 int g_unroll = 8;
 int g_heavy_side = 1;  // heavy-row launch on a side stream (concurrent)
@@ -915,6 +958,16 @@ int launch_mode(SpmmArgs a, int vec, hipStream_t stream) {
                     : launch_g<1, MODE>(a, stream);
   }
   if (side != nullptr) MGCN_HIP_TRY(hipStreamWaitEvent(stream, side->join, 0));
+  if (rc == MGCN_OK && a.relu_mask != nullptr) {
+    // the lane-group kernel fuses the mask when a row is 32 lanes x 4
+    // floats; heavy rows and other layouts get it from Y afterwards
+    const int lanes = (a.F + vec - 1) / vec;
+    const bool fused = vec == 4 && lanes > 16 && lanes <= 32;
+    if (!fused)
+      rc = launch_relu_mask(a.n_rows, a.F, a.Y, a.ldy, nullptr, a.relu_mask, stream);
+    else if (a.n_heavy > 0)
+      rc = launch_relu_mask(a.n_heavy, a.F, a.Y, a.ldy, a.order, a.relu_mask, stream);
+  }
   return rc;
 }
 
@@ -969,6 +1022,10 @@ extern "C" int mgcn_set_option(const char *name, int value) {
     MGCN_REQUIRE(value >= 0 && value <= 2, "gemm_tn_variant must be 0, 1 or 2");
     return gemm_set_tn_variant(value);
   }
+  if (n == "gemm_precision") {
+    MGCN_REQUIRE(value == 0 || value == 1, "gemm_precision must be 0 (f32) or 1 (bf16x6)");
+    return gemm_set_precision(value);
+  }
   if (n == "heavy_side_stream") {
     MGCN_REQUIRE(value == 0 || value == 1, "heavy_side_stream must be 0 or 1");
     g_heavy_side = value;
@@ -987,10 +1044,13 @@ static int choose_vec(int32_t F, const void *p0, int64_t ld0, const void *p1, in
 extern "C" int mgcn_spmm_fwd(int64_t n_rows, int32_t F, const int64_t *rowptr, const int32_t *col,
                              const int32_t *eid, const float *w, const float *H, int64_t ldh,
                              float *Y, int64_t ldy, int reduce, const float *bias, int relu,
-                             int32_t *argmax, uint32_t *win_mask, const int32_t *order,
-                             int64_t n_heavy, int64_t n_giant, void *stream) {
+                             int32_t *argmax, uint32_t *win_mask, uint32_t *relu_mask,
+                             const int32_t *order, int64_t n_heavy, int64_t n_giant,
+                             void *stream) {
   clear_error();
   MGCN_REQUIRE(n_rows >= 0 && F >= 0, "mgcn_spmm_fwd: negative size");
+  MGCN_REQUIRE(relu_mask == nullptr || (relu && F <= 128),
+               "mgcn_spmm_fwd: relu_mask needs relu and F <= 128");
   MGCN_REQUIRE(reduce == MGCN_REDUCE_SUM || reduce == MGCN_REDUCE_MEAN || reduce == MGCN_REDUCE_MAX,
                "mgcn_spmm_fwd: bad reduce %d", reduce);
   if (n_rows == 0 || F == 0) return MGCN_OK;
@@ -1012,6 +1072,7 @@ extern "C" int mgcn_spmm_fwd(int64_t n_rows, int32_t F, const int64_t *rowptr, c
   a.bias = bias;
   a.argmax_out = argmax;
   a.win_mask_out = reduce == MGCN_REDUCE_MAX ? win_mask : nullptr;
+  a.relu_mask = relu_mask;
   MGCN_REQUIRE(order == nullptr || (0 <= n_giant && n_giant <= n_heavy && n_heavy <= n_rows),
                "spmm: need 0 <= n_giant <= n_heavy <= n_rows");
   a.order = order;
@@ -1027,6 +1088,15 @@ extern "C" int mgcn_spmm_fwd(int64_t n_rows, int32_t F, const int64_t *rowptr, c
   hipStream_t s = as_stream(stream);
   if (reduce == MGCN_REDUCE_MAX) return launch_mode<FWD_MAX>(a, vec, s);
   return launch_mode<FWD_SUM>(a, vec, s);
+}
+
+extern "C" int mgcn_relu_mask(int64_t n_rows, int32_t F, const float *Z, int64_t ldz,
+                              uint32_t *relu_mask, void *stream) {
+  clear_error();
+  MGCN_REQUIRE(n_rows >= 0 && F >= 0 && F <= 128, "mgcn_relu_mask: need 0 <= F <= 128");
+  if (n_rows == 0) return MGCN_OK;
+  MGCN_REQUIRE(Z && relu_mask && ldz >= F, "mgcn_relu_mask: bad arguments");
+  return launch_relu_mask(n_rows, F, Z, ldz, nullptr, relu_mask, as_stream(stream));
 }
 
 extern "C" int mgcn_spmm_bwd(int64_t n_rows, int32_t F, const int64_t *rowptr_t,

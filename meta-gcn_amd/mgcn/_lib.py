@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmgcn.so")
 
 # constants mirrored from include/mgcn.h
-ABI_VERSION = 4
+ABI_VERSION = 5
 OK, EINVAL, EINDEX, EHIP, EWORKSPACE = 0, 1, 2, 3, 4
 REDUCE_SUM, REDUCE_MEAN, REDUCE_MAX = 0, 1, 2
 NORM_NONE, NORM_SM, NORM_RW = 0, 1, 2
@@ -41,7 +41,8 @@ SIGNATURES = {
     "mgcn_degree_norm": (_int, [_i64, _vp, _vp, _vp, _vp, _int, _vp, _vp, _vp]),
     "mgcn_edge_norm": (_int, [_i64, _i64, _vp, _vp, _vp, _int, _vp, _vp, _int, _vp, _vp]),
     "mgcn_spmm_fwd": (_int, [_i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _int, _vp,
-                             _int, _vp, _vp, _vp, _i64, _i64, _vp]),
+                             _int, _vp, _vp, _vp, _vp, _i64, _i64, _vp]),
+    "mgcn_relu_mask": (_int, [_i64, _i32, _vp, _i64, _vp, _vp]),
     "mgcn_spmm_bwd": (_int, [_i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _int,
                              _vp, _vp, _vp, _vp, _int, _vp, _i64, _i64, _vp]),
     "mgcn_slot_map_workspace_bytes": (_sz, [_i64]),
@@ -55,7 +56,7 @@ SIGNATURES = {
                             _vp]),
     "mgcn_gemm_nn_supported": (_int, [_i32, _i32]),
     "mgcn_gemm_nn_workspace_bytes": (_sz, [_i64, _i32]),
-    "mgcn_gemm_nn": (_int, [_i64, _i32, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _i64, _vp, _i64,
+    "mgcn_gemm_nn": (_int, [_i64, _i32, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _i64, _vp,
                             _vp, _vp, _vp, _sz, _vp]),
     "mgcn_colsum_workspace_bytes": (_sz, [_i64, _i32]),
     "mgcn_relu_bwd_colsum": (_int, [_i64, _i32, _vp, _vp, _int, _vp, _vp, _vp, _vp, _sz, _vp]),
@@ -77,7 +78,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
     with _lock:
         if _lib is not None and path is None:
             return _lib
-        p = path or LIB_PATH
+        p = path or os.environ.get("MGCN_LIB") or LIB_PATH  # MGCN_LIB: experiment builds
         if not os.path.exists(p):
             raise MgcnError(
                 f"libmgcn.so not found at {p}: build it with "

@@ -310,7 +310,7 @@ def train(train_ds, val_ds, test_ds, enc_sizes=(32,) * 8, residual_hop=0, deg_no
             loss = criterion(x, batch.y.long())
             loss.backward()
             opt.step()
-            loss_sum += float(loss)
+            loss_sum += loss.item()
             graphs += batch_size
         hist["train_loss"].append(loss_sum / max(graphs, 1))
         m = evaluate(model, val_loader, criterion, device)

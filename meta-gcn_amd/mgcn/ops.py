@@ -44,12 +44,15 @@ def _contig_f32(t: torch.Tensor, name: str) -> torch.Tensor:
 
 def spmm_fwd(view: CSRView, w: torch.Tensor | None, H: torch.Tensor, reduce: int,
              bias: torch.Tensor | None = None, relu: bool = False,
-             out: torch.Tensor | None = None, mask_plan: GraphPlan | None = None):
+             out: torch.Tensor | None = None, mask_plan: GraphPlan | None = None,
+             relu_mask: torch.Tensor | None = None):
     """Y[view.n_rows, F] = epi(reduce_k H[col_k] * w_k); returns (Y, argmax).
 
     Max with ``mask_plan`` (the plan ``view`` belongs to): instead of argmax
     the kernel writes every edge's winner bits at its slot (int32
-    [nnz, ceil(F/32)] bit patterns), returned in argmax's place."""
+    [nnz, ceil(F/32)] bit patterns), returned in argmax's place.
+    ``relu_mask`` (int32 [n_rows, 4], with relu and F <= 128) receives the
+    Y > 0 bits the dX GEMM's fused ReLU backward reads (:func:`gemm_nn`)."""
     lib = L.load()
     H = _contig_f32(H, "H")
     dev = L.require_device(H, view.rowptr, w, bias)
@@ -74,7 +77,7 @@ def spmm_fwd(view: CSRView, w: torch.Tensor | None, H: torch.Tensor, reduce: int
         rc = lib.mgcn_spmm_fwd(view.n_rows, F, L.ptr(view.rowptr), L.ptr(view.col),
                                L.ptr(view.eid), L.ptr(w), L.ptr(H), H.stride(0), L.ptr(Y),
                                Y.stride(0), reduce, L.ptr(bias), int(bool(relu)), L.ptr(argmax),
-                               L.ptr(mask), L.ptr(view.order), view.n_heavy,
+                               L.ptr(mask), L.ptr(relu_mask), L.ptr(view.order), view.n_heavy,
                                view.n_giant, L.stream_of(dev))
     if _TIMER is not None:
         _TIMER("spmm_fwd", False)
@@ -165,10 +168,26 @@ def gemm_nn_supported(K: int, N: int) -> bool:
     return bool(L.load().mgcn_gemm_nn_supported(int(K), int(N)))
 
 
+def make_relu_mask(Z: torch.Tensor) -> torch.Tensor:
+    """int32 [rows, 4]: bit b of word v set iff Z[i, 4 b + v] > 0 (F <= 128;
+    ``mgcn_relu_mask``)."""
+    lib = L.load()
+    Z = _contig_f32(Z, "Z")
+    dev = L.require_device(Z)
+    n, F = Z.shape
+    m = torch.empty(n, 4, dtype=torch.int32, device=dev)
+    with torch.cuda.device(dev):
+        rc = lib.mgcn_relu_mask(n, F, L.ptr(Z), Z.stride(0), L.ptr(m), L.stream_of(dev))
+    L.check(rc, "mgcn_relu_mask")
+    return m
+
+
 def gemm_nn(A: torch.Tensor, W: torch.Tensor, transpose_w: bool = False,
-            Z: torch.Tensor | None = None, row_div: torch.Tensor | None = None):
+            Z: torch.Tensor | None = None, row_div: torch.Tensor | None = None,
+            relu_mask: torch.Tensor | None = None):
     """C = A @ W (or A @ W^T) on libmgcn's tall-skinny MFMA kernel
-    (``mgcn_gemm_nn``).  With ``Z``: C = Z > 0 ? A @ W^T : 0 and the column sums
+    (``mgcn_gemm_nn``).  With ``relu_mask`` (from :func:`spmm_fwd` or
+    :func:`make_relu_mask`) or ``Z``: C = Z > 0 ? A @ W^T : 0 and the column sums
     of C are returned too (fused ReLU backward + bias gradient).  Returns
     (C, colsum or None)."""
     lib = L.load()
@@ -176,7 +195,9 @@ def gemm_nn(A: torch.Tensor, W: torch.Tensor, transpose_w: bool = False,
     if A.stride(0) % 4 or A.data_ptr() % 16:
         A = A.contiguous()
     W = W.detach()
-    dev = L.require_device(A, W, Z)
+    dev = L.require_device(A, W, Z, relu_mask)
+    if relu_mask is None and Z is not None:
+        relu_mask = make_relu_mask(Z)
     M, K = A.shape
     if transpose_w:
         N, Kw = W.shape
@@ -189,8 +210,10 @@ def gemm_nn(A: torch.Tensor, W: torch.Tensor, transpose_w: bool = False,
     C = torch.empty(M, N, dtype=torch.float32, device=dev)
     colsum = ws = None
     ws_bytes = 0
-    if Z is not None:
-        Z = _contig_f32(Z, "Z")
+    if relu_mask is not None:
+        if relu_mask.shape != (M, 4) or relu_mask.dtype != torch.int32:
+            raise ValueError(f"gemm_nn: relu_mask must be int32 [{M}, 4]")
+        relu_mask = relu_mask.contiguous()
         colsum = torch.empty(N, dtype=torch.float32, device=dev)
         ws_bytes = int(lib.mgcn_gemm_nn_workspace_bytes(M, N))
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
@@ -198,7 +221,7 @@ def gemm_nn(A: torch.Tensor, W: torch.Tensor, transpose_w: bool = False,
         _TIMER("gemm_nn", True)
     with torch.cuda.device(dev):
         rc = lib.mgcn_gemm_nn(M, K, N, L.ptr(A), A.stride(0), L.ptr(W), sbk, sbn, L.ptr(C),
-                              C.stride(0), L.ptr(Z), Z.stride(0) if Z is not None else 0,
+                              C.stride(0), L.ptr(relu_mask),
                               L.ptr(row_div), L.ptr(colsum), L.ptr(ws), ws_bytes,
                               L.stream_of(dev))
     if _TIMER is not None:
@@ -374,18 +397,26 @@ class _GCNStack(torch.autograd.Function):
     def forward(ctx, x, plan, norm, reduce, relus, *params):
         Ws, bs = params[0::2], params[1::2]
         h = x
-        inputs, outs, args = [], [], []
-        for W, b, relu in zip(Ws, bs, relus):
+        inputs, outs, args, rmasks = [], [], [], []
+        for i, (W, b, relu) in enumerate(zip(Ws, bs, relus)):
             inputs.append(h)
             H = _mm(h, W)
-            h, am = spmm_fwd(plan.fwd, norm.w_fwd, H, reduce, b, relu, mask_plan=plan)
+            # the ReLU mask the next layer's dX GEMM reads (16 B per row)
+            nxt = Ws[i + 1] if i + 1 < len(Ws) else None
+            rm = None
+            if relu and nxt is not None and gemm_nn_supported(nxt.size(1), nxt.size(0)):
+                rm = torch.empty(plan.fwd.n_rows, 4, dtype=torch.int32, device=H.device)
+            h, am = spmm_fwd(plan.fwd, norm.w_fwd, H, reduce, b, relu, mask_plan=plan,
+                             relu_mask=rm)
             outs.append(h)
             args.append(am)  # max: winner bits per edge (adjoint slot order)
+            rmasks.append(rm)
         ctx.plan, ctx.norm, ctx.reduce, ctx.relus = plan, norm, reduce, relus
         ctx.n_layers = len(Ws)
         ctx.has_bias = [b is not None for b in bs]
         ctx.save_for_backward(*inputs, *outs, *[a if a is not None else torch.empty(0)
-                                                for a in args], *Ws)
+                                                for a in args], *Ws,
+                              *[m if m is not None else torch.empty(0) for m in rmasks])
         return h
 
     @staticmethod
@@ -393,7 +424,7 @@ class _GCNStack(torch.autograd.Function):
         n = ctx.n_layers
         saved = ctx.saved_tensors
         inputs, outs = saved[:n], saved[n:2 * n]
-        args, Ws = saved[2 * n:3 * n], saved[3 * n:4 * n]
+        args, Ws, rmasks = saved[2 * n:3 * n], saved[3 * n:4 * n], saved[4 * n:5 * n]
         plan, norm, reduce, relus = ctx.plan, ctx.norm, ctx.reduce, ctx.relus
         gW = [None] * n
         gb = [None] * n
@@ -414,9 +445,10 @@ class _GCNStack(torch.autograd.Function):
             gW[l] = gemm_tn(inputs[l], dH)
             W = Ws[l]
             if l > 0:
-                fused = relus[l - 1] and gemm_nn_supported(W.size(1), W.size(0))
+                fused = relus[l - 1] and rmasks[l - 1].numel() > 0
                 if fused:
-                    dY, db = gemm_nn(dH, W, transpose_w=True, Z=outs[l - 1], row_div=rd)
+                    dY, db = gemm_nn(dH, W, transpose_w=True, relu_mask=rmasks[l - 1],
+                                     row_div=rd)
                     if not ctx.has_bias[l - 1]:
                         db = None
                 else:

@@ -1,4 +1,7 @@
-"""Microbenchmark of the feature-transform GEMMs at config-2 shape (M = 1M, F = 128)."""
+"""Microbenchmark of the feature-transform GEMMs at config-2 shape (M = 1M,
+F = 128), per product arithmetic (gemm_precision 0 = f32 MFMA, 1 = bf16x6),
+with the error against an fp64 product normalised by |A| |B| (the scale of
+an fp32 rounding bound)."""
 import json
 import os
 import sys
@@ -8,8 +11,15 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "meta-gcn_amd")]
 import torch  # noqa: E402
 
 from mgcn._lib import set_option  # noqa: E402
-from mgcn.ops import gemm_nn, gemm_tn  # noqa: E402
+from mgcn.ops import gemm_nn, gemm_tn, make_relu_mask  # noqa: E402
 from bench_spmm import time_it  # noqa: E402
+
+
+def norm_err(C, A, B):
+    """max |C - A B| / (|A| |B|) elementwise, products in fp64."""
+    ref = A.double() @ B.double()
+    scale = A.double().abs() @ B.double().abs()
+    return float(((C.double() - ref).abs() / scale.clamp_min(1e-300)).max())
 
 
 def main():
@@ -19,18 +29,27 @@ def main():
     dH = torch.randn(M, F, device=dev)
     Z = torch.randn(M, F, device=dev)
     W = torch.randn(F, F, device=dev)
+    RM = make_relu_mask(Z)
     fl = 2.0 * M * F * F
-    for name, fn in [("gemm_nn", lambda: gemm_nn(X, W)),
-                     ("gemm_nn_t_relu", lambda: gemm_nn(dH, W, transpose_w=True, Z=Z)),
-                     ("gemm_tn", lambda: gemm_tn(X, dH)),
-                     ("gemm_tn_v1", lambda: gemm_tn(X, dH)),
-                     ("gemm_tn_v2", lambda: gemm_tn(X, dH)),
-                     ("torch_mm", lambda: torch.matmul(X, W)),
+    s = 65536
+    for prec in (0, 1):
+        set_option("gemm_precision", prec)
+        errs = {"nn": norm_err(gemm_nn(X[:s], W)[0], X[:s], W),
+                "tn": norm_err(gemm_tn(X[:s], dH[:s]), X[:s].t(), dH[:s])}
+        for name, fn in [("gemm_nn", lambda: gemm_nn(X, W)),
+                         ("gemm_nn_t_relu", lambda: gemm_nn(dH, W, transpose_w=True, relu_mask=RM)),
+                         ("gemm_tn", lambda: gemm_tn(X, dH))]:
+            med, mn = time_it(fn, 20)
+            print(json.dumps({"kernel": name, "precision": ["f32", "bf16x6"][prec], "ms": med,
+                              "min_ms": mn, "tflops": fl / med / 1e9,
+                              "norm_err": errs["tn" if name == "gemm_tn" else "nn"]}), flush=True)
+    errs = {"nn": norm_err(torch.matmul(X[:s], W), X[:s], W),
+            "tn": norm_err(torch.matmul(X[:s].t(), dH[:s]), X[:s].t(), dH[:s])}
+    for name, fn in [("torch_mm", lambda: torch.matmul(X, W)),
                      ("torch_tn", lambda: torch.matmul(X.t(), dH))]:
-        set_option("gemm_tn_variant", int(name[-1]) if name.startswith("gemm_tn_v") else 0)
         med, mn = time_it(fn, 20)
-        print(json.dumps({"kernel": name, "ms": med, "min_ms": mn, "tflops": fl / med / 1e9}),
-              flush=True)
+        print(json.dumps({"kernel": name, "ms": med, "min_ms": mn, "tflops": fl / med / 1e9,
+                          "norm_err": errs["tn" if name == "torch_tn" else "nn"]}), flush=True)
 
 
 if __name__ == "__main__":

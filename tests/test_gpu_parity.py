@@ -238,12 +238,22 @@ def test_config2_full_size_forward_backward_bitwise(cuda, oracle):
 
 
 # ----------------------------------------------------------------- dense
+@pytest.fixture(params=[1, 0], ids=["bf16x6", "f32"])
+def gemm_precision(request):
+    """Both product arithmetics of the dense GEMMs (bf16x6 is the default)."""
+    import mgcn
+    mgcn.set_option("gemm_precision", request.param)
+    yield request.param
+    mgcn.set_option("gemm_precision", 1)
+
+
 @pytest.mark.parametrize("K,M,N", [(1_000_000, 128, 128), (4097, 128, 128), (3000, 7, 130),
                                    (50, 32, 2), (0, 4, 4), (286_214, 32, 32), (286_214, 2, 32),
-                                   (1001, 17, 5)])
-def test_gemm_tn_matches_fp64(cuda, K, M, N):
-    """dW = A^T B on fp32 MFMA (exact f32 products, f32 accumulation in a
-    different order than any BLAS): |err| <= 1e-5 * sum_k |a_k b_k| + 1e-6."""
+                                   (1001, 17, 5), (77, 128, 256), (1_000_003, 128, 128)])
+def test_gemm_tn_matches_fp64(cuda, K, M, N, gemm_precision):
+    """dW = A^T B (f32 MFMA: exact f32 products; bf16x6: the exact three-term
+    bf16 split, six products on bf16 MFMA; f32 accumulation in a different
+    order than any BLAS): |err| <= 1e-5 * sum_k |a_k b_k| + 1e-6."""
     from mgcn.ops import gemm_tn
     g = torch.Generator(device=cuda).manual_seed(K + M)
     A = torch.randn(K, M, device=cuda, generator=g)
@@ -256,11 +266,67 @@ def test_gemm_tn_matches_fp64(cuda, K, M, N):
     assert torch.equal(C, C2)  # deterministic
 
 
+def test_gemm_bf16x6_error_at_fp32_level(cuda):
+    """The bf16x6 products are no less accurate than exact-f32 MFMA: max
+    error / (|A| |B|) against fp64 within 2x of the f32 form's (measured:
+    3e-7 vs 5e-7 for X W at K = 128), on operands spanning 2^-40..2^40."""
+    import mgcn
+    from mgcn.ops import gemm_nn, gemm_tn
+    g = torch.Generator(device=cuda).manual_seed(5)
+    A = torch.randn(65536, 128, device=cuda, generator=g)
+    A = A * torch.exp2(torch.randint(-40, 40, A.shape, device=cuda, generator=g).float())
+    W = torch.randn(128, 128, device=cuda, generator=g)
+    B = torch.randn(65536, 128, device=cuda, generator=g)
+    errs = {}
+    for prec in (0, 1):
+        mgcn.set_option("gemm_precision", prec)
+        C = gemm_nn(A, W)[0].double()
+        D = gemm_tn(A, B).double()
+        e_nn = ((C - A.double() @ W.double()).abs() / (A.double().abs() @ W.double().abs())).max()
+        e_tn = ((D - A.double().t() @ B.double()).abs() /
+                (A.double().abs().t() @ B.double().abs())).max()
+        errs[prec] = (float(e_nn), float(e_tn))
+    mgcn.set_option("gemm_precision", 1)
+    assert errs[1][0] <= 2 * errs[0][0] + 1e-7, errs
+    assert errs[1][1] <= 2 * errs[0][1] + 1e-7, errs
+
+
+def test_relu_mask_layout(cuda, oracle):
+    """mgcn_relu_mask / the SpMM's fused mask: bit b of word v <=> Z[i, 4b+v] > 0,
+    for the fused F = 128 rows, heavy rows and other F."""
+    from mgcn.ops import make_relu_mask
+    import mgcn
+    g = torch.Generator().manual_seed(3)
+    for F in (128, 100, 64, 32, 7):
+        Z = torch.randn(1000, F, generator=g)
+        Z[::7] = 0.0
+        m = make_relu_mask(Z.to(cuda)).cpu().numpy().view(np.uint32)
+        ref = np.zeros((1000, 4), np.uint32)
+        pos = (Z.numpy() > 0)
+        for f in range(F):
+            ref[:, f & 3] |= pos[:, f].astype(np.uint32) << np.uint32(f >> 2)
+        np.testing.assert_array_equal(m, ref)
+    # fused in the forward SpMM, including heavy rows (star centres)
+    N = 3000
+    s = torch.randint(0, N, (20000,), generator=g)
+    d = torch.randint(0, N, (20000,), generator=g)
+    hub = torch.arange(0, 900)
+    ei = torch.stack([torch.cat([s, hub]), torch.cat([d, torch.zeros_like(hub)])])
+    for F in (128, 64):
+        H = torch.randn(N, F, generator=g).to(cuda)
+        plan = mgcn.build_plan(ei.to(cuda), N)
+        assert plan.fwd.n_heavy > 0
+        norm = plan.norm("sm")
+        rm = torch.empty(N, 4, dtype=torch.int32, device=cuda)
+        Y, _ = mgcn.ops.spmm_fwd(plan.fwd, norm.w_fwd, H, 0, None, True, relu_mask=rm)
+        assert torch.equal(rm, make_relu_mask(Y))
+
+
 @pytest.mark.parametrize("M,K,N,trans", [(1_000_000, 128, 128, False), (1_000_000, 128, 128, True),
                                          (1000, 64, 100, False), (777, 32, 7, True), (1, 128, 128, False),
                                          (286_214, 32, 32, False), (286_214, 32, 32, True),
                                          (5000, 32, 2, False), (3000, 64, 40, True)])
-def test_gemm_nn_matches_fp64(cuda, M, K, N, trans):
+def test_gemm_nn_matches_fp64(cuda, M, K, N, trans, gemm_precision):
     from mgcn.ops import gemm_nn
     g = torch.Generator(device=cuda).manual_seed(M + K + N)
     A = torch.randn(M, K, device=cuda, generator=g)

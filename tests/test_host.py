@@ -33,7 +33,7 @@ def test_library_exports_every_header_symbol():
 def test_abi_version_and_option_errors():
     import mgcn
     lib = mgcn.load()
-    assert lib.mgcn_abi_version() == mgcn._lib.ABI_VERSION == 4
+    assert lib.mgcn_abi_version() == mgcn._lib.ABI_VERSION == 5
     assert lib.mgcn_set_option(b"no_such_option", 1) == 1
     assert b"unknown option" in lib.mgcn_last_error()
     with pytest.raises(mgcn.MgcnError):
@@ -46,17 +46,22 @@ def test_c_abi_rejects_bad_arguments_without_touching_memory():
     import mgcn
     lib = mgcn.load()
     assert lib.mgcn_spmm_fwd(-1, 4, None, None, None, None, None, 4, None, 4, 0, None, 0, None,
-                             None, None, 0, 0, None) == 1
+                             None, None, None, 0, 0, None) == 1
     assert lib.mgcn_spmm_fwd(4, 4, None, None, None, None, None, 4, None, 4, 7, None, 0, None,
-                             None, None, 0, 0, None) == 1
+                             None, None, None, 0, 0, None) == 1
     assert b"bad reduce" in lib.mgcn_last_error()
     assert lib.mgcn_degree_norm(4, None, None, None, None, 9, None, None, None) == 1
     assert lib.mgcn_csr_build(None, None, -1, 0, 0, None, None, None, None, 0, None) == 1
     # zero-sized work is a successful no-op
     assert lib.mgcn_spmm_fwd(0, 4, None, None, None, None, None, 4, None, 4, 0, None, 0, None,
-                             None, None, 0, 0, None) == 0
+                             None, None, None, 0, 0, None) == 0
     assert lib.mgcn_csr_workspace_bytes(1000, 100) > 0
     assert lib.mgcn_gemm_tn_workspace_bytes(1 << 20, 128, 128) >= 128 * 128 * 4
+    # the ReLU mask needs relu and F <= 128
+    assert lib.mgcn_spmm_fwd(4, 256, None, None, None, None, None, 256, None, 256, 0, None, 1,
+                             None, None, 1, None, 0, 0, None) == 1
+    assert lib.mgcn_relu_mask(4, 129, None, 129, None, None) == 1
+    assert lib.mgcn_set_option(b"gemm_precision", 2) == 1
 
 
 def test_no_cpu_fallback():
