@@ -350,6 +350,11 @@ def main():
             if name.startswith("spmm"):
                 b = spmm_bytes(rows_local, nnz_local, F)
                 kern[name] = dict(s, bytes=b, gbs=b / (s["avg_ms"] * 1e-3) / 1e9)
+            elif name == "gemm_bwd":  # dW and dX: 4 rows F F flop; X, dH read, dX + mask
+                fl = 4.0 * rows_local * F * F
+                b = (12 * F + 16) * rows_local
+                kern[name] = dict(s, flop=fl, tflops=fl / (s["avg_ms"] * 1e-3) / 1e12, bytes=b,
+                                  gbs=b / (s["avg_ms"] * 1e-3) / 1e9)
             else:  # F x F feature transforms on MFMA: 2 rows F F flop per launch
                 fl = 2.0 * rows_local * F * F
                 kern[name] = dict(s, flop=fl, tflops=fl / (s["avg_ms"] * 1e-3) / 1e12)

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define MGCN_ABI_VERSION 5
+#define MGCN_ABI_VERSION 6
 
 /* return codes */
 #define MGCN_OK 0
@@ -265,6 +265,30 @@ int mgcn_gemm_nn(int64_t M, int32_t K, int32_t N, const float *A, int64_t lda,
                  const float *B, int64_t sbk, int64_t sbn, float *C, int64_t ldc,
                  const uint32_t *relu_mask, const float *row_div, float *colsum,
                  void *workspace, size_t workspace_bytes, void *stream);
+
+/* 1 if mgcn_gemm_bwd handles (F_in, F_out): 128 x 128 under bf16x6 precision. */
+int mgcn_gemm_bwd_supported(int32_t F_in, int32_t F_out);
+/* Bytes of scratch mgcn_gemm_bwd needs (split-K partials + column sums). */
+size_t mgcn_gemm_bwd_workspace_bytes(int64_t M, int32_t F_in, int32_t F_out);
+
+/*
+ * Both dense adjoints of H = X W (gcn_base_models.py:201) from one pass over
+ * X [M, F_in] (ldx) and dH [M, F_out] (lddh), W [F_in, F_out] row-major (ldw):
+ *   dW  = X^T dH          (accumulate != 0: dW += X^T dH; deterministic split-K)
+ *   dX  = dH W^T          (skipped when dX == NULL)
+ * With relu_mask (mgcn_spmm_fwd layout; the lower layer's output > 0) the
+ * ReLU backward and that layer's bias gradient are fused as in mgcn_gemm_nn:
+ *   dX = mask ? dH W^T : 0 (stored / row_div[m] when row_div != NULL),
+ *   colsum[n] = sum_m dX[m, n] (undivided).
+ * Replaces autograd's two matmul adjoints of `torch.matmul(x, self.weight_node)`
+ * plus the threshold_backward/sum of gcn_model.py:196 and
+ * gcn_base_models.py:240-241 (mgcn_gemm_tn + mgcn_gemm_nn in one launch).
+ */
+int mgcn_gemm_bwd(int64_t M, int32_t F_in, int32_t F_out, const float *X, int64_t ldx,
+                  const float *dH, int64_t lddh, const float *W, int64_t ldw,
+                  float *dW, int64_t lddw, int accumulate, float *dX, int64_t lddx,
+                  const uint32_t *relu_mask, const float *row_div, float *colsum,
+                  void *workspace, size_t workspace_bytes, void *stream);
 
 /* ----------------------------------------------------------- elementwise */
 

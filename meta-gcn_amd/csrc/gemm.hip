@@ -1068,3 +1068,398 @@ extern "C" int mgcn_gemm_nn(int64_t M, int32_t K, int32_t N, const float *A, int
                      (int64_t)grid, N, colsum);
   return check_launch("colsum_fold_kernel");
 }
+
+// ---------------------------------------------------------------------------
+// mgcn_gemm_bwd: both dense adjoints of H = X W from ONE pass over X and dH
+// (F_in = F_out = 128, bf16x6):
+//   dW  = X^T dH                                (split over the chip, as gemm_tn)
+//   dX  = relu'(X) * (dH W^T) [/ row_div]       (as gemm_nn with EPI_RELU*)
+//   colsum[n] = sum_m relu'(X) (dH W^T)[m, n]   (the lower layer's bias gradient)
+// The separate kernels read dH twice and X once (1.5 GB at config 2) plus
+// write dX; here every 32-row chunk of X and dH is loaded once, split into
+// its three bf16 terms in LDS, and feeds both products: 1 GB read + 0.5 GB
+// written per launch.
+//   * persistent grid of kBwGrid 512-thread workgroups (one per CU, fixed so
+//     the split-K fold order is fixed); chunk c goes to workgroup c % grid;
+//   * register prefetch two chunks ahead (two banks of 4 float4 per thread),
+//     LDS double buffer, one barrier per chunk;
+//   * dW: wave w owns the 32 x 32 tiles (w >> 1, 2 (w & 1) + {0, 1}) on
+//     v_mfma_f32_32x32x16_bf16 (operands by ds_read_b64_tr_b16 transposed
+//     reads of the row-major images, as gemm_tn_x6);
+//   * dX: wave w owns output columns 16 w .. 16 w + 15 of the chunk's 32 rows
+//     (two 16 x 16 tiles) on v_mfma_f32_16x16x32_bf16; its W^T fragments are
+//     split once and stay in registers (48 VGPRs), the dH fragments are
+//     ds_read_b128 row reads of the same image the dW pass reads transposed;
+//   * image swizzle: 16-B chunk ch of row r at ch ^ ((r & 3) << 2 | G[(r >> 2) & 3]),
+//     G = {0, 2, 3, 1}: conflict-free for the transposed reads (the four rows
+//     of a read differ in bits 2-3) AND for the 16x16x32 row reads (the lane
+//     groups {0-3, 12-15, 20-27} / {4-11, 16-19, 28-31} of ds_read_b128 land
+//     on 16 distinct chunks; with G = {0, 1, 2, 3} they are 2-way).
+// Roofline at M = 1M: 1.54 GB (X, dH read; dX written; 16 B/row mask) ->
+// 0.24 ms at 6.3 TB/s; 2 x 33.6 GFLOP x 6 bf16 products = 403 GFLOP -> 0.16 ms
+// at 2.5 PF: HBM-bound.
+
+namespace mgcn {
+namespace {
+
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+constexpr int kBwF = 128;
+constexpr int kBwRows = 32;
+constexpr int kBwWaves = 8;
+constexpr int kBwThreads = 64 * kBwWaves;
+constexpr int kBwGrid = 256;
+constexpr int kBwImg = kBwRows * 256;             // one bf16 term image of a chunk operand
+constexpr int kBwMaskOff = 6 * kBwImg;            // [32 rows][4] u32 ReLU mask words
+constexpr int kBwDivOff = kBwMaskOff + kBwRows * 16;  // [32] row divisors
+constexpr int kBwBuf = kBwDivOff + kBwRows * 4;
+
+__device__ __forceinline__ int bw_swz(int row) {
+  return ((row & 3) << 2) | ((0x78 >> (2 * ((row >> 2) & 3))) & 3);
+}
+__device__ __forceinline__ int bw_off(int row, int ch) { return 256 * row + 16 * (ch ^ bw_swz(row)); }
+
+__device__ __forceinline__ f32x4_t mfma16_x6(const bf16x8 &ah, const bf16x8 &am, const bf16x8 &al,
+                                            const bf16x8 &bh, const bf16x8 &bm, const bf16x8 &bl,
+                                            f32x4_t c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bm, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bm, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, c, 0, 0, 0);
+}
+
+struct BwBank {
+  u32x4 v[4];  // X rows q, 16 + q and dH rows q, 16 + q (q = tid >> 5), float4 tid & 31
+  u32x4 mk;    // mask words of row tid & 31
+  uint32_t rd; // row divisor of row tid & 31
+};
+
+// Buffer resource over [base, base + bytes): loads past it return 0 and
+// stores past it are dropped, so the chunk tail and the prefetch past the
+// last chunk need no branches (a branch around a load makes hipcc wait
+// vmcnt(0) for every load in flight, i.e. for the prefetch).  Inputs are
+// wave-uniform; readfirstlane makes that provable.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t bw_rsrc(const void *base, uint32_t bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  void *p = reinterpret_cast<void *>(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(p, 0, (int)__builtin_amdgcn_readfirstlane(bytes),
+                                           0x00020000);
+}
+
+template <int EPI, bool DX>
+__global__ __launch_bounds__(kBwThreads, 1) void gemm_bwd_kernel(
+    const float *__restrict__ X, int64_t ldx, const float *__restrict__ dH, int64_t lddh,
+    const float *__restrict__ W, int64_t ldw, int64_t M, float *__restrict__ dX, int64_t lddx,
+    const uint32_t *__restrict__ relu_mask, const float *__restrict__ row_div,
+    float *__restrict__ dw_partial, float *__restrict__ colsum_partial) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * kBwBuf];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5, lc = lane & 31;
+  const int l16 = lane & 15, g4 = lane >> 4;
+  const int64_t n_chunks = (M + kBwRows - 1) / kBwRows;
+  auto rows_in = [&](int64_t chunk) -> uint32_t {  // valid rows of a chunk (0 past the end)
+    const int64_t r = M - chunk * kBwRows;
+    return (uint32_t)(r <= 0 ? 0 : r >= kBwRows ? kBwRows : r);
+  };
+
+  // dX: W^T fragments of this wave's 16 columns, split once (B[k][n] = W[n][k])
+  bf16x8 wb[4][3];
+  if constexpr (DX) {
+    const float *wp = W + (int64_t)(16 * wave + l16) * ldw + 8 * g4;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = wp[32 * ks + j];
+      split3_bf16(v, wb[ks][0], wb[ks][1], wb[ks][2]);
+    }
+  }
+
+  const int ld_off_x = 4 * (int)((tid >> 5) * ldx + 4 * (tid & 31));
+  const int ld_off_h = 4 * (int)((tid >> 5) * lddh + 4 * (tid & 31));
+  auto load = [&](int64_t chunk, BwBank &b) {
+    const int64_t r0 = chunk * kBwRows;
+    const uint32_t rv = rows_in(chunk);
+    const auto rx = bw_rsrc(X + r0 * ldx, rv * (uint32_t)ldx * 4u);
+    const auto rh = bw_rsrc(dH + r0 * lddh, rv * (uint32_t)lddh * 4u);
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+#ifdef BW_NO_LOAD
+      b.v[m] = u32x4{(uint32_t)m, 1u, 2u, (uint32_t)r0};
+      b.v[2 + m] = u32x4{(uint32_t)m, 3u, 2u, (uint32_t)r0};
+      continue;
+#endif
+      b.v[m] = __builtin_amdgcn_raw_buffer_load_b128(rx, ld_off_x + m * 64 * (int)ldx, 0, 0);
+      b.v[2 + m] = __builtin_amdgcn_raw_buffer_load_b128(rh, ld_off_h + m * 64 * (int)lddh, 0, 0);
+    }
+    if constexpr (DX && EPI != EPI_STORE) {
+      const auto rm = bw_rsrc(relu_mask + r0 * 4, rv * 16u);
+      b.mk = __builtin_amdgcn_raw_buffer_load_b128(rm, 16 * (tid & 31), 0, 0);
+      if constexpr (EPI == EPI_RELU_DIV) {
+        const auto rd = bw_rsrc(row_div + r0, rv * 4u);
+        b.rd = __builtin_amdgcn_raw_buffer_load_b32(rd, 4 * (tid & 31), 0, 0);
+      }
+    }
+#ifndef BW_NO_LOAD_BARRIER
+    __builtin_amdgcn_sched_barrier(0);  // issue the prefetch here, not where the scheduler sinks it
+#endif
+  };
+  // staging of one float4 per thread (m = 0, 1: X rows q, 16 + q; 2, 3: dH),
+  // the mask / divisor words with the last part; called in pieces between the
+  // MFMA steps of the previous chunk so the split VALU work and the LDS
+  // writes run under them
+  auto stage_part = [&](const BwBank &b, char *buf, int m) {
+    const int c4 = tid & 31;
+    const int row = 16 * (m & 1) + (tid >> 5);
+    const int off = bw_off(row, c4 >> 1) + 8 * (c4 & 1);
+    const float4 v = __builtin_bit_cast(float4, b.v[m]);
+    uint32_t hi[2], mid[2], lo[2];
+#ifdef BW_NO_SPLIT
+    hi[0] = b.v[m][0]; hi[1] = b.v[m][1]; mid[0] = b.v[m][2]; mid[1] = b.v[m][3];
+    lo[0] = hi[0] ^ mid[1]; lo[1] = hi[1] ^ mid[0];
+#else
+    split3_pair(f32x2{v.x, v.y}, hi[0], mid[0], lo[0]);
+    split3_pair(f32x2{v.z, v.w}, hi[1], mid[1], lo[1]);
+#endif
+    char *img = buf + (m >> 1) * 3 * kBwImg + off;
+    *reinterpret_cast<uint2 *>(img) = make_uint2(hi[0], hi[1]);
+    *reinterpret_cast<uint2 *>(img + kBwImg) = make_uint2(mid[0], mid[1]);
+    *reinterpret_cast<uint2 *>(img + 2 * kBwImg) = make_uint2(lo[0], lo[1]);
+    if constexpr (DX && EPI != EPI_STORE) {
+      if (m == 3 && wave == 0) {
+        if (h == 0) *reinterpret_cast<u32x4 *>(buf + kBwMaskOff + 16 * lc) = b.mk;
+        if constexpr (EPI == EPI_RELU_DIV)
+          if (h == 1) *reinterpret_cast<uint32_t *>(buf + kBwDivOff + 4 * lc) = b.rd;
+      }
+    }
+  };
+  auto stage = [&](const BwBank &b, char *buf) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) stage_part(b, buf, m);
+  };
+
+  // dW fragment offsets (gemm_tn_x6 mapping): lane = 16 g + 4 q + p reads
+  // row 8 h + q (+ 4) of chunk (col0 >> 3) + 2 (g & 1) + (p >> 1), half p & 1
+  const int q = (lane >> 2) & 3, p = lane & 3;
+  auto frag_off = [&](int col0, int second) {
+    return bw_off(8 * h + q + 4 * second, (col0 >> 3) + 2 * (g4 & 1) + (p >> 1)) + 8 * (p & 1);
+  };
+  const int ti = wave >> 1, tj0 = 2 * (wave & 1);
+  int offa[2], offb[2][2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    offa[r] = frag_off(32 * ti, r);
+    offb[0][r] = 3 * kBwImg + frag_off(32 * tj0, r);
+    offb[1][r] = 3 * kBwImg + frag_off(32 * (tj0 + 1), r);
+  }
+  auto read8 = [&](const char *base, const int (&o)[2]) {
+    const v4i16 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16_t *)(base + o[0]));
+    const v4i16 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16_t *)(base + o[1]));
+    const short y[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+    return __builtin_bit_cast(bf16x8, y);
+  };
+
+  f32x16 accw[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) accw[s][r] = 0.0f;
+  float csum = 0.0f;
+  const int ncol = 16 * wave + l16;  // dX column of this lane
+  const int mword = ncol & 3, mbit = 8 * (ncol >> 5) + ((ncol & 31) >> 2);
+
+  auto compute = [&](int64_t chunk, const char *buf, const BwBank &nb, char *nbuf) {
+    // dW: two 16-row k-steps
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const char *kb = buf + ks * 16 * 256;
+      bf16x8 fa[3], fb[2][3];
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+        fa[t] = read8(kb + t * kBwImg, offa);
+        fb[0][t] = read8(kb + t * kBwImg, offb[0]);
+        fb[1][t] = read8(kb + t * kBwImg, offb[1]);
+      }
+#ifdef BW_NO_MFMA
+      for (int s = 0; s < 2; ++s)
+        accw[s][0] += (float)fa[0][0] + (float)fa[1][1] + (float)fa[2][2] + (float)fb[s][0][3] +
+                      (float)fb[s][1][4] + (float)fb[s][2][5];
+#else
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        accw[s] = mfma_x6(fa[0], fa[1], fa[2], fb[s][0], fb[s][1], fb[s][2], accw[s]);
+#endif
+      stage_part(nb, nbuf, ks);
+      if constexpr (!DX) stage_part(nb, nbuf, 2 + ks);
+    }
+    if constexpr (DX) {
+      f32x4_t acc[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[t][r] = 0.0f;
+      const char *hb = buf + 3 * kBwImg;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int off = bw_off(16 * t + l16, 4 * ks + g4);
+          const bf16x8 ah = *reinterpret_cast<const bf16x8 *>(hb + off);
+          const bf16x8 am = *reinterpret_cast<const bf16x8 *>(hb + kBwImg + off);
+          const bf16x8 al = *reinterpret_cast<const bf16x8 *>(hb + 2 * kBwImg + off);
+#ifdef BW_NO_MFMA
+          acc[t][0] += (float)ah[0] + (float)am[1] + (float)al[2] + (float)wb[ks][0][3] +
+                       (float)wb[ks][1][4] + (float)wb[ks][2][5];
+#else
+          acc[t] = mfma16_x6(ah, am, al, wb[ks][0], wb[ks][1], wb[ks][2], acc[t]);
+#endif
+          if (t == 1 && ks < 2) stage_part(nb, nbuf, 2 + ks);
+        }
+      // epilogue: lane holds rows 16 t + 4 g4 + r of column ncol; rows past M
+      // are zero (their loads returned 0) and their stores fall off the buffer
+      const int64_t r0 = chunk * kBwRows;
+      const auto rx = bw_rsrc(dX + r0 * lddx, rows_in(chunk) * (uint32_t)lddx * 4u);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int lr = 16 * t + 4 * g4 + r;
+          float v = acc[t][r];
+          if constexpr (EPI != EPI_STORE) {
+            const uint32_t wd = *reinterpret_cast<const uint32_t *>(buf + kBwMaskOff + 16 * lr + 4 * mword);
+            v = ((wd >> mbit) & 1u) ? v : 0.0f;
+            csum = __fadd_rn(csum, v);
+            if constexpr (EPI == EPI_RELU_DIV)
+              v = __fdiv_rn(v, *reinterpret_cast<const float *>(buf + kBwDivOff + 4 * lr));
+          }
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rx,
+                                                4 * (int)(lr * lddx + ncol), 0, 0);
+        }
+    }
+  };
+
+  BwBank b0, b1;
+  const int64_t c0 = blockIdx.x;
+  const int64_t G = gridDim.x;
+  load(c0, b0);
+  load(c0 + G, b1);
+  if (c0 < n_chunks) stage(b0, lds);
+  __syncthreads();
+  // iteration m: compute chunk c0 + m G from buffer m & 1, prefetch chunk
+  // m + 2 into the bank chunk m came from, stage chunk m + 1 into the other buffer
+  // (a chunk past the end stages zeros that are never read: no branches)
+  for (int64_t c = c0; c < n_chunks; c += 2 * G) {
+    load(c + 2 * G, b0);
+    compute(c, lds, b1, lds + kBwBuf);
+    __syncthreads();
+    if (c + G >= n_chunks) break;
+    load(c + 3 * G, b1);
+    compute(c + G, lds + kBwBuf, b0, lds);
+    __syncthreads();
+  }
+
+  // dW partial slab of this workgroup; C map: col = lc, row = (r & 3) + 8 (r >> 2) + 4 h
+  float *slab = dw_partial + (int64_t)blockIdx.x * kBwF * kBwF;
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = 32 * ti + (r & 3) + 8 * (r >> 2) + 4 * h;
+      slab[row * kBwF + 32 * (tj0 + s) + lc] = accw[s][r];
+    }
+  if constexpr (DX && EPI != EPI_STORE) {
+    // fold the four row groups of each column in fixed order
+    const float a = __fadd_rn(csum, __shfl_xor(csum, 16, 64));
+    const float b = __fadd_rn(a, __shfl_xor(a, 32, 64));
+    if (lane < 16) colsum_partial[(int64_t)blockIdx.x * kBwF + ncol] = b;
+  }
+}
+
+template <int EPI, bool DX>
+int launch_bwd(int grid, const float *X, int64_t ldx, const float *dH, int64_t lddh,
+               const float *W, int64_t ldw, int64_t M, float *dX, int64_t lddx,
+               const uint32_t *mask, const float *rd, float *dwp, float *csp, hipStream_t s) {
+  hipLaunchKernelGGL((gemm_bwd_kernel<EPI, DX>), dim3(grid), dim3(kBwThreads), 0, s, X, ldx, dH,
+                     lddh, W, ldw, M, dX, lddx, mask, rd, dwp, csp);
+  return check_launch("gemm_bwd_kernel");
+}
+
+}  // namespace
+}  // namespace mgcn
+
+extern "C" int mgcn_gemm_bwd_supported(int32_t F_in, int32_t F_out) {
+  return F_in == kBwF && F_out == kBwF && g_gemm_precision == PREC_BF16X6;
+}
+
+extern "C" size_t mgcn_gemm_bwd_workspace_bytes(int64_t M, int32_t F_in, int32_t F_out) {
+  (void)M;
+  return align_up((size_t)kBwGrid * (size_t)F_in * (size_t)F_out * 4, 256) +
+         align_up((size_t)kBwGrid * (size_t)F_in * 4, 256);
+}
+
+extern "C" int mgcn_gemm_bwd(int64_t M, int32_t F_in, int32_t F_out, const float *X, int64_t ldx,
+                             const float *dH, int64_t lddh, const float *W, int64_t ldw,
+                             float *dW, int64_t lddw, int accumulate, float *dX, int64_t lddx,
+                             const uint32_t *relu_mask, const float *row_div, float *colsum,
+                             void *workspace, size_t workspace_bytes, void *stream) {
+  clear_error();
+  MGCN_REQUIRE(M >= 0, "mgcn_gemm_bwd: negative size");
+  MGCN_REQUIRE(mgcn_gemm_bwd_supported(F_in, F_out),
+               "mgcn_gemm_bwd: unsupported F_in=%d F_out=%d (needs 128 x 128, bf16x6)", F_in, F_out);
+  MGCN_REQUIRE(dW != nullptr && lddw >= F_out, "mgcn_gemm_bwd: bad dW");
+  const int epi = relu_mask == nullptr ? EPI_STORE : row_div != nullptr ? EPI_RELU_DIV : EPI_RELU;
+  MGCN_REQUIRE(epi == EPI_STORE || (dX != nullptr && colsum != nullptr),
+               "mgcn_gemm_bwd: relu_mask needs dX and colsum");
+  MGCN_REQUIRE(row_div == nullptr || relu_mask != nullptr, "mgcn_gemm_bwd: row_div needs relu_mask");
+  hipStream_t s = as_stream(stream);
+  if (M == 0) {
+    if (!accumulate)
+      for (int32_t r = 0; r < F_in; ++r)
+        MGCN_HIP_TRY(hipMemsetAsync(dW + r * lddw, 0, sizeof(float) * F_out, s));
+    if (colsum) MGCN_HIP_TRY(hipMemsetAsync(colsum, 0, sizeof(float) * F_in, s));
+    return MGCN_OK;
+  }
+  MGCN_REQUIRE(X && dH && ldx >= F_in && lddh >= F_out && ldx % 4 == 0 && lddh % 4 == 0 &&
+                   reinterpret_cast<uintptr_t>(X) % 16 == 0 && reinterpret_cast<uintptr_t>(dH) % 16 == 0,
+               "mgcn_gemm_bwd: X/dH must be 16-byte aligned rows");
+  MGCN_REQUIRE(dX == nullptr || (W != nullptr && ldw >= F_out && lddx >= F_in),
+               "mgcn_gemm_bwd: bad W/dX");
+  const size_t need = mgcn_gemm_bwd_workspace_bytes(M, F_in, F_out);
+  if (workspace == nullptr || workspace_bytes < need) {
+    set_error("mgcn_gemm_bwd: workspace %zu < %zu", workspace_bytes, need);
+    return MGCN_EWORKSPACE;
+  }
+  float *dwp = static_cast<float *>(workspace);
+  float *csp = reinterpret_cast<float *>(static_cast<char *>(workspace) +
+                                         align_up((size_t)kBwGrid * F_in * F_out * 4, 256));
+  const int64_t n_chunks = (M + kBwRows - 1) / kBwRows;
+  const int grid = (int)(n_chunks < kBwGrid ? n_chunks : kBwGrid);
+  int rc;
+  if (dX == nullptr)
+    rc = launch_bwd<EPI_STORE, false>(grid, X, ldx, dH, lddh, W, ldw, M, dX, lddx, relu_mask,
+                                      row_div, dwp, csp, s);
+  else if (epi == EPI_RELU_DIV)
+    rc = launch_bwd<EPI_RELU_DIV, true>(grid, X, ldx, dH, lddh, W, ldw, M, dX, lddx, relu_mask,
+                                        row_div, dwp, csp, s);
+  else if (epi == EPI_RELU)
+    rc = launch_bwd<EPI_RELU, true>(grid, X, ldx, dH, lddh, W, ldw, M, dX, lddx, relu_mask,
+                                    row_div, dwp, csp, s);
+  else
+    rc = launch_bwd<EPI_STORE, true>(grid, X, ldx, dH, lddh, W, ldw, M, dX, lddx, relu_mask,
+                                     row_div, dwp, csp, s);
+  if (rc) return rc;
+  const int64_t MN = (int64_t)F_in * F_out;
+  hipLaunchKernelGGL(gemm_reduce_kernel, dim3((unsigned)((MN + 63) / 64)), dim3(256), 0, s, dwp,
+                     grid, MN, F_out, dW, lddw, accumulate);
+  if (int rc2 = check_launch("gemm_reduce_kernel")) return rc2;
+  if (epi == EPI_STORE) return MGCN_OK;
+  hipLaunchKernelGGL(colsum_fold_kernel, dim3((F_in + 63) / 64), dim3(256), 0, s, csp,
+                     (int64_t)grid, F_in, colsum);
+  return check_launch("colsum_fold_kernel");
+}

@@ -230,6 +230,58 @@ def gemm_nn(A: torch.Tensor, W: torch.Tensor, transpose_w: bool = False,
     return C, colsum
 
 
+def gemm_bwd_supported(F_in: int, F_out: int) -> bool:
+    return bool(L.load().mgcn_gemm_bwd_supported(int(F_in), int(F_out)))
+
+
+def gemm_bwd(x: torch.Tensor, dH: torch.Tensor, W: torch.Tensor, want_dx: bool = True,
+             relu_mask: torch.Tensor | None = None, row_div: torch.Tensor | None = None,
+             dW_out: torch.Tensor | None = None, accumulate: bool = False):
+    """Both adjoints of H = x @ W in one pass (``mgcn_gemm_bwd``, F_in = F_out
+    = 128): dW = x^T dH and dX = dH W^T -- with ``relu_mask`` the lower
+    layer's ReLU backward and bias-gradient column sums fused as in
+    :func:`gemm_nn`.  Returns (dW, dX or None, colsum or None)."""
+    lib = L.load()
+    x = _contig_f32(x, "x")
+    dH = _contig_f32(dH, "dH")
+    if x.stride(0) % 4 or x.data_ptr() % 16:
+        x = x.contiguous()
+    if dH.stride(0) % 4 or dH.data_ptr() % 16:
+        dH = dH.contiguous()
+    W = W.detach().contiguous()
+    dev = L.require_device(x, dH, W, relu_mask, row_div)
+    M, F_in = x.shape
+    F_out = dH.size(1)
+    if dH.size(0) != M or tuple(W.shape) != (F_in, F_out):
+        raise ValueError(f"gemm_bwd: x {tuple(x.shape)}, dH {tuple(dH.shape)}, W {tuple(W.shape)}")
+    dW = dW_out if dW_out is not None else torch.empty(F_in, F_out, dtype=torch.float32,
+                                                       device=dev)
+    dX = torch.empty(M, F_in, dtype=torch.float32, device=dev) if want_dx else None
+    colsum = None
+    if relu_mask is not None:
+        if not want_dx:
+            raise ValueError("gemm_bwd: relu_mask needs want_dx")
+        if relu_mask.shape != (M, 4) or relu_mask.dtype != torch.int32:
+            raise ValueError(f"gemm_bwd: relu_mask must be int32 [{M}, 4]")
+        relu_mask = relu_mask.contiguous()
+        colsum = torch.empty(F_in, dtype=torch.float32, device=dev)
+    ws_bytes = int(lib.mgcn_gemm_bwd_workspace_bytes(M, F_in, F_out))
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    if _TIMER is not None:
+        _TIMER("gemm_bwd", True)
+    with torch.cuda.device(dev):
+        rc = lib.mgcn_gemm_bwd(M, F_in, F_out, L.ptr(x), x.stride(0), L.ptr(dH), dH.stride(0),
+                               L.ptr(W), W.stride(0), L.ptr(dW), dW.stride(0),
+                               int(bool(accumulate)), L.ptr(dX),
+                               dX.stride(0) if dX is not None else F_in, L.ptr(relu_mask),
+                               L.ptr(row_div), L.ptr(colsum), L.ptr(ws), ws_bytes,
+                               L.stream_of(dev))
+    if _TIMER is not None:
+        _TIMER("gemm_bwd", False)
+    L.check(rc, "mgcn_gemm_bwd")
+    return dW, dX, colsum
+
+
 def _mm(x: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
     """x @ W on libmgcn when the shape is supported, else hipBLASLt."""
     if gemm_nn_supported(W.size(0), W.size(1)):
@@ -246,8 +298,9 @@ def _mm_t(dH: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
 
 class _Linear(torch.autograd.Function):
     """H = x @ W (gcn_base_models.py:201) with all three products on libmgcn's
-    fp32 MFMA kernels: forward and dX on mgcn_gemm_nn (tall-skinny), dW =
-    x^T dH -- a K = num_nodes reduction -- on the split-K mgcn_gemm_tn."""
+    MFMA kernels: forward on mgcn_gemm_nn (tall-skinny); backward dW = x^T dH
+    (a K = num_nodes reduction) and dX = dH W^T together in one pass of
+    mgcn_gemm_bwd at F = 128, else mgcn_gemm_tn (split-K) + mgcn_gemm_nn."""
 
     @staticmethod
     def forward(ctx, x, W):
@@ -259,6 +312,9 @@ class _Linear(torch.autograd.Function):
         x, W = ctx.saved_tensors
         dx = dW = None
         dH = dH.contiguous()
+        if ctx.needs_input_grad[1] and gemm_bwd_supported(W.size(0), W.size(1)):
+            dW, dx, _ = gemm_bwd(x, dH, W, want_dx=bool(ctx.needs_input_grad[0]))
+            return dx, dW
         if ctx.needs_input_grad[0]:
             dx = _mm_t(dH, W)
         if ctx.needs_input_grad[1]:
@@ -442,10 +498,18 @@ class _GCNStack(torch.autograd.Function):
             am = args[l] if args[l].numel() else None
             dH = spmm_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, adj, win_mask=am,
                           slot_map=plan.slot_map() if am is not None else None)
-            gW[l] = gemm_tn(inputs[l], dH)
             W = Ws[l]
+            fused = l > 0 and relus[l - 1] and rmasks[l - 1].numel() > 0
+            if fused and gemm_bwd_supported(W.size(0), W.size(1)):
+                # dW and dX (+ the lower layer's ReLU / bias gradient) in one pass
+                gW[l], dY, db = gemm_bwd(inputs[l], dH, W, relu_mask=rmasks[l - 1], row_div=rd)
+                gb[l - 1] = db if ctx.has_bias[l - 1] else None
+                continue
+            if l == 0 and not ctx.needs_input_grad[0] and gemm_bwd_supported(W.size(0), W.size(1)):
+                gW[l] = gemm_bwd(inputs[l], dH, W, want_dx=False)[0]  # dW alone, same pass shape
+                continue
+            gW[l] = gemm_tn(inputs[l], dH)
             if l > 0:
-                fused = relus[l - 1] and rmasks[l - 1].numel() > 0
                 if fused:
                     dY, db = gemm_nn(dH, W, transpose_w=True, relu_mask=rmasks[l - 1],
                                      row_div=rd)

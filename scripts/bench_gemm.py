@@ -11,7 +11,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "meta-gcn_amd")]
 import torch  # noqa: E402
 
 from mgcn._lib import set_option  # noqa: E402
-from mgcn.ops import gemm_nn, gemm_tn, make_relu_mask  # noqa: E402
+from mgcn.ops import gemm_bwd, gemm_nn, gemm_tn, make_relu_mask  # noqa: E402
 from bench_spmm import time_it  # noqa: E402
 
 
@@ -43,6 +43,14 @@ def main():
             print(json.dumps({"kernel": name, "precision": ["f32", "bf16x6"][prec], "ms": med,
                               "min_ms": mn, "tflops": fl / med / 1e9,
                               "norm_err": errs["tn" if name == "gemm_tn" else "nn"]}), flush=True)
+    set_option("gemm_precision", 1)
+    # fused adjoints: dW + dX (+ ReLU / bias colsum) from one pass; dW alone
+    for name, fn in [("gemm_bwd_relu", lambda: gemm_bwd(X, dH, W, relu_mask=RM)),
+                     ("gemm_bwd_dw_only", lambda: gemm_bwd(X, dH, W, want_dx=False))]:
+        med, mn = time_it(fn, 20)
+        by = (12 * F + 16) * M if "relu" in name else 8 * F * M
+        print(json.dumps({"kernel": name, "precision": "bf16x6", "ms": med, "min_ms": mn,
+                          "gbs": by / med / 1e6}), flush=True)
     errs = {"nn": norm_err(torch.matmul(X[:s], W), X[:s], W),
             "tn": norm_err(torch.matmul(X[:s].t(), dH[:s]), X[:s].t(), dH[:s])}
     for name, fn in [("torch_mm", lambda: torch.matmul(X, W)),

@@ -346,6 +346,55 @@ def test_gemm_nn_matches_fp64(cuda, M, K, N, trans, gemm_precision):
     assert torch.allclose(cs2.double(), ref_cs, rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("M", [1_000_000, 1_000_003, 4097, 31, 1, 0])
+def test_gemm_bwd_matches_fp64(cuda, M):
+    """Fused adjoints (mgcn_gemm_bwd): dW = X^T dH and dX = dH W^T within
+    1e-5 of the |.|-weighted fp64 sums; the ReLU / row-divisor epilogue
+    equals masking and dividing the plain dX; dW matches mgcn_gemm_tn's
+    bound, is deterministic and accumulates."""
+    from mgcn.ops import gemm_bwd, make_relu_mask
+    g = torch.Generator(device=cuda).manual_seed(M + 1)
+    X = torch.randn(M, 128, device=cuda, generator=g)
+    dH = torch.randn(M, 128, device=cuda, generator=g)
+    W = torch.randn(128, 128, device=cuda, generator=g)
+    dW, dX, cs = gemm_bwd(X, dH, W)
+    assert cs is None
+    ref_w = X.double().t() @ dH.double()
+    bound_w = X.double().abs().t() @ dH.double().abs()
+    assert ((dW.double() - ref_w).abs() <= 1e-5 * bound_w + 1e-6).all()
+    ref_x = dH.double() @ W.double().t()
+    bound_x = dH.double().abs() @ W.double().abs().t()
+    assert ((dX.double() - ref_x).abs() <= 1e-5 * bound_x + 1e-6).all()
+    # dW alone, repeat (deterministic), accumulate
+    dW2, none, _ = gemm_bwd(X, dH, W, want_dx=False)
+    assert none is None and torch.equal(dW, dW2)
+    acc = torch.ones(128, 128, device=cuda)
+    gemm_bwd(X, dH, W, want_dx=False, dW_out=acc, accumulate=True)
+    assert torch.equal(acc, dW + 1.0)
+    # fused ReLU backward (+ mean's row divisor) and bias-gradient column sums
+    Z = torch.randn(M, 128, device=cuda, generator=g)
+    rm = make_relu_mask(Z)
+    dW3, dX3, cs3 = gemm_bwd(X, dH, W, relu_mask=rm)
+    masked = torch.where(Z > 0, dX, torch.zeros_like(dX))
+    assert torch.equal(dW3, dW) and torch.equal(dX3, masked)
+    torch.testing.assert_close(cs3.double(), masked.double().sum(0), rtol=1e-4, atol=1e-3)
+    div = torch.randint(1, 20, (M,), device=cuda, generator=g).float()
+    _, dX4, cs4 = gemm_bwd(X, dH, W, relu_mask=rm, row_div=div)
+    assert torch.equal(dX4, masked / div[:, None]) and torch.equal(cs4, cs3)
+
+
+def test_gemm_bwd_strided_inputs(cuda):
+    """Row strides > F (views into wider buffers) give the contiguous result."""
+    from mgcn.ops import gemm_bwd
+    g = torch.Generator(device=cuda).manual_seed(9)
+    Xw = torch.randn(5000, 136, device=cuda, generator=g)
+    Hw = torch.randn(5000, 132, device=cuda, generator=g)
+    W = torch.randn(128, 128, device=cuda, generator=g)
+    a = gemm_bwd(Xw[:, :128], Hw[:, 4:], W)
+    b = gemm_bwd(Xw[:, :128].contiguous(), Hw[:, 4:].contiguous(), W)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+
+
 def test_gcn_stack_identity_weights_bitwise_vs_oracle(cuda, oracle):
     """3 fused layers with W = I: every layer's aggregation and the whole
     adjoint chain (dx) are bit-exact against the oracle layer by layer."""
