@@ -124,6 +124,83 @@ class DataLoader:
             yield Batch.from_data_list([self.dataset[j] for j in order[i:i + self.batch_size]])
 
 
+class DenseData:
+    """One graph padded to a fixed node count (torch_geometric ToDense
+    output): x [N, F], adj [N, N], mask [N] (bool), y; a DenseDataLoader
+    batch stacks them (x [B, N, F], adj [B, N, N], mask [B, N])."""
+
+    def __init__(self, x=None, adj=None, mask=None, y=None):
+        self.x, self.adj, self.mask, self.y = x, adj, mask, y
+        self.batch = None
+        self.edge_index = None
+
+    @property
+    def num_nodes(self) -> int:
+        return int(self.x.size(-2)) if self.x is not None else int(self.adj.size(-1))
+
+    @property
+    def num_graphs(self) -> int:
+        return int(self.x.size(0)) if self.x.dim() == 3 else 1
+
+    def __contains__(self, key) -> bool:
+        return getattr(self, key, None) is not None
+
+    def to(self, device) -> "DenseData":
+        for k in ("x", "adj", "mask", "y"):
+            v = getattr(self, k)
+            if isinstance(v, torch.Tensor):
+                setattr(self, k, v.to(device))
+        return self
+
+
+class ToDense:
+    """torch_geometric.transforms.ToDense(num_nodes) (PyG 1.3): dense
+    adjacency (duplicate edges summed), node mask, x zero-padded to
+    ``num_nodes`` rows (kernel/datasets.py:91-94)."""
+
+    def __init__(self, num_nodes=None):
+        self.num_nodes = num_nodes
+
+    def __call__(self, data):
+        n0 = data.num_nodes
+        n = n0 if self.num_nodes is None else self.num_nodes
+        assert n0 <= n, f"graph of {n0} nodes does not fit ToDense({n})"
+        adj = torch.zeros(n, n, dtype=torch.float)
+        if data.edge_index.numel():
+            adj.index_put_((data.edge_index[0], data.edge_index[1]),
+                           torch.ones(data.edge_index.size(1)), accumulate=True)
+        mask = torch.zeros(n, dtype=torch.bool)
+        mask[:n0] = True
+        x = None
+        if data.x is not None:
+            x = torch.cat([data.x, data.x.new_zeros([n - data.x.size(0)] + list(data.x.size())[1:])],
+                          dim=0)
+        y = data.y
+        if y is not None and y.size(0) == n0 and n0 != 1:
+            y = torch.cat([y, y.new_zeros([n - n0] + list(y.size())[1:])], dim=0)
+        return DenseData(x=x, adj=adj, mask=mask, y=y)
+
+
+class DenseDataLoader:
+    """torch_geometric.data.DenseDataLoader: stacks every attribute."""
+
+    def __init__(self, dataset, batch_size=1, shuffle=False):
+        self.dataset = dataset
+        self.batch_size = int(batch_size)
+        self.shuffle = shuffle
+
+    def __len__(self):
+        return (len(self.dataset) + self.batch_size - 1) // self.batch_size
+
+    def __iter__(self):
+        n = len(self.dataset)
+        order = torch.randperm(n).tolist() if self.shuffle else list(range(n))
+        for i in range(0, n, self.batch_size):
+            items = [self.dataset[j] for j in order[i:i + self.batch_size]]
+            yield DenseData(**{k: torch.stack([getattr(d, k) for d in items])
+                               for k in ("x", "adj", "mask", "y")})
+
+
 # ---------------------------------------------------------------- TU format
 def _read(folder, prefix, name, dtype):
     path = osp.join(folder, f"{prefix}_{name}.txt")
@@ -354,9 +431,8 @@ def get_dataset(name: str, root: str | None = None, sparse: bool = True, x_deg: 
     """kernel/datasets.py:34-94 ``get_dataset``.  ``root`` holds the TU files
     (default ``<repo>/data/<name>``, the reference's layout); ``synthetic``
     True (or None with the files absent) uses ``synthetic_tu``.  The dense
-    DiffPool variant (``sparse=False``) is out of scope."""
-    if not sparse:
-        raise NotImplementedError("dense (DiffPool) batches are out of scope")
+    DiffPool variant (``sparse=False``) keeps the graphs up to a size limit
+    and pads them with ToDense (:func:`_dense_filter`)."""
     if root is None:
         root = osp.join(osp.dirname(osp.dirname(osp.dirname(osp.dirname(
             osp.abspath(__file__))))), "data", name)
@@ -385,4 +461,23 @@ def get_dataset(name: str, root: str | None = None, sparse: bool = True, x_deg: 
                 dataset.transform = NormalizedDegree(deg.mean().item(), deg.std().item())
         else:
             dataset.transform = NodeFeatureOnes()
+    if not sparse:
+        dataset = _dense_filter(dataset, name)
+    return dataset
+
+
+def _dense_filter(dataset, name):
+    """kernel/datasets.py:72-94: drop graphs above 5 x the mean node count
+    (1.5 x for REDDIT-BINARY), capped at the largest graph, and pad the rest
+    to that size with ToDense (after the feature transform)."""
+    total = max_n = 0
+    for d in dataset._graphs:
+        total += d.num_nodes
+        max_n = max(max_n, d.num_nodes)
+    factor = 1.5 if name == 'REDDIT-BINARY' else 5
+    limit = min(int(total / len(dataset) * factor), max_n)
+    keep = [i for i, d in enumerate(dataset._graphs) if d.num_nodes <= limit]
+    dataset = dataset[torch.tensor(keep)]
+    dataset.transform = ToDense(limit) if dataset.transform is None else \
+        Compose([dataset.transform, ToDense(limit)])
     return dataset

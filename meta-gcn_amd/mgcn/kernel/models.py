@@ -5,8 +5,7 @@ Each is ``Net(dataset, num_layers, hidden)`` with ``reset_parameters()`` and
 ``forward(data) -> log_softmax`` over graphs: convs with ReLU, (JumpingKnowledge),
 ``global_mean_pool`` over ``data.batch``, lin1 + ReLU, dropout 0.5, lin2.
 The pooling-operator nets (TopK, SAGPool, EdgePool, Graclus, DiffPool,
-Set2Set, SortPool, GlobalAttention, HardPool) are out of scope (SURVEY.md
-§8(f) rank 4).
+Set2Set, SortPool, GlobalAttention, HardPool) live in :mod:`.pool_nets`.
 """
 from __future__ import annotations
 

@@ -25,7 +25,7 @@ import torch
 import torch.nn.functional as F
 from torch import tensor
 
-from .data import DataLoader
+from .data import DataLoader, DenseDataLoader
 
 
 class EarlyStopping:
@@ -137,9 +137,10 @@ def cross_validation_with_val_set(dataset, model, folds, epochs, batch_size, lr,
     val_losses, val_accs, test_losses, test_accs, durations = [], [], [], [], []
     for fold, (train_idx, test_idx, val_idx) in enumerate(
             zip(*k_fold(dataset, folds, random_state))):
-        train_loader = DataLoader(dataset[train_idx], batch_size, shuffle=True)
-        val_loader = DataLoader(dataset[val_idx], batch_size, shuffle=False)
-        test_loader = DataLoader(dataset[test_idx], batch_size, shuffle=False)
+        Loader = DenseDataLoader if 'adj' in dataset[0] else DataLoader  # train_eval.py:32-39
+        train_loader = Loader(dataset[train_idx], batch_size, shuffle=True)
+        val_loader = Loader(dataset[val_idx], batch_size, shuffle=False)
+        test_loader = Loader(dataset[test_idx], batch_size, shuffle=False)
         model.to(device).reset_parameters()
         optimizer = torch.optim.Adam(model.parameters(), lr=lr, weight_decay=weight_decay)
         stopper = EarlyStopping(patience=es_patience, mode="min", verbose=True)
@@ -196,8 +197,8 @@ def run_sweep(datasets, nets, layers, hiddens, folds=10, epochs=100, batch_size=
     for name, Net in product(datasets, nets):
         best, best_hyper = (float("inf"), 0.0, 0.0), None
         for num_layers, hidden in product(layers, hiddens):
-            dataset = get_dataset(name, root=root, sparse=True, x_deg=True, add_sl=add_sl,
-                                  synthetic=synthetic)
+            dataset = get_dataset(name, root=root, sparse=Net.__name__ != "DiffPool",
+                                  x_deg=True, add_sl=add_sl, synthetic=synthetic)
             model = Net(dataset, num_layers, hidden)
             val_loss, _, _, _, test_acc, test_std = cross_validation_with_val_set(
                 dataset, model, folds=folds, epochs=epochs, batch_size=batch_size, lr=lr,

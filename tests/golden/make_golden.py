@@ -115,12 +115,37 @@ def _install_stubs():
         if t is not None:
             t.data.fill_(0)
 
-    def _unused_scatter_(*a, **k):
-        raise RuntimeError("placeholder: torch_geometric.utils.scatter_ is not used here")
+    def pyg_scatter_(name, src, index, dim_size=None):
+        # PyG 1.3 torch_geometric/utils/scatter.py (used by HardPooling)
+        assert name in ["add", "mean", "max"]
+        op = getattr(ts, "scatter_{}".format(name))
+        fill_value = -1e38 if name == "max" else 0
+        out = op(src, index, 0, None, dim_size, fill_value)
+        if isinstance(out, tuple):
+            out = out[0]
+        if name == "max":
+            out[out == fill_value] = 0
+        return out
 
-    tgi.glorot, tgi.zeros, tgu.scatter_ = glorot, zeros, _unused_scatter_
+    def filter_adj(edge_index, edge_attr, perm, num_nodes=None):
+        # PyG 1.3 torch_geometric/nn/pool/topk_pool.py filter_adj
+        mask = perm.new_full((num_nodes,), -1)
+        mask[perm] = torch.arange(perm.size(0), dtype=torch.long)
+        row, col = mask[edge_index[0]], mask[edge_index[1]]
+        keep = (row >= 0) & (col >= 0)
+        row, col = row[keep], col[keep]
+        if edge_attr is not None:
+            edge_attr = edge_attr[keep]
+        return torch.stack([row, col], dim=0), edge_attr
+
+    tgi.glorot, tgi.zeros, tgu.scatter_ = glorot, zeros, pyg_scatter_
+    tgp = types.ModuleType("torch_geometric.nn.pool")
+    tgpt = types.ModuleType("torch_geometric.nn.pool.topk_pool")
+    tgpt.filter_adj = filter_adj
     sys.modules.update({"torch_scatter": ts, "torch_geometric": tg, "torch_geometric.nn": tgn,
-                        "torch_geometric.nn.inits": tgi, "torch_geometric.utils": tgu})
+                        "torch_geometric.nn.inits": tgi, "torch_geometric.utils": tgu,
+                        "torch_geometric.nn.pool": tgp,
+                        "torch_geometric.nn.pool.topk_pool": tgpt})
 
 
 def _import_reference():
@@ -253,6 +278,52 @@ def model12_case(gm, name, rng, N, E, L=12, F=32):
     save(name, edge_index=ei, x=x, dout=g, out=out, **params, **grads)
 
 
+def hardpool_case(hap, name, rng, sizes, F, aggr, bias, lonely=True):
+    """HardPooling (hard_attention_pool.py:23-131) in eval mode on a batch of
+    graphs; ``lonely`` gives one node no out-edge (argmax -1 in torch_scatter
+    1.x, which the reference turns into marking the last edge)."""
+    eis, batch, off = [], [], 0
+    for g, n in enumerate(sizes):
+        E = 3 * n
+        s = rng.integers(0, n, E)
+        d = rng.integers(0, n, E)
+        if lonely and g == 0:
+            keep = s != n - 1  # node n - 1 of graph 0 has no out-edge
+            s, d = s[keep], d[keep]
+        eis.append(np.stack([s, d]) + off)
+        batch.append(np.full(n, g))
+        off += n
+    ei = np.concatenate(eis, 1).astype(np.int64)
+    batch = np.concatenate(batch).astype(np.int64)
+    x = rng.standard_normal((off, F)).astype(np.float32)
+    torch.manual_seed(int(rng.integers(0, 2**31)))
+    pool = hap.HardPooling(F, aggr=aggr, bias=bias)
+    if bias:
+        with torch.no_grad():
+            pool.bias.uniform_(-0.5, 0.5)
+    pool.eval()
+    xt = _t(x).requires_grad_(True)
+    out, ei2, _, b2, perm, score = pool(xt, _t(ei), _t(batch))
+    dY = rng.standard_normal(tuple(out.shape)).astype(np.float32)
+    out.backward(_t(dY))
+    save(name, x=x, edge_index=ei, batch=batch, att_weight=pool.att_weight.detach(),
+         bias=None if pool.bias is None else pool.bias.detach(), out=out, out_edge_index=ei2,
+         out_batch=b2, perm=perm, score=score, dY=dY, dx=xt.grad,
+         meta=np.array([aggr]))
+
+
+def main_hardpool():
+    """Only the HardPooling fixtures (``python make_golden.py hardpool``)."""
+    _install_stubs()
+    sys.path.insert(0, REF_SRC)
+    from gcn_meta.models import hard_attention_pool as hap  # noqa: E402
+    rng = np.random.default_rng(20261016)
+    hardpool_case(hap, "hardpool_add", rng, [12, 30, 7], 16, "add", False)
+    hardpool_case(hap, "hardpool_add_bias", rng, [25, 9, 40, 16], 16, "add", True)
+    hardpool_case(hap, "hardpool_mean", rng, [20, 33], 8, "mean", False, lonely=False)
+    print("wrote 3 hardpool fixtures to", OUT_DIR)
+
+
 def main():
     common, gbm, gm = _import_reference()
     rng = np.random.default_rng(20250824)
@@ -305,4 +376,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["hardpool"]:
+        main_hardpool()
+    else:
+        main()
