@@ -55,8 +55,8 @@ def test_get_dataset_featureless_uses_one_hot_degree(tmp_path):
     assert ds.num_features == 3
     nd = NormalizedDegree(1.0, 2.0)(ds._graphs[0].clone())
     assert nd.x.view(-1).tolist() == [0.0, 0.5, 0.0]
-    with pytest.raises(NotImplementedError):
-        get_dataset("TOY", root=str(root), sparse=False)
+    dense = get_dataset("TOY", root=str(root), sparse=False)  # DiffPool's ToDense path
+    assert 'adj' in dense[0] and dense[0].adj.size(0) == dense[0].x.size(0)
 
 
 def test_add_sl_adds_remaining_loops(tmp_path):
