@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define MGCN_ABI_VERSION 6
+#define MGCN_ABI_VERSION 7
 
 /* return codes */
 #define MGCN_OK 0
@@ -309,6 +309,33 @@ int mgcn_relu_bwd_colsum(int64_t n_rows, int32_t F, const float *dZ,
                          const float *Z, int relu, const float *row_div, float *dY,
                          float *db, void *workspace, size_t workspace_bytes,
                          void *stream);
+
+/*
+ * GCNModel's residual join (gcn_model.py:99-105, residual_hop = 1):
+ *   Z = act(Z1 + (R + rbias))      act = ReLU if relu != 0 (layers before the
+ * last, :103) else identity (:105); R = the residual Linear's x Wr^T (its
+ * bias rbias may be NULL).  Replaces `xo + xr` and `self.non_linear(...)`.
+ */
+int mgcn_residual_act(int64_t n_rows, int32_t F, const float *Z1, int64_t ldz1,
+                      const float *R, int64_t ldr, const float *rbias, int relu,
+                      float *Z, int64_t ldz, void *stream);
+
+/* Bytes of scratch mgcn_residual_act_bwd needs for its column sums. */
+size_t mgcn_residual_act_bwd_workspace_bytes(int64_t n_rows, int32_t F);
+
+/*
+ * Adjoint of the residual join and of the layer's own ReLU in one pass:
+ *   dS = relu ? (Z > 0 ? dZ : 0) : dZ          (written when dS != NULL)
+ *   dA = relu1 ? (Z1 > 0 ? dS : 0) : dS        (stored / row_div[i] if given)
+ *   colsums[0:F] = sum_i dA (undivided), colsums[F:2F] = sum_i dS
+ * (deterministic; colsums may be NULL).  dA feeds the adjoint SpMM, dS the
+ * residual Linear's gradients, the sums the two bias gradients.
+ */
+int mgcn_residual_act_bwd(int64_t n_rows, int32_t F, const float *dZ, int64_t lddz,
+                          const float *Z, int64_t ldz, int relu, const float *Z1,
+                          int64_t ldz1, int relu1, const float *row_div, float *dA,
+                          int64_t ldda, float *dS, int64_t ldds, float *colsums,
+                          void *workspace, size_t workspace_bytes, void *stream);
 
 /*
  * Segment mean over contiguous node ranges (PyG global_mean_pool on a

@@ -104,6 +104,111 @@ __global__ __launch_bounds__(kBlock) void colsum_finish_kernel(const float *__re
                       __fadd_rn(red[2][threadIdx.x], red[3][threadIdx.x]));
 }
 
+template <int VEC>
+__device__ __forceinline__ void load_vec(const float *p, float (&v)[VEC]) {
+  if constexpr (VEC == 4) {
+    const float4 a = *reinterpret_cast<const float4 *>(p);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  } else {
+    v[0] = p[0];
+  }
+}
+template <int VEC>
+__device__ __forceinline__ void store_vec(float *p, const float (&v)[VEC]) {
+  if constexpr (VEC == 4)
+    *reinterpret_cast<float4 *>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  else
+    p[0] = v[0];
+}
+
+// GCNModel residual join (gcn_model.py:99-105): Z = act(Z1 + (R + rb)),
+// the residual Linear's bias added to its product first (as F.linear does).
+template <int VEC>
+__global__ __launch_bounds__(kBlock) void residual_act_kernel(
+    int64_t n, int F, const float *__restrict__ Z1, int64_t ldz1, const float *__restrict__ R,
+    int64_t ldr, const float *__restrict__ rb, int relu, float *__restrict__ Z, int64_t ldz) {
+  const int fv = F / VEC;
+  const int64_t total = n * fv;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * kBlock) {
+    const int64_t r = i / fv;
+    const int f0 = (int)(i % fv) * VEC;
+    float z1[VEC], v[VEC], b[VEC];
+    load_vec<VEC>(Z1 + r * ldz1 + f0, z1);
+    load_vec<VEC>(R + r * ldr + f0, v);
+    if (rb != nullptr) load_vec<VEC>(rb + f0, b);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      if (rb != nullptr) v[j] = __fadd_rn(v[j], b[j]);
+      v[j] = __fadd_rn(z1[j], v[j]);
+      if (relu && v[j] < 0.0f) v[j] = 0.0f;
+    }
+    store_vec<VEC>(Z + r * ldz + f0, v);
+  }
+}
+
+// Its adjoint with the layer's own ReLU (Z1 = relu(A Z W + b)):
+//   dS = relu ? (Z > 0 ? dZ : 0) : dZ       (grad of the residual branch R)
+//   dA = relu1 ? (Z1 > 0 ? dS : 0) : dS     (grad of the aggregation, / row_div)
+// and the column sums of dA (bias b) and dS (residual bias rb) into block
+// partials [block][2F] in a fixed row order (colsum_finish_kernel folds them).
+template <int VEC>
+__global__ __launch_bounds__(kBlock) void residual_act_bwd_kernel(
+    int64_t n, int F, const float *__restrict__ dZ, int64_t lddz, const float *__restrict__ Z,
+    int64_t ldz, int relu, const float *__restrict__ Z1, int64_t ldz1, int relu1,
+    const float *__restrict__ row_div, float *__restrict__ dA, int64_t ldda,
+    float *__restrict__ dS, int64_t ldds, float *__restrict__ partial, int T) {
+  __shared__ float red[2][kBlock * VEC];
+  const int R = kBlock / T;
+  const int t_col = threadIdx.x % T, t_row = threadIdx.x / T;
+  for (int c0 = 0; c0 < F; c0 += T * VEC) {
+    const int f0 = c0 + t_col * VEC;
+    const bool ok = t_row < R && f0 < F;
+    float sa[VEC], ss[VEC];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) sa[j] = ss[j] = 0.0f;
+    if (ok) {
+      for (int64_t r = (int64_t)blockIdx.x * R + t_row; r < n; r += (int64_t)gridDim.x * R) {
+        float g[VEC], z[VEC], z1[VEC], a[VEC];
+        load_vec<VEC>(dZ + r * lddz + f0, g);
+        if (relu) load_vec<VEC>(Z + r * ldz + f0, z);
+        if (relu1) load_vec<VEC>(Z1 + r * ldz1 + f0, z1);
+        const float dv = row_div != nullptr ? row_div[r] : 1.0f;
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+          if (relu && !(z[j] > 0.0f)) g[j] = 0.0f;
+          a[j] = (relu1 && !(z1[j] > 0.0f)) ? 0.0f : g[j];
+          ss[j] = __fadd_rn(ss[j], g[j]);
+          sa[j] = __fadd_rn(sa[j], a[j]);
+          if (row_div != nullptr) a[j] = __fdiv_rn(a[j], dv);
+        }
+        if (dS != nullptr) store_vec<VEC>(dS + r * ldds + f0, g);
+        store_vec<VEC>(dA + r * ldda + f0, a);
+      }
+    }
+    if (partial == nullptr) continue;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      red[0][threadIdx.x * VEC + j] = sa[j];
+      red[1][threadIdx.x * VEC + j] = ss[j];
+    }
+    __syncthreads();
+    if (t_row == 0 && f0 < F) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        float a = red[0][t_col * VEC + j], b = red[1][t_col * VEC + j];
+        for (int rr = 1; rr < R; ++rr) {
+          a = __fadd_rn(a, red[0][(rr * T + t_col) * VEC + j]);
+          b = __fadd_rn(b, red[1][(rr * T + t_col) * VEC + j]);
+        }
+        partial[(int64_t)blockIdx.x * 2 * F + f0 + j] = a;
+        partial[(int64_t)blockIdx.x * 2 * F + F + f0 + j] = b;
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // one wave per segment; lanes stride the features
 __global__ __launch_bounds__(kBlock) void segment_mean_kernel(int64_t n_seg, int F,
                                                               const int64_t *__restrict__ ptr,
@@ -193,4 +298,77 @@ extern "C" int mgcn_segment_mean(int64_t n_seg, int32_t F, const int64_t *ptr, c
   hipLaunchKernelGGL(segment_mean_kernel, dim3((unsigned)blocks), dim3(kBlock), 0,
                      as_stream(stream), n_seg, F, ptr, x, ldx, out, ldo);
   return check_launch("segment_mean_kernel");
+}
+
+extern "C" int mgcn_residual_act(int64_t n_rows, int32_t F, const float *Z1, int64_t ldz1,
+                                 const float *R, int64_t ldr, const float *rbias, int relu,
+                                 float *Z, int64_t ldz, void *stream) {
+  clear_error();
+  MGCN_REQUIRE(n_rows >= 0 && F >= 0, "mgcn_residual_act: negative size");
+  if (n_rows == 0 || F == 0) return MGCN_OK;
+  MGCN_REQUIRE(Z1 && R && Z && ldz1 >= F && ldr >= F && ldz >= F,
+               "mgcn_residual_act: bad arguments");
+  const bool v4 = F % 4 == 0 && ldz1 % 4 == 0 && ldr % 4 == 0 && ldz % 4 == 0 &&
+                  (uintptr_t)Z1 % 16 == 0 && (uintptr_t)R % 16 == 0 && (uintptr_t)Z % 16 == 0 &&
+                  (rbias == nullptr || (uintptr_t)rbias % 16 == 0);
+  const int vec = v4 ? 4 : 1;
+  const unsigned g = grid_for(n_rows * (F / vec), kBlock);
+  if (vec == 4)
+    hipLaunchKernelGGL(residual_act_kernel<4>, dim3(g), dim3(kBlock), 0, as_stream(stream), n_rows,
+                       F, Z1, ldz1, R, ldr, rbias, relu, Z, ldz);
+  else
+    hipLaunchKernelGGL(residual_act_kernel<1>, dim3(g), dim3(kBlock), 0, as_stream(stream), n_rows,
+                       F, Z1, ldz1, R, ldr, rbias, relu, Z, ldz);
+  return check_launch("residual_act_kernel");
+}
+
+extern "C" size_t mgcn_residual_act_bwd_workspace_bytes(int64_t n_rows, int32_t F) {
+  return mgcn_colsum_workspace_bytes(n_rows, 2 * (F > 0 ? F : 1));
+}
+
+extern "C" int mgcn_residual_act_bwd(int64_t n_rows, int32_t F, const float *dZ, int64_t lddz,
+                                     const float *Z, int64_t ldz, int relu, const float *Z1,
+                                     int64_t ldz1, int relu1, const float *row_div, float *dA,
+                                     int64_t ldda, float *dS, int64_t ldds, float *colsums,
+                                     void *workspace, size_t workspace_bytes, void *stream) {
+  clear_error();
+  MGCN_REQUIRE(n_rows >= 0 && F >= 0, "mgcn_residual_act_bwd: negative size");
+  hipStream_t s = as_stream(stream);
+  if (F == 0) return MGCN_OK;
+  if (n_rows == 0) {
+    if (colsums) MGCN_HIP_TRY(hipMemsetAsync(colsums, 0, sizeof(float) * 2 * F, s));
+    return MGCN_OK;
+  }
+  MGCN_REQUIRE(dZ && dA && lddz >= F && ldda >= F, "mgcn_residual_act_bwd: bad dZ/dA");
+  MGCN_REQUIRE(!relu || (Z && ldz >= F), "mgcn_residual_act_bwd: relu needs Z");
+  MGCN_REQUIRE(!relu1 || (Z1 && ldz1 >= F), "mgcn_residual_act_bwd: relu1 needs Z1");
+  MGCN_REQUIRE(dS == nullptr || ldds >= F, "mgcn_residual_act_bwd: bad dS");
+  const int nblk = colsum_blocks(n_rows);
+  float *partial = nullptr;
+  if (colsums != nullptr) {
+    const size_t need = mgcn_residual_act_bwd_workspace_bytes(n_rows, F);
+    if (workspace == nullptr || workspace_bytes < need) {
+      set_error("mgcn_residual_act_bwd: workspace %zu < %zu", workspace_bytes, need);
+      return MGCN_EWORKSPACE;
+    }
+    partial = static_cast<float *>(workspace);
+  }
+  auto al = [](const void *p, int64_t ld) { return p == nullptr || ((uintptr_t)p % 16 == 0 && ld % 4 == 0); };
+  const bool v4 = F % 4 == 0 && al(dZ, lddz) && (!relu || al(Z, ldz)) &&
+                  (!relu1 || al(Z1, ldz1)) && al(dA, ldda) && al(dS, ldds);
+  int T = 1;
+  if (v4) {
+    while (T < F / 4 && T < kBlock) T <<= 1;
+    hipLaunchKernelGGL(residual_act_bwd_kernel<4>, dim3(nblk), dim3(kBlock), 0, s, n_rows, F, dZ,
+                       lddz, Z, ldz, relu, Z1, ldz1, relu1, row_div, dA, ldda, dS, ldds, partial, T);
+  } else {
+    while (T < F && T < kBlock) T <<= 1;
+    hipLaunchKernelGGL(residual_act_bwd_kernel<1>, dim3(nblk), dim3(kBlock), 0, s, n_rows, F, dZ,
+                       lddz, Z, ldz, relu, Z1, ldz1, relu1, row_div, dA, ldda, dS, ldds, partial, T);
+  }
+  if (int rc = check_launch("residual_act_bwd_kernel")) return rc;
+  if (colsums == nullptr) return MGCN_OK;
+  hipLaunchKernelGGL(colsum_finish_kernel, dim3((2 * F + 63) / 64), dim3(kBlock), 0, s, partial,
+                     nblk, 2 * F, colsums);
+  return check_launch("colsum_finish_kernel");
 }

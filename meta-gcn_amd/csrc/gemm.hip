@@ -417,10 +417,12 @@ __global__ __launch_bounds__(256, WPS) void gemm_tn_lds_kernel(
       }
 }
 
-// Small C (M, N <= 32: F = 32 layers and the 32 -> 2 projection of config 3):
-// one 32 x 32 MFMA tile per workgroup; the four waves take interleaved
+// Small C (M <= 32, N <= 32 NT: F = 32 layers, the 32 -> 2 projection and,
+// with NT = 2, the [W | Wr^T] pair of a fused residual layer, config 3):
+// NT 32 x 32 MFMA tiles per workgroup; the four waves take interleaved
 // k-steps of the split's K range (wave-level split-K) and their accumulators
 // are folded in wave order through LDS, then one slab per split.
+template <int NT>
 __global__ __launch_bounds__(256) void gemm_tn_small_kernel(
     const float *__restrict__ A, int64_t lda, const float *__restrict__ B, int64_t ldb,
     int64_t K, int M, int N, int64_t k_per_split, float *__restrict__ partial) {
@@ -431,35 +433,52 @@ __global__ __launch_bounds__(256) void gemm_tn_small_kernel(
   const int lr = lane >> 5, lc = lane & 31;
   const int64_t kb = (int64_t)blockIdx.x * k_per_split;
   const int64_t ke = (kb + k_per_split < K) ? kb + k_per_split : K;
-  const bool oka = lc < M, okb = lc < N;
-  const int ia = oka ? lc : 0, jb = okb ? lc : 0;
-  f32x16 acc;
+  const bool oka = lc < M;
+  const int ia = oka ? lc : 0;
+  bool okb[NT];
+  int jb[NT];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+  for (int t = 0; t < NT; ++t) {
+    okb[t] = 32 * t + lc < N;
+    jb[t] = okb[t] ? 32 * t + lc : 0;
+  }
+  f32x16 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
   // wave w takes k-steps w, w + 4, w + 8, ... (2 rows each)
   for (int64_t k = kb + 2 * wave; k < ke; k += 2 * 4 * U) {
-    float a[U], b[U];
+    float a[U], b[U][NT];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t kr = k + 8 * u + lr;
       const bool okk = kr < ke;
       a[u] = (okk && oka) ? A[kr * lda + ia] : 0.0f;
-      b[u] = (okk && okb) ? B[kr * ldb + jb] : 0.0f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) b[u][t] = (okk && okb[t]) ? B[kr * ldb + jb[t]] : 0.0f;
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], b[u], acc, 0, 0, 0);
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], b[u][t], acc[t], 0, 0, 0);
   }
+  float *slab = partial + (int64_t)blockIdx.x * M * N;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) red[wave][r][lane] = acc[r];
-  __syncthreads();
-  if (wave == 0) {
-    float *slab = partial + (int64_t)blockIdx.x * M * N;
+  for (int t = 0; t < NT; ++t) {
+    __syncthreads();
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float v = __fadd_rn(__fadd_rn(red[0][r][lane], red[1][r][lane]),
-                                __fadd_rn(red[2][r][lane], red[3][r][lane]));
-      const int row = (r & 3) + 8 * (r >> 2) + 4 * lr;
-      if (row < M && lc < N) slab[row * N + lc] = v;
+    for (int r = 0; r < 16; ++r) red[wave][r][lane] = acc[t][r];
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float v = __fadd_rn(__fadd_rn(red[0][r][lane], red[1][r][lane]),
+                                  __fadd_rn(red[2][r][lane], red[3][r][lane]));
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * lr;
+        if (row < M && okb[t]) slab[row * N + 32 * t + lc] = v;
+      }
     }
   }
 }
@@ -552,9 +571,13 @@ extern "C" int mgcn_gemm_tn(int64_t K, int32_t M, int32_t N, const float *A, int
   kps = (kps + 63) / 64 * 64;  // whole chunks of every variant (and whole kU groups)
   const int used = (int)((K + kps - 1) / kps);
   float *partial = static_cast<float *>(workspace);
-  if (M <= 32 && N <= 32) {
-    hipLaunchKernelGGL(gemm_tn_small_kernel, dim3(used), dim3(256), 0, s, A, lda, B, ldb, K, M, N,
-                       kps, partial);
+  if (M <= 32 && N <= 64) {
+    if (N <= 32)
+      hipLaunchKernelGGL(gemm_tn_small_kernel<1>, dim3(used), dim3(256), 0, s, A, lda, B, ldb, K,
+                         M, N, kps, partial);
+    else
+      hipLaunchKernelGGL(gemm_tn_small_kernel<2>, dim3(used), dim3(256), 0, s, A, lda, B, ldb, K,
+                         M, N, kps, partial);
     if (int rc = check_launch("gemm_tn_small_kernel")) return rc;
   } else if (tn_lds(M, N) && reinterpret_cast<uintptr_t>(A) % 16 == 0 &&
              reinterpret_cast<uintptr_t>(B) % 16 == 0 && lda % 4 == 0 && ldb % 4 == 0) {

@@ -26,7 +26,8 @@ from torch.nn.utils.rnn import pad_sequence
 
 from . import _lib as L
 from .graph import plan_for
-from .ops import aggregate_plan, gcn_stack, linear, linear_bias, scatter_  # noqa: F401
+from .ops import (aggregate_plan, gcn_stack, linear, linear_bias, residual_gcn_layer,  # noqa: F401
+                  scatter_)
 
 
 # --------------------------------------------------------------- inits (PyG)
@@ -378,8 +379,30 @@ class GCNModel(nn.Module):
         if self.final_type != 'none':
             self.final.reset_parameters()
 
+    fuse_residual = True  # class switch (tests compare against the step-for-step path)
+
+    def _residual_fusable(self, x, edge_index_K, edge_attr_K):
+        """residual_hop = 1 with single additive kernels, ReLU joins and no
+        active dropout: each layer + its residual runs as one fused node."""
+        if not self.fuse_residual or self.residual_hop != 1 or \
+                getattr(self, 'num_residuals', 0) != self.num_layers:
+            return False
+        if not isinstance(edge_index_K, torch.Tensor) or edge_attr_K is not None:
+            return False
+        if x.device.type != "cuda" or not isinstance(self.non_linear, nn.ReLU):
+            return False
+        if self.training and self.dropout.p > 0:
+            return False
+        for layer in self.gcn_net:
+            if len(layer.gcn.node_models) != 1 or layer.non_linear_name not in ('relu', 'none'):
+                return False
+        return True
+
     def forward(self, x, edge_index_K, edge_attr_K=None, deg_K=None, edge_weight_K=None,
                 **kwargs):
+        if self._residual_fusable(x, edge_index_K, edge_attr_K):
+            x = self._forward_residual_fused(x, edge_index_K, deg_K, edge_weight_K)
+            return self._readout(x, **kwargs)
         # gcn_model.py:86-125, step for step
         xr = None
         add_xr_at = -1
@@ -396,6 +419,24 @@ class GCNModel(nn.Module):
                     else:
                         xo = xo + xr
             x = xo
+        return self._readout(x, **kwargs)
+
+    def _forward_residual_fused(self, x, edge_index, deg, edge_weight):
+        if isinstance(deg, (list, tuple)):
+            deg = deg[0]
+        if isinstance(edge_weight, (list, tuple)):
+            edge_weight = edge_weight[0]
+        plan = plan_for(edge_index, x.size(0))
+        last = self.num_layers - 1
+        for n, (layer, res) in enumerate(zip(self.gcn_net, self.residuals)):
+            nm = layer.gcn.node_models[0]
+            norm = plan.norm(nm.deg_norm, deg=deg,
+                             edge_weight=edge_weight if nm.deg_norm is not None else None)
+            x = residual_gcn_layer(x, plan, norm, nm.aggr, layer.non_linear_name == 'relu',
+                                   n < last, nm.weight_node, nm.bias, res.weight, res.bias)
+        return x
+
+    def _readout(self, x, **kwargs):
         x = self.final(x)
         if self.pred_on == 'graph':
             assert 'batch_slices_x' in kwargs

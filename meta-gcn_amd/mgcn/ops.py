@@ -537,6 +537,99 @@ def gcn_stack(x: torch.Tensor, plan: GraphPlan, norm: NormPlan, Ws, bs, relus,
                            *params)
 
 
+# ------------------------------------------------------- residual GCN layer
+def residual_act(Z1: torch.Tensor, R: torch.Tensor, rbias: torch.Tensor | None,
+                 relu: bool) -> torch.Tensor:
+    """Z = act(Z1 + (R + rbias)) (``mgcn_residual_act``)."""
+    lib = L.load()
+    dev = L.require_device(Z1, R, rbias)
+    n, F = Z1.shape
+    Z = torch.empty(n, F, dtype=torch.float32, device=dev)
+    rb = rbias.detach().contiguous() if rbias is not None else None
+    with torch.cuda.device(dev):
+        rc = lib.mgcn_residual_act(n, F, L.ptr(Z1), Z1.stride(0), L.ptr(R), R.stride(0), L.ptr(rb),
+                                   int(bool(relu)), L.ptr(Z), Z.stride(0), L.stream_of(dev))
+    L.check(rc, "mgcn_residual_act")
+    return Z
+
+
+def residual_act_bwd(dZ, Z, relu, Z1, relu1, dA, dS, row_div=None, want_sums=True):
+    """dS / dA / their column sums (``mgcn_residual_act_bwd``); returns the
+    [2F] sums (dA | dS) or None."""
+    lib = L.load()
+    dev = L.require_device(dZ, dA)
+    n, F = dZ.shape
+    sums = torch.empty(2 * F, dtype=torch.float32, device=dev) if want_sums else None
+    ws_bytes = int(lib.mgcn_residual_act_bwd_workspace_bytes(n, F)) if want_sums else 0
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev) if want_sums else None
+    with torch.cuda.device(dev):
+        rc = lib.mgcn_residual_act_bwd(
+            n, F, L.ptr(dZ), dZ.stride(0), L.ptr(Z), Z.stride(0) if Z is not None else F,
+            int(bool(relu)), L.ptr(Z1), Z1.stride(0) if Z1 is not None else F, int(bool(relu1)),
+            L.ptr(row_div), L.ptr(dA), dA.stride(0), L.ptr(dS),
+            dS.stride(0) if dS is not None else F, L.ptr(sums), L.ptr(ws), ws_bytes,
+            L.stream_of(dev))
+    L.check(rc, "mgcn_residual_act_bwd")
+    return sums
+
+
+class _ResidualGCNLayer(torch.autograd.Function):
+    """One GCNModel layer with its residual Linear (gcn_model.py:92-105,
+    residual_hop = 1) as a single autograd node:
+
+        [H | R] = x @ [W | Wr^T]                 one GEMM, x read once
+        Z1 = relu1(A_norm H + b)                 SpMM, bias/ReLU epilogue
+        Z  = relu2(Z1 + (R + br))                mgcn_residual_act
+
+    backward: mgcn_residual_act_bwd gives dA (into the adjoint SpMM), dS and
+    both bias gradients in one pass; the adjoint SpMM writes dH beside dS,
+    so dx = [dH | dS] @ [W | Wr^T]^T and [dW | dWr^T] = x^T [dH | dS] are one
+    GEMM each.  Forward values are the layer-by-layer path's bit for bit;
+    gradients agree within fp32 GEMM tolerance (different summation order)."""
+
+    @staticmethod
+    def forward(ctx, x, plan, norm, reduce, relu1, relu2, W, b, Wr, br):
+        F_out = W.size(1)
+        Wc = torch.cat([W.detach(), Wr.detach().t()], dim=1)
+        HR = _mm(x, Wc)
+        Z1, mask = spmm_fwd(plan.fwd, norm.w_fwd, HR[:, :F_out], reduce, b, relu1, mask_plan=plan)
+        Z = residual_act(Z1, HR[:, F_out:], br, relu2)
+        ctx.plan, ctx.norm, ctx.reduce, ctx.relu1, ctx.relu2 = plan, norm, reduce, relu1, relu2
+        ctx.has_b, ctx.has_br = b is not None, br is not None
+        ctx.save_for_backward(x, Z1, Z, Wc, mask)
+        return Z
+
+    @staticmethod
+    def backward(ctx, dZ):
+        x, Z1, Z, Wc, mask = ctx.saved_tensors
+        plan, norm = ctx.plan, ctx.norm
+        n, F_out = Z.shape
+        dZ = dZ.contiguous()
+        mean = ctx.reduce == L.REDUCE_MEAN
+        DH = torch.empty(n, 2 * F_out, dtype=torch.float32, device=dZ.device)
+        dA = torch.empty(n, F_out, dtype=torch.float32, device=dZ.device)
+        sums = residual_act_bwd(dZ, Z, ctx.relu2, Z1, ctx.relu1, dA, DH[:, F_out:],
+                                row_div=plan.in_cnt if mean else None)
+        spmm_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dA,
+                 L.REDUCE_SUM if mean else ctx.reduce, out=DH[:, :F_out], win_mask=mask,
+                 slot_map=plan.slot_map() if mask is not None else None)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = _mm_t(DH, Wc)
+        dWc = gemm_tn(x, DH)
+        db = sums[:F_out] if ctx.has_b else None
+        dbr = sums[F_out:] if ctx.has_br else None
+        return (dx, None, None, None, None, None, dWc[:, :F_out], db,
+                dWc[:, F_out:].t().contiguous(), dbr)
+
+
+def residual_gcn_layer(x, plan: GraphPlan, norm: NormPlan, aggr: str, relu1: bool, relu2: bool,
+                       W, b, Wr, br):
+    """See :class:`_ResidualGCNLayer`."""
+    return _ResidualGCNLayer.apply(x, plan, norm, L.REDUCE_CODES[aggr], bool(relu1), bool(relu2),
+                                   W, b, Wr, br)
+
+
 # ---------------------------------------------------------------- scatter_
 class _SegmentReduce(torch.autograd.Function):
     """torch_scatter 1.x scatter_{add,mean,max}(src, index, 0, None, dim_size)

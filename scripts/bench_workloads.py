@@ -51,7 +51,8 @@ def config3(args, dev):
                      residual_hop=1, dropout=0.0, final_type='proj', pred_on='node',
                      deg_norm='sm', aggr='add', bias=False).to(dev)
     opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=5e-4)
-    crit = torch.nn.CrossEntropyLoss()
+    from mgcn.botnet import CrossEntropyLoss
+    crit = CrossEntropyLoss()
 
     def step():
         opt.zero_grad()

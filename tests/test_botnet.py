@@ -100,3 +100,18 @@ def test_train_botnet_small(cuda, tmp_path, aggr, focal):
     assert 0.0 <= t["acc"] <= 1.0 and math.isfinite(t["loss"])
     state = torch.load(str(tmp_path / "best.pt"), weights_only=True)
     assert all(v.device.type == "cuda" for v in state.values())
+
+
+def test_cross_entropy_matches_torch():
+    import torch
+    from mgcn.botnet import CrossEntropyLoss
+    g = torch.Generator().manual_seed(0)
+    s = torch.randn(1000, 2, generator=g, requires_grad=True)
+    y = torch.randint(0, 2, (1000,), generator=g)
+    for red in ("mean", "sum", "none"):
+        a = CrossEntropyLoss(red)(s, y)
+        b = torch.nn.CrossEntropyLoss(reduction=red)(s, y)
+        torch.testing.assert_close(a, b)
+    ga, = torch.autograd.grad(CrossEntropyLoss()(s, y), s)
+    gb, = torch.autograd.grad(torch.nn.CrossEntropyLoss()(s, y), s)
+    torch.testing.assert_close(ga, gb)

@@ -573,3 +573,62 @@ def test_linear_matches_torch(cuda, M, fin, fout):
     assert ((lin.weight.grad.double() - ref_dw).abs() <= 1e-5 * bound + 1e-6).all()
     ref_db = dy.double().sum(0)
     assert ((lin.bias.grad.double() - ref_db).abs() <= 1e-5 * dy.double().abs().sum(0) + 1e-6).all()
+
+
+@pytest.mark.parametrize("aggr,deg_norm,bias", [("add", "sm", False), ("mean", "rw", True),
+                                                ("max", None, True)])
+def test_gcn_model_residual_fused_matches_step_by_step(cuda, aggr, deg_norm, bias):
+    """GCNModel(residual_hop=1) through the fused residual layer node equals
+    the step-for-step path (gcn_model.py:86-125): forward bitwise, gradients
+    within fp32 GEMM tolerance; includes a skewed (heavy-row) graph."""
+    from mgcn.models import GCNModel
+    rng = np.random.default_rng(21)
+    N = 4000
+    ei = _t(_graph(rng, N, 30000, heavy=3000), cuda)
+    deg = torch.bincount(ei[0], minlength=N).float()
+    x = torch.randn(N, 1, device=cuda)
+    torch.manual_seed(3)
+    model = GCNModel(1, [32] * 5, 2, non_linear='relu', non_linear_layer_wise='relu',
+                     residual_hop=1, dropout=0.0, final_type='proj', pred_on='node',
+                     deg_norm=deg_norm, aggr=aggr, bias=bias).to(cuda)
+    dout = torch.randn(N, 2, device=cuda)
+    res = {}
+    for fused in (True, False):
+        GCNModel.fuse_residual = fused
+        try:
+            for p in model.parameters():
+                p.grad = None
+            out = model(x, ei, deg_K=deg)
+            out.backward(dout)
+            res[fused] = (out.detach().clone(),
+                          {k: p.grad.clone() for k, p in model.named_parameters()})
+        finally:
+            GCNModel.fuse_residual = True
+    assert torch.equal(res[True][0], res[False][0])
+    for k, g in res[False][1].items():
+        scale = max(1.0, float(g.abs().max()))
+        torch.testing.assert_close(res[True][1][k], g, rtol=1e-4, atol=1e-5 * scale, msg=k)
+
+
+def test_residual_act_kernels(cuda):
+    """mgcn_residual_act / _bwd against torch on strided operands."""
+    from mgcn.ops import residual_act, residual_act_bwd
+    g = torch.Generator(device=cuda).manual_seed(2)
+    n, F = 3001, 32
+    Z1 = torch.relu(torch.randn(n, F, device=cuda, generator=g))
+    HR = torch.randn(n, 2 * F, device=cuda, generator=g)
+    rb = torch.randn(F, device=cuda, generator=g)
+    for relu in (True, False):
+        Z = residual_act(Z1, HR[:, F:], rb, relu)
+        ref = Z1 + (HR[:, F:] + rb)
+        assert torch.equal(Z, torch.relu(ref) if relu else ref)
+        dZ = torch.randn(n, F, device=cuda, generator=g)
+        DH = torch.zeros(n, 2 * F, device=cuda)
+        dA = torch.empty(n, F, device=cuda)
+        div = torch.randint(1, 9, (n,), device=cuda, generator=g).float()
+        sums = residual_act_bwd(dZ, Z, relu, Z1, True, dA, DH[:, F:], row_div=div)
+        dS = torch.where(Z > 0, dZ, torch.zeros_like(dZ)) if relu else dZ
+        a = torch.where(Z1 > 0, dS, torch.zeros_like(dS))
+        assert torch.equal(DH[:, F:], dS) and torch.equal(dA, a / div[:, None])
+        torch.testing.assert_close(sums[:F].double(), a.double().sum(0), rtol=1e-5, atol=1e-4)
+        torch.testing.assert_close(sums[F:].double(), dS.double().sum(0), rtol=1e-5, atol=1e-4)
