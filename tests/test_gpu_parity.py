@@ -632,3 +632,37 @@ def test_residual_act_kernels(cuda):
         assert torch.equal(DH[:, F:], dS) and torch.equal(dA, a / div[:, None])
         torch.testing.assert_close(sums[:F].double(), a.double().sum(0), rtol=1e-5, atol=1e-4)
         torch.testing.assert_close(sums[F:].double(), dS.double().sum(0), rtol=1e-5, atol=1e-4)
+
+
+def test_int64_offsets_beyond_2_31_elements(cuda):
+    """N F > 2^31 (config 5 gathers from a 51 GB [50M, 256] matrix): forward
+    and adjoint SpMM rows sampled across the whole range equal a sequential
+    fp32 restatement in COO order bit for bit (scripts/config5_check.py runs
+    the full config-5 size: profiles/r01/config5_check.json)."""
+    from mgcn import _lib as L
+    from mgcn.ops import spmm_bwd, spmm_fwd
+    import mgcn
+    N, P, F = 20_000_000, 20_000_000, 128  # N F = 2.56e9
+    g = torch.Generator(device=cuda).manual_seed(5)
+    s = torch.randint(0, N, (P,), device=cuda, generator=g)
+    d = torch.randint(0, N, (P,), device=cuda, generator=g)
+    ar = torch.arange(N, device=cuda)
+    ei = torch.stack([torch.cat([s, d, ar]), torch.cat([d, s, ar])])
+    del s, d, ar
+    plan = mgcn.build_plan(ei, N)
+    norm = plan.norm("sm")
+    del ei
+    X = torch.randn(N, F, device=cuda, generator=g)
+    Y, _ = spmm_fwd(plan.fwd, norm.w_fwd, X, L.REDUCE_SUM)
+    dH = spmm_bwd(plan.bwd, norm.w_bwd, None, X, L.REDUCE_SUM)
+    rows = torch.cat([torch.tensor([N - 1, N - 2]),
+                      torch.from_numpy(np.random.default_rng(0).integers(N // 2, N, 14))])
+    for view, w, out in ((plan.fwd, norm.w_fwd, Y), (plan.bwd, norm.w_bwd, dH)):
+        for r in rows.tolist():
+            b, e = int(view.rowptr[r]), int(view.rowptr[r + 1])
+            xs = X[view.col[b:e].long()].cpu().numpy()
+            ww = w[b:e].cpu().numpy()
+            acc = np.zeros(F, dtype=np.float32)
+            for k in range(e - b):
+                acc = (acc + (xs[k] * ww[k]).astype(np.float32)).astype(np.float32)
+            np.testing.assert_array_equal(out[r].cpu().numpy(), acc)
