@@ -333,6 +333,9 @@ def main():
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
         "higher_is_better": True, "scaling": scaling,
         "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "arithmetic": ("aggregation fp32 (bitwise = reference); dense x@W / dW / dX products as "
+                       "bf16x6 (exact 3-term bf16 split of each fp32 operand, 6 MFMA products, "
+                       "fp32 accumulate; error at fp32 level, tests/test_gpu_parity.py)"),
         "config": {"workload": workload, "nodes": N, "edges": n_edges, "nnz": nnz, "feat": F,
                    "layers": L, "global_batch": world if do_replica else 1,
                    "parallelism": parallelism},
