@@ -16,7 +16,7 @@ dev = torch.device("cuda:0")
 M, F = 1_000_000, 128
 X = torch.randn(M, F, device=dev); dH = torch.randn(M, F, device=dev)
 W = torch.randn(F, F, device=dev); RM = make_relu_mask(torch.randn(M, F, device=dev))
-out = {"lib": os.environ["MGCN_LIB"]}
+out = {"lib": os.environ["MGCN_LIB"], "opts": os.environ.get("MGCN_OPTIONS", "")}
 for name, fn in [("relu", lambda: gemm_bwd(X, dH, W, relu_mask=RM)),
                  ("dw_only", lambda: gemm_bwd(X, dH, W, want_dx=False)),
                  ("tn", lambda: gemm_tn(X, dH)),
@@ -26,8 +26,9 @@ for name, fn in [("relu", lambda: gemm_bwd(X, dH, W, relu_mask=RM)),
 print(json.dumps(out), flush=True)
 '''.replace("ROOT", repr(ROOT))
 
-for lib in sys.argv[1:]:
-    env = dict(os.environ, MGCN_LIB=os.path.abspath(lib))
+for spec in sys.argv[1:]:
+    lib, _, opts = spec.partition(":")
+    env = dict(os.environ, MGCN_LIB=os.path.abspath(lib), MGCN_OPTIONS=opts)
     r = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True,
                        timeout=300)
     print(r.stdout.strip() or r.stderr[-2000:], flush=True)
