@@ -16,9 +16,12 @@ backward to every weight and bias (no optimizer step, as the metric defines).
 
     edges/s = E * L / t_step          (E = 10M graph edges, loops not counted)
 
-N > 1 GPUs (torch.distributed.run, one rank per GPU, RCCL): the same graph
-sharded by destination-node range (mgcn.dist); `value` is the whole job's
-edges/s, `scaling` "strong" (total work fixed).
+N > 1 GPUs (torch.distributed.run, one rank per GPU, RCCL): `value` is the
+whole job's edges/s of data-parallel replicas (every rank its own config-2
+graph, one bucketed gradient all-reduce per step; `scaling` "weak"); the same
+run also times ONE graph sharded by destination-node range (mgcn.dist) and
+reports it under `sharded` (`scaling` "strong").  `--mode replica|shard`
+measures one of them.
 """
 from __future__ import annotations
 
@@ -356,6 +359,11 @@ def main():
             elif name == "gemm_bwd":  # dW and dX: 4 rows F F flop; X, dH read, dX + mask
                 fl = 4.0 * rows_local * F * F
                 b = (12 * F + 16) * rows_local
+                kern[name] = dict(s, flop=fl, tflops=fl / (s["avg_ms"] * 1e-3) / 1e12, bytes=b,
+                                  gbs=b / (s["avg_ms"] * 1e-3) / 1e9)
+            elif name == "gemm_bwd_dw":  # dW alone: 2 rows F F flop; X, dH read
+                fl = 2.0 * rows_local * F * F
+                b = 8 * F * rows_local
                 kern[name] = dict(s, flop=fl, tflops=fl / (s["avg_ms"] * 1e-3) / 1e12, bytes=b,
                                   gbs=b / (s["avg_ms"] * 1e-3) / 1e9)
             else:  # F x F feature transforms on MFMA: 2 rows F F flop per launch

@@ -986,7 +986,7 @@ extern "C" int mgcn_debug_heavy_prof(unsigned long long *host) {
 
 extern "C" int mgcn_set_option(const char *name, int value) {
   clear_error();
-  if (name == nullptr) return MGCN_EINVAL;
+  MGCN_REQUIRE(name != nullptr, "mgcn_set_option: null name");
   const std::string n(name);
   if (n == "spmm_vec") {
     MGCN_REQUIRE(value == 0 || value == 1 || value == 2 || value == 4, "spmm_vec must be 0,1,2,4");
@@ -1084,7 +1084,8 @@ extern "C" int mgcn_spmm_fwd(int64_t n_rows, int32_t F, const int64_t *rowptr, c
   if (reduce == MGCN_REDUCE_MAX && argmax != nullptr &&
       reinterpret_cast<uintptr_t>(argmax) % (4 * vec))
     vec = 1;
-  if (bias != nullptr && reinterpret_cast<uintptr_t>(bias) % 4) return MGCN_EINVAL;
+  MGCN_REQUIRE(bias == nullptr || reinterpret_cast<uintptr_t>(bias) % 4 == 0,
+               "mgcn_spmm_fwd: bias not 4-byte aligned");
   hipStream_t s = as_stream(stream);
   if (reduce == MGCN_REDUCE_MAX) return launch_mode<FWD_MAX>(a, vec, s);
   return launch_mode<FWD_SUM>(a, vec, s);

@@ -12,8 +12,10 @@ unchanged after swapping the import:
 
 The aggregation (gather, degree normalisation, reduce, bias, ReLU) is one HIP
 kernel per direction (:func:`mgcn.ops.aggregate`); the feature transform
-``x @ W`` stays ``torch.matmul`` exactly as the reference writes it
-(gcn_base_models.py:201).
+``x @ W`` (gcn_base_models.py:201) runs on libmgcn's MFMA GEMMs through
+:func:`mgcn.ops.linear` (bf16x6 arithmetic, fp32 accuracy), with a fused
+backward (dW, dX, ReLU mask, bias column sums in one kernel); residual layers
+fuse their skip projection into the same GEMM (:func:`mgcn.ops.residual_gcn_layer`).
 """
 from __future__ import annotations
 

@@ -268,7 +268,7 @@ def gemm_bwd(x: torch.Tensor, dH: torch.Tensor, W: torch.Tensor, want_dx: bool =
     ws_bytes = int(lib.mgcn_gemm_bwd_workspace_bytes(M, F_in, F_out))
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
     if _TIMER is not None:
-        _TIMER("gemm_bwd", True)
+        _TIMER("gemm_bwd" if want_dx else "gemm_bwd_dw", True)
     with torch.cuda.device(dev):
         rc = lib.mgcn_gemm_bwd(M, F_in, F_out, L.ptr(x), x.stride(0), L.ptr(dH), dH.stride(0),
                                L.ptr(W), W.stride(0), L.ptr(dW), dW.stride(0),
@@ -277,7 +277,7 @@ def gemm_bwd(x: torch.Tensor, dH: torch.Tensor, W: torch.Tensor, want_dx: bool =
                                L.ptr(row_div), L.ptr(colsum), L.ptr(ws), ws_bytes,
                                L.stream_of(dev))
     if _TIMER is not None:
-        _TIMER("gemm_bwd", False)
+        _TIMER("gemm_bwd" if want_dx else "gemm_bwd_dw", False)
     L.check(rc, "mgcn_gemm_bwd")
     return dW, dX, colsum
 
