@@ -150,10 +150,22 @@ __device__ __forceinline__ f32x2 widen_bf16x2(uint32_t p) {
 }
 
 // one pair of floats -> its hi / mid / lo bf16 pairs (v_cvt_pk_bf16_f32, RNE)
+// Range edge: |x| >= ~3.396e38 rounds to bf16 inf, and x - inf = -inf, so
+// the terms would sum to NaN where fp32 gives a finite or infinite product.
+// hi and mid therefore come from x and r clamped to +-kSplitMax (the largest
+// float whose RNE bf16 is finite, v_med3_f32): for finite x the split stays
+// exact (hi = 0x7f7f.. then r = x - hi exactly), for x = +-inf it is
+// (+-M, +-M, +-inf) -- a product with w is +-inf (NaN for w = 0), as in fp32.
+constexpr float kSplitMax = 0x1.fefffep+127f;  // 0x7f7f7fff = 3.3961514e38
+__device__ __forceinline__ float split_clamp(float v) {
+  return __builtin_amdgcn_fmed3f(v, -kSplitMax, kSplitMax);
+}
 __device__ __forceinline__ void split3_pair(f32x2 x, uint32_t &hi, uint32_t &mid, uint32_t &lo) {
-  hi = __builtin_bit_cast(uint32_t, __builtin_convertvector(x, bf16x2));
+  const f32x2 xc = {split_clamp(x.x), split_clamp(x.y)};
+  hi = __builtin_bit_cast(uint32_t, __builtin_convertvector(xc, bf16x2));
   const f32x2 r = x - widen_bf16x2(hi);  // exact (Sterbenz)
-  mid = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, bf16x2));
+  const f32x2 rc = {split_clamp(r.x), split_clamp(r.y)};
+  mid = __builtin_bit_cast(uint32_t, __builtin_convertvector(rc, bf16x2));
   lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(r - widen_bf16x2(mid), bf16x2));
 }
 
@@ -946,13 +958,15 @@ __global__ __launch_bounds__(kNNThreads, P == PREC_BF16X6 ? 1 : 2) void gemm_nn_
 template <int K, int NT, int EPI, int P>
 int nn_blocks(int64_t M) {
   // resident capacity of this instantiation (queried once), capped by work
-  static int per_cu = 0;
+  static std::atomic<int> per_cu_cache{0};  // same code object on every device
+  int per_cu = per_cu_cache.load(std::memory_order_relaxed);
   if (per_cu == 0) {
     int b = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gemm_nn_kernel<K, NT, EPI, P>, kNNThreads,
                                                      0) != hipSuccess || b < 1)
       b = 1;
     per_cu = b;
+    per_cu_cache.store(b, std::memory_order_relaxed);
   }
   constexpr int GS = (K == 32) ? 2 : 1;
   const int64_t units = ((M + 31) / 32 + GS - 1) / GS;

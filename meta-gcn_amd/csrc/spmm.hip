@@ -873,11 +873,16 @@ int launch_heavy_hb(SpmmArgs a, const int32_t *rows, int64_t n, int lds_budget,
   BE &= ~15;
   if (BE < 16) BE = 16;  // a small budget still gets one 16-edge batch (<= 21 KB)
   const size_t lds = sizeof(float) * ((size_t)2 * FC * (BE + 4) + (size_t)12 * BE);
-  static bool attr_set = false;  // one instantiation per (VEC, MODE, HB)
-  if (!attr_set) {
+  // the 160 KB dynamic-LDS attribute is per device: one bit per device id,
+  // per instantiation (VEC, MODE, HB); racing threads at worst both set it
+  static std::atomic<uint64_t> attr_set{0};
+  int dev = 0;
+  MGCN_HIP_TRY(hipGetDevice(&dev));
+  const uint64_t bit = uint64_t(1) << (dev & 63);
+  if (!(attr_set.load(std::memory_order_acquire) & bit)) {
     MGCN_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(&spmm_heavy_kernel<VEC, MODE, HB>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    attr_set = true;
+    attr_set.fetch_or(bit, std::memory_order_release);
   }
   hipLaunchKernelGGL((spmm_heavy_kernel<VEC, MODE, HB>), dim3((unsigned)n), dim3(HB), lds, stream,
                      a, FC, BE);

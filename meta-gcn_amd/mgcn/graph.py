@@ -158,6 +158,16 @@ class GraphPlan:
         code = L.NORM_CODES[method]
         if edge_weight is not None:
             deg = None
+        if torch.is_grad_enabled():
+            # The per-slot weights are built outside autograd: no gradient
+            # flows back into edge_weight / deg.  The reference's degnorm_const
+            # (gcn_base_models.py:102-140) is differentiable in them, so a
+            # caller that wants that gradient must not get a silent zero.
+            for name, t in (("edge_weight", edge_weight), ("deg", deg)):
+                if t is not None and t.requires_grad:
+                    raise NotImplementedError(
+                        f"mgcn: gradient with respect to {name} is not implemented; pass "
+                        f"{name}.detach() (or run under torch.no_grad())")
         key = (code, _tkey(deg), _tkey(edge_weight))
         hit = self.norms.get(key)
         if hit is not None and _alive(hit[1]):
@@ -171,6 +181,10 @@ class GraphPlan:
 
 
 def _tkey(t: torch.Tensor | None):
+    # (storage, version counter, geometry): an in-place update through the
+    # tensor bumps _version and misses the cache; writes through ``.data``
+    # (which do not bump it) are invisible here -- call plan.norms.clear()
+    # after such a write.
     if t is None:
         return None
     return (t.data_ptr(), t._version, tuple(t.shape), tuple(t.stride()), t.dtype)

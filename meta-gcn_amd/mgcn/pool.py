@@ -42,11 +42,16 @@ EPS = 1e-15
 
 
 # ------------------------------------------------------------- utilities
-def scatter_max_arg(src: torch.Tensor, index: torch.Tensor, dim_size: int):
-    """torch_scatter 1.x ``scatter_max(src, index, 0, None, dim_size)`` for
-    [E] / [E, F] ``src``: (max, argmax) per row, argmax = the winning
-    position in ``src`` (ties: the later one, torch_scatter's CPU scan), -1
-    and value 0 for empty rows.  No autograd (callers use the argmax)."""
+def scatter_max_arg(src: torch.Tensor, index: torch.Tensor, dim_size: int,
+                    fill_value: float | None = None):
+    """torch_scatter 1.x ``scatter_max(src, index, 0, None, dim_size,
+    fill_value)`` for [E] / [E, F] ``src``: (max, argmax) per row, argmax =
+    the winning position in ``src`` (ties: the later one, torch_scatter's CPU
+    scan), -1 and value 0 for empty rows.  With ``fill_value`` the scan starts
+    from it (``src >= out``): an entry below it never wins, so a row whose
+    maximum is below ``fill_value`` (or that is empty) gets argmax -1 and
+    value ``fill_value`` (hard_attention_pool.py:76 passes -1e16).  No
+    autograd (callers use the argmax)."""
     squeeze = src.dim() == 1
     x = (src.unsqueeze(1) if squeeze else src).detach().contiguous()
     E = x.size(0)
@@ -54,6 +59,11 @@ def scatter_max_arg(src: torch.Tensor, index: torch.Tensor, dim_size: int):
     view = build_view(index, ids, int(dim_size), E)
     out, arg = spmm_fwd(view, None, x, L.REDUCE_MAX)
     arg = arg.to(torch.int64)
+    if fill_value is not None:
+        fill = torch.tensor(fill_value, dtype=out.dtype, device=out.device)
+        lose = (arg < 0) | (out < fill)
+        arg = arg.masked_fill(lose, -1)
+        out = torch.where(lose, fill, out)
     return (out.squeeze(1), arg.squeeze(1)) if squeeze else (out, arg)
 
 
@@ -605,7 +615,9 @@ class HardPooling(torch.nn.Module):
         else:
             if self.sample:
                 alpha = alpha + gumbel_samples(alpha)
-            _, argmax = scatter_max_arg(alpha, edge_index[0], N)  # [N, 1]
+            # torch_scatter.scatter_max(..., fill_value=-1e16) (:76): a node
+            # whose out-edge scores are all below -1e16 has no winner (-1)
+            _, argmax = scatter_max_arg(alpha, edge_index[0], N, fill_value=-1e16)  # [N, 1]
             E = alpha.size(0)
             hot = torch.zeros(E, device=alpha.device, dtype=alpha.dtype)
             hot[argmax.view(-1) % max(E, 1)] = 1.0  # -1 (no out-edge) -> last edge

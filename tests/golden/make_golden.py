@@ -278,10 +278,13 @@ def model12_case(gm, name, rng, N, E, L=12, F=32):
     save(name, edge_index=ei, x=x, dout=g, out=out, **params, **grads)
 
 
-def hardpool_case(hap, name, rng, sizes, F, aggr, bias, lonely=True):
+def hardpool_case(hap, name, rng, sizes, F, aggr, bias, lonely=True, sunk=0):
     """HardPooling (hard_attention_pool.py:23-131) in eval mode on a batch of
     graphs; ``lonely`` gives one node no out-edge (argmax -1 in torch_scatter
-    1.x, which the reference turns into marking the last edge)."""
+    1.x, which the reference turns into marking the last edge).  ``sunk``
+    nodes get features -sign(att_weight[:F]) * 1e17, so every out-edge score
+    of theirs is far below scatter_max's fill_value -1e16 (:76): no winner,
+    argmax -1, as for a node without out-edges."""
     eis, batch, off = [], [], 0
     for g, n in enumerate(sizes):
         E = 3 * n
@@ -302,6 +305,10 @@ def hardpool_case(hap, name, rng, sizes, F, aggr, bias, lonely=True):
         with torch.no_grad():
             pool.bias.uniform_(-0.5, 0.5)
     pool.eval()
+    if sunk:
+        a_src = pool.att_weight.detach().numpy()[0, :F]
+        for v in rng.choice(off, sunk, replace=False):
+            x[v] = -np.sign(a_src).astype(np.float32) * np.float32(1e17)
     xt = _t(x).requires_grad_(True)
     out, ei2, _, b2, perm, score = pool(xt, _t(ei), _t(batch))
     dY = rng.standard_normal(tuple(out.shape)).astype(np.float32)
@@ -321,7 +328,8 @@ def main_hardpool():
     hardpool_case(hap, "hardpool_add", rng, [12, 30, 7], 16, "add", False)
     hardpool_case(hap, "hardpool_add_bias", rng, [25, 9, 40, 16], 16, "add", True)
     hardpool_case(hap, "hardpool_mean", rng, [20, 33], 8, "mean", False, lonely=False)
-    print("wrote 3 hardpool fixtures to", OUT_DIR)
+    hardpool_case(hap, "hardpool_sunk", rng, [18, 26], 8, "add", False, lonely=False, sunk=6)
+    print("wrote 4 hardpool fixtures to", OUT_DIR)
 
 
 def main():

@@ -291,6 +291,45 @@ def test_gemm_bf16x6_error_at_fp32_level(cuda):
     assert errs[1][1] <= 2 * errs[0][1] + 1e-7, errs
 
 
+def test_gemm_nonfinite_and_range_edge_operands(cuda, gemm_precision):
+    """+-inf and |x| near FLT_MAX (where bf16 RNE overflows, 3.3962e38 ..
+    3.4028e38) in either operand: the products are +-inf where fp32 matmul
+    gives +-inf and finite (within the usual bound) where it is finite --
+    never the NaN of inf - inf inside the bf16 split."""
+    from mgcn.ops import gemm_nn, gemm_tn
+    g = torch.Generator(device=cuda).manual_seed(17)
+    M, K = 4097, 128
+    A = torch.randn(M, K, device=cuda, generator=g) * 1e-3
+    W = torch.rand(K, K, device=cuda, generator=g) * 0.1 + 0.1  # positive: signs predictable
+    A[0, 0] = float("inf")
+    A[1, 3] = float("-inf")
+    A[2, 5] = 3.4e38
+    A[3, 7] = -3.39e38
+    A[4, 9] = 3.3961514e38
+    A[5, 11] = torch.finfo(torch.float32).max
+    B = torch.rand(M, K, device=cuda, generator=g) * 0.1 + 0.1
+    for C, ref, bound in (
+            (gemm_nn(A, W)[0], A.double() @ W.double(), A.double().abs() @ W.double().abs()),
+            (gemm_tn(A, B), A.double().t() @ B.double(), A.double().abs().t() @ B.double().abs())):
+        C = C.double()
+        inf = torch.isinf(ref)
+        assert inf.any() and not torch.isnan(C).any()
+        assert torch.equal(C[inf], ref[inf])  # same signed infinities
+        fin = ~inf
+        assert torch.isfinite(C[fin]).all()
+        assert ((C[fin] - ref[fin]).abs() <= 1e-5 * bound[fin] + 1e-6).all()
+    # the other operand: W with an inf column entry and a near-FLT_MAX one
+    A2 = torch.rand(M, K, device=cuda, generator=g) * 0.1 + 0.1
+    W2 = W.clone()
+    W2[4, 2] = float("inf")
+    W2[6, 9] = 3.4e38
+    C = gemm_nn(A2, W2)[0].double()
+    ref = A2.double() @ W2.double()
+    assert torch.equal(torch.isinf(C), torch.isinf(ref)) and not torch.isnan(C).any()
+    fin = torch.isfinite(ref)
+    assert ((C[fin] - ref[fin]).abs() <= 1e-5 * (A2.double() @ W2.double().abs())[fin]).all()
+
+
 def test_relu_mask_layout(cuda, oracle):
     """mgcn_relu_mask / the SpMM's fused mask: bit b of word v <=> Z[i, 4b+v] > 0,
     for the fused F = 128 rows, heavy rows and other F."""

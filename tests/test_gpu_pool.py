@@ -299,7 +299,8 @@ def test_dense_sage_and_diff_pool(cuda):
     torch.testing.assert_close(ent.cpu(), (-S * torch.log(S + 1e-15)).sum(-1).mean())
 
 
-@pytest.mark.parametrize("name", ["hardpool_add", "hardpool_add_bias", "hardpool_mean"])
+@pytest.mark.parametrize("name", ["hardpool_add", "hardpool_add_bias", "hardpool_mean",
+                                  "hardpool_sunk"])
 def test_hard_pooling_matches_reference(cuda, name):
     """Eval-mode HardPooling == the reference module (fixtures from
     hard_attention_pool.py itself): pooled features and dx bitwise, kept

@@ -152,3 +152,20 @@ def test_oracle_is_not_imported_by_product():
                 text = open(os.path.join(dirpath, f)).read()
                 assert "import oracle" not in text and "from oracle" not in text, f
                 assert "liboracle" not in text, f
+
+
+def test_norm_rejects_grad_requiring_edge_weight_and_deg():
+    """degnorm_const is differentiable in edge_weight / deg in the reference
+    (gcn_base_models.py:102-140); the per-slot weights here are built
+    outside autograd, so asking for that gradient raises instead of
+    silently returning none (checked before any device work)."""
+    from mgcn.graph import GraphPlan
+    plan = GraphPlan(num_nodes=3, nnz=4, device=torch.device("cpu"), fwd=None, bwd=None,
+                     in_cnt=torch.ones(3))
+    ew = torch.ones(4, requires_grad=True)
+    with pytest.raises(NotImplementedError, match="edge_weight"):
+        plan.norm("sm", edge_weight=ew)
+    with pytest.raises(NotImplementedError, match="deg"):
+        plan.norm("rw", deg=torch.ones(3, requires_grad=True))
+    with pytest.raises(NotImplementedError, match="edge_weight"):
+        plan.norm(None, edge_weight=ew)

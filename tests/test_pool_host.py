@@ -70,7 +70,7 @@ def test_hardpool_fixtures_are_consistent():
     """The reference's eval-mode HardPooling output: kept nodes are the
     targets of the selected edges, the pooled edge list is the induced
     subgraph relabelled, batch follows perm."""
-    for name in ("hardpool_add", "hardpool_add_bias", "hardpool_mean"):
+    for name in ("hardpool_add", "hardpool_add_bias", "hardpool_mean", "hardpool_sunk"):
         d = np.load(os.path.join(GOLDEN, name + ".npz"))
         perm = d["perm"]
         assert np.all(np.diff(perm) > 0)
