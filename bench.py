@@ -346,7 +346,9 @@ def main():
         "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "arithmetic": ("aggregation fp32 (bitwise = reference); dense x@W / dW / dX products as "
                        "bf16x6 (exact 3-term bf16 split of each fp32 operand, 6 MFMA products, "
-                       "fp32 accumulate; error at fp32 level, tests/test_gpu_parity.py)"),
+                       "fp32 accumulate; error at fp32 level, tests/test_gpu_parity.py); "
+                       "layers fused as (A x) W in one launch per direction "
+                       "(mgcn_spmm_xw_fwd / _bwd; tests/test_gpu_fused.py)"),
         "config": {"workload": workload, "nodes": N, "edges": n_edges, "nnz": nnz, "feat": F,
                    "layers": L, "global_batch": world if do_replica else 1,
                    "parallelism": parallelism},
@@ -361,7 +363,19 @@ def main():
         nnz_local = nnz // world if shard_only else nnz
         kern = {}
         for name, s in ks.items():
-            if name.startswith("spmm"):
+            if name.startswith("spmm_xw"):
+                # fused layer kernels: the SpMM's bytes (gathered rows + output rows);
+                # the adjoint also reads X (4 N F) -- the dW-only form writes no dX
+                b = spmm_bytes(rows_local, nnz_local, F)
+                fl = 2.0 * rows_local * F * F
+                if name == "spmm_xw_bwd":
+                    b += 4 * rows_local * F
+                    fl *= 2
+                elif name == "spmm_xw_bwd_dw":
+                    pass  # X read instead of the output write: the same count
+                kern[name] = dict(s, bytes=b, gbs=b / (s["avg_ms"] * 1e-3) / 1e9, flop=fl,
+                                  tflops=fl / (s["avg_ms"] * 1e-3) / 1e12)
+            elif name.startswith("spmm"):
                 b = spmm_bytes(rows_local, nnz_local, F)
                 kern[name] = dict(s, bytes=b, gbs=b / (s["avg_ms"] * 1e-3) / 1e9)
             elif name == "gemm_bwd":  # dW and dX: 4 rows F F flop; X, dH read, dX + mask

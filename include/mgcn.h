@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define MGCN_ABI_VERSION 7
+#define MGCN_ABI_VERSION 8
 
 /* return codes */
 #define MGCN_OK 0
@@ -289,6 +289,57 @@ int mgcn_gemm_bwd(int64_t M, int32_t F_in, int32_t F_out, const float *X, int64_
                   float *dW, int64_t lddw, int accumulate, float *dX, int64_t lddx,
                   const uint32_t *relu_mask, const float *row_div, float *colsum,
                   void *workspace, size_t workspace_bytes, void *stream);
+
+/* ------------------------------------------------- fused layer forward */
+
+/* 1 if mgcn_spmm_xw_fwd / _bwd handle (F_in, F_out, reduce): 128 x 128, sum or
+ * mean, under the bf16x6 product arithmetic (gemm_precision 1, the default). */
+int mgcn_spmm_xw_supported(int32_t F_in, int32_t F_out, int reduce);
+
+/*
+ * One GCN layer forward in one launch, aggregating before transforming:
+ *   Y[i] = epi( (reduce_{k in row i} X[col_k] * w_k) . W + bias )
+ * over the fwd CSR view (rowptr/col as mgcn_spmm_fwd; w nullable), X
+ * [n_cols, F_in] (ldx, 16-byte aligned rows, under 4 GiB), W [F_in, F_out] row-major (ldw),
+ * reduce SUM or MEAN (divides the aggregated row by max(in-degree, 1)), epi =
+ * optional ReLU, relu_mask (nullable, needs relu) in mgcn_spmm_fwd's layout.
+ * Equals mgcn_gemm_nn (X W) followed by mgcn_spmm_fwd up to the association
+ * of the sums (A (X W) = (A X) W for a linear aggregator): the reference's
+ * `x @ weight_node` then gather / scale / scatter_add
+ * (gcn_base_models.py:201, 223-241; PyG GCNConv x @ W then propagate) without
+ * materialising X W.  Rows with heavy degree are handled, but slowly (one
+ * lane group per row): callers route skewed graphs to the two-launch path.
+ */
+int mgcn_spmm_xw_fwd(int64_t n_rows, int64_t n_cols, int32_t F_in, int32_t F_out, const int64_t *rowptr,
+                     const int32_t *col, const float *w, const float *X, int64_t ldx,
+                     const float *W, int64_t ldw, const float *bias, float *Y, int64_t ldy,
+                     int reduce, int relu, uint32_t *relu_mask, void *stream);
+
+/* Bytes of scratch mgcn_spmm_xw_bwd needs (split-K partials + column sums). */
+size_t mgcn_spmm_xw_bwd_workspace_bytes(int64_t n_rows);
+
+/*
+ * One GCN layer backward in one launch (F_in = F_out = 128; sum / mean
+ * aggregation, whose adjoint is a plain sum once dY is pre-divided):
+ *   dH  = reduce_{k in row s} dY[col_k] * w_k  [* row_scale[s]]   (bwd view:
+ *         rows = source nodes; = mgcn_spmm_bwd's dH, bit for bit)
+ *   dW  = X^T dH   (accumulate != 0: dW += ...; deterministic split-K)
+ *   dX  = dH W^T   with relu_mask / row_div / colsum as mgcn_gemm_bwd
+ *         (skipped when dX == NULL)
+ * dH is never written: it goes from the gather into LDS and through both
+ * MFMA products.  Replaces mgcn_spmm_bwd + mgcn_gemm_bwd (the adjoints of
+ * gcn_base_models.py:201-241: autograd's index_add of the gathered dY and
+ * the two matmul adjoints, plus the ReLU / bias gradient of the layer below,
+ * gcn_model.py:196).  dY rows [n_cols, 128] (lddy, 16-byte aligned, under
+ * 4 GiB), X [n_rows, 128] (ldx, 16-byte aligned), W [128, 128] row-major.
+ */
+int mgcn_spmm_xw_bwd(int64_t n_rows, int64_t n_cols, int32_t F_in, int32_t F_out,
+                     const int64_t *rowptr_t, const int32_t *col_t, const float *w_t,
+                     const float *row_scale, const float *dY, int64_t lddy, const float *X,
+                     int64_t ldx, const float *W, int64_t ldw, float *dW, int64_t lddw,
+                     int accumulate, float *dX, int64_t lddx, const uint32_t *relu_mask,
+                     const float *row_div, float *colsum, void *workspace,
+                     size_t workspace_bytes, void *stream);
 
 /* ----------------------------------------------------------- elementwise */
 

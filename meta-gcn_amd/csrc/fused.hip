@@ -1,0 +1,700 @@
+// Fused GCN layer kernels on gfx950: the aggregation and the layer's dense
+// product in one pass, forward and backward (F_in = F_out = 128, sum / mean).
+//
+// Forward:   Y = epi( (A_norm X) W + b ),   epi = optional ReLU (+ row mask)
+// Backward:  dH = A_norm^T dY [* row_scale];  dW = X^T dH;
+//            dX = relu'(lower) (dH W^T) [/ row_div],  colsum = sum_rows dX
+//
+// The reference computes a layer as  x @ W  then  gather -> * norm ->
+// scatter_add  (src/gcn_meta/models/gcn_base_models.py:201, 223-237; PyG
+// GCNConv: x @ W then propagate), and autograd runs the adjoints in reverse.
+// Unfused here that is two launches per direction: mgcn_gemm_nn (reads X,
+// writes H = X W) + mgcn_spmm_fwd (gathers H), and mgcn_spmm_bwd (writes dH)
+// + mgcn_gemm_bwd (reads X and dH, writes dX).  For a linear aggregator
+// A (X W) = (A X) W, so the forward gathers X itself and multiplies the
+// aggregated rows of a 32-row chunk by W on MFMA in the same workgroup, and
+// the backward multiplies the chunk's dH rows by W^T and X^T before they
+// ever leave the workgroup.  H and dH never exist: per layer at config 2 this
+// removes 1 GB of HBM traffic in each direction and a launch.  Max does not
+// commute with W and keeps the two-launch path.
+//
+// Numerics: aggregated rows are summed exactly as the SpMM sums (edge order,
+// separately rounded products and adds: mgcn_spmm_fwd / _bwd bit for bit);
+// the dense products are the bf16x6 MFMA arithmetic of gemm.hip.  The
+// forward's association differs from the reference's (A (X W) vs (A X) W),
+// so the layer output matches within fp32 tolerance, not bitwise -- except
+// for W = I, where every bf16x6 product is exact.  The backward's dX is
+// mgcn_gemm_bwd's bit for bit (same dH, same products and order); dW and
+// the column sums fold the same products over a different split-K grid.
+//
+// Chunk layout (both directions): persistent 512-thread workgroups (8
+// waves), two per CU; chunk c (rows 32 c .. 32 c + 31) goes to workgroup
+// c % grid.
+//   Phase A (gather): row 16 p + 2 wave + grp of the chunk is owned by the
+//     32-lane group grp of wave `wave` in pass p; lane gl holds features
+//     4 gl .. 4 gl + 3 of every gathered 512-B row, U gathers in flight per
+//     group, folded in edge order; the finished row is split into the
+//     chunk's bf16 hi / mid / lo images (x6.h layout).
+//   Phase B (MFMA): wave w owns output columns 16 w .. 16 w + 15 of the
+//     chunk (v_mfma_f32_16x16x32_bf16); the backward's dW tiles are
+//     gemm_bwd's (32x32x16 on transposed image reads).  Results go to an
+//     fp32 staging tile in LDS.
+//   The staged tile is written out as whole 512-B rows (16 B per lane) at
+//   the start of the next chunk, beside its gathers: 4-byte column stores
+//   straight from the MFMA layout cost 0.19 ms per 512 MB (store issue).
+//
+// Roofline: HBM-bound like the SpMM, with the GEMMs' bytes removed:
+//   forward  8 (N + 1) + nnz (4 col + 4 w + 4 F) + 4 N F (+ 16 N mask)
+//   backward the same + 4 N F (X) (+ 16 N mask)
+// and 2 N F^2 (forward) / 4 N F^2 (backward) x 6 bf16 MFMA flops under it.
+
+#include "mgcn_internal.h"
+#include "x6.h"
+
+namespace mgcn {
+namespace {
+
+using namespace x6;
+
+constexpr int kXwF = 128;
+constexpr int kXwRows = 32;
+constexpr int kXwWaves = 8;
+constexpr int kXwThreads = 64 * kXwWaves;
+constexpr int kXwImg = kXwRows * 256;          // one bf16 term image of a chunk
+constexpr int kXwStageLd = kXwF + 4;           // backward staging row stride (floats)
+constexpr int kXwStage = kXwRows * kXwStageLd * 4;
+constexpr int kXfStage = kXwRows * kXwF * 4;   // forward staging tile (unpadded: 2 fit)
+constexpr int kXwPerCU = 2;  // resident workgroups per CU the grid is sized for
+
+constexpr int EPI_STORE = 0, EPI_RELU = 1, EPI_RELU_DIV = 2;
+
+// Aggregate one row in the 32-lane group `grp` of the wave (both groups of a
+// wave call this together): acc = sum_k X[col_k] * w_k in edge order,
+// products and sums rounded separately -- the SpMM's arithmetic, bit for bit.
+// Lane gl holds features 4 gl .. 4 gl + 3; edge metadata is loaded 32 edges
+// at a time lane-parallel and broadcast by ds_bpermute; U gathers of whole
+// 512-B rows are in flight per group before any is folded.
+template <int U>
+__device__ __forceinline__ void gather_row(const __amdgpu_buffer_rsrc_t rx, uint32_t ldx_b,
+                                           const int64_t *__restrict__ rowptr,
+                                           const int32_t *__restrict__ col,
+                                           const float *__restrict__ w, int64_t row, bool row_ok,
+                                           int gl, int grp, float (&acc)[4], int64_t &deg_out) {
+  const bool has_w = w != nullptr;
+  const int64_t beg = row_ok ? rowptr[row] : 0;
+  const int64_t deg = row_ok ? rowptr[row + 1] - beg : 0;
+  const int64_t odeg = __shfl_xor(deg, 32, 64);
+  const int64_t maxdeg = deg > odeg ? deg : odeg;
+  acc[0] = acc[1] = acc[2] = acc[3] = 0.0f;
+  for (int64_t e0 = 0; e0 < maxdeg; e0 += 32) {
+    const int64_t my = e0 + gl;
+    int mc = 0;
+    float mw = 1.0f;
+    if (my < deg) {
+      mc = col[beg + my];
+      if (has_w) mw = w[beg + my];
+    }
+    const int64_t rem = deg - e0;
+    const int nb = rem <= 0 ? 0 : (rem < 32 ? (int)rem : 32);
+    const int64_t remw = maxdeg - e0;
+    const int nbmax = remw < 32 ? (int)remw : 32;  // wave-uniform
+    for (int k0 = 0; k0 < nbmax; k0 += U) {
+      float4 xv[U];
+      float wk[U];
+      bool ok[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = k0 + u;
+        const int ck = __shfl(mc, 32 * grp + (k & 31), 64);
+        wk[u] = __shfl(mw, 32 * grp + (k & 31), 64);
+        ok[u] = k < nb;
+        // past-the-row edges get an offset beyond the buffer: no access, zeros
+        const uint32_t off = ok[u] ? (uint32_t)ck * ldx_b + 16u * gl : 0xfffffff0u;
+        xv[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0));
+      }
+      // fold in strictly ascending edge order (as the SpMM, bit for bit)
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (ok[u]) {
+          acc[0] = __fadd_rn(acc[0], __fmul_rn(xv[u].x, wk[u]));
+          acc[1] = __fadd_rn(acc[1], __fmul_rn(xv[u].y, wk[u]));
+          acc[2] = __fadd_rn(acc[2], __fmul_rn(xv[u].z, wk[u]));
+          acc[3] = __fadd_rn(acc[3], __fmul_rn(xv[u].w, wk[u]));
+        }
+      }
+    }
+  }
+  deg_out = deg;
+}
+
+// One row's four features -> its three bf16 term images (lane gl of the group)
+__device__ __forceinline__ void store_row_terms(char *img_base, int lr, int gl, const float (&v)[4]) {
+  uint32_t hi[2], mid[2], lo[2];
+  split3_pair(f32x2{v[0], v[1]}, hi[0], mid[0], lo[0]);
+  split3_pair(f32x2{v[2], v[3]}, hi[1], mid[1], lo[1]);
+  char *img = img_base + img_off(lr, gl >> 1) + 8 * (gl & 1);
+  *reinterpret_cast<uint2 *>(img) = make_uint2(hi[0], hi[1]);
+  *reinterpret_cast<uint2 *>(img + kXwImg) = make_uint2(mid[0], mid[1]);
+  *reinterpret_cast<uint2 *>(img + 2 * kXwImg) = make_uint2(lo[0], lo[1]);
+}
+
+// 16x16x32 products of the chunk's 32 rows (A image at `img`) with this
+// wave's 16 columns of B (fragments in registers): acc[t] = rows 16 t + 4 g4 + r
+__device__ __forceinline__ void mfma_rows(const char *img, const bf16x8 (&b)[3], int ks, int l16,
+                                          int g4, f32x4_t (&acc)[2]) {
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int off = img_off(16 * t + l16, 4 * ks + g4);
+    const bf16x8 ah = *reinterpret_cast<const bf16x8 *>(img + off);
+    const bf16x8 am = *reinterpret_cast<const bf16x8 *>(img + kXwImg + off);
+    const bf16x8 al = *reinterpret_cast<const bf16x8 *>(img + 2 * kXwImg + off);
+    acc[t] = mfma16_x6(ah, am, al, b[0], b[1], b[2], acc[t]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Forward.  LDS: two image sets and two fp32 staging tiles, double-buffered
+// so that one barrier per chunk orders everything: chunk c's images are
+// written before barrier c and read after it; its output rows are staged
+// after barrier c and written out after barrier c + 1.  80 KB: two per CU.
+constexpr int kXfBuf = 3 * kXwImg;
+constexpr int kXfStageOff = 2 * kXfBuf;
+constexpr int kXfLds = kXfStageOff + 2 * kXfStage;
+static_assert(2 * kXfLds <= 160 * 1024, "two forward workgroups per CU");
+
+struct XwArgs {
+  int64_t n_rows;
+  const int64_t *rowptr;
+  const int32_t *col;
+  const float *w;     // per-slot weights, nullable
+  const float *X;     // gathered rows [n_cols][128]
+  int64_t ldx;
+  int64_t n_cols;
+  const float *W;     // [128][128], Y = Z W
+  int64_t ldw;
+  const float *bias;  // nullable
+  float *Y;
+  int64_t ldy;
+  uint32_t *relu_mask;  // nullable; [n_rows][4], bit b of word v <=> Y[row][4 b + v] > 0
+  int mean;
+  int relu;
+};
+
+template <int U>
+__global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_fwd_kernel(const XwArgs a) {
+  __shared__ __attribute__((aligned(16))) char lds[kXfLds];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int gl = lane & 31, grp = lane >> 5;
+  const int l16 = lane & 15, g4 = lane >> 4;
+  const int64_t n_chunks = (a.n_rows + kXwRows - 1) / kXwRows;
+  const bool has_b = a.bias != nullptr;
+  // gathers through one buffer resource over X: 32-bit offsets, 1 VGPR each
+  const auto rx = buf_rsrc(a.X, (uint32_t)(a.n_cols * a.ldx * 4));
+  const uint32_t ldx_b = (uint32_t)a.ldx * 4u;
+
+  // W fragments of this wave's 16 output columns: B[k][n] = W[k][n], lane
+  // (g4, l16) holds k = 32 ks + 8 g4 + j of column n = 16 wave + l16
+  const int ncol = 16 * wave + l16;
+  bf16x8 wb[4][3];
+  {
+    const float *wp = a.W + (int64_t)(8 * g4) * a.ldw + ncol;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = wp[(int64_t)(32 * ks + j) * a.ldw];
+      split3_bf16(v, wb[ks][0], wb[ks][1], wb[ks][2]);
+    }
+  }
+  const float bcol = has_b ? a.bias[ncol] : 0.0f;
+
+  // staged rows of chunk `c` -> Y (thread: rows tid >> 5 and 16 + (tid >> 5),
+  // float4 gl), and the ReLU mask words of each row from four ballots
+  auto flush = [&](int64_t c, const float *stage) {
+    const int64_t r0 = c * kXwRows;
+    const int64_t left = a.n_rows - r0;
+    const uint32_t rows_in = (uint32_t)(left >= kXwRows ? kXwRows : left);
+    const auto ry = buf_rsrc(a.Y + r0 * a.ldy, rows_in * (uint32_t)a.ldy * 4u);
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int lr = 16 * m + (tid >> 5);
+      const float4 v = *reinterpret_cast<const float4 *>(stage + lr * kXwF + 4 * gl);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ry,
+                                             4 * (int)(lr * a.ldy + 4 * gl), 0, 0);
+      if (a.relu_mask != nullptr) {
+        // word j of the row: bit gl <=> feature 4 gl + j > 0 (the SpMM's layout)
+        const uint32_t m0 = (uint32_t)(__ballot(v.x > 0.0f) >> (32 * grp));
+        const uint32_t m1 = (uint32_t)(__ballot(v.y > 0.0f) >> (32 * grp));
+        const uint32_t m2 = (uint32_t)(__ballot(v.z > 0.0f) >> (32 * grp));
+        const uint32_t m3 = (uint32_t)(__ballot(v.w > 0.0f) >> (32 * grp));
+        if (gl == 0 && (uint32_t)lr < rows_in)
+          *reinterpret_cast<uint4 *>(a.relu_mask + (r0 + lr) * 4) = make_uint4(m0, m1, m2, m3);
+      }
+    }
+  };
+
+  int it = 0;
+  for (int64_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x, ++it) {
+    char *buf = lds + (it & 1) * kXfBuf;
+    float *stage = reinterpret_cast<float *>(lds + kXfStageOff + (it & 1) * kXfStage);
+
+    // ---- Phase A: aggregate the chunk's rows into the bf16 images --------
+#pragma unroll 1
+    for (int p = 0; p < 2; ++p) {
+      const int lr = 16 * p + 2 * wave + grp;
+      const int64_t row = chunk * kXwRows + lr;
+      int64_t deg;
+      float acc[4];
+      gather_row<U>(rx, ldx_b, a.rowptr, a.col, a.w, row, row < a.n_rows, gl, grp, acc, deg);
+      if (a.mean) {
+        const float c = (float)(deg > 1 ? deg : 1);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = __fdiv_rn(acc[j], c);
+      }
+      store_row_terms(buf, lr, gl, acc);
+    }
+    __syncthreads();
+    // the previous chunk's output rows (staged before this barrier) go out
+    if (it > 0)
+      flush(chunk - gridDim.x, reinterpret_cast<const float *>(lds + kXfStageOff +
+                                                                ((it + 1) & 1) * kXfStage));
+
+    // ---- Phase B: Y = Z W (+ b), ReLU -> staging tile ----------------------
+    f32x4_t acc2[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc2[t][r] = 0.0f;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) mfma_rows(buf, wb[ks], ks, l16, g4, acc2);
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = acc2[t][r];
+        if (has_b) v = __fadd_rn(v, bcol);
+        if (a.relu) v = (v < 0.0f) ? 0.0f : v;
+        stage[(16 * t + 4 * g4 + r) * kXwF + ncol] = v;
+      }
+  }
+  if (it > 0) {
+    __syncthreads();
+    flush(blockIdx.x + (int64_t)(it - 1) * gridDim.x,
+          reinterpret_cast<const float *>(lds + kXfStageOff + ((it + 1) & 1) * kXfStage));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Backward.  LDS: X images, dH images (single-buffered: two barriers per
+// chunk), the chunk's mask / divisor words, the dX staging tile.  dX: wave w
+// owns columns 16 w .. +15; its W^T fragments are re-read from L2 (W is
+// 64 KB) and split per chunk -- held for the whole kernel they would take 48
+// VGPRs beside the gather's and dW's.
+constexpr int kXbHOff = 3 * kXwImg;
+constexpr int kXbMaskOff = 6 * kXwImg;                 // [32][4] mask words
+constexpr int kXbDivOff = kXbMaskOff + kXwRows * 16;   // [32] row divisors
+constexpr int kXbStageOff = kXbDivOff + kXwRows * 4;
+constexpr int kXbLds = kXbStageOff + kXwStage;
+
+struct XbArgs {
+  int64_t n_rows;  // source nodes: rows of the bwd view, of X and of dX
+  const int64_t *rowptr;
+  const int32_t *col;
+  const float *w;
+  const float *row_scale;  // nullable ('rw')
+  const float *dY;         // gathered rows [n_cols][128]
+  int64_t lddy;
+  int64_t n_cols;
+  const float *X;  // layer input [n_rows][128]
+  int64_t ldx;
+  const float *W;  // [128][128], H = X W
+  int64_t ldw;
+  float *dX;  // nullable
+  int64_t lddx;
+  const uint32_t *relu_mask;  // lower layer's output > 0 (mgcn_spmm_fwd layout)
+  const float *row_div;
+  float *dw_partial;      // [grid][128][128]
+  float *colsum_partial;  // [grid][128]
+};
+
+template <int U, bool DX, int EPI>
+__global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(const XbArgs a) {
+  __shared__ __attribute__((aligned(16))) char lds[kXbLds];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int gl = lane & 31, grp = lane >> 5;
+  const int h = lane >> 5, lc = lane & 31;
+  const int l16 = lane & 15, g4 = lane >> 4;
+  const int64_t n_chunks = (a.n_rows + kXwRows - 1) / kXwRows;
+  const auto rdy = buf_rsrc(a.dY, (uint32_t)(a.n_cols * a.lddy * 4));
+  const uint32_t ldy_b = (uint32_t)a.lddy * 4u;
+  float *stage = reinterpret_cast<float *>(lds + kXbStageOff);
+  const float *wp = a.W + (int64_t)(16 * wave + l16) * a.ldw + 8 * g4;  // B[k][n] = W[n][k]
+
+  // dW fragment offsets (gemm_bwd mapping): lane = 16 g + 4 q + p reads
+  // row 8 h + q (+ 4) of chunk (col0 >> 3) + 2 (g & 1) + (p >> 1), half p & 1
+  const int q = (lane >> 2) & 3, p4 = lane & 3;
+  auto frag_off = [&](int col0, int second) {
+    return img_off(8 * h + q + 4 * second, (col0 >> 3) + 2 * (g4 & 1) + (p4 >> 1)) + 8 * (p4 & 1);
+  };
+  const int ti = wave >> 1, tj0 = 2 * (wave & 1);
+  int offa[2], offb[2][2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    offa[r] = frag_off(32 * ti, r);
+    offb[0][r] = kXbHOff + frag_off(32 * tj0, r);
+    offb[1][r] = kXbHOff + frag_off(32 * (tj0 + 1), r);
+  }
+  auto read8 = [&](const char *base, const int (&o)[2]) {
+    const v4i16 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16_t *)(base + o[0]));
+    const v4i16 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16_t *)(base + o[1]));
+    const short y[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+    return __builtin_bit_cast(bf16x8, y);
+  };
+
+  f32x16 accw[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) accw[s][r] = 0.0f;
+  float csum = 0.0f;
+  const int ncol = 16 * wave + l16;  // dX column of this lane
+  const int mword = ncol & 3, mbit = 8 * (ncol >> 5) + ((ncol & 31) >> 2);
+  const int xoff = 4 * (int)((tid >> 5) * a.ldx + 4 * (tid & 31));
+
+  // staged dX rows of chunk `c` -> dX (16 B per lane, whole rows)
+  auto flush = [&](int64_t c) {
+    const int64_t r0 = c * kXwRows;
+    const int64_t left = a.n_rows - r0;
+    const uint32_t rows_in = (uint32_t)(left >= kXwRows ? kXwRows : left);
+    const auto rx = buf_rsrc(a.dX + r0 * a.lddx, rows_in * (uint32_t)a.lddx * 4u);
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int lr = 16 * m + (tid >> 5);
+      const u32x4 v = *reinterpret_cast<const u32x4 *>(stage + lr * kXwStageLd + 4 * lc);
+      __builtin_amdgcn_raw_buffer_store_b128(v, rx, 4 * (int)(lr * a.lddx + 4 * lc), 0, 0);
+    }
+  };
+
+  int it = 0;
+  for (int64_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x, ++it) {
+    const int64_t r0 = chunk * kXwRows;
+    const int64_t left = a.n_rows - r0;
+    const uint32_t rows_in = (uint32_t)(left >= kXwRows ? kXwRows : left);
+    if constexpr (DX) {
+      if (it > 0) flush(chunk - gridDim.x);
+    }
+    // the chunk's X rows (q and 16 + q, float4 tid & 31), issued first so
+    // they land under the gathers
+    const auto rxx = buf_rsrc(a.X + r0 * a.ldx, rows_in * (uint32_t)a.ldx * 4u);
+    const u32x4 xa = __builtin_amdgcn_raw_buffer_load_b128(rxx, xoff, 0, 0);
+    const u32x4 xb = __builtin_amdgcn_raw_buffer_load_b128(rxx, xoff + 64 * (int)a.ldx, 0, 0);
+
+    // ---- Phase A: dH rows of the chunk -> bf16 images; X rows -> images --
+#pragma unroll 1
+    for (int p = 0; p < 2; ++p) {
+      const int lr = 16 * p + 2 * wave + grp;
+      const int64_t row = r0 + lr;
+      const bool row_ok = row < a.n_rows;
+      int64_t deg;
+      float acc[4];
+      gather_row<U>(rdy, ldy_b, a.rowptr, a.col, a.w, row, row_ok, gl, grp, acc, deg);
+      if (a.row_scale != nullptr && row_ok) {
+        const float sc = a.row_scale[row];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = __fmul_rn(acc[j], sc);
+      }
+      store_row_terms(lds + kXbHOff, lr, gl, acc);
+    }
+    // mask / divisor words of the chunk's rows (wave 0; latency under the X split)
+    u32x4 mk = {0u, 0u, 0u, 0u};
+    uint32_t rd = 0u;
+    if constexpr (DX && EPI != EPI_STORE) {
+      if (wave == 0) {
+        const auto rm = buf_rsrc(a.relu_mask + r0 * 4, rows_in * 16u);
+        mk = __builtin_amdgcn_raw_buffer_load_b128(rm, 16 * lc, 0, 0);
+        if constexpr (EPI == EPI_RELU_DIV) {
+          const auto rdv = buf_rsrc(a.row_div + r0, rows_in * 4u);
+          rd = __builtin_amdgcn_raw_buffer_load_b32(rdv, 4 * lc, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const float4 v = __builtin_bit_cast(float4, m == 0 ? xa : xb);
+      const float f[4] = {v.x, v.y, v.z, v.w};
+      store_row_terms(lds, 16 * m + (tid >> 5), lc, f);
+    }
+    if constexpr (DX && EPI != EPI_STORE) {
+      if (wave == 0) {
+        if (h == 0) *reinterpret_cast<u32x4 *>(lds + kXbMaskOff + 16 * lc) = mk;
+        if constexpr (EPI == EPI_RELU_DIV)
+          if (h == 1) *reinterpret_cast<uint32_t *>(lds + kXbDivOff + 4 * lc) = rd;
+      }
+    }
+    __syncthreads();
+
+    // ---- Phase B1: dW += X^T dH (two 16-row k-steps) ---------------------
+    // this wave's W^T fragments for k-steps 0, 1 are in flight under the dW
+    // MFMAs (k-steps 2, 3 are loaded while 0, 1 run)
+    float4 wr[4][2];
+    if constexpr (DX) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) wr[ks][j] = *reinterpret_cast<const float4 *>(wp + 32 * ks + 4 * j);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const char *kb = lds + ks * 16 * 256;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 fa[3], fb[3];
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+          fa[t] = read8(kb + t * kXwImg, offa);
+          fb[t] = read8(kb + t * kXwImg, offb[s]);
+        }
+        accw[s] = mfma_x6(fa[0], fa[1], fa[2], fb[0], fb[1], fb[2], accw[s]);
+      }
+    }
+    // ---- Phase B2: dX = relu'(lower) (dH W^T) [/ row_div] -> staging ------
+    if constexpr (DX) {
+      f32x4_t acc2[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc2[t][r] = 0.0f;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        if (ks < 2) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            wr[ks + 2][j] = *reinterpret_cast<const float4 *>(wp + 32 * (ks + 2) + 4 * j);
+        }
+        bf16x8 wb[3];
+        const float v[8] = {wr[ks][0].x, wr[ks][0].y, wr[ks][0].z, wr[ks][0].w,
+                            wr[ks][1].x, wr[ks][1].y, wr[ks][1].z, wr[ks][1].w};
+        split3_bf16(v, wb[0], wb[1], wb[2]);
+        mfma_rows(lds + kXbHOff, wb, ks, l16, g4, acc2);
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int lr = 16 * t + 4 * g4 + r;
+          float v = acc2[t][r];
+          if constexpr (EPI != EPI_STORE) {
+            const uint32_t wd = *reinterpret_cast<const uint32_t *>(lds + kXbMaskOff + 16 * lr + 4 * mword);
+            v = ((wd >> mbit) & 1u) ? v : 0.0f;
+            csum = __fadd_rn(csum, v);
+            if constexpr (EPI == EPI_RELU_DIV)
+              v = __fdiv_rn(v, *reinterpret_cast<const float *>(lds + kXbDivOff + 4 * lr));
+          }
+          stage[lr * kXwStageLd + ncol] = v;
+        }
+    }
+    __syncthreads();
+  }
+  if constexpr (DX) {
+    if (it > 0) flush(blockIdx.x + (int64_t)(it - 1) * gridDim.x);  // staged before the last barrier
+  }
+
+  // dW partial slab of this workgroup; C map: col = lc, row = (r & 3) + 8 (r >> 2) + 4 h
+  float *slab = a.dw_partial + (int64_t)blockIdx.x * kXwF * kXwF;
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = 32 * ti + (r & 3) + 8 * (r >> 2) + 4 * h;
+      slab[row * kXwF + 32 * (tj0 + s) + lc] = accw[s][r];
+    }
+  if constexpr (DX && EPI != EPI_STORE) {
+    // fold the four row groups of each column in fixed order
+    const float c1 = __fadd_rn(csum, __shfl_xor(csum, 16, 64));
+    const float c2 = __fadd_rn(c1, __shfl_xor(c1, 32, 64));
+    if (lane < 16) a.colsum_partial[(int64_t)blockIdx.x * kXwF + ncol] = c2;
+  }
+}
+
+int g_xw_unroll = 4;
+
+int xw_grid() {
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 256;
+  return kXwPerCU * cus;
+}
+
+template <int U>
+int launch_xw(const XwArgs &a, hipStream_t s) {
+  const int64_t n_chunks = (a.n_rows + kXwRows - 1) / kXwRows;
+  int64_t grid = xw_grid();
+  if (grid > n_chunks) grid = n_chunks;
+  hipLaunchKernelGGL((spmm_xw_fwd_kernel<U>), dim3((unsigned)grid), dim3(kXwThreads), 0, s, a);
+  return check_launch("spmm_xw_fwd_kernel");
+}
+
+template <int U, bool DX, int EPI>
+int launch_xb(const XbArgs &a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL((spmm_xw_bwd_kernel<U, DX, EPI>), dim3((unsigned)grid), dim3(kXwThreads), 0, s,
+                     a);
+  return check_launch("spmm_xw_bwd_kernel");
+}
+
+template <int U>
+int launch_xb_u(const XbArgs &a, int epi, int grid, hipStream_t s) {
+  if (a.dX == nullptr) return launch_xb<U, false, EPI_STORE>(a, grid, s);
+  if (epi == EPI_RELU_DIV) return launch_xb<U, true, EPI_RELU_DIV>(a, grid, s);
+  if (epi == EPI_RELU) return launch_xb<U, true, EPI_RELU>(a, grid, s);
+  return launch_xb<U, true, EPI_STORE>(a, grid, s);
+}
+
+}  // namespace
+
+int xw_set_unroll(int value) {
+  if (value != 4 && value != 8) {
+    set_error("spmm_xw_unroll must be 4 or 8");
+    return MGCN_EINVAL;
+  }
+  g_xw_unroll = value;
+  return MGCN_OK;
+}
+
+}  // namespace mgcn
+
+using namespace mgcn;
+
+extern "C" int mgcn_spmm_xw_supported(int32_t F_in, int32_t F_out, int reduce) {
+  return F_in == kXwF && F_out == kXwF && gemm_precision_is_x6() &&
+         (reduce == MGCN_REDUCE_SUM || reduce == MGCN_REDUCE_MEAN);
+}
+
+extern "C" int mgcn_spmm_xw_fwd(int64_t n_rows, int64_t n_cols, int32_t F_in, int32_t F_out,
+                                const int64_t *rowptr, const int32_t *col, const float *w,
+                                const float *X, int64_t ldx, const float *W, int64_t ldw,
+                                const float *bias, float *Y, int64_t ldy, int reduce, int relu,
+                                uint32_t *relu_mask, void *stream) {
+  clear_error();
+  MGCN_REQUIRE(n_rows >= 0, "mgcn_spmm_xw_fwd: negative size");
+  MGCN_REQUIRE(mgcn_spmm_xw_supported(F_in, F_out, reduce),
+               "mgcn_spmm_xw_fwd: unsupported F_in=%d F_out=%d reduce=%d (needs 128 x 128, sum/mean, "
+               "bf16x6)",
+               F_in, F_out, reduce);
+  MGCN_REQUIRE(relu_mask == nullptr || relu, "mgcn_spmm_xw_fwd: relu_mask needs relu");
+  if (n_rows == 0) return MGCN_OK;
+  MGCN_REQUIRE(rowptr && X && W && Y, "mgcn_spmm_xw_fwd: null array");
+  MGCN_REQUIRE(ldx >= F_in && ldx % 4 == 0 && reinterpret_cast<uintptr_t>(X) % 16 == 0,
+               "mgcn_spmm_xw_fwd: X must have 16-byte aligned rows");
+  MGCN_REQUIRE(ldw >= F_out && ldy >= F_out, "mgcn_spmm_xw_fwd: leading dimension too small");
+  MGCN_REQUIRE(n_cols > 0 && (uint64_t)n_cols * (uint64_t)ldx * 4u <= 0xfffffff0ull,
+               "mgcn_spmm_xw_fwd: X must hold 1 .. 4 GiB - 1 bytes (32-bit gather offsets)");
+  MGCN_REQUIRE((uint64_t)kXwRows * (uint64_t)ldy * 4u < (1ull << 31),
+               "mgcn_spmm_xw_fwd: ldy too large");
+  MGCN_REQUIRE(bias == nullptr || reinterpret_cast<uintptr_t>(bias) % 4 == 0,
+               "mgcn_spmm_xw_fwd: bias not 4-byte aligned");
+  MGCN_REQUIRE(relu_mask == nullptr || reinterpret_cast<uintptr_t>(relu_mask) % 16 == 0,
+               "mgcn_spmm_xw_fwd: relu_mask not 16-byte aligned");
+  XwArgs a{};
+  a.n_rows = n_rows;
+  a.rowptr = rowptr;
+  a.col = col;
+  a.w = w;
+  a.X = X;
+  a.ldx = ldx;
+  a.n_cols = n_cols;
+  a.W = W;
+  a.ldw = ldw;
+  a.bias = bias;
+  a.Y = Y;
+  a.ldy = ldy;
+  a.relu_mask = relu_mask;
+  a.mean = reduce == MGCN_REDUCE_MEAN;
+  a.relu = relu != 0;
+  hipStream_t s = as_stream(stream);
+  return g_xw_unroll == 4 ? launch_xw<4>(a, s) : launch_xw<8>(a, s);
+}
+
+extern "C" size_t mgcn_spmm_xw_bwd_workspace_bytes(int64_t n_rows) {
+  (void)n_rows;
+  const size_t g = (size_t)xw_grid();
+  return align_up(g * kXwF * kXwF * 4, 256) + align_up(g * kXwF * 4, 256);
+}
+
+extern "C" int mgcn_spmm_xw_bwd(int64_t n_rows, int64_t n_cols, int32_t F_in, int32_t F_out,
+                                const int64_t *rowptr_t, const int32_t *col_t, const float *w_t,
+                                const float *row_scale, const float *dY, int64_t lddy,
+                                const float *X, int64_t ldx, const float *W, int64_t ldw,
+                                float *dW, int64_t lddw, int accumulate, float *dX, int64_t lddx,
+                                const uint32_t *relu_mask, const float *row_div, float *colsum,
+                                void *workspace, size_t workspace_bytes, void *stream) {
+  clear_error();
+  MGCN_REQUIRE(n_rows >= 0, "mgcn_spmm_xw_bwd: negative size");
+  MGCN_REQUIRE(mgcn_spmm_xw_supported(F_in, F_out, MGCN_REDUCE_SUM),
+               "mgcn_spmm_xw_bwd: unsupported F_in=%d F_out=%d (needs 128 x 128, bf16x6)", F_in,
+               F_out);
+  MGCN_REQUIRE(dW != nullptr && lddw >= F_out, "mgcn_spmm_xw_bwd: bad dW");
+  const int epi = relu_mask == nullptr ? EPI_STORE : row_div != nullptr ? EPI_RELU_DIV : EPI_RELU;
+  MGCN_REQUIRE(epi == EPI_STORE || (dX != nullptr && colsum != nullptr),
+               "mgcn_spmm_xw_bwd: relu_mask needs dX and colsum");
+  MGCN_REQUIRE(row_div == nullptr || relu_mask != nullptr,
+               "mgcn_spmm_xw_bwd: row_div needs relu_mask");
+  hipStream_t s = as_stream(stream);
+  if (n_rows == 0) {
+    if (!accumulate)
+      for (int32_t r = 0; r < F_in; ++r)
+        MGCN_HIP_TRY(hipMemsetAsync(dW + r * lddw, 0, sizeof(float) * F_out, s));
+    if (colsum) MGCN_HIP_TRY(hipMemsetAsync(colsum, 0, sizeof(float) * F_in, s));
+    return MGCN_OK;
+  }
+  MGCN_REQUIRE(rowptr_t && dY && X, "mgcn_spmm_xw_bwd: null array");
+  MGCN_REQUIRE(lddy >= F_out && lddy % 4 == 0 && reinterpret_cast<uintptr_t>(dY) % 16 == 0,
+               "mgcn_spmm_xw_bwd: dY must have 16-byte aligned rows");
+  MGCN_REQUIRE(ldx >= F_in && ldx % 4 == 0 && reinterpret_cast<uintptr_t>(X) % 16 == 0,
+               "mgcn_spmm_xw_bwd: X must have 16-byte aligned rows");
+  MGCN_REQUIRE(n_cols > 0 && (uint64_t)n_cols * (uint64_t)lddy * 4u <= 0xfffffff0ull,
+               "mgcn_spmm_xw_bwd: dY must hold 1 .. 4 GiB - 1 bytes (32-bit gather offsets)");
+  MGCN_REQUIRE((uint64_t)kXwRows * (uint64_t)(ldx > lddx ? ldx : lddx) * 4u < (1ull << 31),
+               "mgcn_spmm_xw_bwd: leading dimension too large");
+  MGCN_REQUIRE(dX == nullptr || (W != nullptr && ldw >= F_out && lddx >= F_in),
+               "mgcn_spmm_xw_bwd: bad W/dX");
+  MGCN_REQUIRE(relu_mask == nullptr || reinterpret_cast<uintptr_t>(relu_mask) % 16 == 0,
+               "mgcn_spmm_xw_bwd: relu_mask not 16-byte aligned");
+  const size_t need = mgcn_spmm_xw_bwd_workspace_bytes(n_rows);
+  if (workspace == nullptr || workspace_bytes < need) {
+    set_error("mgcn_spmm_xw_bwd: workspace %zu < %zu", workspace_bytes, need);
+    return MGCN_EWORKSPACE;
+  }
+  const int64_t n_chunks = (n_rows + kXwRows - 1) / kXwRows;
+  int grid = xw_grid();
+  if (grid > n_chunks) grid = (int)n_chunks;
+  XbArgs a{};
+  a.n_rows = n_rows;
+  a.rowptr = rowptr_t;
+  a.col = col_t;
+  a.w = w_t;
+  a.row_scale = row_scale;
+  a.dY = dY;
+  a.lddy = lddy;
+  a.n_cols = n_cols;
+  a.X = X;
+  a.ldx = ldx;
+  a.W = W;
+  a.ldw = ldw;
+  a.dX = dX;
+  a.lddx = lddx;
+  a.relu_mask = relu_mask;
+  a.row_div = row_div;
+  a.dw_partial = static_cast<float *>(workspace);
+  a.colsum_partial = reinterpret_cast<float *>(static_cast<char *>(workspace) +
+                                               align_up((size_t)xw_grid() * kXwF * kXwF * 4, 256));
+  int rc = g_xw_unroll == 4 ? launch_xb_u<4>(a, epi, grid, s) : launch_xb_u<8>(a, epi, grid, s);
+  if (rc) return rc;
+  rc = launch_split_reduce(a.dw_partial, grid, (int64_t)kXwF * kXwF, kXwF, dW, lddw, accumulate, s);
+  if (rc || epi == EPI_STORE) return rc;
+  return launch_colsum_fold(a.colsum_partial, grid, kXwF, colsum, s);
+}

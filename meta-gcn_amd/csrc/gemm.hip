@@ -19,11 +19,12 @@
 // 8 TB/s: MFMA-bound (the GEMMs are compute-bound at F=128).
 
 #include "mgcn_internal.h"
+#include "x6.h"
 
 namespace mgcn {
 namespace {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
+using namespace x6;
 
 constexpr int kTile = 128;   // C tile per workgroup (M and N)
 constexpr int kU = 4;        // k-steps (of 2 rows) in flight per iteration (8: -25%, occupancy 3 -> 2)
@@ -139,61 +140,6 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 constexpr int PREC_F32 = 0, PREC_BF16X6 = 1;
 int g_gemm_precision = PREC_BF16X6;
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-// bf16 pair (one VGPR) -> the two floats it holds (exact)
-__device__ __forceinline__ f32x2 widen_bf16x2(uint32_t p) {
-  return f32x2{__uint_as_float(p << 16), __uint_as_float(p & 0xffff0000u)};
-}
-
-// one pair of floats -> its hi / mid / lo bf16 pairs (v_cvt_pk_bf16_f32, RNE)
-// Range edge: |x| >= ~3.396e38 rounds to bf16 inf, and x - inf = -inf, so
-// the terms would sum to NaN where fp32 gives a finite or infinite product.
-// hi and mid therefore come from x and r clamped to +-kSplitMax (the largest
-// float whose RNE bf16 is finite, v_med3_f32): for finite x the split stays
-// exact (hi = 0x7f7f.. then r = x - hi exactly), for x = +-inf it is
-// (+-M, +-M, +-inf) -- a product with w is +-inf (NaN for w = 0), as in fp32.
-constexpr float kSplitMax = 0x1.fefffep+127f;  // 0x7f7f7fff = 3.3961514e38
-__device__ __forceinline__ float split_clamp(float v) {
-  return __builtin_amdgcn_fmed3f(v, -kSplitMax, kSplitMax);
-}
-__device__ __forceinline__ void split3_pair(f32x2 x, uint32_t &hi, uint32_t &mid, uint32_t &lo) {
-  const f32x2 xc = {split_clamp(x.x), split_clamp(x.y)};
-  hi = __builtin_bit_cast(uint32_t, __builtin_convertvector(xc, bf16x2));
-  const f32x2 r = x - widen_bf16x2(hi);  // exact (Sterbenz)
-  const f32x2 rc = {split_clamp(r.x), split_clamp(r.y)};
-  mid = __builtin_bit_cast(uint32_t, __builtin_convertvector(rc, bf16x2));
-  lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(r - widen_bf16x2(mid), bf16x2));
-}
-
-__device__ __forceinline__ void split3_bf16(const float (&x)[8], bf16x8 &hi, bf16x8 &mid,
-                                            bf16x8 &lo) {
-  uint32_t h[4], m[4], l[4];
-#pragma unroll
-  for (int p = 0; p < 4; ++p) split3_pair(f32x2{x[2 * p], x[2 * p + 1]}, h[p], m[p], l[p]);
-  hi = __builtin_bit_cast(bf16x8, h);
-  mid = __builtin_bit_cast(bf16x8, m);
-  lo = __builtin_bit_cast(bf16x8, l);
-}
-
-// six-product bf16 MFMA chain on one accumulator, smallest terms first
-__device__ __forceinline__ f32x16 mfma_x6(const bf16x8 &ah, const bf16x8 &am, const bf16x8 &al,
-                                          const bf16x8 &bh, const bf16x8 &bm, const bf16x8 &bl,
-                                          f32x16 c) {
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, c, 0, 0, 0);
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, c, 0, 0, 0);
-}
-
-
-typedef short v4i16 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) v4i16 lds_v4i16_t;
 
 // dW for M, N multiples of 128 in bf16x6.  Per chunk of 16 k-rows, each
 // thread loads 2 float4 of each operand (coalesced 512-B rows), splits them
@@ -646,6 +592,7 @@ extern "C" int mgcn_gemm_tn(int64_t K, int32_t M, int32_t N, const float *A, int
 
 namespace mgcn {
 namespace {
+using namespace x6;
 
 constexpr int kNNWaves = 8;  // waves per workgroup
 constexpr int kNNThreads = 64 * kNNWaves;
@@ -1048,6 +995,23 @@ __global__ __launch_bounds__(256) void colsum_fold_kernel(const float *__restric
 
 }  // namespace
 
+// launchers of the split-K / column-sum folds for other translation units
+// (fused.hip's backward writes the same partial slabs)
+int launch_split_reduce(const float *partial, int splits, int64_t MN, int N, float *C,
+                        int64_t ldc, int accumulate, hipStream_t s) {
+  hipLaunchKernelGGL(gemm_reduce_kernel, dim3((unsigned)((MN + 63) / 64)), dim3(256), 0, s,
+                     partial, splits, MN, N, C, ldc, accumulate);
+  return check_launch("gemm_reduce_kernel");
+}
+
+int launch_colsum_fold(const float *partial, int64_t nparts, int N, float *out, hipStream_t s) {
+  hipLaunchKernelGGL(colsum_fold_kernel, dim3((N + 63) / 64), dim3(256), 0, s, partial, nparts, N,
+                     out);
+  return check_launch("colsum_fold_kernel");
+}
+
+int gemm_precision_is_x6() { return g_gemm_precision == PREC_BF16X6; }
+
 int gemm_set_precision(int value) {
   if (value != PREC_F32 && value != PREC_BF16X6) return MGCN_EINVAL;
   g_gemm_precision = value;
@@ -1138,8 +1102,8 @@ extern "C" int mgcn_gemm_nn(int64_t M, int32_t K, int32_t N, const float *A, int
 
 namespace mgcn {
 namespace {
+using namespace x6;
 
-typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
 constexpr int kBwF = 128;
 constexpr int kBwRows = 32;
@@ -1151,41 +1115,11 @@ constexpr int kBwMaskOff = 6 * kBwImg;            // [32 rows][4] u32 ReLU mask 
 constexpr int kBwDivOff = kBwMaskOff + kBwRows * 16;  // [32] row divisors
 constexpr int kBwBuf = kBwDivOff + kBwRows * 4;
 
-__device__ __forceinline__ int bw_swz(int row) {
-  return ((row & 3) << 2) | ((0x78 >> (2 * ((row >> 2) & 3))) & 3);
-}
-__device__ __forceinline__ int bw_off(int row, int ch) { return 256 * row + 16 * (ch ^ bw_swz(row)); }
-
-__device__ __forceinline__ f32x4_t mfma16_x6(const bf16x8 &ah, const bf16x8 &am, const bf16x8 &al,
-                                            const bf16x8 &bh, const bf16x8 &bm, const bf16x8 &bl,
-                                            f32x4_t c) {
-  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bm, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bh, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bm, c, 0, 0, 0);
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, c, 0, 0, 0);
-}
-
 struct BwBank {
   u32x4 v[4];  // X rows q, 16 + q and dH rows q, 16 + q (q = tid >> 5), float4 tid & 31
   u32x4 mk;    // mask words of row tid & 31
   uint32_t rd; // row divisor of row tid & 31
 };
-
-// Buffer resource over [base, base + bytes): loads past it return 0 and
-// stores past it are dropped, so the chunk tail and the prefetch past the
-// last chunk need no branches (a branch around a load makes hipcc wait
-// vmcnt(0) for every load in flight, i.e. for the prefetch).  Inputs are
-// wave-uniform; readfirstlane makes that provable.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t bw_rsrc(const void *base, uint32_t bytes) {
-  const uint64_t a = reinterpret_cast<uint64_t>(base);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-  void *p = reinterpret_cast<void *>(((uint64_t)hi << 32) | lo);
-  return __builtin_amdgcn_make_buffer_rsrc(p, 0, (int)__builtin_amdgcn_readfirstlane(bytes),
-                                           0x00020000);
-}
 
 template <int EPI, bool DX>
 __global__ __launch_bounds__(kBwThreads, 1) void gemm_bwd_kernel(
@@ -1223,8 +1157,8 @@ __global__ __launch_bounds__(kBwThreads, 1) void gemm_bwd_kernel(
   auto load = [&](int64_t chunk, BwBank &b) {
     const int64_t r0 = chunk * kBwRows;
     const uint32_t rv = rows_in(chunk);
-    const auto rx = bw_rsrc(X + r0 * ldx, rv * (uint32_t)ldx * 4u);
-    const auto rh = bw_rsrc(dH + r0 * lddh, rv * (uint32_t)lddh * 4u);
+    const auto rx = buf_rsrc(X + r0 * ldx, rv * (uint32_t)ldx * 4u);
+    const auto rh = buf_rsrc(dH + r0 * lddh, rv * (uint32_t)lddh * 4u);
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
 #ifdef BW_NO_LOAD
@@ -1236,10 +1170,10 @@ __global__ __launch_bounds__(kBwThreads, 1) void gemm_bwd_kernel(
       b.v[2 + m] = __builtin_amdgcn_raw_buffer_load_b128(rh, ld_off_h + m * 64 * (int)lddh, 0, 0);
     }
     if constexpr (DX && EPI != EPI_STORE) {
-      const auto rm = bw_rsrc(relu_mask + r0 * 4, rv * 16u);
+      const auto rm = buf_rsrc(relu_mask + r0 * 4, rv * 16u);
       b.mk = __builtin_amdgcn_raw_buffer_load_b128(rm, 16 * (tid & 31), 0, 0);
       if constexpr (EPI == EPI_RELU_DIV) {
-        const auto rd = bw_rsrc(row_div + r0, rv * 4u);
+        const auto rd = buf_rsrc(row_div + r0, rv * 4u);
         b.rd = __builtin_amdgcn_raw_buffer_load_b32(rd, 4 * (tid & 31), 0, 0);
       }
     }
@@ -1254,7 +1188,7 @@ __global__ __launch_bounds__(kBwThreads, 1) void gemm_bwd_kernel(
   auto stage_part = [&](const BwBank &b, char *buf, int m) {
     const int c4 = tid & 31;
     const int row = 16 * (m & 1) + (tid >> 5);
-    const int off = bw_off(row, c4 >> 1) + 8 * (c4 & 1);
+    const int off = img_off(row, c4 >> 1) + 8 * (c4 & 1);
     const float4 v = __builtin_bit_cast(float4, b.v[m]);
     uint32_t hi[2], mid[2], lo[2];
 #ifdef BW_NO_SPLIT
@@ -1285,7 +1219,7 @@ __global__ __launch_bounds__(kBwThreads, 1) void gemm_bwd_kernel(
   // row 8 h + q (+ 4) of chunk (col0 >> 3) + 2 (g & 1) + (p >> 1), half p & 1
   const int q = (lane >> 2) & 3, p = lane & 3;
   auto frag_off = [&](int col0, int second) {
-    return bw_off(8 * h + q + 4 * second, (col0 >> 3) + 2 * (g4 & 1) + (p >> 1)) + 8 * (p & 1);
+    return img_off(8 * h + q + 4 * second, (col0 >> 3) + 2 * (g4 & 1) + (p >> 1)) + 8 * (p & 1);
   };
   const int ti = wave >> 1, tj0 = 2 * (wave & 1);
   int offa[2], offb[2][2];
@@ -1346,7 +1280,7 @@ __global__ __launch_bounds__(kBwThreads, 1) void gemm_bwd_kernel(
       for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-          const int off = bw_off(16 * t + l16, 4 * ks + g4);
+          const int off = img_off(16 * t + l16, 4 * ks + g4);
           const bf16x8 ah = *reinterpret_cast<const bf16x8 *>(hb + off);
           const bf16x8 am = *reinterpret_cast<const bf16x8 *>(hb + kBwImg + off);
           const bf16x8 al = *reinterpret_cast<const bf16x8 *>(hb + 2 * kBwImg + off);
@@ -1361,7 +1295,7 @@ __global__ __launch_bounds__(kBwThreads, 1) void gemm_bwd_kernel(
       // epilogue: lane holds rows 16 t + 4 g4 + r of column ncol; rows past M
       // are zero (their loads returned 0) and their stores fall off the buffer
       const int64_t r0 = chunk * kBwRows;
-      const auto rx = bw_rsrc(dX + r0 * lddx, rows_in(chunk) * (uint32_t)lddx * 4u);
+      const auto rx = buf_rsrc(dX + r0 * lddx, rows_in(chunk) * (uint32_t)lddx * 4u);
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll

@@ -59,5 +59,11 @@ inline unsigned grid_for(int64_t work_items, int block) {
 // mgcn_set_option("gemm_tn_variant") -> gemm.hip
 int gemm_set_tn_variant(int value);
 int gemm_set_precision(int value);
+int gemm_precision_is_x6();  // 1 under bf16x6 (the fused kernels need it)
+int xw_set_unroll(int value);  // fused.hip
+// deterministic folds of per-workgroup partials (gemm.hip)
+int launch_split_reduce(const float *partial, int splits, int64_t MN, int N, float *C,
+                        int64_t ldc, int accumulate, hipStream_t s);
+int launch_colsum_fold(const float *partial, int64_t nparts, int N, float *out, hipStream_t s);
 
 }  // namespace mgcn

@@ -1031,6 +1031,7 @@ extern "C" int mgcn_set_option(const char *name, int value) {
     MGCN_REQUIRE(value == 0 || value == 1, "gemm_precision must be 0 (f32) or 1 (bf16x6)");
     return gemm_set_precision(value);
   }
+  if (n == "spmm_xw_unroll") return xw_set_unroll(value);
   if (n == "heavy_side_stream") {
     MGCN_REQUIRE(value == 0 || value == 1, "heavy_side_stream must be 0 or 1");
     g_heavy_side = value;

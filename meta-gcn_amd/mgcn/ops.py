@@ -16,6 +16,8 @@ max routes through the saved argmax), so the adjoint is bit-identical too.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib as L
@@ -23,6 +25,16 @@ from .graph import CSRView, GraphPlan, NormPlan, plan_for
 
 
 _TIMER = None  # optional callable(name, start: bool), e.g. bench.py's HIP-event timer
+# fused aggregate-then-transform forward for 128 -> 128 sum / mean layers
+# (mgcn_spmm_xw_fwd); MGCN_FUSE_XW=0 selects the GEMM + SpMM launches
+_FUSE_XW = os.environ.get("MGCN_FUSE_XW", "1") != "0"
+
+
+def set_fused_layers(enabled: bool) -> None:
+    """Use (True, the default) or bypass the fused aggregate+transform layer
+    kernels (mgcn_spmm_xw_fwd / _bwd) where they apply."""
+    global _FUSE_XW
+    _FUSE_XW = bool(enabled)
 
 
 def set_kernel_timer(timer) -> None:
@@ -83,6 +95,103 @@ def spmm_fwd(view: CSRView, w: torch.Tensor | None, H: torch.Tensor, reduce: int
         _TIMER("spmm_fwd", False)
     L.check(rc, "mgcn_spmm_fwd")
     return Y, (mask if mask is not None else argmax)
+
+
+def spmm_xw_supported(view: CSRView, F_in: int, F_out: int, reduce: int) -> bool:
+    """True when :func:`spmm_xw_fwd` takes this layer: 128 -> 128, sum or mean,
+    and no heavy rows (skewed graphs keep the GEMM + heavy-row SpMM path)."""
+    return (view.n_heavy == 0 and
+            bool(L.load().mgcn_spmm_xw_supported(int(F_in), int(F_out), int(reduce))))
+
+
+def spmm_xw_fwd(view: CSRView, w: torch.Tensor | None, X: torch.Tensor, W: torch.Tensor,
+                reduce: int, bias: torch.Tensor | None = None, relu: bool = False,
+                relu_mask: torch.Tensor | None = None) -> torch.Tensor:
+    """Y = epi((reduce_k X[col_k] * w_k) @ W + bias) in one launch
+    (``mgcn_spmm_xw_fwd``): the layer's GEMM fused behind its aggregation, so
+    X @ W is never written.  Sum / mean only (they commute with W)."""
+    lib = L.load()
+    X = _contig_f32(X, "X")
+    if X.stride(0) % 4 or X.data_ptr() % 16:
+        X = X.contiguous()
+    W = W.detach()
+    dev = L.require_device(X, W, view.rowptr, w, bias, relu_mask)
+    if X.size(0) != view.n_cols:
+        raise ValueError(f"X has {X.size(0)} rows, graph has {view.n_cols} source nodes")
+    F_in, F_out = W.shape
+    if X.size(1) != F_in:
+        raise ValueError(f"spmm_xw_fwd: X is [{X.size(0)}, {X.size(1)}], W is [{F_in}, {F_out}]")
+    if W.dtype != torch.float32 or W.stride(1) != 1:
+        W = W.to(torch.float32).contiguous()
+    if bias is not None:
+        bias = bias.detach().to(torch.float32).contiguous()
+        if bias.numel() != F_out:
+            raise ValueError(f"bias has {bias.numel()} entries, expected {F_out}")
+    Y = torch.empty(view.n_rows, F_out, dtype=torch.float32, device=dev)
+    if _TIMER is not None:
+        _TIMER("spmm_xw_fwd", True)
+    with torch.cuda.device(dev):
+        rc = lib.mgcn_spmm_xw_fwd(view.n_rows, view.n_cols, F_in, F_out, L.ptr(view.rowptr),
+                                  L.ptr(view.col), L.ptr(w), L.ptr(X), X.stride(0), L.ptr(W),
+                                  W.stride(0), L.ptr(bias), L.ptr(Y), Y.stride(0), reduce,
+                                  int(bool(relu)), L.ptr(relu_mask), L.stream_of(dev))
+    if _TIMER is not None:
+        _TIMER("spmm_xw_fwd", False)
+    L.check(rc, "mgcn_spmm_xw_fwd")
+    return Y
+
+
+def spmm_xw_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tensor | None,
+                dY: torch.Tensor, X: torch.Tensor, W: torch.Tensor, want_dx: bool = True,
+                relu_mask: torch.Tensor | None = None, row_div: torch.Tensor | None = None):
+    """Both adjoints of a 128 -> 128 sum / mean layer from one pass
+    (``mgcn_spmm_xw_bwd``): dH = A^T dY [* row_scale] stays on chip, and
+    dW = X^T dH, dX = dH W^T (with the lower layer's ReLU mask / row divisor /
+    bias column sums, as :func:`gemm_bwd`) are formed from it.  Returns
+    (dW, dX or None, colsum or None)."""
+    lib = L.load()
+    dY = _contig_f32(dY, "dY")
+    X = _contig_f32(X, "X")
+    if dY.stride(0) % 4 or dY.data_ptr() % 16:
+        dY = dY.contiguous()
+    if X.stride(0) % 4 or X.data_ptr() % 16:
+        X = X.contiguous()
+    W = W.detach()
+    if W.dtype != torch.float32 or W.stride(1) != 1:
+        W = W.to(torch.float32).contiguous()
+    dev = L.require_device(dY, X, W, view_t.rowptr, w_t, row_scale, relu_mask, row_div)
+    M, F_in = X.shape
+    F_out = W.size(1)
+    if M != view_t.n_rows or dY.size(0) != view_t.n_cols or dY.size(1) != F_out:
+        raise ValueError(f"spmm_xw_bwd: X {tuple(X.shape)}, dY {tuple(dY.shape)} do not fit the "
+                         f"graph ({view_t.n_rows} sources, {view_t.n_cols} destinations)")
+    dW = torch.empty(F_in, F_out, dtype=torch.float32, device=dev)
+    dX = torch.empty(M, F_in, dtype=torch.float32, device=dev) if want_dx else None
+    colsum = None
+    if relu_mask is not None:
+        if not want_dx:
+            raise ValueError("spmm_xw_bwd: relu_mask needs want_dx")
+        if relu_mask.shape != (M, 4) or relu_mask.dtype != torch.int32:
+            raise ValueError(f"spmm_xw_bwd: relu_mask must be int32 [{M}, 4]")
+        relu_mask = relu_mask.contiguous()
+        colsum = torch.empty(F_in, dtype=torch.float32, device=dev)
+    ws_bytes = int(lib.mgcn_spmm_xw_bwd_workspace_bytes(M))
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    tname = "spmm_xw_bwd" if want_dx else "spmm_xw_bwd_dw"
+    if _TIMER is not None:
+        _TIMER(tname, True)
+    with torch.cuda.device(dev):
+        rc = lib.mgcn_spmm_xw_bwd(M, view_t.n_cols, F_in, F_out, L.ptr(view_t.rowptr),
+                                  L.ptr(view_t.col), L.ptr(w_t), L.ptr(row_scale), L.ptr(dY),
+                                  dY.stride(0), L.ptr(X), X.stride(0), L.ptr(W), W.stride(0),
+                                  L.ptr(dW), dW.stride(0), 0, L.ptr(dX),
+                                  dX.stride(0) if dX is not None else 0, L.ptr(relu_mask),
+                                  L.ptr(row_div), L.ptr(colsum), L.ptr(ws), ws_bytes,
+                                  L.stream_of(dev))
+    if _TIMER is not None:
+        _TIMER(tname, False)
+    L.check(rc, "mgcn_spmm_xw_bwd")
+    return dW, dX, colsum
 
 
 def spmm_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tensor | None,
@@ -456,14 +565,19 @@ class _GCNStack(torch.autograd.Function):
         inputs, outs, args, rmasks = [], [], [], []
         for i, (W, b, relu) in enumerate(zip(Ws, bs, relus)):
             inputs.append(h)
-            H = _mm(h, W)
             # the ReLU mask the next layer's dX GEMM reads (16 B per row)
             nxt = Ws[i + 1] if i + 1 < len(Ws) else None
             rm = None
             if relu and nxt is not None and gemm_nn_supported(nxt.size(1), nxt.size(0)):
-                rm = torch.empty(plan.fwd.n_rows, 4, dtype=torch.int32, device=H.device)
-            h, am = spmm_fwd(plan.fwd, norm.w_fwd, H, reduce, b, relu, mask_plan=plan,
-                             relu_mask=rm)
+                rm = torch.empty(plan.fwd.n_rows, 4, dtype=torch.int32, device=h.device)
+            if _FUSE_XW and spmm_xw_supported(plan.fwd, W.size(0), W.size(1), reduce):
+                # (A h) W in one launch: h @ W is never written (sum / mean)
+                h, am = spmm_xw_fwd(plan.fwd, norm.w_fwd, h, W, reduce, b, relu,
+                                    relu_mask=rm), None
+            else:
+                H = _mm(h, W)
+                h, am = spmm_fwd(plan.fwd, norm.w_fwd, H, reduce, b, relu, mask_plan=plan,
+                                 relu_mask=rm)
             outs.append(h)
             args.append(am)  # max: winner bits per edge (adjoint slot order)
             rmasks.append(rm)
@@ -496,10 +610,24 @@ class _GCNStack(torch.autograd.Function):
         dx = None
         for l in range(top, -1, -1):
             am = args[l] if args[l].numel() else None
-            dH = spmm_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, adj, win_mask=am,
-                          slot_map=plan.slot_map() if am is not None else None)
             W = Ws[l]
             fused = l > 0 and relus[l - 1] and rmasks[l - 1].numel() > 0
+            if (_FUSE_XW and am is None and
+                    spmm_xw_supported(plan.bwd, W.size(0), W.size(1), adj)):
+                # adjoint SpMM + dW + dX (+ the lower layer's ReLU / bias
+                # gradient) in one pass: dH never leaves the chip
+                if fused:
+                    gW[l], dY, db = spmm_xw_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY,
+                                                inputs[l], W, relu_mask=rmasks[l - 1],
+                                                row_div=rd)
+                    gb[l - 1] = db if ctx.has_bias[l - 1] else None
+                    continue
+                if l == 0 and not ctx.needs_input_grad[0]:
+                    gW[l] = spmm_xw_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, inputs[l],
+                                        W, want_dx=False)[0]
+                    continue
+            dH = spmm_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, adj, win_mask=am,
+                          slot_map=plan.slot_map() if am is not None else None)
             if fused and gemm_bwd_supported(W.size(0), W.size(1)):
                 # dW and dX (+ the lower layer's ReLU / bias gradient) in one pass
                 gW[l], dY, db = gemm_bwd(inputs[l], dH, W, relu_mask=rmasks[l - 1], row_div=rd)

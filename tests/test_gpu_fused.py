@@ -1,0 +1,234 @@
+"""GPU parity of the fused layer kernels (mgcn_spmm_xw_fwd / mgcn_spmm_xw_bwd).
+
+The forward aggregates X first and multiplies by W in the same launch:
+(A X) W instead of the reference's A (X W) (gcn_base_models.py:201, 223-237).
+Bars, per test:
+  * W = I: every bf16x6 product is exact, so the fused forward equals the
+    oracle's aggregation (the reference's index_select * norm -> scatter_add
+    order) BIT FOR BIT, masks included;
+  * random W: |Y - Y64| <= 1e-5 * (|Z| |W|) + 1e-6, Y64 the fp64 product of
+    the (bit-exact) fp32 aggregate Z -- the same bound the GEMM tests use;
+  * backward: dX is mgcn_spmm_bwd + mgcn_gemm_bwd's BIT FOR BIT (same dH,
+    same products and order), dW within 1e-5 of the |.|-weighted fp64 sum,
+    bias column sums within fp32 summation-order tolerance.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _t(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def _graph(rng, N, E, hub=0):
+    s = rng.integers(0, N, E)
+    d = rng.integers(0, N, E)
+    if hub:  # destination 0 and source 1 get `hub` extra edges (long rows)
+        d = np.concatenate([d, np.zeros(hub, np.int64), rng.integers(0, N, hub)])
+        s = np.concatenate([s, rng.integers(0, N, hub), np.ones(hub, np.int64)])
+    s = np.concatenate([s, np.arange(N)])
+    d = np.concatenate([d, np.arange(N)])
+    return np.stack([s, d]).astype(np.int64)
+
+
+GRAPHS = [
+    # N, E, hub
+    (20000, 200000, 0),
+    (4097, 40000, 0),     # last chunk partial
+    (33, 100, 0),
+    (1, 0, 0),
+    (3000, 20000, 700),   # rows far longer than a 32-edge metadata batch
+]
+
+
+def _plan(cuda, ei, N, deg_norm):
+    from mgcn.graph import plan_for
+    plan = plan_for(_t(ei, cuda), N)
+    return plan, plan.norm(deg_norm)
+
+
+@pytest.mark.parametrize("N,E,hub", GRAPHS)
+@pytest.mark.parametrize("deg_norm,aggr,bias,relu", [("sm", "add", True, True),
+                                                     ("rw", "mean", False, True),
+                                                     (None, "add", True, False),
+                                                     ("sm", "mean", True, False)])
+def test_fused_forward_identity_weights_bitwise(cuda, oracle, N, E, hub, deg_norm, aggr, bias,
+                                                relu):
+    from mgcn import _lib as L
+    from mgcn import ops
+    rng = np.random.default_rng(N + E + hub)
+    ei = _graph(rng, N, E, hub)
+    F = 128
+    X = rng.standard_normal((N, F)).astype(np.float32)
+    b = rng.uniform(-0.5, 0.5, F).astype(np.float32) if bias else None
+    plan, norm = _plan(cuda, ei, N, deg_norm)
+    rm = torch.empty(N, 4, dtype=torch.int32, device=cuda) if relu else None
+    Y = ops.spmm_xw_fwd(plan.fwd, norm.w_fwd, _t(X, cuda), torch.eye(F, device=cuda),
+                        L.REDUCE_CODES[aggr], None if b is None else _t(b, cuda), relu,
+                        relu_mask=rm)
+    wf, _, _ = oracle.edge_factors(ei, N, deg_norm)
+    y_ref, _ = oracle.aggr_fwd(ei, X, wf, aggr, b, relu)
+    np.testing.assert_array_equal(Y.cpu().numpy(), y_ref)
+    if relu:
+        assert torch.equal(rm, ops.make_relu_mask(Y))
+
+
+@pytest.mark.parametrize("N,E,hub", GRAPHS)
+@pytest.mark.parametrize("aggr", ["add", "mean"])
+def test_fused_forward_random_weights_vs_fp64(cuda, oracle, N, E, hub, aggr):
+    from mgcn import _lib as L
+    from mgcn import ops
+    rng = np.random.default_rng(7 * N + E)
+    ei = _graph(rng, N, E, hub)
+    F = 128
+    X = rng.standard_normal((N, F)).astype(np.float32)
+    W = (rng.standard_normal((F, F)) * 0.1).astype(np.float32)
+    b = rng.uniform(-0.5, 0.5, F).astype(np.float32)
+    plan, norm = _plan(cuda, ei, N, "sm")
+    Y = ops.spmm_xw_fwd(plan.fwd, norm.w_fwd, _t(X, cuda), _t(W, cuda), L.REDUCE_CODES[aggr],
+                        _t(b, cuda), False).cpu().numpy().astype(np.float64)
+    wf, _, _ = oracle.edge_factors(ei, N, "sm")
+    Z, _ = oracle.aggr_fwd(ei, X, wf, aggr)  # the kernel's own aggregate, bit for bit
+    ref = Z.astype(np.float64) @ W.astype(np.float64) + b
+    bound = np.abs(Z).astype(np.float64) @ np.abs(W).astype(np.float64) + np.abs(b)
+    assert (np.abs(Y - ref) <= 1e-5 * bound + 1e-6).all()
+    # and against the reference's association A (X W) in fp64
+    H = X.astype(np.float64) @ W.astype(np.float64)
+    src, dst = ei
+    w = wf.astype(np.float64)
+    ref2 = np.zeros((N, F))
+    np.add.at(ref2, dst, H[src] * w[:, None])
+    if aggr == "mean":
+        ref2 /= np.maximum(np.bincount(dst, minlength=N), 1)[:, None]
+    ref2 += b
+    assert (np.abs(Y - ref2) <= 1e-5 * bound + 1e-6).all()
+
+
+@pytest.mark.parametrize("N,E,hub", GRAPHS)
+@pytest.mark.parametrize("deg_norm,epi", [("sm", "relu"), ("rw", "relu_div"), (None, "store"),
+                                          ("sm", "dw_only")])
+def test_fused_backward_vs_two_launch(cuda, N, E, hub, deg_norm, epi):
+    from mgcn import _lib as L
+    from mgcn import ops
+    rng = np.random.default_rng(3 * N + E + len(epi))
+    ei = _graph(rng, N, E, hub)
+    F = 128
+    plan, norm = _plan(cuda, ei, N, deg_norm)
+    g = torch.Generator(device=cuda).manual_seed(N)
+    X = torch.randn(N, F, device=cuda, generator=g)
+    W = torch.randn(F, F, device=cuda, generator=g) * 0.1
+    dY = torch.randn(N, F, device=cuda, generator=g)
+    rm = ops.make_relu_mask(torch.randn(N, F, device=cuda, generator=g))
+    rd = plan.in_cnt if epi == "relu_div" else None
+    mask = rm if epi in ("relu", "relu_div") else None
+    dH = ops.spmm_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, L.REDUCE_SUM)
+    want_dx = epi != "dw_only"
+    dWa, dXa, csa = ops.gemm_bwd(X, dH, W, want_dx=want_dx, relu_mask=mask, row_div=rd)
+    dWb, dXb, csb = ops.spmm_xw_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, X, W,
+                                    want_dx=want_dx, relu_mask=mask, row_div=rd)
+    if want_dx:
+        assert torch.equal(dXa, dXb)
+    else:
+        assert dXb is None
+    ref = X.double().t() @ dH.double()
+    bound = X.double().abs().t() @ dH.double().abs()
+    assert ((dWb.double() - ref).abs() <= 1e-5 * bound + 1e-6).all()
+    if mask is not None:
+        torch.testing.assert_close(csb, csa, rtol=1e-4, atol=1e-3)
+        undiv = dXb if rd is None else dXb * rd[:, None]
+        torch.testing.assert_close(csb.double(), undiv.double().sum(0), rtol=1e-4, atol=1e-3)
+    # deterministic, and dW alone is the same dW
+    dWc = ops.spmm_xw_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, X, W, want_dx=False)[0]
+    assert torch.equal(dWb, dWc)
+
+
+def test_fused_backward_accumulate_and_empty(cuda):
+    """accumulate adds into dW; zero rows give a zero dW / colsum."""
+    from mgcn import _lib as L
+    from mgcn import ops
+    lib = L.load()
+    rng = np.random.default_rng(5)
+    N, F = 2000, 128
+    ei = _graph(rng, N, 20000)
+    plan, norm = _plan(cuda, ei, N, "sm")
+    X = torch.randn(N, F, device=cuda)
+    W = torch.randn(F, F, device=cuda)
+    dY = torch.randn(N, F, device=cuda)
+    dW = ops.spmm_xw_bwd(plan.bwd, norm.w_bwd, None, dY, X, W, want_dx=False)[0]
+    acc = torch.ones(F, F, device=cuda)
+    ws_bytes = int(lib.mgcn_spmm_xw_bwd_workspace_bytes(N))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=cuda)
+    v = plan.bwd
+    rc = lib.mgcn_spmm_xw_bwd(N, N, F, F, L.ptr(v.rowptr), L.ptr(v.col), L.ptr(norm.w_bwd), None,
+                              L.ptr(dY), F, L.ptr(X), F, L.ptr(W), F, L.ptr(acc), F, 1, None, 0,
+                              None, None, None, L.ptr(ws), ws_bytes, L.stream_of(cuda))
+    L.check(rc, "mgcn_spmm_xw_bwd")
+    assert torch.equal(acc, dW + 1.0)
+    dW0 = torch.full((F, F), 5.0, device=cuda)
+    cs0 = torch.full((F,), 5.0, device=cuda)
+    rc = lib.mgcn_spmm_xw_bwd(0, 1, F, F, L.ptr(v.rowptr), None, None, None, L.ptr(dY), F,
+                              L.ptr(X), F, L.ptr(W), F, L.ptr(dW0), F, 0, L.ptr(X), F,
+                              L.ptr(torch.zeros(1, 4, dtype=torch.int32, device=cuda)), None,
+                              L.ptr(cs0), L.ptr(ws), ws_bytes, L.stream_of(cuda))
+    L.check(rc, "mgcn_spmm_xw_bwd(empty)")
+    assert not dW0.any() and not cs0.any()
+
+
+def test_fused_kernels_reject_unsupported(cuda):
+    from mgcn import _lib as L
+    from mgcn import ops
+    rng = np.random.default_rng(6)
+    N = 500
+    plan, norm = _plan(cuda, _graph(rng, N, 4000), N, "sm")
+    assert not plan.fwd.n_heavy
+    assert ops.spmm_xw_supported(plan.fwd, 128, 128, L.REDUCE_SUM)
+    assert not ops.spmm_xw_supported(plan.fwd, 64, 64, L.REDUCE_SUM)
+    assert not ops.spmm_xw_supported(plan.fwd, 128, 128, L.REDUCE_MAX)
+    with pytest.raises(L.MgcnError, match="unsupported"):
+        ops.spmm_xw_fwd(plan.fwd, norm.w_fwd, torch.randn(N, 64, device=cuda),
+                        torch.randn(64, 64, device=cuda), L.REDUCE_SUM)
+    with pytest.raises(L.MgcnError, match="unsupported"):
+        ops.spmm_xw_fwd(plan.fwd, norm.w_fwd, torch.randn(N, 128, device=cuda),
+                        torch.randn(128, 128, device=cuda), L.REDUCE_MAX)
+
+
+@pytest.mark.parametrize("aggr,deg_norm", [("add", "sm"), ("mean", "rw")])
+def test_gcn_stack_fused_vs_two_launch(cuda, aggr, deg_norm):
+    """The stack with the fused kernels against the same stack on the
+    GEMM + SpMM launches: outputs within fp32 association tolerance, dx
+    bitwise below the top layer's first adjoint (same dH, same products) up
+    to the forward's differences, all gradients within tolerance."""
+    from mgcn import ops
+    from mgcn.models import GCNLayer, GCNStack
+    torch.manual_seed(0)
+    rng = np.random.default_rng(13)
+    N, F = 20000, 128
+    ei = _t(_graph(rng, N, 200000), cuda)
+    layers = [GCNLayer(F, F, deg_norm=deg_norm, aggr=aggr, bias=True,
+                       non_linear='relu' if i < 2 else 'none').to(cuda) for i in range(3)]
+    for layer in layers:
+        with torch.no_grad():
+            layer.gcn.node_models[0].bias.uniform_(-0.1, 0.1)
+    stack = GCNStack(layers)
+    x = torch.randn(N, F, device=cuda, requires_grad=True)
+    dZ = torch.randn(N, F, device=cuda)
+    outs = []
+    for fused in (True, False):
+        ops.set_fused_layers(fused)
+        try:
+            for p in stack.parameters():
+                p.grad = None
+            x.grad = None
+            y = stack(x, ei)
+            y.backward(dZ)
+            outs.append((y.detach(), x.grad.clone(), [p.grad.clone() for p in stack.parameters()]))
+        finally:
+            ops.set_fused_layers(True)
+    (ya, xa, ga), (yb, xb, gb) = outs
+    torch.testing.assert_close(ya, yb, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(xa, xb, rtol=1e-4, atol=1e-5)
+    for a, b in zip(ga, gb):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-3)

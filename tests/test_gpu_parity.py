@@ -474,8 +474,19 @@ def test_gcn_stack_identity_weights_bitwise_vs_oracle(cuda, oracle):
 
 
 def test_gcn_stack_matches_layer_by_layer(cuda):
-    """Fused stack == the same GCNLayers run one by one (forward and dW
-    bitwise: same kernels; db within fp32 summation-order tolerance)."""
+    """Stack on the GEMM + SpMM launches == the same GCNLayers run one by one
+    (forward and dW bitwise: same kernels; db within fp32 summation-order
+    tolerance).  The fused aggregate+transform kernels are compared with
+    this path in tests/test_gpu_fused.py."""
+    from mgcn import ops
+    ops.set_fused_layers(False)
+    try:
+        _stack_vs_layers(cuda)
+    finally:
+        ops.set_fused_layers(True)
+
+
+def _stack_vs_layers(cuda):
     from mgcn.models import GCNLayer, GCNStack
     torch.manual_seed(0)
     rng = np.random.default_rng(12)
