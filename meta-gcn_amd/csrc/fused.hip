@@ -319,6 +319,17 @@ struct XbArgs {
   float *colsum_partial;  // [grid][128]
 };
 
+#ifdef MGCN_XW_PROFILE
+// phase timestamps of workgroup 0, waves 0 and 7 (scripts/prof_fused.py):
+// [wave][chunk iteration][stamp]
+__device__ unsigned long long g_xprof[2][64][6];
+#define XPROF(it, k)                                                                      \
+  if (blockIdx.x == 0 && (wave == 0 || wave == 7) && (it) < 64 && lane == 0)              \
+    g_xprof[wave == 7][it][k] = __builtin_readcyclecounter();
+#else
+#define XPROF(it, k)
+#endif
+
 template <int U, bool DX, int EPI>
 __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(const XbArgs a) {
   __shared__ __attribute__((aligned(16))) char lds[kXbLds];
@@ -384,6 +395,7 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
     const int64_t r0 = chunk * kXwRows;
     const int64_t left = a.n_rows - r0;
     const uint32_t rows_in = (uint32_t)(left >= kXwRows ? kXwRows : left);
+    XPROF(it, 0);
     if constexpr (DX) {
       if (it > 0) flush(chunk - gridDim.x);
     }
@@ -409,6 +421,7 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
       }
       store_row_terms(lds + kXbHOff, lr, gl, acc);
     }
+    XPROF(it, 1);
     // mask / divisor words of the chunk's rows (wave 0; latency under the X split)
     u32x4 mk = {0u, 0u, 0u, 0u};
     uint32_t rd = 0u;
@@ -436,6 +449,7 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
       }
     }
     __syncthreads();
+    XPROF(it, 2);
 
     // ---- Phase B1: dW += X^T dH (two 16-row k-steps) ---------------------
     // this wave's W^T fragments for k-steps 0, 1 are in flight under the dW
@@ -461,6 +475,7 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
         accw[s] = mfma_x6(fa[0], fa[1], fa[2], fb[0], fb[1], fb[2], accw[s]);
       }
     }
+    XPROF(it, 3);
     // ---- Phase B2: dX = relu'(lower) (dH W^T) [/ row_div] -> staging ------
     if constexpr (DX) {
       f32x4_t acc2[2];
@@ -497,7 +512,9 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
           stage[lr * kXwStageLd + ncol] = v;
         }
     }
+    XPROF(it, 4);
     __syncthreads();
+    XPROF(it, 5);
   }
   if constexpr (DX) {
     if (it > 0) flush(blockIdx.x + (int64_t)(it - 1) * gridDim.x);  // staged before the last barrier
@@ -698,3 +715,11 @@ extern "C" int mgcn_spmm_xw_bwd(int64_t n_rows, int64_t n_cols, int32_t F_in, in
   if (rc || epi == EPI_STORE) return rc;
   return launch_colsum_fold(a.colsum_partial, grid, kXwF, colsum, s);
 }
+
+#ifdef MGCN_XW_PROFILE
+extern "C" int mgcn_debug_xw_prof(unsigned long long *host) {
+  MGCN_HIP_TRY(hipDeviceSynchronize());
+  MGCN_HIP_TRY(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_xprof), sizeof(g_xprof)));
+  return MGCN_OK;
+}
+#endif
