@@ -93,23 +93,27 @@ def spmm_bytes(n_rows: int, nnz: int, F: int) -> int:
 
 def pmc_traffic(kernel: str, args, world: int):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
-    (profiles/<round>/pmc_spmm.json: FETCH_SIZE and WRITE_SIZE in separate
-    passes, FETCH_SIZE corrected by the factor calibrated on a no-reuse gather
-    of known size).  PMC needs its own profiler run, so bench.py reports the
+    (profiles/<round>/pmc_fused.json or pmc_spmm.json: FETCH_SIZE and
+    WRITE_SIZE in separate passes, FETCH_SIZE corrected by the factors
+    calibrated on known-size launches, scripts/pmc_summary.py).  PMC needs its own profiler run, so bench.py reports the
     committed measurement of this exact kernel/config, or None."""
     if world != 1 or (args.nodes, args.pairs, args.feat) != (1_000_000, 5_000_000, 128):
         return None, None
     pdir = os.path.join(ROOT, "profiles")
-    rounds = sorted(d for d in os.listdir(pdir) if os.path.exists(
-        os.path.join(pdir, d, "pmc_spmm.json"))) if os.path.isdir(pdir) else []
-    if not rounds:
+    if not os.path.isdir(pdir):
         return None, None
-    path = os.path.join(pdir, rounds[-1], "pmc_spmm.json")
-    with open(path) as f:
-        k = json.load(f)["kernels"].get(kernel)
-    if not k:
-        return None, None
-    return k["traffic_bytes"], os.path.relpath(path, ROOT)
+    # the newest round's summary that holds this kernel (pmc_fused.json: the
+    # fused layer kernels; pmc_spmm.json: the unfused SpMMs)
+    for rnd in sorted(os.listdir(pdir), reverse=True):
+        for fname in ("pmc_fused.json", "pmc_spmm.json"):
+            path = os.path.join(pdir, rnd, fname)
+            if not os.path.exists(path):
+                continue
+            with open(path) as f:
+                k = json.load(f)["kernels"].get(kernel)
+            if k:
+                return k["traffic_bytes"], os.path.relpath(path, ROOT)
+    return None, None
 
 
 # ------------------------------------------------------------ CPU baseline
