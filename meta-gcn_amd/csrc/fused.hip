@@ -127,6 +127,99 @@ __device__ __forceinline__ void gather_row(const __amdgpu_buffer_rsrc_t rx, uint
   deg_out = deg;
 }
 
+// Pipelined form for a wave that walks a known sequence of rows: the row
+// pointer pair of row k + 2 and the first 32 edge slots (col, w) of row k + 1
+// are loaded while row k's feature rows are gathered, so a row costs one
+// gather round trip instead of three dependent ones (rowptr -> col -> row).
+struct RowMeta {
+  int64_t beg, deg;
+  int mc;
+  float mw;
+};
+
+__device__ __forceinline__ void meta_rowptr(const int64_t *__restrict__ rowptr, int64_t row,
+                                            bool ok, RowMeta &m) {
+  m.beg = ok ? rowptr[row] : 0;
+  m.deg = ok ? rowptr[row + 1] - m.beg : 0;
+}
+
+__device__ __forceinline__ void meta_first(const int32_t *__restrict__ col,
+                                           const float *__restrict__ w, int gl, RowMeta &m) {
+  m.mc = 0;
+  m.mw = 1.0f;
+  if (gl < m.deg) {
+    m.mc = col[m.beg + gl];
+    if (w != nullptr) m.mw = w[m.beg + gl];
+  }
+}
+
+template <int U>
+__device__ __forceinline__ void gather_row_meta(const __amdgpu_buffer_rsrc_t rx, uint32_t ldx_b,
+                                                const int32_t *__restrict__ col,
+                                                const float *__restrict__ w, const RowMeta &m,
+                                                int gl, int grp, float (&acc)[4]) {
+  const int64_t beg = m.beg, deg = m.deg;
+  const int64_t odeg = __shfl_xor(deg, 32, 64);
+  const int64_t maxdeg = deg > odeg ? deg : odeg;
+  acc[0] = acc[1] = acc[2] = acc[3] = 0.0f;
+  int mc = m.mc;
+  float mw = m.mw;
+  for (int64_t e0 = 0; e0 < maxdeg; e0 += 32) {
+    if (e0 > 0) {  // rows longer than one metadata batch load the rest in place
+      const int64_t my = e0 + gl;
+      mc = 0;
+      mw = 1.0f;
+      if (my < deg) {
+        mc = col[beg + my];
+        if (w != nullptr) mw = w[beg + my];
+      }
+    }
+    const int64_t rem = deg - e0;
+    const int nb = rem <= 0 ? 0 : (rem < 32 ? (int)rem : 32);
+    const int64_t remw = maxdeg - e0;
+    const int nbmax = remw < 32 ? (int)remw : 32;  // wave-uniform
+    for (int k0 = 0; k0 < nbmax; k0 += U) {
+      float4 xv[U];
+      float wk[U];
+      bool ok[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = k0 + u;
+        const int ck = __shfl(mc, 32 * grp + (k & 31), 64);
+        wk[u] = __shfl(mw, 32 * grp + (k & 31), 64);
+        ok[u] = k < nb;
+        const uint32_t off = ok[u] ? (uint32_t)ck * ldx_b + 16u * gl : 0xfffffff0u;
+        xv[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0));
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (ok[u]) {
+          acc[0] = __fadd_rn(acc[0], __fmul_rn(xv[u].x, wk[u]));
+          acc[1] = __fadd_rn(acc[1], __fmul_rn(xv[u].y, wk[u]));
+          acc[2] = __fadd_rn(acc[2], __fmul_rn(xv[u].z, wk[u]));
+          acc[3] = __fadd_rn(acc[3], __fmul_rn(xv[u].w, wk[u]));
+        }
+      }
+    }
+  }
+}
+
+// The row sequence of one lane group in the chunk loop: row k is slot
+// 16 (k & 1) + 2 wave + grp of the workgroup's chunk k >> 1 (chunks
+// blockIdx.x + i gridDim.x).  Used by the forward (-2.5 %); the backward has
+// no registers to spare for the extra state (its spills cost more).
+struct RowSeq {
+  int64_t base;  // blockIdx.x * 32 + 2 wave + grp
+  int64_t step;  // gridDim.x * 32
+  int64_t n_rows;
+  __device__ __forceinline__ int64_t row(int64_t k) const { return base + (k >> 1) * step + 16 * (k & 1); }
+};
+
+// chunks of this workgroup in a grid-stride chunk loop
+__device__ __forceinline__ int64_t my_chunks(int64_t n_chunks) {
+  return blockIdx.x < n_chunks ? (n_chunks - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+}
+
 // One row's four features -> its three bf16 term images (lane gl of the group)
 __device__ __forceinline__ void store_row_terms(char *img_base, int lr, int gl, const float (&v)[4]) {
   uint32_t hi[2], mid[2], lo[2];
@@ -235,6 +328,13 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_fwd_kernel(c
     }
   };
 
+  const int64_t n_my = my_chunks(n_chunks);
+  const RowSeq seq{(int64_t)blockIdx.x * kXwRows + 2 * wave + grp, (int64_t)gridDim.x * kXwRows,
+                   a.n_rows};
+  RowMeta cur, nxt;
+  meta_rowptr(a.rowptr, seq.row(0), seq.row(0) < a.n_rows, cur);
+  meta_first(a.col, a.w, gl, cur);
+  meta_rowptr(a.rowptr, seq.row(1), seq.row(1) < a.n_rows, nxt);
   int it = 0;
   for (int64_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x, ++it) {
     char *buf = lds + (it & 1) * kXfBuf;
@@ -244,16 +344,21 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_fwd_kernel(c
 #pragma unroll 1
     for (int p = 0; p < 2; ++p) {
       const int lr = 16 * p + 2 * wave + grp;
-      const int64_t row = chunk * kXwRows + lr;
-      int64_t deg;
+      const int64_t k = 2 * it + p;
+      meta_first(a.col, a.w, gl, nxt);
+      RowMeta nn;
+      const int64_t r2 = seq.row(k + 2);
+      meta_rowptr(a.rowptr, r2, r2 < a.n_rows && k + 2 < 2 * n_my, nn);
       float acc[4];
-      gather_row<U>(rx, ldx_b, a.rowptr, a.col, a.w, row, row < a.n_rows, gl, grp, acc, deg);
+      gather_row_meta<U>(rx, ldx_b, a.col, a.w, cur, gl, grp, acc);
       if (a.mean) {
-        const float c = (float)(deg > 1 ? deg : 1);
+        const float c = (float)(cur.deg > 1 ? cur.deg : 1);
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[j] = __fdiv_rn(acc[j], c);
       }
       store_row_terms(buf, lr, gl, acc);
+      cur = nxt;
+      nxt = nn;
     }
     __syncthreads();
     // the previous chunk's output rows (staged before this barrier) go out
