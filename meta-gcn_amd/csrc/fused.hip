@@ -79,25 +79,28 @@ __device__ __forceinline__ void gather_row(const __amdgpu_buffer_rsrc_t rx, uint
                                            const int64_t *__restrict__ rowptr,
                                            const int32_t *__restrict__ col,
                                            const float *__restrict__ w, int64_t row, bool row_ok,
-                                           int gl, int grp, float (&acc)[4], int64_t &deg_out) {
+                                           int gl, int grp, float (&acc)[4], int &deg_out) {
   const bool has_w = w != nullptr;
   const int64_t beg = row_ok ? rowptr[row] : 0;
-  const int64_t deg = row_ok ? rowptr[row + 1] - beg : 0;
-  const int64_t odeg = __shfl_xor(deg, 32, 64);
-  const int64_t maxdeg = deg > odeg ? deg : odeg;
+  // a row's degree fits 32 bits; the edge slots are addressed from beg
+  const int deg = row_ok ? (int)(rowptr[row + 1] - beg) : 0;
+  const int odeg = __shfl_xor(deg, 32, 64);
+  const int maxdeg = deg > odeg ? deg : odeg;
+  const int32_t *__restrict__ colr = col + beg;
+  const float *__restrict__ wr = has_w ? w + beg : nullptr;
   acc[0] = acc[1] = acc[2] = acc[3] = 0.0f;
-  for (int64_t e0 = 0; e0 < maxdeg; e0 += 32) {
-    const int64_t my = e0 + gl;
+  for (int e0 = 0; e0 < maxdeg; e0 += 32) {
+    const int my = e0 + gl;
     int mc = 0;
     float mw = 1.0f;
     if (my < deg) {
-      mc = col[beg + my];
-      if (has_w) mw = w[beg + my];
+      mc = colr[my];
+      if (has_w) mw = wr[my];
     }
-    const int64_t rem = deg - e0;
-    const int nb = rem <= 0 ? 0 : (rem < 32 ? (int)rem : 32);
-    const int64_t remw = maxdeg - e0;
-    const int nbmax = remw < 32 ? (int)remw : 32;  // wave-uniform
+    const int rem = deg - e0;
+    const int nb = rem <= 0 ? 0 : (rem < 32 ? rem : 32);
+    const int remw = maxdeg - e0;
+    const int nbmax = remw < 32 ? remw : 32;  // wave-uniform
     for (int k0 = 0; k0 < nbmax; k0 += U) {
       float4 xv[U];
       float wk[U];
@@ -490,8 +493,17 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
       const int lr = 16 * m + (tid >> 5);
-      const u32x4 v = *reinterpret_cast<const u32x4 *>(stage + lr * kXwStageLd + 4 * lc);
-      __builtin_amdgcn_raw_buffer_store_b128(v, rx, 4 * (int)(lr * a.lddx + 4 * lc), 0, 0);
+      float4 v = *reinterpret_cast<const float4 *>(stage + lr * kXwStageLd + 4 * lc);
+      if constexpr (EPI == EPI_RELU_DIV) {
+        // mean: the row's divisor rides in the staging row's padding
+        const float d = stage[lr * kXwStageLd + kXwF];
+        v.x = __fdiv_rn(v.x, d);
+        v.y = __fdiv_rn(v.y, d);
+        v.z = __fdiv_rn(v.z, d);
+        v.w = __fdiv_rn(v.w, d);
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rx,
+                                             4 * (int)(lr * a.lddx + 4 * lc), 0, 0);
     }
   };
 
@@ -516,7 +528,7 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
       const int lr = 16 * p + 2 * wave + grp;
       const int64_t row = r0 + lr;
       const bool row_ok = row < a.n_rows;
-      int64_t deg;
+      int deg;
       float acc[4];
       gather_row<U>(rdy, ldy_b, a.rowptr, a.col, a.w, row, row_ok, gl, grp, acc, deg);
       if (a.row_scale != nullptr && row_ok) {
@@ -611,11 +623,15 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
             const uint32_t wd = *reinterpret_cast<const uint32_t *>(lds + kXbMaskOff + 16 * lr + 4 * mword);
             v = ((wd >> mbit) & 1u) ? v : 0.0f;
             csum = __fadd_rn(csum, v);
-            if constexpr (EPI == EPI_RELU_DIV)
-              v = __fdiv_rn(v, *reinterpret_cast<const float *>(lds + kXbDivOff + 4 * lr));
           }
           stage[lr * kXwStageLd + ncol] = v;
         }
+      if constexpr (EPI == EPI_RELU_DIV) {
+        // divided at the flush (outside this register-heavy epilogue): the
+        // column sums take the undivided values, as in mgcn_gemm_bwd
+        if (wave == 0 && h == 0)
+          stage[lc * kXwStageLd + kXwF] = *reinterpret_cast<const float *>(lds + kXbDivOff + 4 * lc);
+      }
     }
     XPROF(it, 4);
     __syncthreads();
