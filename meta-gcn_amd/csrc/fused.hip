@@ -61,7 +61,8 @@ constexpr int kXwRows = 32;
 constexpr int kXwWaves = 8;
 constexpr int kXwThreads = 64 * kXwWaves;
 constexpr int kXwImg = kXwRows * 256;          // one bf16 term image of a chunk
-constexpr int kXwStageLd = kXwF + 4;           // backward staging row stride (floats)
+constexpr int kXwStageLd = kXwF + 8;           // backward staging row: 128 values, the row's
+                                               // 4 ReLU mask words, its divisor, padding
 constexpr int kXwStage = kXwRows * kXwStageLd * 4;
 constexpr int kXfStage = kXwRows * kXwF * 4;   // forward staging tile (unpadded: 2 fit)
 constexpr int kXwPerCU = 2;  // resident workgroups per CU the grid is sized for
@@ -479,12 +480,15 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
   for (int s = 0; s < 2; ++s)
 #pragma unroll
     for (int r = 0; r < 16; ++r) accw[s][r] = 0.0f;
-  float csum = 0.0f;
   const int ncol = 16 * wave + l16;  // dX column of this lane
-  const int mword = ncol & 3, mbit = 8 * (ncol >> 5) + ((ncol & 31) >> 2);
   const int xoff = 4 * (int)((tid >> 5) * a.ldx + 4 * (tid & 31));
 
   // staged dX rows of chunk `c` -> dX (16 B per lane, whole rows)
+  // The ReLU mask, the bias column sums and mean's division are applied here,
+  // on whole staged rows, rather than in the MFMA epilogue (whose registers
+  // are the kernel's peak): thread (q, lc) owns features 4 lc .. 4 lc + 3 of
+  // rows q and 16 + q; feature 4 lc + j is bit lc of the row's mask word j.
+  float cs[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // column sums of this thread's features
   auto flush = [&](int64_t c) {
     const int64_t r0 = c * kXwRows;
     const int64_t left = a.n_rows - r0;
@@ -493,17 +497,25 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
       const int lr = 16 * m + (tid >> 5);
-      float4 v = *reinterpret_cast<const float4 *>(stage + lr * kXwStageLd + 4 * lc);
-      if constexpr (EPI == EPI_RELU_DIV) {
-        // mean: the row's divisor rides in the staging row's padding
-        const float d = stage[lr * kXwStageLd + kXwF];
-        v.x = __fdiv_rn(v.x, d);
-        v.y = __fdiv_rn(v.y, d);
-        v.z = __fdiv_rn(v.z, d);
-        v.w = __fdiv_rn(v.w, d);
+      const float *srow = stage + lr * kXwStageLd;
+      float v[4];
+      *reinterpret_cast<float4 *>(v) = *reinterpret_cast<const float4 *>(srow + 4 * lc);
+      if constexpr (EPI != EPI_STORE) {
+        const u32x4 mw = *reinterpret_cast<const u32x4 *>(srow + kXwF);
+        // rows past the end were staged from zero dH rows with zero mask words
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[j] = ((mw[j] >> lc) & 1u) ? v[j] : 0.0f;
+          cs[j] = __fadd_rn(cs[j], v[j]);
+        }
+        if constexpr (EPI == EPI_RELU_DIV) {
+          const float d = srow[kXwF + 4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = __fdiv_rn(v[j], d);
+        }
       }
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rx,
-                                             4 * (int)(lr * a.lddx + 4 * lc), 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, *reinterpret_cast<float4 *>(v)),
+                                             rx, 4 * (int)(lr * a.lddx + 4 * lc), 0, 0);
     }
   };
 
@@ -616,21 +628,15 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int lr = 16 * t + 4 * g4 + r;
-          float v = acc2[t][r];
-          if constexpr (EPI != EPI_STORE) {
-            const uint32_t wd = *reinterpret_cast<const uint32_t *>(lds + kXbMaskOff + 16 * lr + 4 * mword);
-            v = ((wd >> mbit) & 1u) ? v : 0.0f;
-            csum = __fadd_rn(csum, v);
-          }
-          stage[lr * kXwStageLd + ncol] = v;
+        for (int r = 0; r < 4; ++r) stage[(16 * t + 4 * g4 + r) * kXwStageLd + ncol] = acc2[t][r];
+      if constexpr (EPI != EPI_STORE) {
+        // the chunk's mask words (and divisors) travel with the staged rows
+        if (wave == 0 && h == 0) {
+          *reinterpret_cast<u32x4 *>(stage + lc * kXwStageLd + kXwF) =
+              *reinterpret_cast<const u32x4 *>(lds + kXbMaskOff + 16 * lc);
+          if constexpr (EPI == EPI_RELU_DIV)
+            stage[lc * kXwStageLd + kXwF + 4] = *reinterpret_cast<const float *>(lds + kXbDivOff + 4 * lc);
         }
-      if constexpr (EPI == EPI_RELU_DIV) {
-        // divided at the flush (outside this register-heavy epilogue): the
-        // column sums take the undivided values, as in mgcn_gemm_bwd
-        if (wave == 0 && h == 0)
-          stage[lc * kXwStageLd + kXwF] = *reinterpret_cast<const float *>(lds + kXbDivOff + 4 * lc);
       }
     }
     XPROF(it, 4);
@@ -651,10 +657,18 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
       slab[row * kXwF + 32 * (tj0 + s) + lc] = accw[s][r];
     }
   if constexpr (DX && EPI != EPI_STORE) {
-    // fold the four row groups of each column in fixed order
-    const float c1 = __fadd_rn(csum, __shfl_xor(csum, 16, 64));
-    const float c2 = __fadd_rn(c1, __shfl_xor(c1, 32, 64));
-    if (lane < 16) a.colsum_partial[(int64_t)blockIdx.x * kXwF + ncol] = c2;
+    // fold the 16 row slots of each column in fixed order (the X images are free)
+    __syncthreads();
+    float *red = reinterpret_cast<float *>(lds);  // [16][128]
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[(tid >> 5) * kXwF + 4 * lc + j] = cs[j];
+    __syncthreads();
+    if (tid < kXwF) {
+      float c = 0.0f;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) c = __fadd_rn(c, red[q * kXwF + tid]);
+      a.colsum_partial[(int64_t)blockIdx.x * kXwF + tid] = c;
+    }
   }
 }
 
