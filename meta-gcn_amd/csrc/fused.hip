@@ -69,6 +69,8 @@ constexpr int kXwPerCU = 2;  // resident workgroups per CU the grid is sized for
 
 constexpr int EPI_STORE = 0, EPI_RELU = 1, EPI_RELU_DIV = 2;
 
+typedef __attribute__((address_space(3))) void lds_void_t;
+
 // Aggregate one row in the 32-lane group `grp` of the wave (both groups of a
 // wave call this together): acc = sum_k X[col_k] * w_k in edge order,
 // products and sums rounded separately -- the SpMM's arithmetic, bit for bit.
@@ -405,7 +407,9 @@ constexpr int kXbHOff = 3 * kXwImg;
 constexpr int kXbMaskOff = 6 * kXwImg;                 // [32][4] mask words
 constexpr int kXbDivOff = kXbMaskOff + kXwRows * 16;   // [32] row divisors
 constexpr int kXbStageOff = kXbDivOff + kXwRows * 4;
-constexpr int kXbLds = kXbStageOff + kXwStage;
+constexpr int kXbColsumOff = kXbStageOff + kXwStage;     // [512 threads][4] column sums
+constexpr int kXbLds = kXbColsumOff + kXwThreads * 16;
+static_assert(2 * kXbLds <= 160 * 1024, "two backward workgroups per CU");
 
 struct XbArgs {
   int64_t n_rows;  // source nodes: rows of the bwd view, of X and of dX
@@ -488,7 +492,11 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
   // on whole staged rows, rather than in the MFMA epilogue (whose registers
   // are the kernel's peak): thread (q, lc) owns features 4 lc .. 4 lc + 3 of
   // rows q and 16 + q; feature 4 lc + j is bit lc of the row's mask word j.
-  float cs[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // column sums of this thread's features
+  // column sums of this thread's features, kept in LDS (registers are the
+  // kernel's limit)
+  float *cs = reinterpret_cast<float *>(lds + kXbColsumOff) + 4 * tid;
+  if constexpr (DX && EPI != EPI_STORE)
+    *reinterpret_cast<float4 *>(cs) = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   auto flush = [&](int64_t c) {
     const int64_t r0 = c * kXwRows;
     const int64_t left = a.n_rows - r0;
@@ -503,11 +511,14 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
       if constexpr (EPI != EPI_STORE) {
         const u32x4 mw = *reinterpret_cast<const u32x4 *>(srow + kXwF);
         // rows past the end were staged from zero dH rows with zero mask words
+        float c[4];
+        *reinterpret_cast<float4 *>(c) = *reinterpret_cast<const float4 *>(cs);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           v[j] = ((mw[j] >> lc) & 1u) ? v[j] : 0.0f;
-          cs[j] = __fadd_rn(cs[j], v[j]);
+          c[j] = __fadd_rn(c[j], v[j]);
         }
+        *reinterpret_cast<float4 *>(cs) = *reinterpret_cast<const float4 *>(c);
         if constexpr (EPI == EPI_RELU_DIV) {
           const float d = srow[kXwF + 4];
 #pragma unroll
@@ -533,6 +544,18 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
     const auto rxx = buf_rsrc(a.X + r0 * a.ldx, rows_in * (uint32_t)a.ldx * 4u);
     const u32x4 xa = __builtin_amdgcn_raw_buffer_load_b128(rxx, xoff, 0, 0);
     const u32x4 xb = __builtin_amdgcn_raw_buffer_load_b128(rxx, xoff + 64 * (int)a.ldx, 0, 0);
+    // the chunk's mask / divisor words straight into LDS (LDS-DMA: no registers
+    // held across the gathers); rows past the end read row r0 and are never used
+    if constexpr (DX && EPI != EPI_STORE) {
+      if (wave == 0 && h == 0) {
+        const int64_t mr = r0 + ((uint32_t)lc < rows_in ? lc : 0);
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a.relu_mask + mr * 4),
+                                         (lds_void_t *)(lds + kXbMaskOff), 16, 0, 0);
+        if constexpr (EPI == EPI_RELU_DIV)
+          __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a.row_div + mr),
+                                           (lds_void_t *)(lds + kXbDivOff), 4, 0, 0);
+      }
+    }
 
     // ---- Phase A: dH rows of the chunk -> bf16 images; X rows -> images --
 #pragma unroll 1
@@ -551,45 +574,30 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
       store_row_terms(lds + kXbHOff, lr, gl, acc);
     }
     XPROF(it, 1);
-    // mask / divisor words of the chunk's rows (wave 0; latency under the X split)
-    u32x4 mk = {0u, 0u, 0u, 0u};
-    uint32_t rd = 0u;
-    if constexpr (DX && EPI != EPI_STORE) {
-      if (wave == 0) {
-        const auto rm = buf_rsrc(a.relu_mask + r0 * 4, rows_in * 16u);
-        mk = __builtin_amdgcn_raw_buffer_load_b128(rm, 16 * lc, 0, 0);
-        if constexpr (EPI == EPI_RELU_DIV) {
-          const auto rdv = buf_rsrc(a.row_div + r0, rows_in * 4u);
-          rd = __builtin_amdgcn_raw_buffer_load_b32(rdv, 4 * lc, 0, 0);
-        }
-      }
-    }
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
       const float4 v = __builtin_bit_cast(float4, m == 0 ? xa : xb);
       const float f[4] = {v.x, v.y, v.z, v.w};
       store_row_terms(lds, 16 * m + (tid >> 5), lc, f);
     }
-    if constexpr (DX && EPI != EPI_STORE) {
-      if (wave == 0) {
-        if (h == 0) *reinterpret_cast<u32x4 *>(lds + kXbMaskOff + 16 * lc) = mk;
-        if constexpr (EPI == EPI_RELU_DIV)
-          if (h == 1) *reinterpret_cast<uint32_t *>(lds + kXbDivOff + 4 * lc) = rd;
-      }
+    // the mask / divisor LDS-DMA (older than this wave's gathers) has landed
+    if constexpr (DX && EPI != EPI_STORE)
+      if (wave == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // this wave's W^T fragments (B[k][n] = W[n][k], 32 floats per lane): issued
+    // before the barrier, so the L2 round trip (thousands of cycles while the
+    // other workgroup's gathers load the memory system) is hidden by the
+    // barrier wait and the dW MFMAs
+    float4 wr[4][2];
+    if constexpr (DX) {
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) wr[ks][j] = *reinterpret_cast<const float4 *>(wp + 32 * ks + 4 * j);
     }
     __syncthreads();
     XPROF(it, 2);
 
     // ---- Phase B1: dW += X^T dH (two 16-row k-steps) ---------------------
-    // this wave's W^T fragments for k-steps 0, 1 are in flight under the dW
-    // MFMAs (k-steps 2, 3 are loaded while 0, 1 run)
-    float4 wr[4][2];
-    if constexpr (DX) {
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) wr[ks][j] = *reinterpret_cast<const float4 *>(wp + 32 * ks + 4 * j);
-    }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const char *kb = lds + ks * 16 * 256;
@@ -614,11 +622,6 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
         for (int r = 0; r < 4; ++r) acc2[t][r] = 0.0f;
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        if (ks < 2) {
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            wr[ks + 2][j] = *reinterpret_cast<const float4 *>(wp + 32 * (ks + 2) + 4 * j);
-        }
         bf16x8 wb[3];
         const float v[8] = {wr[ks][0].x, wr[ks][0].y, wr[ks][0].z, wr[ks][0].w,
                             wr[ks][1].x, wr[ks][1].y, wr[ks][1].z, wr[ks][1].w};
@@ -657,16 +660,14 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
       slab[row * kXwF + 32 * (tj0 + s) + lc] = accw[s][r];
     }
   if constexpr (DX && EPI != EPI_STORE) {
-    // fold the 16 row slots of each column in fixed order (the X images are free)
+    // fold the 16 row slots of each column in fixed order: thread (q, lc)
+    // holds features 4 lc .. 4 lc + 3 at cs slot 32 q + lc
     __syncthreads();
-    float *red = reinterpret_cast<float *>(lds);  // [16][128]
-#pragma unroll
-    for (int j = 0; j < 4; ++j) red[(tid >> 5) * kXwF + 4 * lc + j] = cs[j];
-    __syncthreads();
+    const float *red = reinterpret_cast<const float *>(lds + kXbColsumOff);
     if (tid < kXwF) {
       float c = 0.0f;
 #pragma unroll
-      for (int q = 0; q < 16; ++q) c = __fadd_rn(c, red[q * kXwF + tid]);
+      for (int q = 0; q < 16; ++q) c = __fadd_rn(c, red[4 * (32 * q + (tid >> 2)) + (tid & 3)]);
       a.colsum_partial[(int64_t)blockIdx.x * kXwF + tid] = c;
     }
   }
