@@ -28,7 +28,8 @@ from torch.nn.utils.rnn import pad_sequence
 
 from . import _lib as L
 from .graph import plan_for
-from .ops import (aggregate_plan, gcn_stack, linear, linear_bias, residual_gcn_layer,  # noqa: F401
+from .ops import (aggregate_plan, gcn_layer, gcn_stack, linear, linear_bias,  # noqa: F401
+                  residual_gcn_layer,  # noqa: F401
                   scatter_)
 
 
@@ -165,11 +166,15 @@ class NodeModelAdditive(NodeModelBase):
             raise NotImplementedError(
                 "edge_attr messages (gcn_base_models.py:204-227) are not supported by the "
                 "mgcn engine")
-        x = linear(x, self.weight_node)  # torch.matmul(x, W), gcn_base_models.py:201
         plan = plan_for(edge_index, x.size(0))
         # deg_norm None ignores edge_weight entirely (gcn_base_models.py:209-211)
         norm = plan.norm(self.deg_norm, deg=deg,
                          edge_weight=edge_weight if self.deg_norm is not None else None)
+        if self.aggr != 'max':
+            # torch.matmul(x, W) (gcn_base_models.py:201) fused behind the
+            # aggregation where the kernels apply
+            return gcn_layer(x, self.weight_node, plan, norm, self.aggr, self.bias, relu)
+        x = linear(x, self.weight_node)  # torch.matmul(x, W), gcn_base_models.py:201
         return aggregate_plan(x, plan, norm, self.aggr, self.bias, relu)
 
 

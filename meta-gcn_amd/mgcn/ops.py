@@ -549,6 +549,51 @@ def aggregate_plan(H: torch.Tensor, plan: GraphPlan, norm: NormPlan, aggr: str =
     return _Aggregate.apply(H, bias, plan, norm, L.REDUCE_CODES[aggr], bool(relu))
 
 
+class _LayerXW(torch.autograd.Function):
+    """One GCN layer  y = epi((A_norm x) W + b)  on the fused kernels: the
+    forward is one mgcn_spmm_xw_fwd launch, the backward one relu_bwd_colsum
+    (this layer's ReLU / bias gradient; mean's division) and one
+    mgcn_spmm_xw_bwd (dW and dx from on-chip dH).  Same gradients as
+    linear() + aggregate_plan() up to the association of the forward sums."""
+
+    @staticmethod
+    def forward(ctx, x, W, bias, plan: GraphPlan, norm: NormPlan, reduce: int, relu: bool):
+        Y = spmm_xw_fwd(plan.fwd, norm.w_fwd, x, W, reduce, bias, relu)
+        ctx.plan, ctx.norm, ctx.reduce, ctx.relu = plan, norm, reduce, relu
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(x, W, Y if relu else None)
+        return Y
+
+    @staticmethod
+    def backward(ctx, dZ):
+        x, W, Y = ctx.saved_tensors
+        plan, norm = ctx.plan, ctx.norm
+        need_b = ctx.has_bias and ctx.needs_input_grad[2]
+        mean = ctx.reduce == L.REDUCE_MEAN
+        dY, db = relu_bwd_colsum(dZ.contiguous(), Y, ctx.relu, need_b,
+                                 row_div=plan.in_cnt if mean else None)
+        dW, dx, _ = spmm_xw_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, x, W,
+                                want_dx=ctx.needs_input_grad[0])
+        return dx, dW, db, None, None, None, None
+
+
+def gcn_layer(x: torch.Tensor, W: torch.Tensor, plan: GraphPlan, norm: NormPlan,
+              aggr: str = "add", bias: torch.Tensor | None = None,
+              relu: bool = False) -> torch.Tensor:
+    """``aggregate_plan(x @ W, plan, norm, aggr, bias, relu)`` -- the
+    reference's ``x @ weight_node`` then gather / scale / scatter (+ bias,
+    ReLU) (gcn_base_models.py:201-241) -- as one fused launch per direction
+    where the kernels apply (128 -> 128, sum / mean, no heavy rows); otherwise
+    the GEMM and the aggregation run as separate launches."""
+    reduce = L.REDUCE_CODES[aggr]
+    if (_FUSE_XW and x.dim() == 2 and x.dtype == torch.float32 and W.dtype == torch.float32
+            and x.is_cuda and x.size(0) == plan.fwd.n_cols == plan.fwd.n_rows
+            and spmm_xw_supported(plan.fwd, W.size(0), W.size(1), reduce)
+            and plan.bwd.n_heavy == 0):
+        return _LayerXW.apply(x, W, bias, plan, norm, reduce, bool(relu))
+    return aggregate_plan(linear(x, W), plan, norm, aggr, bias, relu)
+
+
 class _GCNStack(torch.autograd.Function):
     """A chain of GCN layers  Z_l = act_l(A_norm (Z_{l-1} W_l) + b_l)  as one
     autograd node, so the backward can fuse across layer boundaries: the

@@ -34,7 +34,7 @@ from torch.nn import Parameter
 
 from .graph import cache_key, plan_for
 from .models import glorot, zeros
-from .ops import aggregate_plan, scatter_
+from .ops import aggregate_plan, gcn_layer, scatter_
 
 
 def uniform(size, tensor):
@@ -143,7 +143,6 @@ class GCNConv(nn.Module):
         zeros(self.bias)
 
     def forward(self, x, edge_index, edge_weight=None, relu=False):
-        x = torch.matmul(x, self.weight)
         N = x.size(0)
         fill = 2 if self.improved else 1
         if edge_weight is None:
@@ -154,7 +153,8 @@ class GCNConv(nn.Module):
         ei, ew = _with_loops(edge_index, edge_weight, N, fill)
         plan = plan_for(ei, N)
         norm = plan.norm('sm', edge_weight=ew)
-        return aggregate_plan(x, plan, norm, 'add', self.bias, relu)
+        # x @ W, then propagate: one fused launch per direction where it applies
+        return gcn_layer(x, self.weight, plan, norm, 'add', self.bias, relu)
 
     def __repr__(self):
         return '{}({}, {})'.format(self.__class__.__name__, self.in_channels, self.out_channels)
@@ -217,12 +217,16 @@ class SAGEConv(nn.Module):
         N = x.size(0)
         ei, ew = _with_loops(edge_index, edge_weight, N, 1)
         plan = plan_for(ei, N)
-        out = aggregate_plan(x, plan, plan.norm(None, edge_weight=ew), 'mean')
+        norm = plan.norm(None, edge_weight=ew)
         if self.concat:
+            out = aggregate_plan(x, plan, norm, 'mean')
             out = torch.cat([x, out], dim=-1)
-        out = torch.matmul(out, self.weight)
-        if self.bias is not None:
-            out = out + self.bias
+            out = torch.matmul(out, self.weight)
+            if self.bias is not None:
+                out = out + self.bias
+        else:
+            # mean of the neighbourhood, then @ W + b: the fused kernel's own order
+            out = gcn_layer(x, self.weight, plan, norm, 'mean', self.bias)
         if self.normalize:
             out = F.normalize(out, p=2, dim=-1)
         return out
@@ -251,9 +255,12 @@ class GraphConv(nn.Module):
 
     def forward(self, x, edge_index, edge_weight=None, size=None):
         x = x.unsqueeze(-1) if x.dim() == 1 else x
-        h = torch.matmul(x, self.weight)
         plan = plan_for(edge_index, x.size(0))
-        agg = aggregate_plan(h, plan, plan.norm(None, edge_weight=edge_weight), self.aggr)
+        norm = plan.norm(None, edge_weight=edge_weight)
+        if self.aggr == 'max':
+            agg = aggregate_plan(torch.matmul(x, self.weight), plan, norm, 'max')
+        else:
+            agg = gcn_layer(x, self.weight, plan, norm, self.aggr)
         return agg + self.lin(x)
 
     def __repr__(self):
