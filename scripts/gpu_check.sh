@@ -1,0 +1,26 @@
+#!/bin/bash
+# GPU pass used during development: full GPU suite, smoke, default bench and a
+# rocprofv3 --kernel-trace --stats run of the same bench command.
+# Usage (repo root on the GPU box): bash scripts/gpu_check.sh <tag> [pytest -k expr]
+# Every GPU step has its own limit; the chain stops at the first failure.
+set -e -o pipefail
+R=$PWD
+T=${1:-dev}
+O=$R/gpurun_out/$T
+mkdir -p $O
+K=${2:-}
+if [ -n "$K" ]; then
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "$K" \
+    > $O/gpu_tests.log 2>&1
+else
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+    > $O/gpu_tests.log 2>&1
+fi
+tail -3 $O/gpu_tests.log
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+timeout -k 10 300 python -u bench.py > $O/bench_default.json 2> $O/bench_default.err
+cat $O/bench_default.json
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench -- \
+  python3 $R/bench.py --no-cpu-baseline > $O/bench_under_rocprof.json 2> $O/bench_under_rocprof.err
+echo gpu_check $T done
