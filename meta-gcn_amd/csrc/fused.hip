@@ -65,7 +65,10 @@ constexpr int kXwStageLd = kXwF + 8;           // backward staging row: 128 valu
                                                // 4 ReLU mask words, its divisor, padding
 constexpr int kXwStage = kXwRows * kXwStageLd * 4;
 constexpr int kXfStage = kXwRows * kXwF * 4;   // forward staging tile (unpadded: 2 fit)
-constexpr int kXwPerCU = 2;  // resident workgroups per CU the grid is sized for
+#ifndef MGCN_XW_PER_CU
+#define MGCN_XW_PER_CU 2
+#endif
+constexpr int kXwPerCU = MGCN_XW_PER_CU;  // resident workgroups per CU the grid is sized for
 
 constexpr int EPI_STORE = 0, EPI_RELU = 1, EPI_RELU_DIV = 2;
 

@@ -230,6 +230,7 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(const SpmmArgs a) {
           float wk[U];
           int ek[U];
           bool ok[U];
+          uint32_t wbits[U];  // BWD_MAXM: the edge's winner word
 #pragma unroll
           for (int u = 0; u < U; ++u) {
             const int k = k0 + u;
@@ -243,17 +244,12 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(const SpmmArgs a) {
             const float *src = X + (int64_t)ck * a.ldx + f0;
             if constexpr (MODE == BWD_MAXM) {
               // dY row and the edge's winner bits (at its fwd slot) are loaded
-              // together -- no load waits on a test -- then selected
-#pragma unroll
-              for (int j = 0; j < VEC; ++j) xv[u].v[j] = 0.0f;
-              if (ok[u]) {
-                const int64_t W = (a.F + 31) >> 5;
-                const uint32_t word = a.win_mask[(int64_t)ek[u] * W + (f0 >> 5)];
-                const F32v<VEC> g = load_f<VEC>(src);
-                const uint32_t bits = word >> (f0 & 31);
-#pragma unroll
-                for (int j = 0; j < VEC; ++j) xv[u].v[j] = ((bits >> j) & 1u) ? g.v[j] : 0.0f;
-              }
+              // unconditionally (masked edges read row 0 / word 0, never
+              // used) and selected in the fold: a select here, between the
+              // loads, would make every load wait for the previous one
+              const int64_t W = (a.F + 31) >> 5;
+              wbits[u] = a.win_mask[ok[u] ? (int64_t)ek[u] * W + (f0 >> 5) : 0];
+              xv[u] = load_f<VEC>(ok[u] ? src : X);
             } else if constexpr (MODE == BWD_MAX) {
               // route dY only through the (d, f) entries whose argmax is this edge
 #pragma unroll
@@ -286,6 +282,11 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(const SpmmArgs a) {
 #pragma unroll
           for (int u = 0; u < U; ++u) {
             if (ok[u]) {
+              if constexpr (MODE == BWD_MAXM) {
+                const uint32_t bits = wbits[u] >> (f0 & 31);
+#pragma unroll
+                for (int j = 0; j < VEC; ++j) xv[u].v[j] = ((bits >> j) & 1u) ? xv[u].v[j] : 0.0f;
+              }
 #pragma unroll
               for (int j = 0; j < VEC; ++j) {
                 const float p = __fmul_rn(xv[u].v[j], wk[u]);

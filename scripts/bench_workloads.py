@@ -74,7 +74,7 @@ def config4(args, dev):
     X, Ws, bs, dY = make_inputs(N, 128, 3)
     X, dY = X.to(dev), dY.to(dev)
     res = {"workload": "config4 ER N=1M E=10M F=128, 3-layer stacks deg_norm=None", "edges": n_edges}
-    for aggr in ("add", "mean", "max"):
+    for aggr in args.aggr.split(","):
         layers = []
         for i in range(3):
             layer = GCNLayer(128, 128, deg_norm=None, aggr=aggr, bias=True,
@@ -100,6 +100,7 @@ def main():
     ap.add_argument("--workload", choices=["config3", "config4"], required=True)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--aggr", default="add,mean,max", help="config4: aggregators to run")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     fn = {"config3": config3, "config4": config4}[args.workload]
