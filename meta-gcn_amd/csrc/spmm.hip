@@ -175,7 +175,13 @@ template <int VEC, int G, int U, int MODE>
 __global__ __launch_bounds__(kBlock) void spmm_kernel(const SpmmArgs a) {
   constexpr int RPW = 64 / G;  // rows per wave
   constexpr bool kFwd = (MODE == FWD_SUM || MODE == FWD_MAX);
-  constexpr bool kNeedEid = (MODE == FWD_MAX || MODE == BWD_MAX);
+  // the forward max tracks its winner as the edge's position in the row (the
+  // winner bits are per slot; argmax rows are mapped to edge ids at the end)
+  constexpr bool kNeedEid = (MODE == BWD_MAX);
+  // forward max, F a multiple of 128 at 4 x 32 lanes: winner bits assembled
+  // in LDS (one 16-B record per edge and 128-feature chunk, 32 edges a window)
+  constexpr bool kWinLds = (MODE == FWD_MAX && VEC == 4 && G == 32);
+  __shared__ __attribute__((aligned(16))) uint32_t win_rec[kWinLds ? kWaves * 2 * 32 * 4 : 1];
   const int lane = threadIdx.x & 63;
   const int gl = lane & (G - 1);
   const int grp = lane / G;
@@ -237,7 +243,8 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(const SpmmArgs a) {
             const int kk = k & (G - 1);
             const int ck = bcast_i<G>(mc, gbase, kk);
             wk[u] = bcast_f<G>(mw, gbase, kk);
-            ek[u] = (kNeedEid || MODE == BWD_MAXM) ? bcast_i<G>(me, gbase, kk) : 0;
+            ek[u] = (MODE == FWD_MAX) ? (int)(e0 + k)
+                    : (kNeedEid || MODE == BWD_MAXM) ? bcast_i<G>(me, gbase, kk) : 0;
             float cntk = 1.0f;
             if constexpr (MODE == BWD_MEAN) cntk = bcast_f<G>(mcnt, gbase, kk);
             ok[u] = (k < nb) && f_ok;
@@ -306,32 +313,53 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(const SpmmArgs a) {
 
       if constexpr (MODE == FWD_MAX) {
         if (a.win_mask_out != nullptr) {
-          // winner bits of every edge of this row, at its own (fwd) slot: a
-          // second pass over the row's edge ids; each 32-bit word is OR-ed
-          // over its lanes (all lanes of the group take part)
-          int32_t winner[VEC];
+          // winner bits of every edge of this row, at its own (fwd) slot
+          int32_t winner[VEC];  // position of the winning edge in the row, -1: none
 #pragma unroll
           for (int j = 0; j < VEC; ++j) winner[j] = (acc.v[j] == MGCN_MAX_FILL) ? -1 : arg.v[j];
           const int64_t W = (a.F + 31) >> 5;
-          constexpr int LW = (32 / VEC) < G ? (32 / VEC) : G;  // lanes per word in a group
-          for (int64_t e0 = 0; e0 < maxdeg; e0 += G) {
-            const int64_t my = e0 + gl;
-            int32_t me = -1;
-            if (my < deg) me = a.eid[beg + my];
-            const int64_t rem = deg - e0;
-            const int nb = rem <= 0 ? 0 : (rem < G ? (int)rem : G);
-            const int64_t remw = maxdeg - e0;
-            const int nbmax = remw < G ? (int)remw : G;  // wave-uniform
-            for (int k = 0; k < nbmax; ++k) {
-              const int32_t ek = bcast_i<G>(me, gbase, k);
-              uint32_t v = 0;
+          if (kWinLds && (a.F & 127) == 0) {
+            // each lane ORs its four winner bits into the window's records
+            // (word gl / 8 of an edge's record, bit 4 (gl % 8) + j), then
+            // lane gl writes record gl out: 512 contiguous bytes per group.
+            // One wave's LDS operations execute in order, so the zeroing,
+            // the ORs and the read-back of a window need no barrier.
+            uint32_t *rec = win_rec + ((int)(threadIdx.x >> 6) * 2 + grp) * 32 * 4;
+            for (int64_t w0 = 0; w0 < maxdeg; w0 += 32) {
+              *reinterpret_cast<uint4 *>(rec + 4 * gl) = make_uint4(0u, 0u, 0u, 0u);
+              __builtin_amdgcn_wave_barrier();
 #pragma unroll
-              for (int j = 0; j < VEC; ++j) v |= (winner[j] == ek ? 1u : 0u) << j;
-              v <<= (f0 & 31);
+              for (int j = 0; j < VEC; ++j) {
+                const int64_t p = winner[j] - w0;
+                if (winner[j] >= 0 && p >= 0 && p < 32)
+                  atomicOr(rec + 4 * p + (gl >> 3), 1u << (((gl & 7) << 2) + j));
+              }
+              __builtin_amdgcn_wave_barrier();
+              const uint4 r = *reinterpret_cast<const uint4 *>(rec + 4 * gl);
+              if (w0 + gl < deg)
+                *reinterpret_cast<uint4 *>(a.win_mask_out + (beg + w0 + gl) * W + 4 * c) = r;
+              __builtin_amdgcn_wave_barrier();
+            }
+          } else {
+            // a pass over the row's edge positions; each 32-bit word is OR-ed
+            // over its lanes (all lanes of the group take part)
+            constexpr int LW = (32 / VEC) < G ? (32 / VEC) : G;  // lanes per word in a group
+            for (int64_t e0 = 0; e0 < maxdeg; e0 += G) {
+              const int64_t rem = deg - e0;
+              const int nb = rem <= 0 ? 0 : (rem < G ? (int)rem : G);
+              const int64_t remw = maxdeg - e0;
+              const int nbmax = remw < G ? (int)remw : G;  // wave-uniform
+              for (int k = 0; k < nbmax; ++k) {
+                const int32_t ek = (int32_t)(e0 + k);
+                uint32_t v = 0;
 #pragma unroll
-              for (int off = 1; off < LW; off <<= 1) v |= __shfl_xor(v, off, 64);
-              if (k < nb && f_ok && (f0 & 31) == 0)
-                a.win_mask_out[(beg + e0 + k) * W + (f0 >> 5)] = v;
+                for (int j = 0; j < VEC; ++j) v |= (winner[j] == ek ? 1u : 0u) << j;
+                v <<= (f0 & 31);
+#pragma unroll
+                for (int off = 1; off < LW; off <<= 1) v |= __shfl_xor(v, off, 64);
+                if (k < nb && f_ok && (f0 & 31) == 0)
+                  a.win_mask_out[(beg + e0 + k) * W + (f0 >> 5)] = v;
+              }
             }
           }
         }
@@ -368,7 +396,12 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(const SpmmArgs a) {
           }
         }
         if constexpr (MODE == FWD_MAX) {
-          if (a.argmax_out != nullptr) store_i<VEC>(a.argmax_out + row * a.F + f0, arg);
+          if (a.argmax_out != nullptr) {
+            // winner positions -> edge ids (torch_scatter's argmax)
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) arg.v[j] = arg.v[j] >= 0 ? a.eid[beg + arg.v[j]] : -1;
+            store_i<VEC>(a.argmax_out + row * a.F + f0, arg);
+          }
         }
       } else {
         if (a.row_scale != nullptr) {
