@@ -85,25 +85,6 @@ __global__ __launch_bounds__(kBlock) void relu_bwd_colsum_kernel(
   }
 }
 
-// db[f] = fold of the block partials: 4 interleaved groups of blocks, each in
-// block order, then the 4 group sums in order (deterministic).
-__global__ __launch_bounds__(kBlock) void colsum_finish_kernel(const float *__restrict__ partial,
-                                                               int nblk, int F,
-                                                               float *__restrict__ db) {
-  __shared__ float red[4][64];
-  const int g = threadIdx.x >> 6;
-  const int f = blockIdx.x * 64 + (threadIdx.x & 63);
-  float s = 0.0f;
-  if (f < F)
-#pragma unroll 8
-    for (int b = g; b < nblk; b += 4) s = __fadd_rn(s, partial[(int64_t)b * F + f]);
-  red[g][threadIdx.x & 63] = s;
-  __syncthreads();
-  if (g == 0 && f < F)
-    db[f] = __fadd_rn(__fadd_rn(red[0][threadIdx.x], red[1][threadIdx.x]),
-                      __fadd_rn(red[2][threadIdx.x], red[3][threadIdx.x]));
-}
-
 template <int VEC>
 __device__ __forceinline__ void load_vec(const float *p, float (&v)[VEC]) {
   if constexpr (VEC == 4) {
@@ -151,7 +132,7 @@ __global__ __launch_bounds__(kBlock) void residual_act_kernel(
 //   dS = relu ? (Z > 0 ? dZ : 0) : dZ       (grad of the residual branch R)
 //   dA = relu1 ? (Z1 > 0 ? dS : 0) : dS     (grad of the aggregation, / row_div)
 // and the column sums of dA (bias b) and dS (residual bias rb) into block
-// partials [block][2F] in a fixed row order (colsum_finish_kernel folds them).
+// partials [block][2F] in a fixed row order (launch_colsum_fold folds them).
 template <int VEC>
 __global__ __launch_bounds__(kBlock) void residual_act_bwd_kernel(
     int64_t n, int F, const float *__restrict__ dZ, int64_t lddz, const float *__restrict__ Z,
@@ -281,9 +262,7 @@ extern "C" int mgcn_relu_bwd_colsum(int64_t n_rows, int32_t F, const float *dZ, 
   }
   if (int rc = check_launch("relu_bwd_colsum_kernel")) return rc;
   if (db != nullptr) {
-    hipLaunchKernelGGL(colsum_finish_kernel, dim3((F + 63) / 64), dim3(kBlock), 0, s,
-                       partial, nblk, F, db);
-    return check_launch("colsum_finish_kernel");
+    return launch_colsum_fold(partial, nblk, F, db, s);
   }
   return MGCN_OK;
 }
@@ -368,7 +347,5 @@ extern "C" int mgcn_residual_act_bwd(int64_t n_rows, int32_t F, const float *dZ,
   }
   if (int rc = check_launch("residual_act_bwd_kernel")) return rc;
   if (colsums == nullptr) return MGCN_OK;
-  hipLaunchKernelGGL(colsum_finish_kernel, dim3((2 * F + 63) / 64), dim3(kBlock), 0, s, partial,
-                     nblk, 2 * F, colsums);
-  return check_launch("colsum_finish_kernel");
+  return launch_colsum_fold(partial, nblk, 2 * F, colsums, s);
 }

@@ -441,31 +441,6 @@ __global__ __launch_bounds__(256) void gemm_tn_small_kernel(
   }
 }
 
-// C[e] (+)= sum over splits of partial[split][e], in split order within each of
-// 4 interleaved groups, the groups then folded in order: deterministic.
-__global__ __launch_bounds__(256) void gemm_reduce_kernel(const float *__restrict__ partial,
-                                                          int splits, int64_t MN, int N,
-                                                          float *__restrict__ C, int64_t ldc,
-                                                          int accumulate) {
-  __shared__ float red[4][64];
-  const int g = threadIdx.x >> 6;  // split group
-  const int64_t e = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
-  float s = 0.0f;
-  if (e < MN) {
-#pragma unroll 8
-    for (int sp = g; sp < splits; sp += 4) s = __fadd_rn(s, partial[(int64_t)sp * MN + e]);
-  }
-  red[g][threadIdx.x & 63] = s;
-  __syncthreads();
-  if (g == 0 && e < MN) {
-    float v = __fadd_rn(__fadd_rn(red[0][threadIdx.x], red[1][threadIdx.x]),
-                        __fadd_rn(red[2][threadIdx.x], red[3][threadIdx.x]));
-    const int64_t row = e / N, col = e % N;
-    float *dst = C + row * ldc + col;
-    *dst = accumulate ? __fadd_rn(*dst, v) : v;
-  }
-}
-
 bool tn_lds(int M, int N) { return M % kTile == 0 && N % kTile == 0; }
 
 // LDS-staged dW variants (mgcn_set_option "gemm_tn_variant"; measured at
@@ -559,9 +534,7 @@ extern "C" int mgcn_gemm_tn(int64_t K, int32_t M, int32_t N, const float *A, int
     if (int rc = check_launch("gemm_tn_partial_kernel")) return rc;
   }
   const int64_t MN = (int64_t)M * N;
-  hipLaunchKernelGGL(gemm_reduce_kernel, dim3((unsigned)((MN + 63) / 64)), dim3(256), 0, s,
-                     partial, used, MN, N, C, ldc, accumulate);
-  return check_launch("gemm_reduce_kernel");
+  return launch_fold(partial, used, MN, N, C, ldc, accumulate, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -586,7 +559,7 @@ extern "C" int mgcn_gemm_tn(int64_t K, int32_t M, int32_t N, const float *A, int
 //   EPI_RELU   (the previous layer's ReLU backward fused into dX):
 //              C = Z > 0 ? acc : 0, and per-workgroup column sums of C written
 //              to colsum_partial[workgroup][N] (the bias gradient, folded in
-//              workgroup order by colsum_fold_kernel -- deterministic).
+//              workgroup order by launch_colsum_fold -- deterministic).
 // Roofline: 2 M K N FLOP on 157 TF fp32 MFMA vs 4 M (K + N) bytes (+ 4 M N
 // for Z); at K = N = 128: 0.21 ms MFMA vs 0.13 ms (0.19 with Z) at 8 TB/s.
 
@@ -975,39 +948,61 @@ int launch_nn(int64_t M, int N, const float *A, int64_t lda, const float *B, int
                                   grid_out, s);
 }
 
-__global__ __launch_bounds__(256) void colsum_fold_kernel(const float *__restrict__ partial,
-                                                          int64_t nparts, int N,
-                                                          float *__restrict__ out) {
-  __shared__ float red[4][64];
-  const int g = threadIdx.x >> 6;
-  const int f = blockIdx.x * 64 + (threadIdx.x & 63);
-  float s = 0.0f;
-  if (f < N) {
-#pragma unroll 8
-    for (int64_t p = g; p < nparts; p += 4) s = __fadd_rn(s, partial[p * N + f]);
+// Deterministic fold of split partial sums: C[e] (+)= sum over sp of
+// partial[sp][e] (C[e] at row e / N, column e % N).  A 256-thread block owns
+// EB consecutive elements and T = 256 / EB interleaved split groups per
+// element; group g adds splits g, g + T, ... in order, then the T group sums
+// meet in a fixed binary tree.  EB shrinks with MN so that small folds (dW of
+// F = 32 layers, bias column sums) still spread over many lanes: the 4-group
+// form of round 1 left 12-13 us per fold of 32 x 32 or 32 values.
+__global__ __launch_bounds__(256) void fold_partials_kernel(const float *__restrict__ partial,
+                                                            int64_t splits, int64_t MN, int N,
+                                                            float *__restrict__ C, int64_t ldc,
+                                                            int accumulate, int log_eb) {
+  __shared__ float red[256];
+  const int EB = 1 << log_eb, T = 256 >> log_eb;
+  const int el = threadIdx.x & (EB - 1), g = threadIdx.x >> log_eb;
+  const int64_t e = (int64_t)blockIdx.x * EB + el;
+  float acc = 0.0f;
+  if (e < MN) {
+#pragma unroll 4
+    for (int64_t sp = g; sp < splits; sp += T) acc = __fadd_rn(acc, partial[sp * MN + e]);
   }
-  red[g][threadIdx.x & 63] = s;
+  red[threadIdx.x] = acc;
   __syncthreads();
-  if (g == 0 && f < N)
-    out[f] = __fadd_rn(__fadd_rn(red[0][threadIdx.x], red[1][threadIdx.x]),
-                       __fadd_rn(red[2][threadIdx.x], red[3][threadIdx.x]));
+  for (int h = T >> 1; h >= 1; h >>= 1) {
+    if (g < h) red[threadIdx.x] = __fadd_rn(red[threadIdx.x], red[threadIdx.x + h * EB]);
+    __syncthreads();
+  }
+  if (g == 0 && e < MN) {
+    const float v = red[el];
+    float *dst = C + (e / N) * ldc + (e % N);
+    *dst = accumulate ? __fadd_rn(*dst, v) : v;
+  }
 }
 
 }  // namespace
 
-// launchers of the split-K / column-sum folds for other translation units
-// (fused.hip's backward writes the same partial slabs)
+// launchers of the split-K / column-sum folds, also for other translation
+// units (fused.hip's backward and elementwise.hip write the same partial slabs)
+int launch_fold(const float *partial, int64_t splits, int64_t MN, int N, float *C, int64_t ldc,
+                int accumulate, hipStream_t s) {
+  if (MN <= 0) return MGCN_OK;
+  int log_eb = 0;  // EB = clamp(pow2 <= MN / 256, 1, 16)
+  while (log_eb < 4 && (MN >> (log_eb + 9)) > 0) ++log_eb;
+  const int64_t blocks = (MN + (1 << log_eb) - 1) >> log_eb;
+  hipLaunchKernelGGL(fold_partials_kernel, dim3((unsigned)blocks), dim3(256), 0, s, partial,
+                     splits, MN, N, C, ldc, accumulate, log_eb);
+  return check_launch("fold_partials_kernel");
+}
+
 int launch_split_reduce(const float *partial, int splits, int64_t MN, int N, float *C,
                         int64_t ldc, int accumulate, hipStream_t s) {
-  hipLaunchKernelGGL(gemm_reduce_kernel, dim3((unsigned)((MN + 63) / 64)), dim3(256), 0, s,
-                     partial, splits, MN, N, C, ldc, accumulate);
-  return check_launch("gemm_reduce_kernel");
+  return launch_fold(partial, splits, MN, N, C, ldc, accumulate, s);
 }
 
 int launch_colsum_fold(const float *partial, int64_t nparts, int N, float *out, hipStream_t s) {
-  hipLaunchKernelGGL(colsum_fold_kernel, dim3((N + 63) / 64), dim3(256), 0, s, partial, nparts, N,
-                     out);
-  return check_launch("colsum_fold_kernel");
+  return launch_fold(partial, nparts, N, N, out, N, 0, s);
 }
 
 int gemm_precision_is_x6() { return g_gemm_precision == PREC_BF16X6; }
@@ -1065,9 +1060,7 @@ extern "C" int mgcn_gemm_nn(int64_t M, int32_t K, int32_t N, const float *A, int
   else
     rc = launch_nn<128>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, relu_mask, row_div, partial, &grid, s);
   if (rc || epi == EPI_STORE) return rc;
-  hipLaunchKernelGGL(colsum_fold_kernel, dim3((N + 63) / 64), dim3(256), 0, s, partial,
-                     (int64_t)grid, N, colsum);
-  return check_launch("colsum_fold_kernel");
+  return launch_colsum_fold(partial, grid, N, colsum, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -1426,11 +1419,7 @@ extern "C" int mgcn_gemm_bwd(int64_t M, int32_t F_in, int32_t F_out, const float
                                      row_div, dwp, csp, s);
   if (rc) return rc;
   const int64_t MN = (int64_t)F_in * F_out;
-  hipLaunchKernelGGL(gemm_reduce_kernel, dim3((unsigned)((MN + 63) / 64)), dim3(256), 0, s, dwp,
-                     grid, MN, F_out, dW, lddw, accumulate);
-  if (int rc2 = check_launch("gemm_reduce_kernel")) return rc2;
+  if (int rc2 = launch_fold(dwp, grid, MN, F_out, dW, lddw, accumulate, s)) return rc2;
   if (epi == EPI_STORE) return MGCN_OK;
-  hipLaunchKernelGGL(colsum_fold_kernel, dim3((F_in + 63) / 64), dim3(256), 0, s, csp,
-                     (int64_t)grid, F_in, colsum);
-  return check_launch("colsum_fold_kernel");
+  return launch_colsum_fold(csp, grid, F_in, colsum, s);
 }

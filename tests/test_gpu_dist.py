@@ -85,3 +85,28 @@ def test_sharded_gpu_matches_one_rank(cuda, aggr):
         np.testing.assert_array_equal(r["dX"], single["dX"][lo:hi])
         for g, g1 in zip(r["grads"], single["grads"]):  # re-associated partial sums
             np.testing.assert_allclose(g, g1, rtol=1e-5, atol=1e-5 * np.abs(g1).max())
+
+
+def test_bench_two_ranks_end_to_end(cuda):
+    """bench.py's N > 1 path as the driver launches it (torch.distributed.run,
+    one process per rank), at a reduced size, with gloo and both ranks on
+    cuda:0: the replica measurement (`value`, weak) and the dst-range sharded
+    one (`sharded`, strong) both run and rank 0 prints one JSON line."""
+    import json
+    import subprocess
+    root = os.path.dirname(HERE)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--nodes", "20000", "--pairs", "100000", "--dist-backend", "gloo", "--one-device",
+           "--no-cpu-baseline"]
+    out = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 2 and r["scaling"] == "weak" and r["value"] > 0
+    assert r["config"]["parallelism"] == "dp2" and r["config"]["global_batch"] == 2
+    assert r["sharded"]["scaling"] == "strong" and r["sharded"]["value"] > 0
+    assert r["roofline"]["frac"] > 0

@@ -147,6 +147,9 @@ CASES = [
     (3000, 30000, 7, "sm", "add", True, 1000),
     (5000, 20000, 32, "sm", "add", False, 300),  # skewed, no heavy row: degree order only
     (5000, 20000, 16, None, "max", False, 300),
+    (4000, 40000, 256, "sm", "max", True, 0),     # two 128-feature chunks of winner records
+    (2000, 80000, 128, None, "max", False, 0),    # light rows of degree 20..65: several
+                                                  # 32-edge winner windows per row
 ]
 
 
