@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define MGCN_ABI_VERSION 8
+#define MGCN_ABI_VERSION 9
 
 /* return codes */
 #define MGCN_OK 0
@@ -242,6 +242,20 @@ size_t mgcn_gemm_tn_workspace_bytes(int64_t K, int32_t M, int32_t N);
 int mgcn_gemm_tn(int64_t K, int32_t M, int32_t N, const float *A, int64_t lda,
                  const float *B, int64_t ldb, float *C, int64_t ldc, int accumulate,
                  void *workspace, size_t workspace_bytes, void *stream);
+
+/*
+ * mgcn_gemm_tn with the product's columns split over two outputs: columns
+ * [0, N1) of A^T B go to C1 [M, N1] (row stride ldc1), columns [N1, N) go
+ * TRANSPOSED to C2t [N - N1, M] (row stride ldc2t).  Workspace as
+ * mgcn_gemm_tn(K, M, N).  Replaces the two weight gradients of a GCNModel
+ * layer and its residual Linear (gcn_model.py:94-105: weight_node [F_in,
+ * F_out] and the Linear's weight [F_out, F_in]) from ONE pass over x and
+ * [dH | dS], each written in its parameter's own layout.
+ */
+int mgcn_gemm_tn_split(int64_t K, int32_t M, int32_t N, int32_t N1, const float *A, int64_t lda,
+                       const float *B, int64_t ldb, float *C1, int64_t ldc1, float *C2t,
+                       int64_t ldc2t, int accumulate, void *workspace, size_t workspace_bytes,
+                       void *stream);
 
 /* 1 if mgcn_gemm_nn handles this (K, N): K in {32, 64, 128}, 1 <= N <= 128. */
 int mgcn_gemm_nn_supported(int32_t K, int32_t N);

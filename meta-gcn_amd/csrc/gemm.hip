@@ -478,21 +478,21 @@ extern "C" size_t mgcn_gemm_tn_workspace_bytes(int64_t K, int32_t M, int32_t N) 
   return align_up((size_t)gemm_splits(K, M, N) * (size_t)M * (size_t)N * sizeof(float), 256);
 }
 
-extern "C" int mgcn_gemm_tn(int64_t K, int32_t M, int32_t N, const float *A, int64_t lda,
-                            const float *B, int64_t ldb, float *C, int64_t ldc, int accumulate,
-                            void *workspace, size_t workspace_bytes, void *stream) {
-  clear_error();
-  MGCN_REQUIRE(K >= 0 && M >= 0 && N >= 0, "mgcn_gemm_tn: negative size");
-  hipStream_t s = as_stream(stream);
+namespace {
+// C = A^T B; columns [N1, N) go transposed to C2 (N1 == N: plain C)
+int gemm_tn_impl(int64_t K, int32_t M, int32_t N, const float *A, int64_t lda, const float *B,
+                 int64_t ldb, float *C, int64_t ldc, int32_t N1, float *C2, int64_t ldc2,
+                 int accumulate, void *workspace, size_t workspace_bytes, hipStream_t s) {
   if (M == 0 || N == 0) return MGCN_OK;
-  MGCN_REQUIRE(C != nullptr && ldc >= N, "mgcn_gemm_tn: bad C");
   if (K == 0) {
-    if (!accumulate)
-      for (int32_t r = 0; r < M; ++r)
-        MGCN_HIP_TRY(hipMemsetAsync(C + r * ldc, 0, sizeof(float) * N, s));
+    if (!accumulate) {
+      for (int32_t r = 0; r < M && N1 > 0; ++r)
+        MGCN_HIP_TRY(hipMemsetAsync(C + r * ldc, 0, sizeof(float) * N1, s));
+      for (int32_t r = 0; r < N - N1; ++r)
+        MGCN_HIP_TRY(hipMemsetAsync(C2 + r * ldc2, 0, sizeof(float) * M, s));
+    }
     return MGCN_OK;
   }
-  MGCN_REQUIRE(A && B && lda >= M && ldb >= N, "mgcn_gemm_tn: bad A/B");
   const int tiles_m = (M + kTile - 1) / kTile, tiles_n = (N + kTile - 1) / kTile;
   const int splits = gemm_splits(K, M, N);
   const size_t need = mgcn_gemm_tn_workspace_bytes(K, M, N);
@@ -534,7 +534,35 @@ extern "C" int mgcn_gemm_tn(int64_t K, int32_t M, int32_t N, const float *A, int
     if (int rc = check_launch("gemm_tn_partial_kernel")) return rc;
   }
   const int64_t MN = (int64_t)M * N;
-  return launch_fold(partial, used, MN, N, C, ldc, accumulate, s);
+  return launch_fold_split(partial, used, MN, N, C, ldc, N1, C2, ldc2, accumulate, s);
+}
+}  // namespace
+
+extern "C" int mgcn_gemm_tn(int64_t K, int32_t M, int32_t N, const float *A, int64_t lda,
+                            const float *B, int64_t ldb, float *C, int64_t ldc, int accumulate,
+                            void *workspace, size_t workspace_bytes, void *stream) {
+  clear_error();
+  MGCN_REQUIRE(K >= 0 && M >= 0 && N >= 0, "mgcn_gemm_tn: negative size");
+  if (M == 0 || N == 0) return MGCN_OK;
+  MGCN_REQUIRE(C != nullptr && ldc >= N, "mgcn_gemm_tn: bad C");
+  MGCN_REQUIRE(K == 0 || (A && B && lda >= M && ldb >= N), "mgcn_gemm_tn: bad A/B");
+  return gemm_tn_impl(K, M, N, A, lda, B, ldb, C, ldc, N, nullptr, 0, accumulate, workspace,
+                      workspace_bytes, as_stream(stream));
+}
+
+extern "C" int mgcn_gemm_tn_split(int64_t K, int32_t M, int32_t N, int32_t N1, const float *A,
+                                  int64_t lda, const float *B, int64_t ldb, float *C1,
+                                  int64_t ldc1, float *C2t, int64_t ldc2t, int accumulate,
+                                  void *workspace, size_t workspace_bytes, void *stream) {
+  clear_error();
+  MGCN_REQUIRE(K >= 0 && M >= 0 && N >= 0 && 0 <= N1 && N1 <= N,
+               "mgcn_gemm_tn_split: need K, M, N >= 0 and 0 <= N1 <= N");
+  if (M == 0 || N == 0) return MGCN_OK;
+  MGCN_REQUIRE(N1 == 0 || (C1 != nullptr && ldc1 >= N1), "mgcn_gemm_tn_split: bad C1");
+  MGCN_REQUIRE(N1 == N || (C2t != nullptr && ldc2t >= M), "mgcn_gemm_tn_split: bad C2t");
+  MGCN_REQUIRE(K == 0 || (A && B && lda >= M && ldb >= N), "mgcn_gemm_tn_split: bad A/B");
+  return gemm_tn_impl(K, M, N, A, lda, B, ldb, C1, ldc1, N1, C2t, ldc2t, accumulate, workspace,
+                      workspace_bytes, as_stream(stream));
 }
 
 // ---------------------------------------------------------------------------
@@ -958,7 +986,9 @@ int launch_nn(int64_t M, int N, const float *A, int64_t lda, const float *B, int
 __global__ __launch_bounds__(256) void fold_partials_kernel(const float *__restrict__ partial,
                                                             int64_t splits, int64_t MN, int N,
                                                             float *__restrict__ C, int64_t ldc,
-                                                            int accumulate, int log_eb) {
+                                                            int accumulate, int log_eb, int N1,
+                                                            float *__restrict__ C2,
+                                                            int64_t ldc2) {
   __shared__ float red[256];
   const int EB = 1 << log_eb, T = 256 >> log_eb;
   const int el = threadIdx.x & (EB - 1), g = threadIdx.x >> log_eb;
@@ -976,7 +1006,8 @@ __global__ __launch_bounds__(256) void fold_partials_kernel(const float *__restr
   }
   if (g == 0 && e < MN) {
     const float v = red[el];
-    float *dst = C + (e / N) * ldc + (e % N);
+    const int64_t row = e / N, col = e % N;
+    float *dst = col < N1 ? C + row * ldc + col : C2 + (col - N1) * ldc2 + row;
     *dst = accumulate ? __fadd_rn(*dst, v) : v;
   }
 }
@@ -987,12 +1018,18 @@ __global__ __launch_bounds__(256) void fold_partials_kernel(const float *__restr
 // units (fused.hip's backward and elementwise.hip write the same partial slabs)
 int launch_fold(const float *partial, int64_t splits, int64_t MN, int N, float *C, int64_t ldc,
                 int accumulate, hipStream_t s) {
+  return launch_fold_split(partial, splits, MN, N, C, ldc, N, nullptr, 0, accumulate, s);
+}
+
+// columns [N1, N) of the folded [MN / N, N] result go transposed to C2
+int launch_fold_split(const float *partial, int64_t splits, int64_t MN, int N, float *C,
+                      int64_t ldc, int N1, float *C2, int64_t ldc2, int accumulate, hipStream_t s) {
   if (MN <= 0) return MGCN_OK;
   int log_eb = 0;  // EB = clamp(pow2 <= MN / 256, 1, 16)
   while (log_eb < 4 && (MN >> (log_eb + 9)) > 0) ++log_eb;
   const int64_t blocks = (MN + (1 << log_eb) - 1) >> log_eb;
   hipLaunchKernelGGL(fold_partials_kernel, dim3((unsigned)blocks), dim3(256), 0, s, partial,
-                     splits, MN, N, C, ldc, accumulate, log_eb);
+                     splits, MN, N, C, ldc, accumulate, log_eb, N1, C2, ldc2);
   return check_launch("fold_partials_kernel");
 }
 

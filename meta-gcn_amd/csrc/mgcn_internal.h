@@ -65,6 +65,8 @@ int xw_set_unroll(int value);  // fused.hip
 // deterministic fold of split partials: C[e] (+)= sum_sp partial[sp * MN + e]
 int launch_fold(const float *partial, int64_t splits, int64_t MN, int N, float *C, int64_t ldc,
                 int accumulate, hipStream_t s);
+int launch_fold_split(const float *partial, int64_t splits, int64_t MN, int N, float *C,
+                      int64_t ldc, int N1, float *C2, int64_t ldc2, int accumulate, hipStream_t s);
 int launch_split_reduce(const float *partial, int splits, int64_t MN, int N, float *C,
                         int64_t ldc, int accumulate, hipStream_t s);
 int launch_colsum_fold(const float *partial, int64_t nparts, int N, float *out, hipStream_t s);

@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmgcn.so")
 
 # constants mirrored from include/mgcn.h
-ABI_VERSION = 8
+ABI_VERSION = 9
 OK, EINVAL, EINDEX, EHIP, EWORKSPACE = 0, 1, 2, 3, 4
 REDUCE_SUM, REDUCE_MEAN, REDUCE_MAX = 0, 1, 2
 NORM_NONE, NORM_SM, NORM_RW = 0, 1, 2
@@ -54,6 +54,8 @@ SIGNATURES = {
     "mgcn_gemm_tn_workspace_bytes": (_sz, [_i64, _i32, _i32]),
     "mgcn_gemm_tn": (_int, [_i64, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _int, _vp, _sz,
                             _vp]),
+    "mgcn_gemm_tn_split": (_int, [_i64, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _vp,
+                                  _i64, _int, _vp, _sz, _vp]),
     "mgcn_gemm_nn_supported": (_int, [_i32, _i32]),
     "mgcn_gemm_nn_workspace_bytes": (_sz, [_i64, _i32]),
     "mgcn_gemm_nn": (_int, [_i64, _i32, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _i64, _vp,
@@ -154,8 +156,33 @@ def require_device(*tensors: torch.Tensor | None) -> torch.device:
 
 
 def stream_of(device: torch.device):
-    """The caller's current HIP stream on `device` (kernels launch there)."""
-    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+    """The caller's current HIP stream on `device` (kernels launch there).
+    The raw handle straight from the C++ stream registry: a torch Stream
+    object per launch costs more host time than the launch (config 3 issues
+    ~200 launches a step and is bound by host issue)."""
+    return ctypes.c_void_p(torch._C._cuda_getCurrentRawStream(device.index))
+
+
+class _NoGuard:
+    __slots__ = ()
+
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *exc):
+        return False
+
+
+_NO_GUARD = _NoGuard()
+
+
+def device_guard(device: torch.device):
+    """torch.cuda.device(device) when it differs from the current device,
+    else a no-op context (the common case; the full guard costs two device
+    switches of host time per launch)."""
+    if device.index is None or device.index == torch._C._cuda_getDevice():
+        return _NO_GUARD
+    return torch.cuda.device(device)
 
 
 def set_option(name: str, value: int) -> None:

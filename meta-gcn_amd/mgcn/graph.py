@@ -82,7 +82,7 @@ def schedule_rows(view: CSRView, thr: int = HEAVY_THRESHOLD) -> CSRView:
                      device=dev)
     n_heavy = ctypes.c_int64(0)
     n_giant = ctypes.c_int64(0)
-    with torch.cuda.device(dev):
+    with L.device_guard(dev):
         rc = lib.mgcn_row_schedule(view.n_rows, L.ptr(view.rowptr), int(thr), L.ptr(order),
                                    ctypes.byref(n_heavy), ctypes.byref(n_giant), L.ptr(ws),
                                    ws.numel(), L.stream_of(dev))
@@ -135,7 +135,7 @@ class GraphPlan:
             out = torch.empty(max(self.nnz, 1), dtype=torch.int32, device=dev)
             ws = torch.empty(int(lib.mgcn_slot_map_workspace_bytes(self.nnz)), dtype=torch.uint8,
                              device=dev)
-            with torch.cuda.device(dev):
+            with L.device_guard(dev):
                 rc = lib.mgcn_slot_map(self.nnz, L.ptr(self.fwd.eid), L.ptr(self.bwd.eid),
                                        L.ptr(out), L.ptr(ws), ws.numel(), L.stream_of(dev))
             L.check(rc, "mgcn_slot_map")
@@ -223,7 +223,7 @@ def build_view(key: torch.Tensor, other: torch.Tensor, n_key: int, n_other: int)
     eid = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)[:nnz]
     ws_bytes = int(lib.mgcn_csr_workspace_bytes(nnz, n_key))
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
-    with torch.cuda.device(dev):
+    with L.device_guard(dev):
         rc = lib.mgcn_csr_build(L.ptr(key), L.ptr(other), nnz, n_key, n_other, L.ptr(rowptr),
                                 L.ptr(col), L.ptr(eid), L.ptr(ws), ws_bytes, L.stream_of(dev))
     L.check(rc, "mgcn_csr_build")
@@ -256,7 +256,7 @@ def _build_norm(g: GraphPlan, code: int, deg, edge_weight) -> NormPlan:
         deg_in = _f32(deg, n, "deg", dev)
         dg = torch.empty(n, dtype=torch.float32, device=dev)
         dinv = torch.empty(n, dtype=torch.float32, device=dev)
-        with torch.cuda.device(dev):
+        with L.device_guard(dev):
             rc = lib.mgcn_degree_norm(n, L.ptr(g.bwd.rowptr), L.ptr(g.bwd.eid), L.ptr(deg_in),
                                       L.ptr(ew), code, L.ptr(dg), L.ptr(dinv), L.stream_of(dev))
         L.check(rc, "mgcn_degree_norm")
@@ -274,7 +274,7 @@ def _edge_norm(view: CSRView, rows_are_dst: bool, dinv, ew, code) -> torch.Tenso
     lib = L.load()
     dev = view.rowptr.device
     w = torch.empty(max(view.nnz, 1), dtype=torch.float32, device=dev)[:view.nnz]
-    with torch.cuda.device(dev):
+    with L.device_guard(dev):
         rc = lib.mgcn_edge_norm(view.n_rows, view.nnz, L.ptr(view.rowptr), L.ptr(view.col),
                                 L.ptr(view.eid), int(rows_are_dst), L.ptr(dinv), L.ptr(ew), code,
                                 L.ptr(w), L.stream_of(dev))

@@ -85,7 +85,7 @@ def spmm_fwd(view: CSRView, w: torch.Tensor | None, H: torch.Tensor, reduce: int
             raise ValueError(f"bias has {bias.numel()} entries, expected {F}")
     if _TIMER is not None:
         _TIMER("spmm_fwd", True)
-    with torch.cuda.device(dev):
+    with L.device_guard(dev):
         rc = lib.mgcn_spmm_fwd(view.n_rows, F, L.ptr(view.rowptr), L.ptr(view.col),
                                L.ptr(view.eid), L.ptr(w), L.ptr(H), H.stride(0), L.ptr(Y),
                                Y.stride(0), reduce, L.ptr(bias), int(bool(relu)), L.ptr(argmax),
@@ -130,7 +130,7 @@ def spmm_xw_fwd(view: CSRView, w: torch.Tensor | None, X: torch.Tensor, W: torch
     Y = torch.empty(view.n_rows, F_out, dtype=torch.float32, device=dev)
     if _TIMER is not None:
         _TIMER("spmm_xw_fwd", True)
-    with torch.cuda.device(dev):
+    with L.device_guard(dev):
         rc = lib.mgcn_spmm_xw_fwd(view.n_rows, view.n_cols, F_in, F_out, L.ptr(view.rowptr),
                                   L.ptr(view.col), L.ptr(w), L.ptr(X), X.stride(0), L.ptr(W),
                                   W.stride(0), L.ptr(bias), L.ptr(Y), Y.stride(0), reduce,
@@ -180,7 +180,7 @@ def spmm_xw_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tens
     tname = "spmm_xw_bwd" if want_dx else "spmm_xw_bwd_dw"
     if _TIMER is not None:
         _TIMER(tname, True)
-    with torch.cuda.device(dev):
+    with L.device_guard(dev):
         rc = lib.mgcn_spmm_xw_bwd(M, view_t.n_cols, F_in, F_out, L.ptr(view_t.rowptr),
                                   L.ptr(view_t.col), L.ptr(w_t), L.ptr(row_scale), L.ptr(dY),
                                   dY.stride(0), L.ptr(X), X.stride(0), L.ptr(W), W.stride(0),
@@ -208,7 +208,7 @@ def spmm_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tensor 
                                                  device=dev)
     if _TIMER is not None:
         _TIMER("spmm_bwd", True)
-    with torch.cuda.device(dev):
+    with L.device_guard(dev):
         rc = lib.mgcn_spmm_bwd(view_t.n_rows, F, L.ptr(view_t.rowptr), L.ptr(view_t.col),
                                L.ptr(view_t.eid), L.ptr(w_t), L.ptr(row_scale), L.ptr(dY),
                                dY.stride(0), L.ptr(dH), dH.stride(0), reduce, L.ptr(cnt),
@@ -238,7 +238,7 @@ def relu_bwd_colsum(dZ: torch.Tensor, Z: torch.Tensor | None, relu: bool, want_d
         return dY, None
     ws_bytes = int(lib.mgcn_colsum_workspace_bytes(n, F)) if want_db else 0
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev) if want_db else None
-    with torch.cuda.device(dev):
+    with L.device_guard(dev):
         rc = lib.mgcn_relu_bwd_colsum(n, F, L.ptr(dZ), L.ptr(Z.contiguous() if relu else None),
                                       int(bool(relu)), L.ptr(row_div), L.ptr(dY if write else None),
                                       L.ptr(db),
@@ -263,7 +263,7 @@ def gemm_tn(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor | None = None,
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
     if _TIMER is not None:
         _TIMER("gemm_tn", True)
-    with torch.cuda.device(dev):
+    with L.device_guard(dev):
         rc = lib.mgcn_gemm_tn(K, M, N, L.ptr(A), A.stride(0), L.ptr(B), B.stride(0), L.ptr(C),
                               C.stride(0), int(bool(accumulate)), L.ptr(ws), ws_bytes,
                               L.stream_of(dev))
@@ -271,6 +271,35 @@ def gemm_tn(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor | None = None,
         _TIMER("gemm_tn", False)
     L.check(rc, "mgcn_gemm_tn")
     return C
+
+
+def gemm_tn_split(A: torch.Tensor, B: torch.Tensor, n1: int):
+    """(C1, C2t) with A^T B = [C1 | C2t^T]: columns [0, n1) as C1 [M, n1],
+    the rest transposed as C2t [N - n1, M], both contiguous, from one
+    ``mgcn_gemm_tn_split`` pass (two parameter gradients in their own
+    layouts, no copies)."""
+    lib = L.load()
+    A = _contig_f32(A, "A")
+    B = _contig_f32(B, "B")
+    dev = L.require_device(A, B)
+    K, M = A.shape
+    N = B.size(1)
+    if B.size(0) != K or not 0 <= n1 <= N:
+        raise ValueError(f"gemm_tn_split: A {tuple(A.shape)}, B {tuple(B.shape)}, n1 {n1}")
+    C1 = torch.empty(M, n1, dtype=torch.float32, device=dev)
+    C2 = torch.empty(N - n1, M, dtype=torch.float32, device=dev)
+    ws_bytes = int(lib.mgcn_gemm_tn_workspace_bytes(K, M, N))
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    if _TIMER is not None:
+        _TIMER("gemm_tn", True)
+    with L.device_guard(dev):
+        rc = lib.mgcn_gemm_tn_split(K, M, N, n1, L.ptr(A), A.stride(0), L.ptr(B), B.stride(0),
+                                    L.ptr(C1), max(n1, 1), L.ptr(C2), max(M, 1), 0, L.ptr(ws),
+                                    ws_bytes, L.stream_of(dev))
+    if _TIMER is not None:
+        _TIMER("gemm_tn", False)
+    L.check(rc, "mgcn_gemm_tn_split")
+    return C1, C2
 
 
 def gemm_nn_supported(K: int, N: int) -> bool:
@@ -285,7 +314,7 @@ def make_relu_mask(Z: torch.Tensor) -> torch.Tensor:
     dev = L.require_device(Z)
     n, F = Z.shape
     m = torch.empty(n, 4, dtype=torch.int32, device=dev)
-    with torch.cuda.device(dev):
+    with L.device_guard(dev):
         rc = lib.mgcn_relu_mask(n, F, L.ptr(Z), Z.stride(0), L.ptr(m), L.stream_of(dev))
     L.check(rc, "mgcn_relu_mask")
     return m
@@ -328,7 +357,7 @@ def gemm_nn(A: torch.Tensor, W: torch.Tensor, transpose_w: bool = False,
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
     if _TIMER is not None:
         _TIMER("gemm_nn", True)
-    with torch.cuda.device(dev):
+    with L.device_guard(dev):
         rc = lib.mgcn_gemm_nn(M, K, N, L.ptr(A), A.stride(0), L.ptr(W), sbk, sbn, L.ptr(C),
                               C.stride(0), L.ptr(relu_mask),
                               L.ptr(row_div), L.ptr(colsum), L.ptr(ws), ws_bytes,
@@ -378,7 +407,7 @@ def gemm_bwd(x: torch.Tensor, dH: torch.Tensor, W: torch.Tensor, want_dx: bool =
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
     if _TIMER is not None:
         _TIMER("gemm_bwd" if want_dx else "gemm_bwd_dw", True)
-    with torch.cuda.device(dev):
+    with L.device_guard(dev):
         rc = lib.mgcn_gemm_bwd(M, F_in, F_out, L.ptr(x), x.stride(0), L.ptr(dH), dH.stride(0),
                                L.ptr(W), W.stride(0), L.ptr(dW), dW.stride(0),
                                int(bool(accumulate)), L.ptr(dX),
@@ -484,7 +513,7 @@ def max_mask(plan: GraphPlan, argmax: torch.Tensor) -> torch.Tensor:
     W = (F + 31) // 32
     dev = argmax.device
     mask = torch.empty(max(plan.nnz, 1), W, dtype=torch.int32, device=dev)
-    with torch.cuda.device(dev):
+    with L.device_guard(dev):
         rc = lib.mgcn_max_mask(plan.fwd.n_rows, F, L.ptr(plan.fwd.rowptr), L.ptr(plan.fwd.eid),
                                L.ptr(argmax), L.ptr(mask), L.stream_of(dev))
     L.check(rc, "mgcn_max_mask")
@@ -719,7 +748,7 @@ def residual_act(Z1: torch.Tensor, R: torch.Tensor, rbias: torch.Tensor | None,
     n, F = Z1.shape
     Z = torch.empty(n, F, dtype=torch.float32, device=dev)
     rb = rbias.detach().contiguous() if rbias is not None else None
-    with torch.cuda.device(dev):
+    with L.device_guard(dev):
         rc = lib.mgcn_residual_act(n, F, L.ptr(Z1), Z1.stride(0), L.ptr(R), R.stride(0), L.ptr(rb),
                                    int(bool(relu)), L.ptr(Z), Z.stride(0), L.stream_of(dev))
     L.check(rc, "mgcn_residual_act")
@@ -735,7 +764,7 @@ def residual_act_bwd(dZ, Z, relu, Z1, relu1, dA, dS, row_div=None, want_sums=Tru
     sums = torch.empty(2 * F, dtype=torch.float32, device=dev) if want_sums else None
     ws_bytes = int(lib.mgcn_residual_act_bwd_workspace_bytes(n, F)) if want_sums else 0
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev) if want_sums else None
-    with torch.cuda.device(dev):
+    with L.device_guard(dev):
         rc = lib.mgcn_residual_act_bwd(
             n, F, L.ptr(dZ), dZ.stride(0), L.ptr(Z), Z.stride(0) if Z is not None else F,
             int(bool(relu)), L.ptr(Z1), Z1.stride(0) if Z1 is not None else F, int(bool(relu1)),
@@ -789,11 +818,11 @@ class _ResidualGCNLayer(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dx = _mm_t(DH, Wc)
-        dWc = gemm_tn(x, DH)
+        # [dW | dWr^T] = x^T [dH | dS] in one pass, dWr written transposed
+        dW, dWr = gemm_tn_split(x, DH, F_out)
         db = sums[:F_out] if ctx.has_b else None
         dbr = sums[F_out:] if ctx.has_br else None
-        return (dx, None, None, None, None, None, dWc[:, :F_out], db,
-                dWc[:, F_out:].t().contiguous(), dbr)
+        return (dx, None, None, None, None, None, dW, db, dWr, dbr)
 
 
 def residual_gcn_layer(x, plan: GraphPlan, norm: NormPlan, aggr: str, relu1: bool, relu2: bool,
@@ -868,7 +897,7 @@ class _SegmentMean(torch.autograd.Function):
         dev = L.require_device(x, ptr)
         G = ptr.numel() - 1
         out = torch.empty(G, x.size(1), dtype=torch.float32, device=dev)
-        with torch.cuda.device(dev):
+        with L.device_guard(dev):
             rc = lib.mgcn_segment_mean(G, x.size(1), L.ptr(ptr), L.ptr(x), x.stride(0), L.ptr(out),
                                        out.stride(0), L.stream_of(dev))
         L.check(rc, "mgcn_segment_mean")

@@ -23,7 +23,13 @@ import torch  # noqa: E402
 from bench import batch_graphs, make_botnet_graph, make_er_graph, make_inputs  # noqa: E402
 
 
+HOST = {}
+
+
 def timed(step, steps, warmup):
+    """Seconds per step; HOST['ms'] = host time to issue one step (the time the
+    Python loop takes before the final sync): when it is close to the step
+    time, the workload is bound by launch issue, not by the GPU."""
     step()
     torch.cuda.synchronize()
     for _ in range(warmup):
@@ -32,8 +38,11 @@ def timed(step, steps, warmup):
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
+    t_issue = time.perf_counter() - t0
     torch.cuda.synchronize()
-    return (time.perf_counter() - t0) / steps
+    t = (time.perf_counter() - t0) / steps
+    HOST["ms"] = t_issue / steps * 1e3
+    return t
 
 
 def config3(args, dev):
@@ -63,7 +72,7 @@ def config3(args, dev):
     return {"workload": "config3 botnet-shaped 2x143,107 nodes, 12-layer GCNModel F=32 rh=1, "
                         "CE + Adam", "nodes": N, "edges": n_edges, "max_in_degree":
             int(torch.bincount(ei[1], minlength=N).max()), "ms_per_step": t * 1e3,
-            "edges_per_s": n_edges * 12 / t}
+            "edges_per_s": n_edges * 12 / t, "host_issue_ms_per_step": HOST["ms"]}
 
 
 def config4(args, dev):

@@ -269,6 +269,24 @@ def test_gemm_tn_matches_fp64(cuda, K, M, N, gemm_precision):
     assert torch.equal(C, C2)  # deterministic
 
 
+@pytest.mark.parametrize("K,M,N,n1", [(286_214, 32, 64, 32), (4097, 128, 256, 128),
+                                      (3000, 7, 130, 5), (1001, 17, 5, 0), (1001, 17, 5, 5),
+                                      (0, 4, 6, 2)])
+def test_gemm_tn_split_equals_gemm_tn(cuda, K, M, N, n1):
+    """mgcn_gemm_tn_split (the residual layer's [dW | dWr^T] in one pass):
+    the same products and fold as mgcn_gemm_tn, columns [n1, N) written
+    transposed -- bitwise equal to slicing the plain product."""
+    from mgcn.ops import gemm_tn, gemm_tn_split
+    g = torch.Generator(device=cuda).manual_seed(K + N)
+    A = torch.randn(K, M, device=cuda, generator=g)
+    B = torch.randn(K, N, device=cuda, generator=g)
+    C = gemm_tn(A, B)
+    C1, C2t = gemm_tn_split(A, B, n1)
+    assert C1.shape == (M, n1) and C2t.shape == (N - n1, M)
+    assert C1.is_contiguous() and C2t.is_contiguous()
+    assert torch.equal(C1, C[:, :n1]) and torch.equal(C2t, C[:, n1:].t())
+
+
 def test_gemm_bf16x6_error_at_fp32_level(cuda):
     """The bf16x6 products are no less accurate than exact-f32 MFMA: max
     error / (|A| |B|) against fp64 within 2x of the f32 form's (measured:
