@@ -346,14 +346,19 @@ size_t mgcn_spmm_xw_bwd_workspace_bytes(int64_t n_rows);
  * the two matmul adjoints, plus the ReLU / bias gradient of the layer below,
  * gcn_model.py:196).  dY rows [n_cols, 128] (lddy, 16-byte aligned, under
  * 4 GiB), X [n_rows, 128] (ldx, 16-byte aligned), W [128, 128] row-major.
+ * Max (win_mask + slot_map, both or neither): the adjoint of
+ * mgcn_spmm_fwd(MAX) -- each edge's dY row counts only at the features whose
+ * winner it was (its bits in win_mask at its fwd slot slot_map[k], as
+ * mgcn_spmm_bwd(MAX, win_mask, slot_map)); dH bit for bit that function's.
  */
 int mgcn_spmm_xw_bwd(int64_t n_rows, int64_t n_cols, int32_t F_in, int32_t F_out,
                      const int64_t *rowptr_t, const int32_t *col_t, const float *w_t,
                      const float *row_scale, const float *dY, int64_t lddy, const float *X,
                      int64_t ldx, const float *W, int64_t ldw, float *dW, int64_t lddw,
                      int accumulate, float *dX, int64_t lddx, const uint32_t *relu_mask,
-                     const float *row_div, float *colsum, void *workspace,
-                     size_t workspace_bytes, void *stream);
+                     const float *row_div, float *colsum, const uint32_t *win_mask,
+                     const int32_t *slot_map, void *workspace, size_t workspace_bytes,
+                     void *stream);
 
 /* ----------------------------------------------------------- elementwise */
 

@@ -80,12 +80,18 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 // Lane gl holds features 4 gl .. 4 gl + 3; edge metadata is loaded 32 edges
 // at a time lane-parallel and broadcast by ds_bpermute; U gathers of whole
 // 512-B rows are in flight per group before any is folded.
-template <int U>
+// MAXM (the max adjoint): each edge's dY row counts only at the features
+// whose forward winner it was -- the edge's winner word (found through
+// slot_map, the fwd slot of each bwd slot; word gl / 8 of its 16-B record,
+// bits 4 (gl % 8) + j) is loaded beside the row and selects in the fold.
+template <int U, bool MAXM = false>
 __device__ __forceinline__ void gather_row(const __amdgpu_buffer_rsrc_t rx, uint32_t ldx_b,
                                            const int64_t *__restrict__ rowptr,
                                            const int32_t *__restrict__ col,
                                            const float *__restrict__ w, int64_t row, bool row_ok,
-                                           int gl, int grp, float (&acc)[4], int &deg_out) {
+                                           int gl, int grp, float (&acc)[4], int &deg_out,
+                                           const uint32_t *__restrict__ win = nullptr,
+                                           const int32_t *__restrict__ slot_map = nullptr) {
   const bool has_w = w != nullptr;
   const int64_t beg = row_ok ? rowptr[row] : 0;
   // a row's degree fits 32 bits; the edge slots are addressed from beg
@@ -97,11 +103,12 @@ __device__ __forceinline__ void gather_row(const __amdgpu_buffer_rsrc_t rx, uint
   acc[0] = acc[1] = acc[2] = acc[3] = 0.0f;
   for (int e0 = 0; e0 < maxdeg; e0 += 32) {
     const int my = e0 + gl;
-    int mc = 0;
+    int mc = 0, ms = 0;
     float mw = 1.0f;
     if (my < deg) {
       mc = colr[my];
       if (has_w) mw = wr[my];
+      if constexpr (MAXM) ms = slot_map[beg + my];
     }
     const int rem = deg - e0;
     const int nb = rem <= 0 ? 0 : (rem < 32 ? rem : 32);
@@ -111,6 +118,7 @@ __device__ __forceinline__ void gather_row(const __amdgpu_buffer_rsrc_t rx, uint
       float4 xv[U];
       float wk[U];
       bool ok[U];
+      uint32_t wbits[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int k = k0 + u;
@@ -120,11 +128,23 @@ __device__ __forceinline__ void gather_row(const __amdgpu_buffer_rsrc_t rx, uint
         // past-the-row edges get an offset beyond the buffer: no access, zeros
         const uint32_t off = ok[u] ? (uint32_t)ck * ldx_b + 16u * gl : 0xfffffff0u;
         xv[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0));
+        if constexpr (MAXM) {
+          // loaded unconditionally (masked edges read word 0, never used)
+          const int sk = __shfl(ms, 32 * grp + (k & 31), 64);
+          wbits[u] = win[ok[u] ? (int64_t)sk * 4 + (gl >> 3) : 0];
+        }
       }
       // fold in strictly ascending edge order (as the SpMM, bit for bit)
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (ok[u]) {
+          if constexpr (MAXM) {
+            const uint32_t bits = wbits[u] >> (4 * (gl & 7));
+            xv[u].x = (bits & 1u) ? xv[u].x : 0.0f;
+            xv[u].y = (bits & 2u) ? xv[u].y : 0.0f;
+            xv[u].z = (bits & 4u) ? xv[u].z : 0.0f;
+            xv[u].w = (bits & 8u) ? xv[u].w : 0.0f;
+          }
           acc[0] = __fadd_rn(acc[0], __fmul_rn(xv[u].x, wk[u]));
           acc[1] = __fadd_rn(acc[1], __fmul_rn(xv[u].y, wk[u]));
           acc[2] = __fadd_rn(acc[2], __fmul_rn(xv[u].z, wk[u]));
@@ -433,6 +453,8 @@ struct XbArgs {
   const float *row_div;
   float *dw_partial;      // [grid][128][128]
   float *colsum_partial;  // [grid][128]
+  const uint32_t *win_mask;  // max adjoint: winner bits per fwd slot ([nnz][4])
+  const int32_t *slot_map;   // max adjoint: fwd slot of every bwd slot
 };
 
 #ifdef MGCN_XW_PROFILE
@@ -446,7 +468,7 @@ __device__ unsigned long long g_xprof[2][64][6];
 #define XPROF(it, k)
 #endif
 
-template <int U, bool DX, int EPI>
+template <int U, bool DX, int EPI, bool MAXM>
 __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(const XbArgs a) {
   __shared__ __attribute__((aligned(16))) char lds[kXbLds];
   const int tid = threadIdx.x;
@@ -568,7 +590,8 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
       const bool row_ok = row < a.n_rows;
       int deg;
       float acc[4];
-      gather_row<U>(rdy, ldy_b, a.rowptr, a.col, a.w, row, row_ok, gl, grp, acc, deg);
+      gather_row<U, MAXM>(rdy, ldy_b, a.rowptr, a.col, a.w, row, row_ok, gl, grp, acc, deg,
+                          a.win_mask, a.slot_map);
       if (a.row_scale != nullptr && row_ok) {
         const float sc = a.row_scale[row];
 #pragma unroll
@@ -695,19 +718,25 @@ int launch_xw(const XwArgs &a, hipStream_t s) {
   return check_launch("spmm_xw_fwd_kernel");
 }
 
-template <int U, bool DX, int EPI>
+template <int U, bool DX, int EPI, bool MAXM>
 int launch_xb(const XbArgs &a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((spmm_xw_bwd_kernel<U, DX, EPI>), dim3((unsigned)grid), dim3(kXwThreads), 0, s,
-                     a);
+  hipLaunchKernelGGL((spmm_xw_bwd_kernel<U, DX, EPI, MAXM>), dim3((unsigned)grid),
+                     dim3(kXwThreads), 0, s, a);
   return check_launch("spmm_xw_bwd_kernel");
+}
+
+template <int U, bool MAXM>
+int launch_xb_m(const XbArgs &a, int epi, int grid, hipStream_t s) {
+  if (a.dX == nullptr) return launch_xb<U, false, EPI_STORE, MAXM>(a, grid, s);
+  if (epi == EPI_RELU_DIV) return launch_xb<U, true, EPI_RELU_DIV, MAXM>(a, grid, s);
+  if (epi == EPI_RELU) return launch_xb<U, true, EPI_RELU, MAXM>(a, grid, s);
+  return launch_xb<U, true, EPI_STORE, MAXM>(a, grid, s);
 }
 
 template <int U>
 int launch_xb_u(const XbArgs &a, int epi, int grid, hipStream_t s) {
-  if (a.dX == nullptr) return launch_xb<U, false, EPI_STORE>(a, grid, s);
-  if (epi == EPI_RELU_DIV) return launch_xb<U, true, EPI_RELU_DIV>(a, grid, s);
-  if (epi == EPI_RELU) return launch_xb<U, true, EPI_RELU>(a, grid, s);
-  return launch_xb<U, true, EPI_STORE>(a, grid, s);
+  return a.win_mask != nullptr ? launch_xb_m<U, true>(a, epi, grid, s)
+                               : launch_xb_m<U, false>(a, epi, grid, s);
 }
 
 }  // namespace
@@ -787,9 +816,12 @@ extern "C" int mgcn_spmm_xw_bwd(int64_t n_rows, int64_t n_cols, int32_t F_in, in
                                 const float *X, int64_t ldx, const float *W, int64_t ldw,
                                 float *dW, int64_t lddw, int accumulate, float *dX, int64_t lddx,
                                 const uint32_t *relu_mask, const float *row_div, float *colsum,
+                                const uint32_t *win_mask, const int32_t *slot_map,
                                 void *workspace, size_t workspace_bytes, void *stream) {
   clear_error();
   MGCN_REQUIRE(n_rows >= 0, "mgcn_spmm_xw_bwd: negative size");
+  MGCN_REQUIRE((win_mask == nullptr) == (slot_map == nullptr),
+               "mgcn_spmm_xw_bwd: win_mask and slot_map go together (max adjoint)");
   MGCN_REQUIRE(mgcn_spmm_xw_supported(F_in, F_out, MGCN_REDUCE_SUM),
                "mgcn_spmm_xw_bwd: unsupported F_in=%d F_out=%d (needs 128 x 128, bf16x6)", F_in,
                F_out);
@@ -845,6 +877,8 @@ extern "C" int mgcn_spmm_xw_bwd(int64_t n_rows, int64_t n_cols, int32_t F_in, in
   a.lddx = lddx;
   a.relu_mask = relu_mask;
   a.row_div = row_div;
+  a.win_mask = win_mask;
+  a.slot_map = slot_map;
   a.dw_partial = static_cast<float *>(workspace);
   a.colsum_partial = reinterpret_cast<float *>(static_cast<char *>(workspace) +
                                                align_up((size_t)xw_grid() * kXwF * kXwF * 4, 256));

@@ -143,11 +143,14 @@ def spmm_xw_fwd(view: CSRView, w: torch.Tensor | None, X: torch.Tensor, W: torch
 
 def spmm_xw_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tensor | None,
                 dY: torch.Tensor, X: torch.Tensor, W: torch.Tensor, want_dx: bool = True,
-                relu_mask: torch.Tensor | None = None, row_div: torch.Tensor | None = None):
-    """Both adjoints of a 128 -> 128 sum / mean layer from one pass
-    (``mgcn_spmm_xw_bwd``): dH = A^T dY [* row_scale] stays on chip, and
-    dW = X^T dH, dX = dH W^T (with the lower layer's ReLU mask / row divisor /
-    bias column sums, as :func:`gemm_bwd`) are formed from it.  Returns
+                relu_mask: torch.Tensor | None = None, row_div: torch.Tensor | None = None,
+                win_mask: torch.Tensor | None = None, slot_map: torch.Tensor | None = None):
+    """Both adjoints of a 128 -> 128 layer from one pass (``mgcn_spmm_xw_bwd``):
+    dH = A^T dY [* row_scale] stays on chip, and dW = X^T dH, dX = dH W^T
+    (with the lower layer's ReLU mask / row divisor / bias column sums, as
+    :func:`gemm_bwd`) are formed from it.  Max: ``win_mask`` (the forward's
+    winner bits, :func:`spmm_fwd` with ``mask_plan``) and the plan's
+    ``slot_map`` route dY as :func:`spmm_bwd` does.  Returns
     (dW, dX or None, colsum or None)."""
     lib = L.load()
     dY = _contig_f32(dY, "dY")
@@ -165,6 +168,11 @@ def spmm_xw_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tens
     if M != view_t.n_rows or dY.size(0) != view_t.n_cols or dY.size(1) != F_out:
         raise ValueError(f"spmm_xw_bwd: X {tuple(X.shape)}, dY {tuple(dY.shape)} do not fit the "
                          f"graph ({view_t.n_rows} sources, {view_t.n_cols} destinations)")
+    if (win_mask is None) != (slot_map is None):
+        raise ValueError("spmm_xw_bwd: win_mask and slot_map go together (max adjoint)")
+    if win_mask is not None and (win_mask.dtype != torch.int32 or win_mask.dim() != 2
+                                 or win_mask.size(1) != (F_out + 31) // 32):
+        raise ValueError("spmm_xw_bwd: win_mask must be int32 [nnz, ceil(F/32)]")
     dW = torch.empty(F_in, F_out, dtype=torch.float32, device=dev)
     dX = torch.empty(M, F_in, dtype=torch.float32, device=dev) if want_dx else None
     colsum = None
@@ -186,8 +194,8 @@ def spmm_xw_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tens
                                   dY.stride(0), L.ptr(X), X.stride(0), L.ptr(W), W.stride(0),
                                   L.ptr(dW), dW.stride(0), 0, L.ptr(dX),
                                   dX.stride(0) if dX is not None else 0, L.ptr(relu_mask),
-                                  L.ptr(row_div), L.ptr(colsum), L.ptr(ws), ws_bytes,
-                                  L.stream_of(dev))
+                                  L.ptr(row_div), L.ptr(colsum), L.ptr(win_mask),
+                                  L.ptr(slot_map), L.ptr(ws), ws_bytes, L.stream_of(dev))
     if _TIMER is not None:
         _TIMER(tname, False)
     L.check(rc, "mgcn_spmm_xw_bwd")
@@ -686,19 +694,23 @@ class _GCNStack(torch.autograd.Function):
             am = args[l] if args[l].numel() else None
             W = Ws[l]
             fused = l > 0 and relus[l - 1] and rmasks[l - 1].numel() > 0
-            if (_FUSE_XW and am is None and
-                    spmm_xw_supported(plan.bwd, W.size(0), W.size(1), adj)):
+            if (_FUSE_XW and
+                    spmm_xw_supported(plan.bwd, W.size(0), W.size(1), L.REDUCE_SUM)):
                 # adjoint SpMM + dW + dX (+ the lower layer's ReLU / bias
-                # gradient) in one pass: dH never leaves the chip
-                if fused:
+                # gradient) in one pass: dH never leaves the chip (max: the
+                # adjoint routes dY through the forward's winner bits; with dX
+                # that form measured slower than the two launches, 1.53 vs
+                # 1.42 ms at config 4, so max fuses only the dW-only layer)
+                sm = plan.slot_map() if am is not None else None
+                if fused and am is None:
                     gW[l], dY, db = spmm_xw_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY,
                                                 inputs[l], W, relu_mask=rmasks[l - 1],
-                                                row_div=rd)
+                                                row_div=rd, win_mask=am, slot_map=sm)
                     gb[l - 1] = db if ctx.has_bias[l - 1] else None
                     continue
                 if l == 0 and not ctx.needs_input_grad[0]:
                     gW[l] = spmm_xw_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, inputs[l],
-                                        W, want_dx=False)[0]
+                                        W, want_dx=False, win_mask=am, slot_map=sm)[0]
                     continue
             dH = spmm_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, adj, win_mask=am,
                           slot_map=plan.slot_map() if am is not None else None)

@@ -145,6 +145,42 @@ def test_fused_backward_vs_two_launch(cuda, N, E, hub, deg_norm, epi):
     assert torch.equal(dWb, dWc)
 
 
+@pytest.mark.parametrize("N,E,hub", GRAPHS)
+@pytest.mark.parametrize("deg_norm,epi", [(None, "relu"), ("sm", "store"), (None, "dw_only")])
+def test_fused_max_backward_vs_two_launch(cuda, N, E, hub, deg_norm, epi):
+    """Max adjoint inside the fused backward (winner bits through slot_map):
+    dX bitwise equal to mgcn_spmm_bwd(MAX) + mgcn_gemm_bwd, dW within the
+    fp64-bounded tolerance of X^T dH."""
+    from mgcn import _lib as L
+    from mgcn import ops
+    rng = np.random.default_rng(7 * N + E + len(epi))
+    ei = _graph(rng, N, E, hub)
+    F = 128
+    plan, norm = _plan(cuda, ei, N, deg_norm)
+    g = torch.Generator(device=cuda).manual_seed(N + 1)
+    H = torch.randn(N, F, device=cuda, generator=g)
+    X = torch.randn(N, F, device=cuda, generator=g)
+    W = torch.randn(F, F, device=cuda, generator=g) * 0.1
+    dY = torch.randn(N, F, device=cuda, generator=g)
+    _, win = ops.spmm_fwd(plan.fwd, norm.w_fwd, H, L.REDUCE_MAX, mask_plan=plan)
+    sm = plan.slot_map()
+    mask = ops.make_relu_mask(torch.randn(N, F, device=cuda, generator=g)) \
+        if epi == "relu" else None
+    dH = ops.spmm_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, L.REDUCE_MAX, win_mask=win,
+                      slot_map=sm)
+    want_dx = epi != "dw_only"
+    dWa, dXa, csa = ops.gemm_bwd(X, dH, W, want_dx=want_dx, relu_mask=mask)
+    dWb, dXb, csb = ops.spmm_xw_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, X, W,
+                                    want_dx=want_dx, relu_mask=mask, win_mask=win, slot_map=sm)
+    if want_dx:
+        assert torch.equal(dXa, dXb)
+    ref = X.double().t() @ dH.double()
+    bound = X.double().abs().t() @ dH.double().abs()
+    assert ((dWb.double() - ref).abs() <= 1e-5 * bound + 1e-6).all()
+    if mask is not None:
+        torch.testing.assert_close(csb, csa, rtol=1e-4, atol=1e-3)
+
+
 def test_fused_backward_accumulate_and_empty(cuda):
     """accumulate adds into dW; zero rows give a zero dW / colsum."""
     from mgcn import _lib as L
@@ -164,7 +200,8 @@ def test_fused_backward_accumulate_and_empty(cuda):
     v = plan.bwd
     rc = lib.mgcn_spmm_xw_bwd(N, N, F, F, L.ptr(v.rowptr), L.ptr(v.col), L.ptr(norm.w_bwd), None,
                               L.ptr(dY), F, L.ptr(X), F, L.ptr(W), F, L.ptr(acc), F, 1, None, 0,
-                              None, None, None, L.ptr(ws), ws_bytes, L.stream_of(cuda))
+                              None, None, None, None, None, L.ptr(ws), ws_bytes,
+                              L.stream_of(cuda))
     L.check(rc, "mgcn_spmm_xw_bwd")
     assert torch.equal(acc, dW + 1.0)
     dW0 = torch.full((F, F), 5.0, device=cuda)
@@ -172,7 +209,7 @@ def test_fused_backward_accumulate_and_empty(cuda):
     rc = lib.mgcn_spmm_xw_bwd(0, 1, F, F, L.ptr(v.rowptr), None, None, None, L.ptr(dY), F,
                               L.ptr(X), F, L.ptr(W), F, L.ptr(dW0), F, 0, L.ptr(X), F,
                               L.ptr(torch.zeros(1, 4, dtype=torch.int32, device=cuda)), None,
-                              L.ptr(cs0), L.ptr(ws), ws_bytes, L.stream_of(cuda))
+                              L.ptr(cs0), None, None, L.ptr(ws), ws_bytes, L.stream_of(cuda))
     L.check(rc, "mgcn_spmm_xw_bwd(empty)")
     assert not dW0.any() and not cs0.any()
 
@@ -195,7 +232,8 @@ def test_fused_kernels_reject_unsupported(cuda):
                         torch.randn(128, 128, device=cuda), L.REDUCE_MAX)
 
 
-@pytest.mark.parametrize("aggr,deg_norm", [("add", "sm"), ("mean", "rw")])
+@pytest.mark.parametrize("aggr,deg_norm", [("add", "sm"), ("mean", "rw"), ("max", None),
+                                           ("max", "sm")])
 def test_gcn_stack_fused_vs_two_launch(cuda, aggr, deg_norm):
     """The stack with the fused kernels against the same stack on the
     GEMM + SpMM launches: outputs within fp32 association tolerance, dx
