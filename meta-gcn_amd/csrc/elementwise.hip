@@ -17,6 +17,23 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kMaxPartialBlocks = 1024;
 
+template <int VEC>
+__device__ __forceinline__ void load_vec(const float *p, float (&v)[VEC]) {
+  if constexpr (VEC == 4) {
+    const float4 a = *reinterpret_cast<const float4 *>(p);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  } else {
+    v[0] = p[0];
+  }
+}
+template <int VEC>
+__device__ __forceinline__ void store_vec(float *p, const float (&v)[VEC]) {
+  if constexpr (VEC == 4)
+    *reinterpret_cast<float4 *>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  else
+    p[0] = v[0];
+}
+
 // Block b owns rows b, b + gridDim.x, ... ; thread t owns columns
 // [c*T*4 + t_col*4, +4) for column chunk c, where T threads cover a row.
 template <int VEC>
@@ -35,35 +52,40 @@ __global__ __launch_bounds__(kBlock) void relu_bwd_colsum_kernel(
 #pragma unroll
     for (int j = 0; j < VEC; ++j) acc[j] = 0.0f;
     if (f_ok) {
-      for (int64_t r = (int64_t)blockIdx.x * R + t_row; r < n; r += (int64_t)gridDim.x * R) {
-        const int64_t off = r * F + f0;
-        float g[VEC], z[VEC];
-        if constexpr (VEC == 4) {
-          const float4 a = *reinterpret_cast<const float4 *>(dZ + off);
-          g[0] = a.x; g[1] = a.y; g[2] = a.z; g[3] = a.w;
+      // kUR rows per step, their loads issued before any is used: with the
+      // dY store in the loop a row at a time waited a full memory round
+      // trip per row (mean's top layer: 0.41 ms at config 2).  Rows are
+      // still summed in ascending order: the same column sums bit for bit.
+      constexpr int kUR = 4;
+      const int64_t stride = (int64_t)gridDim.x * R;
+      for (int64_t r0 = (int64_t)blockIdx.x * R + t_row; r0 < n; r0 += kUR * stride) {
+        float g[kUR][VEC], z[kUR][VEC], dv[kUR];
+#pragma unroll
+        for (int u = 0; u < kUR; ++u) {
+          const int64_t r = r0 + u * stride;
+          const bool ok = r < n;
+          const int64_t off = (ok ? r : 0) * F + f0;
+          load_vec<VEC>(dZ + off, g[u]);
+          if (relu) load_vec<VEC>(Z + off, z[u]);
+          dv[u] = row_div != nullptr ? row_div[ok ? r : 0] : 1.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < kUR; ++u) {
+          const int64_t r = r0 + u * stride;
+          if (r >= n) break;
           if (relu) {
-            const float4 b = *reinterpret_cast<const float4 *>(Z + off);
-            z[0] = b.x; z[1] = b.y; z[2] = b.z; z[3] = b.w;
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) g[u][j] = (z[u][j] > 0.0f) ? g[u][j] : 0.0f;
           }
-        } else {
-          g[0] = dZ[off];
-          if (relu) z[0] = Z[off];
-        }
-        if (relu) {
+          if ((relu || row_div != nullptr) && dY != nullptr) {
+            float o[VEC];  // mean aggregation: rows pre-divided by their count
 #pragma unroll
-          for (int j = 0; j < VEC; ++j) g[j] = (z[j] > 0.0f) ? g[j] : 0.0f;
-        }
-        if ((relu || row_div != nullptr) && dY != nullptr) {
-          float o[VEC];  // mean aggregation: rows pre-divided by their count
+            for (int j = 0; j < VEC; ++j) o[j] = row_div != nullptr ? __fdiv_rn(g[u][j], dv[u]) : g[u][j];
+            store_vec<VEC>(dY + r * F + f0, o);
+          }
 #pragma unroll
-          for (int j = 0; j < VEC; ++j) o[j] = row_div != nullptr ? __fdiv_rn(g[j], row_div[r]) : g[j];
-          if constexpr (VEC == 4)
-            *reinterpret_cast<float4 *>(dY + off) = make_float4(o[0], o[1], o[2], o[3]);
-          else
-            dY[off] = o[0];
+          for (int j = 0; j < VEC; ++j) acc[j] = __fadd_rn(acc[j], g[u][j]);
         }
-#pragma unroll
-        for (int j = 0; j < VEC; ++j) acc[j] = __fadd_rn(acc[j], g[j]);
       }
     }
     if (partial == nullptr) continue;
@@ -85,22 +107,6 @@ __global__ __launch_bounds__(kBlock) void relu_bwd_colsum_kernel(
   }
 }
 
-template <int VEC>
-__device__ __forceinline__ void load_vec(const float *p, float (&v)[VEC]) {
-  if constexpr (VEC == 4) {
-    const float4 a = *reinterpret_cast<const float4 *>(p);
-    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-  } else {
-    v[0] = p[0];
-  }
-}
-template <int VEC>
-__device__ __forceinline__ void store_vec(float *p, const float (&v)[VEC]) {
-  if constexpr (VEC == 4)
-    *reinterpret_cast<float4 *>(p) = make_float4(v[0], v[1], v[2], v[3]);
-  else
-    p[0] = v[0];
-}
 
 // GCNModel residual join (gcn_model.py:99-105): Z = act(Z1 + (R + rb)),
 // the residual Linear's bias added to its product first (as F.linear does).
@@ -149,22 +155,37 @@ __global__ __launch_bounds__(kBlock) void residual_act_bwd_kernel(
 #pragma unroll
     for (int j = 0; j < VEC; ++j) sa[j] = ss[j] = 0.0f;
     if (ok) {
-      for (int64_t r = (int64_t)blockIdx.x * R + t_row; r < n; r += (int64_t)gridDim.x * R) {
-        float g[VEC], z[VEC], z1[VEC], a[VEC];
-        load_vec<VEC>(dZ + r * lddz + f0, g);
-        if (relu) load_vec<VEC>(Z + r * ldz + f0, z);
-        if (relu1) load_vec<VEC>(Z1 + r * ldz1 + f0, z1);
-        const float dv = row_div != nullptr ? row_div[r] : 1.0f;
+      // kUR rows per step with their loads issued first (see
+      // relu_bwd_colsum_kernel); rows summed in ascending order as before
+      constexpr int kUR = 4;
+      const int64_t stride = (int64_t)gridDim.x * R;
+      for (int64_t r0 = (int64_t)blockIdx.x * R + t_row; r0 < n; r0 += kUR * stride) {
+        float g[kUR][VEC], z[kUR][VEC], z1[kUR][VEC], dv[kUR];
 #pragma unroll
-        for (int j = 0; j < VEC; ++j) {
-          if (relu && !(z[j] > 0.0f)) g[j] = 0.0f;
-          a[j] = (relu1 && !(z1[j] > 0.0f)) ? 0.0f : g[j];
-          ss[j] = __fadd_rn(ss[j], g[j]);
-          sa[j] = __fadd_rn(sa[j], a[j]);
-          if (row_div != nullptr) a[j] = __fdiv_rn(a[j], dv);
+        for (int u = 0; u < kUR; ++u) {
+          const int64_t r0u = r0 + u * stride;
+          const int64_t r = r0u < n ? r0u : 0;
+          load_vec<VEC>(dZ + r * lddz + f0, g[u]);
+          if (relu) load_vec<VEC>(Z + r * ldz + f0, z[u]);
+          if (relu1) load_vec<VEC>(Z1 + r * ldz1 + f0, z1[u]);
+          dv[u] = row_div != nullptr ? row_div[r] : 1.0f;
         }
-        if (dS != nullptr) store_vec<VEC>(dS + r * ldds + f0, g);
-        store_vec<VEC>(dA + r * ldda + f0, a);
+#pragma unroll
+        for (int u = 0; u < kUR; ++u) {
+          const int64_t r = r0 + u * stride;
+          if (r >= n) break;
+          float a[VEC];
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) {
+            if (relu && !(z[u][j] > 0.0f)) g[u][j] = 0.0f;
+            a[j] = (relu1 && !(z1[u][j] > 0.0f)) ? 0.0f : g[u][j];
+            ss[j] = __fadd_rn(ss[j], g[u][j]);
+            sa[j] = __fadd_rn(sa[j], a[j]);
+            if (row_div != nullptr) a[j] = __fdiv_rn(a[j], dv[u]);
+          }
+          if (dS != nullptr) store_vec<VEC>(dS + r * ldds + f0, g[u]);
+          store_vec<VEC>(dA + r * ldda + f0, a);
+        }
       }
     }
     if (partial == nullptr) continue;
