@@ -194,13 +194,31 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(const SpmmArgs a) {
   const float *__restrict__ X = a.X;
   const bool has_w = a.w != nullptr;
 
-  for (int64_t wv = (int64_t)blockIdx.x * kWaves + wave_in_block; wv < n_row_groups;
-       wv += wave_stride) {
+  // Row metadata runs ahead of the rows: the row pointers of the next task
+  // and the row id of the one after are loaded while the current row is
+  // gathered, so a task costs col -> rows instead of order -> rowptr -> col
+  // -> rows round trips (short rows, config 3's F = 32 light rows, are
+  // bound by that chain).
+  auto row_of = [&](int64_t wv, bool &ok) -> int64_t {
     const int64_t item = wv * RPW + grp;
-    const bool row_ok = item < n_work;
-    const int64_t row = !row_ok ? 0 : light != nullptr ? (int64_t)light[item] : item;
-    const int64_t beg = row_ok ? a.rowptr[row] : 0;
-    const int64_t deg = row_ok ? a.rowptr[row + 1] - beg : 0;
+    ok = wv < n_row_groups && item < n_work;
+    return !ok ? 0 : light != nullptr ? (int64_t)light[item] : item;
+  };
+  const int64_t wv0 = (int64_t)blockIdx.x * kWaves + wave_in_block;
+  bool ok_n, ok_nn;
+  int64_t row_n = row_of(wv0, ok_n);
+  int64_t beg_n = ok_n ? a.rowptr[row_n] : 0, end_n = ok_n ? a.rowptr[row_n + 1] : 0;
+  int64_t row_nn = row_of(wv0 + wave_stride, ok_nn);
+  for (int64_t wv = wv0; wv < n_row_groups; wv += wave_stride) {
+    const bool row_ok = ok_n;
+    const int64_t row = row_n;
+    const int64_t beg = beg_n;
+    const int64_t deg = end_n - beg_n;
+    row_n = row_nn;
+    ok_n = ok_nn;
+    beg_n = ok_n ? a.rowptr[row_n] : 0;
+    end_n = ok_n ? a.rowptr[row_n + 1] : 0;
+    row_nn = row_of(wv + 2 * wave_stride, ok_nn);
     const int64_t maxdeg = (RPW > 1) ? wave_max_over_groups<G>(deg) : deg;
 
     for (int c = 0; c < a.n_chunks; ++c) {
