@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define MGCN_ABI_VERSION 9
+#define MGCN_ABI_VERSION 10
 
 /* return codes */
 #define MGCN_OK 0
@@ -323,11 +323,17 @@ int mgcn_spmm_xw_supported(int32_t F_in, int32_t F_out, int reduce);
  * (gcn_base_models.py:201, 223-241; PyG GCNConv x @ W then propagate) without
  * materialising X W.  Rows with heavy degree are handled, but slowly (one
  * lane group per row): callers route skewed graphs to the two-launch path.
+ * Z (nullable, [n_rows, F_in], ldz, 16-byte aligned rows) receives the
+ * aggregated rows before W -- for MEAN before the division -- so the
+ * backward can form dW = Z^T dY' (dY' = dY pre-divided by the counts for
+ * MEAN) with mgcn_gemm_bwd instead of a second gather over the graph
+ * (the adjoint of `x @ weight_node`, gcn_base_models.py:201, reassociated).
  */
 int mgcn_spmm_xw_fwd(int64_t n_rows, int64_t n_cols, int32_t F_in, int32_t F_out, const int64_t *rowptr,
                      const int32_t *col, const float *w, const float *X, int64_t ldx,
                      const float *W, int64_t ldw, const float *bias, float *Y, int64_t ldy,
-                     int reduce, int relu, uint32_t *relu_mask, void *stream);
+                     int reduce, int relu, uint32_t *relu_mask, float *Z, int64_t ldz,
+                     void *stream);
 
 /* Bytes of scratch mgcn_spmm_xw_bwd needs (split-K partials + column sums). */
 size_t mgcn_spmm_xw_bwd_workspace_bytes(int64_t n_rows);
@@ -350,6 +356,9 @@ size_t mgcn_spmm_xw_bwd_workspace_bytes(int64_t n_rows);
  * mgcn_spmm_fwd(MAX) -- each edge's dY row counts only at the features whose
  * winner it was (its bits in win_mask at its fwd slot slot_map[k], as
  * mgcn_spmm_bwd(MAX, win_mask, slot_map)); dH bit for bit that function's.
+ * dX only: X == NULL and dW == NULL (dX required, no win_mask) -- the
+ * gather, dX = dH W^T and its epilogue, nothing else; dX bit for bit the
+ * full form's.  Pair with mgcn_spmm_xw_fwd's Z and mgcn_gemm_bwd (dW-only).
  */
 int mgcn_spmm_xw_bwd(int64_t n_rows, int64_t n_cols, int32_t F_in, int32_t F_out,
                      const int64_t *rowptr_t, const int32_t *col_t, const float *w_t,

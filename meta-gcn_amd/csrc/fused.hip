@@ -298,6 +298,8 @@ struct XwArgs {
   float *Y;
   int64_t ldy;
   uint32_t *relu_mask;  // nullable; [n_rows][4], bit b of word v <=> Y[row][4 b + v] > 0
+  float *Z;             // nullable; the aggregated rows before W (and before mean's division)
+  int64_t ldz;
   int mean;
   int relu;
 };
@@ -380,6 +382,17 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_fwd_kernel(c
       meta_rowptr(a.rowptr, r2, r2 < a.n_rows && k + 2 < 2 * n_my, nn);
       float acc[4];
       gather_row_meta<U>(rx, ldx_b, a.col, a.w, cur, gl, grp, acc);
+      if (a.Z != nullptr) {
+        // the aggregate the backward's dW = Z^T dY reads (whole 512-B rows;
+        // rows past the end fall outside the chunk's buffer range)
+        const int64_t r0 = chunk * kXwRows;
+        const int64_t left = a.n_rows - r0;
+        const uint32_t rows_in = (uint32_t)(left >= kXwRows ? kXwRows : left);
+        const auto rz = buf_rsrc(a.Z + r0 * a.ldz, rows_in * (uint32_t)a.ldz * 4u);
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(u32x4, make_float4(acc[0], acc[1], acc[2], acc[3])), rz,
+            4 * (int)(lr * a.ldz + 4 * gl), 0, 0);
+      }
       if (a.mean) {
         const float c = (float)(cur.deg > 1 ? cur.deg : 1);
 #pragma unroll
@@ -468,7 +481,10 @@ __device__ unsigned long long g_xprof[2][64][6];
 #define XPROF(it, k)
 #endif
 
-template <int U, bool DX, int EPI, bool MAXM>
+// DW = false: dX only (X == NULL) -- the caller forms dW = Z^T dY from the
+// forward's aggregate (mgcn_gemm_bwd, dW-only), so the chunk's X rows, their
+// images and the dW MFMAs drop out.
+template <int U, bool DX, int EPI, bool MAXM, bool DW = true>
 __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(const XbArgs a) {
   __shared__ __attribute__((aligned(16))) char lds[kXbLds];
   const int tid = threadIdx.x;
@@ -511,6 +527,18 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
     for (int r = 0; r < 16; ++r) accw[s][r] = 0.0f;
   const int ncol = 16 * wave + l16;  // dX column of this lane
   const int xoff = 4 * (int)((tid >> 5) * a.ldx + 4 * (tid & 31));
+  // dX only: no dW accumulators, so this wave's W^T fragments are split once
+  // and held (48 VGPRs) instead of re-read from L2 every chunk
+  bf16x8 wt[DW ? 1 : 4][3];
+  if constexpr (!DW) {
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const float4 w0 = *reinterpret_cast<const float4 *>(wp + 32 * ks);
+      const float4 w1 = *reinterpret_cast<const float4 *>(wp + 32 * ks + 4);
+      const float v[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+      split3_bf16(v, wt[ks][0], wt[ks][1], wt[ks][2]);
+    }
+  }
 
   // staged dX rows of chunk `c` -> dX (16 B per lane, whole rows)
   // The ReLU mask, the bias column sums and mean's division are applied here,
@@ -566,9 +594,12 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
     }
     // the chunk's X rows (q and 16 + q, float4 tid & 31), issued first so
     // they land under the gathers
-    const auto rxx = buf_rsrc(a.X + r0 * a.ldx, rows_in * (uint32_t)a.ldx * 4u);
-    const u32x4 xa = __builtin_amdgcn_raw_buffer_load_b128(rxx, xoff, 0, 0);
-    const u32x4 xb = __builtin_amdgcn_raw_buffer_load_b128(rxx, xoff + 64 * (int)a.ldx, 0, 0);
+    u32x4 xa{}, xb{};
+    if constexpr (DW) {
+      const auto rxx = buf_rsrc(a.X + r0 * a.ldx, rows_in * (uint32_t)a.ldx * 4u);
+      xa = __builtin_amdgcn_raw_buffer_load_b128(rxx, xoff, 0, 0);
+      xb = __builtin_amdgcn_raw_buffer_load_b128(rxx, xoff + 64 * (int)a.ldx, 0, 0);
+    }
     // the chunk's mask / divisor words straight into LDS (LDS-DMA: no registers
     // held across the gathers); rows past the end read row r0 and are never used
     if constexpr (DX && EPI != EPI_STORE) {
@@ -600,11 +631,13 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
       store_row_terms(lds + kXbHOff, lr, gl, acc);
     }
     XPROF(it, 1);
+    if constexpr (DW) {
 #pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      const float4 v = __builtin_bit_cast(float4, m == 0 ? xa : xb);
-      const float f[4] = {v.x, v.y, v.z, v.w};
-      store_row_terms(lds, 16 * m + (tid >> 5), lc, f);
+      for (int m = 0; m < 2; ++m) {
+        const float4 v = __builtin_bit_cast(float4, m == 0 ? xa : xb);
+        const float f[4] = {v.x, v.y, v.z, v.w};
+        store_row_terms(lds, 16 * m + (tid >> 5), lc, f);
+      }
     }
     // the mask / divisor LDS-DMA (older than this wave's gathers) has landed
     if constexpr (DX && EPI != EPI_STORE)
@@ -614,7 +647,7 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
     // other workgroup's gathers load the memory system) is hidden by the
     // barrier wait and the dW MFMAs
     float4 wr[4][2];
-    if constexpr (DX) {
+    if constexpr (DX && DW) {
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
@@ -625,7 +658,7 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
 
     // ---- Phase B1: dW += X^T dH (two 16-row k-steps) ---------------------
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < (DW ? 2 : 0); ++ks) {
       const char *kb = lds + ks * 16 * 256;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -648,11 +681,15 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
         for (int r = 0; r < 4; ++r) acc2[t][r] = 0.0f;
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        bf16x8 wb[3];
-        const float v[8] = {wr[ks][0].x, wr[ks][0].y, wr[ks][0].z, wr[ks][0].w,
-                            wr[ks][1].x, wr[ks][1].y, wr[ks][1].z, wr[ks][1].w};
-        split3_bf16(v, wb[0], wb[1], wb[2]);
-        mfma_rows(lds + kXbHOff, wb, ks, l16, g4, acc2);
+        if constexpr (DW) {
+          bf16x8 wb[3];
+          const float v[8] = {wr[ks][0].x, wr[ks][0].y, wr[ks][0].z, wr[ks][0].w,
+                              wr[ks][1].x, wr[ks][1].y, wr[ks][1].z, wr[ks][1].w};
+          split3_bf16(v, wb[0], wb[1], wb[2]);
+          mfma_rows(lds + kXbHOff, wb, ks, l16, g4, acc2);
+        } else {
+          mfma_rows(lds + kXbHOff, wt[ks], ks, l16, g4, acc2);
+        }
       }
 #pragma unroll
       for (int t = 0; t < 2; ++t)
@@ -679,7 +716,7 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
   // dW partial slab of this workgroup; C map: col = lc, row = (r & 3) + 8 (r >> 2) + 4 h
   float *slab = a.dw_partial + (int64_t)blockIdx.x * kXwF * kXwF;
 #pragma unroll
-  for (int s = 0; s < 2; ++s)
+  for (int s = 0; s < (DW ? 2 : 0); ++s)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int row = 32 * ti + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -718,11 +755,19 @@ int launch_xw(const XwArgs &a, hipStream_t s) {
   return check_launch("spmm_xw_fwd_kernel");
 }
 
-template <int U, bool DX, int EPI, bool MAXM>
+template <int U, bool DX, int EPI, bool MAXM, bool DW = true>
 int launch_xb(const XbArgs &a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((spmm_xw_bwd_kernel<U, DX, EPI, MAXM>), dim3((unsigned)grid),
+  hipLaunchKernelGGL((spmm_xw_bwd_kernel<U, DX, EPI, MAXM, DW>), dim3((unsigned)grid),
                      dim3(kXwThreads), 0, s, a);
   return check_launch("spmm_xw_bwd_kernel");
+}
+
+// dX only (no X, no dW), sum adjoint
+template <int U>
+int launch_xb_dx(const XbArgs &a, int epi, int grid, hipStream_t s) {
+  if (epi == EPI_RELU_DIV) return launch_xb<U, true, EPI_RELU_DIV, false, false>(a, grid, s);
+  if (epi == EPI_RELU) return launch_xb<U, true, EPI_RELU, false, false>(a, grid, s);
+  return launch_xb<U, true, EPI_STORE, false, false>(a, grid, s);
 }
 
 template <int U, bool MAXM>
@@ -763,7 +808,7 @@ extern "C" int mgcn_spmm_xw_fwd(int64_t n_rows, int64_t n_cols, int32_t F_in, in
                                 const int64_t *rowptr, const int32_t *col, const float *w,
                                 const float *X, int64_t ldx, const float *W, int64_t ldw,
                                 const float *bias, float *Y, int64_t ldy, int reduce, int relu,
-                                uint32_t *relu_mask, void *stream) {
+                                uint32_t *relu_mask, float *Z, int64_t ldz, void *stream) {
   clear_error();
   MGCN_REQUIRE(n_rows >= 0, "mgcn_spmm_xw_fwd: negative size");
   MGCN_REQUIRE(mgcn_spmm_xw_supported(F_in, F_out, reduce),
@@ -784,6 +829,9 @@ extern "C" int mgcn_spmm_xw_fwd(int64_t n_rows, int64_t n_cols, int32_t F_in, in
                "mgcn_spmm_xw_fwd: bias not 4-byte aligned");
   MGCN_REQUIRE(relu_mask == nullptr || reinterpret_cast<uintptr_t>(relu_mask) % 16 == 0,
                "mgcn_spmm_xw_fwd: relu_mask not 16-byte aligned");
+  MGCN_REQUIRE(Z == nullptr || (ldz >= F_in && ldz % 4 == 0 && reinterpret_cast<uintptr_t>(Z) % 16 == 0 &&
+                                (uint64_t)kXwRows * (uint64_t)ldz * 4u < (1ull << 31)),
+               "mgcn_spmm_xw_fwd: Z must have 16-byte aligned rows (ldz >= F_in)");
   XwArgs a{};
   a.n_rows = n_rows;
   a.rowptr = rowptr;
@@ -798,6 +846,8 @@ extern "C" int mgcn_spmm_xw_fwd(int64_t n_rows, int64_t n_cols, int32_t F_in, in
   a.Y = Y;
   a.ldy = ldy;
   a.relu_mask = relu_mask;
+  a.Z = Z;
+  a.ldz = ldz;
   a.mean = reduce == MGCN_REDUCE_MEAN;
   a.relu = relu != 0;
   hipStream_t s = as_stream(stream);
@@ -825,7 +875,12 @@ extern "C" int mgcn_spmm_xw_bwd(int64_t n_rows, int64_t n_cols, int32_t F_in, in
   MGCN_REQUIRE(mgcn_spmm_xw_supported(F_in, F_out, MGCN_REDUCE_SUM),
                "mgcn_spmm_xw_bwd: unsupported F_in=%d F_out=%d (needs 128 x 128, bf16x6)", F_in,
                F_out);
-  MGCN_REQUIRE(dW != nullptr && lddw >= F_out, "mgcn_spmm_xw_bwd: bad dW");
+  // X == NULL and dW == NULL: dX only (dW formed by the caller from Z^T dY)
+  const bool dx_only = X == nullptr && dW == nullptr;
+  MGCN_REQUIRE(dx_only || (X != nullptr && dW != nullptr && lddw >= F_out),
+               "mgcn_spmm_xw_bwd: bad dW (X and dW are given together, or both NULL for dX only)");
+  MGCN_REQUIRE(!dx_only || (dX != nullptr && win_mask == nullptr),
+               "mgcn_spmm_xw_bwd: the dX-only form needs dX and takes no win_mask");
   const int epi = relu_mask == nullptr ? EPI_STORE : row_div != nullptr ? EPI_RELU_DIV : EPI_RELU;
   MGCN_REQUIRE(epi == EPI_STORE || (dX != nullptr && colsum != nullptr),
                "mgcn_spmm_xw_bwd: relu_mask needs dX and colsum");
@@ -833,17 +888,18 @@ extern "C" int mgcn_spmm_xw_bwd(int64_t n_rows, int64_t n_cols, int32_t F_in, in
                "mgcn_spmm_xw_bwd: row_div needs relu_mask");
   hipStream_t s = as_stream(stream);
   if (n_rows == 0) {
-    if (!accumulate)
+    if (!accumulate && dW != nullptr)
       for (int32_t r = 0; r < F_in; ++r)
         MGCN_HIP_TRY(hipMemsetAsync(dW + r * lddw, 0, sizeof(float) * F_out, s));
     if (colsum) MGCN_HIP_TRY(hipMemsetAsync(colsum, 0, sizeof(float) * F_in, s));
     return MGCN_OK;
   }
-  MGCN_REQUIRE(rowptr_t && dY && X, "mgcn_spmm_xw_bwd: null array");
+  MGCN_REQUIRE(rowptr_t && dY, "mgcn_spmm_xw_bwd: null array");
   MGCN_REQUIRE(lddy >= F_out && lddy % 4 == 0 && reinterpret_cast<uintptr_t>(dY) % 16 == 0,
                "mgcn_spmm_xw_bwd: dY must have 16-byte aligned rows");
-  MGCN_REQUIRE(ldx >= F_in && ldx % 4 == 0 && reinterpret_cast<uintptr_t>(X) % 16 == 0,
+  MGCN_REQUIRE(dx_only || (ldx >= F_in && ldx % 4 == 0 && reinterpret_cast<uintptr_t>(X) % 16 == 0),
                "mgcn_spmm_xw_bwd: X must have 16-byte aligned rows");
+  if (dx_only) ldx = 0;
   MGCN_REQUIRE(n_cols > 0 && (uint64_t)n_cols * (uint64_t)lddy * 4u <= 0xfffffff0ull,
                "mgcn_spmm_xw_bwd: dY must hold 1 .. 4 GiB - 1 bytes (32-bit gather offsets)");
   MGCN_REQUIRE((uint64_t)kXwRows * (uint64_t)(ldx > lddx ? ldx : lddx) * 4u < (1ull << 31),
@@ -882,7 +938,13 @@ extern "C" int mgcn_spmm_xw_bwd(int64_t n_rows, int64_t n_cols, int32_t F_in, in
   a.dw_partial = static_cast<float *>(workspace);
   a.colsum_partial = reinterpret_cast<float *>(static_cast<char *>(workspace) +
                                                align_up((size_t)xw_grid() * kXwF * kXwF * 4, 256));
-  int rc = g_xw_unroll == 4 ? launch_xb_u<4>(a, epi, grid, s) : launch_xb_u<8>(a, epi, grid, s);
+  int rc;
+  if (dx_only) {
+    rc = g_xw_unroll == 4 ? launch_xb_dx<4>(a, epi, grid, s) : launch_xb_dx<8>(a, epi, grid, s);
+    if (rc || epi == EPI_STORE) return rc;
+    return launch_colsum_fold(a.colsum_partial, grid, kXwF, colsum, s);
+  }
+  rc = g_xw_unroll == 4 ? launch_xb_u<4>(a, epi, grid, s) : launch_xb_u<8>(a, epi, grid, s);
   if (rc) return rc;
   rc = launch_split_reduce(a.dw_partial, grid, (int64_t)kXwF * kXwF, kXwF, dW, lddw, accumulate, s);
   if (rc || epi == EPI_STORE) return rc;

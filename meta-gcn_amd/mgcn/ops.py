@@ -106,10 +106,12 @@ def spmm_xw_supported(view: CSRView, F_in: int, F_out: int, reduce: int) -> bool
 
 def spmm_xw_fwd(view: CSRView, w: torch.Tensor | None, X: torch.Tensor, W: torch.Tensor,
                 reduce: int, bias: torch.Tensor | None = None, relu: bool = False,
-                relu_mask: torch.Tensor | None = None) -> torch.Tensor:
+                relu_mask: torch.Tensor | None = None, want_z: bool = False):
     """Y = epi((reduce_k X[col_k] * w_k) @ W + bias) in one launch
     (``mgcn_spmm_xw_fwd``): the layer's GEMM fused behind its aggregation, so
-    X @ W is never written.  Sum / mean only (they commute with W)."""
+    X @ W is never written.  Sum / mean only (they commute with W).  With
+    ``want_z`` returns (Y, Z): Z = the aggregated rows before W (for mean
+    before the division), from which the backward forms dW = Z^T dY."""
     lib = L.load()
     X = _contig_f32(X, "X")
     if X.stride(0) % 4 or X.data_ptr() % 16:
@@ -128,17 +130,19 @@ def spmm_xw_fwd(view: CSRView, w: torch.Tensor | None, X: torch.Tensor, W: torch
         if bias.numel() != F_out:
             raise ValueError(f"bias has {bias.numel()} entries, expected {F_out}")
     Y = torch.empty(view.n_rows, F_out, dtype=torch.float32, device=dev)
+    Z = torch.empty(view.n_rows, F_in, dtype=torch.float32, device=dev) if want_z else None
     if _TIMER is not None:
         _TIMER("spmm_xw_fwd", True)
     with L.device_guard(dev):
         rc = lib.mgcn_spmm_xw_fwd(view.n_rows, view.n_cols, F_in, F_out, L.ptr(view.rowptr),
                                   L.ptr(view.col), L.ptr(w), L.ptr(X), X.stride(0), L.ptr(W),
                                   W.stride(0), L.ptr(bias), L.ptr(Y), Y.stride(0), reduce,
-                                  int(bool(relu)), L.ptr(relu_mask), L.stream_of(dev))
+                                  int(bool(relu)), L.ptr(relu_mask), L.ptr(Z),
+                                  Z.stride(0) if Z is not None else 0, L.stream_of(dev))
     if _TIMER is not None:
         _TIMER("spmm_xw_fwd", False)
     L.check(rc, "mgcn_spmm_xw_fwd")
-    return Y
+    return (Y, Z) if want_z else Y
 
 
 def spmm_xw_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tensor | None,
@@ -154,26 +158,32 @@ def spmm_xw_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tens
     (dW, dX or None, colsum or None)."""
     lib = L.load()
     dY = _contig_f32(dY, "dY")
-    X = _contig_f32(X, "X")
     if dY.stride(0) % 4 or dY.data_ptr() % 16:
         dY = dY.contiguous()
-    if X.stride(0) % 4 or X.data_ptr() % 16:
-        X = X.contiguous()
+    dx_only = X is None  # dW formed by the caller (Z^T dY, :func:`gemm_bwd`)
+    if not dx_only:
+        X = _contig_f32(X, "X")
+        if X.stride(0) % 4 or X.data_ptr() % 16:
+            X = X.contiguous()
     W = W.detach()
     if W.dtype != torch.float32 or W.stride(1) != 1:
         W = W.to(torch.float32).contiguous()
     dev = L.require_device(dY, X, W, view_t.rowptr, w_t, row_scale, relu_mask, row_div)
-    M, F_in = X.shape
-    F_out = W.size(1)
-    if M != view_t.n_rows or dY.size(0) != view_t.n_cols or dY.size(1) != F_out:
-        raise ValueError(f"spmm_xw_bwd: X {tuple(X.shape)}, dY {tuple(dY.shape)} do not fit the "
+    F_in, F_out = W.shape
+    M = view_t.n_rows if dx_only else X.size(0)
+    if dx_only and (not want_dx or win_mask is not None):
+        raise ValueError("spmm_xw_bwd: X=None (dX only) needs want_dx and no win_mask")
+    if (not dx_only and X.size(1) != F_in) or M != view_t.n_rows or \
+            dY.size(0) != view_t.n_cols or dY.size(1) != F_out:
+        raise ValueError(f"spmm_xw_bwd: X {None if dx_only else tuple(X.shape)}, dY "
+                         f"{tuple(dY.shape)} do not fit the "
                          f"graph ({view_t.n_rows} sources, {view_t.n_cols} destinations)")
     if (win_mask is None) != (slot_map is None):
         raise ValueError("spmm_xw_bwd: win_mask and slot_map go together (max adjoint)")
     if win_mask is not None and (win_mask.dtype != torch.int32 or win_mask.dim() != 2
                                  or win_mask.size(1) != (F_out + 31) // 32):
         raise ValueError("spmm_xw_bwd: win_mask must be int32 [nnz, ceil(F/32)]")
-    dW = torch.empty(F_in, F_out, dtype=torch.float32, device=dev)
+    dW = None if dx_only else torch.empty(F_in, F_out, dtype=torch.float32, device=dev)
     dX = torch.empty(M, F_in, dtype=torch.float32, device=dev) if want_dx else None
     colsum = None
     if relu_mask is not None:
@@ -185,14 +195,15 @@ def spmm_xw_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tens
         colsum = torch.empty(F_in, dtype=torch.float32, device=dev)
     ws_bytes = int(lib.mgcn_spmm_xw_bwd_workspace_bytes(M))
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
-    tname = "spmm_xw_bwd" if want_dx else "spmm_xw_bwd_dw"
+    tname = "spmm_xw_bwd_dx" if dx_only else "spmm_xw_bwd" if want_dx else "spmm_xw_bwd_dw"
     if _TIMER is not None:
         _TIMER(tname, True)
     with L.device_guard(dev):
         rc = lib.mgcn_spmm_xw_bwd(M, view_t.n_cols, F_in, F_out, L.ptr(view_t.rowptr),
                                   L.ptr(view_t.col), L.ptr(w_t), L.ptr(row_scale), L.ptr(dY),
-                                  dY.stride(0), L.ptr(X), X.stride(0), L.ptr(W), W.stride(0),
-                                  L.ptr(dW), dW.stride(0), 0, L.ptr(dX),
+                                  dY.stride(0), L.ptr(X), 0 if dx_only else X.stride(0),
+                                  L.ptr(W), W.stride(0), L.ptr(dW),
+                                  0 if dx_only else dW.stride(0), 0, L.ptr(dX),
                                   dX.stride(0) if dX is not None else 0, L.ptr(relu_mask),
                                   L.ptr(row_div), L.ptr(colsum), L.ptr(win_mask),
                                   L.ptr(slot_map), L.ptr(ws), ws_bytes, L.stream_of(dev))
@@ -644,8 +655,9 @@ class _GCNStack(torch.autograd.Function):
     def forward(ctx, x, plan, norm, reduce, relus, *params):
         Ws, bs = params[0::2], params[1::2]
         h = x
-        inputs, outs, args, rmasks = [], [], [], []
+        inputs, outs, args, rmasks, zs = [], [], [], [], []
         for i, (W, b, relu) in enumerate(zip(Ws, bs, relus)):
+            z = None
             inputs.append(h)
             # the ReLU mask the next layer's dX GEMM reads (16 B per row)
             nxt = Ws[i + 1] if i + 1 < len(Ws) else None
@@ -653,9 +665,13 @@ class _GCNStack(torch.autograd.Function):
             if relu and nxt is not None and gemm_nn_supported(nxt.size(1), nxt.size(0)):
                 rm = torch.empty(plan.fwd.n_rows, 4, dtype=torch.int32, device=h.device)
             if _FUSE_XW and spmm_xw_supported(plan.fwd, W.size(0), W.size(1), reduce):
-                # (A h) W in one launch: h @ W is never written (sum / mean)
+                # (A h) W in one launch: h @ W is never written (sum / mean);
+                # the aggregate A h is kept for dW = (A h)^T dY
+                want_z = bool(ctx.needs_input_grad[5 + 2 * i])
                 h, am = spmm_xw_fwd(plan.fwd, norm.w_fwd, h, W, reduce, b, relu,
-                                    relu_mask=rm), None
+                                    relu_mask=rm, want_z=want_z), None
+                if want_z:
+                    h, z = h
             else:
                 H = _mm(h, W)
                 h, am = spmm_fwd(plan.fwd, norm.w_fwd, H, reduce, b, relu, mask_plan=plan,
@@ -663,12 +679,14 @@ class _GCNStack(torch.autograd.Function):
             outs.append(h)
             args.append(am)  # max: winner bits per edge (adjoint slot order)
             rmasks.append(rm)
+            zs.append(z)
         ctx.plan, ctx.norm, ctx.reduce, ctx.relus = plan, norm, reduce, relus
         ctx.n_layers = len(Ws)
         ctx.has_bias = [b is not None for b in bs]
         ctx.save_for_backward(*inputs, *outs, *[a if a is not None else torch.empty(0)
                                                 for a in args], *Ws,
-                              *[m if m is not None else torch.empty(0) for m in rmasks])
+                              *[m if m is not None else torch.empty(0) for m in rmasks],
+                              *[z if z is not None else torch.empty(0) for z in zs])
         return h
 
     @staticmethod
@@ -677,6 +695,7 @@ class _GCNStack(torch.autograd.Function):
         saved = ctx.saved_tensors
         inputs, outs = saved[:n], saved[n:2 * n]
         args, Ws, rmasks = saved[2 * n:3 * n], saved[3 * n:4 * n], saved[4 * n:5 * n]
+        zs = saved[5 * n:6 * n]
         plan, norm, reduce, relus = ctx.plan, ctx.norm, ctx.reduce, ctx.relus
         gW = [None] * n
         gb = [None] * n
@@ -694,6 +713,20 @@ class _GCNStack(torch.autograd.Function):
             am = args[l] if args[l].numel() else None
             W = Ws[l]
             fused = l > 0 and relus[l - 1] and rmasks[l - 1].numel() > 0
+            if zs[l].numel() and (fused or l == 0) and gemm_bwd_supported(W.size(0), W.size(1)):
+                # dW = Z^T dY from the forward's aggregate Z = A h (a dense
+                # pass over Z and dY, no gather); mean: Z is the undivided sum
+                # and dY arrives divided by the counts, so Z^T dY is the same
+                # product.  The gather runs only for dX (+ the lower layer's
+                # ReLU / bias gradient); the bottom layer needs no gather at all.
+                gW[l] = gemm_bwd(zs[l], dY, W, want_dx=False)[0]
+                if fused:
+                    _, dY, db = spmm_xw_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, None,
+                                            W, relu_mask=rmasks[l - 1], row_div=rd)
+                    gb[l - 1] = db if ctx.has_bias[l - 1] else None
+                elif ctx.needs_input_grad[0]:
+                    dx = spmm_xw_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, None, W)[1]
+                continue
             if (_FUSE_XW and
                     spmm_xw_supported(plan.bwd, W.size(0), W.size(1), L.REDUCE_SUM)):
                 # adjoint SpMM + dW + dX (+ the lower layer's ReLU / bias

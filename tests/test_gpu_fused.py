@@ -321,3 +321,53 @@ def test_single_layer_modules_fused_vs_two_launch(cuda, kind):
     torch.testing.assert_close(xa, xb, rtol=1e-4, atol=1e-5)
     for a, b in zip(ga, gb):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("N,E,hub", GRAPHS)
+@pytest.mark.parametrize("deg_norm,aggr,epi", [("sm", "add", "relu"), ("rw", "mean", "relu_div"),
+                                               (None, "add", "store")])
+def test_z_dw_and_dx_only_backward(cuda, oracle, N, E, hub, deg_norm, aggr, epi):
+    """The reassociated backward of the GCN stack: the forward's Z (the
+    aggregate before W; mean: before the division) is bitwise the sum SpMM of
+    X; dW = Z^T dY' (mgcn_gemm_bwd, dW only; mean: dY' = dY / count) is within
+    the fp64-bounded tolerance of the reference's X^T (A^T dY); the dX-only
+    backward (X = NULL, dW = NULL) is bitwise the full fused form's dX and
+    column sums."""
+    from mgcn import _lib as L
+    from mgcn import ops
+    rng = np.random.default_rng(11 * N + E + len(epi))
+    ei = _graph(rng, N, E, hub)
+    F = 128
+    plan, norm = _plan(cuda, ei, N, deg_norm)
+    reduce = L.REDUCE_CODES[aggr]
+    g = torch.Generator(device=cuda).manual_seed(N + 7)
+    X = torch.randn(N, F, device=cuda, generator=g)
+    W = torch.randn(F, F, device=cuda, generator=g) * 0.1
+    dY = torch.randn(N, F, device=cuda, generator=g)
+    Y0 = ops.spmm_xw_fwd(plan.fwd, norm.w_fwd, X, W, reduce)
+    Y, Z = ops.spmm_xw_fwd(plan.fwd, norm.w_fwd, X, W, reduce, want_z=True)
+    assert torch.equal(Y, Y0)
+    Zs = ops.spmm_fwd(plan.fwd, norm.w_fwd, X, L.REDUCE_SUM)
+    Zs = Zs[0] if isinstance(Zs, tuple) else Zs
+    assert torch.equal(Z, Zs)
+    # dW from Z: mean pairs the undivided Z with the pre-divided dY
+    dYp = dY / plan.in_cnt[:, None] if aggr == "mean" else dY
+    dW = ops.gemm_bwd(Z, dYp, W, want_dx=False)[0]
+    dH = ops.spmm_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dYp, L.REDUCE_SUM)
+    ref = X.double().t() @ dH.double()
+    bound = X.double().abs().t() @ dH.double().abs()
+    # two fp32-rounded association orders of the same product
+    assert ((dW.double() - ref).abs() <= 4e-5 * bound + 1e-6).all()
+    rm = ops.make_relu_mask(torch.randn(N, F, device=cuda, generator=g))
+    rd = plan.in_cnt if epi == "relu_div" else None
+    mask = rm if epi in ("relu", "relu_div") else None
+    _, dXa, csa = ops.spmm_xw_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dYp, X, W,
+                                  relu_mask=mask, row_div=rd)
+    dWb, dXb, csb = ops.spmm_xw_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dYp, None, W,
+                                    relu_mask=mask, row_div=rd)
+    assert dWb is None
+    assert torch.equal(dXa, dXb)
+    if mask is not None:
+        assert torch.equal(csa, csb)
+    with pytest.raises(ValueError, match="dX only"):
+        ops.spmm_xw_bwd(plan.bwd, norm.w_bwd, None, dYp, None, W, want_dx=False)
