@@ -294,6 +294,8 @@ size_t mgcn_gemm_bwd_workspace_bytes(int64_t M, int32_t F_in, int32_t F_out);
  * ReLU backward and that layer's bias gradient are fused as in mgcn_gemm_nn:
  *   dX = mask ? dH W^T : 0 (stored / row_div[m] when row_div != NULL),
  *   colsum[n] = sum_m dX[m, n] (undivided).
+ * With dX == NULL and colsum != NULL: colsum[n] = sum_m dH[m, n] (F_out
+ * entries; the bias gradient when dH is a layer output's gradient).
  * Replaces autograd's two matmul adjoints of `torch.matmul(x, self.weight_node)`
  * plus the threshold_backward/sum of gcn_model.py:196 and
  * gcn_base_models.py:240-241 (mgcn_gemm_tn + mgcn_gemm_nn in one launch).

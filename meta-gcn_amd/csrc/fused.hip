@@ -484,6 +484,9 @@ __device__ unsigned long long g_xprof[2][64][6];
 // DW = false: dX only (X == NULL) -- the caller forms dW = Z^T dY from the
 // forward's aggregate (mgcn_gemm_bwd, dW-only), so the chunk's X rows, their
 // images and the dW MFMAs drop out.
+#ifndef XB_META
+#define XB_META 1
+#endif
 template <int U, bool DX, int EPI, bool MAXM, bool DW = true>
 __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(const XbArgs a) {
   __shared__ __attribute__((aligned(16))) char lds[kXbLds];
@@ -583,6 +586,18 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
     }
   };
 
+  // dX only: the row metadata runs one row ahead as in the forward
+  // (gather_row_meta: row k + 1's first edge slots and row k + 2's pointers
+  // load under row k's gathers)
+  const int64_t n_my = my_chunks(n_chunks);
+  const RowSeq seq{(int64_t)blockIdx.x * kXwRows + 2 * wave + grp, (int64_t)gridDim.x * kXwRows,
+                   a.n_rows};
+  RowMeta cur{}, nxt{};
+  if constexpr (!DW && !MAXM && XB_META) {
+    meta_rowptr(a.rowptr, seq.row(0), seq.row(0) < a.n_rows, cur);
+    meta_first(a.col, a.w, gl, cur);
+    meta_rowptr(a.rowptr, seq.row(1), seq.row(1) < a.n_rows, nxt);
+  }
   int it = 0;
   for (int64_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x, ++it) {
     const int64_t r0 = chunk * kXwRows;
@@ -621,8 +636,19 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
       const bool row_ok = row < a.n_rows;
       int deg;
       float acc[4];
-      gather_row<U, MAXM>(rdy, ldy_b, a.rowptr, a.col, a.w, row, row_ok, gl, grp, acc, deg,
-                          a.win_mask, a.slot_map);
+      if constexpr (!DW && !MAXM && XB_META) {
+        const int64_t k = 2 * it + p;
+        meta_first(a.col, a.w, gl, nxt);
+        RowMeta nn;
+        const int64_t rk2 = seq.row(k + 2);
+        meta_rowptr(a.rowptr, rk2, rk2 < a.n_rows && k + 2 < 2 * n_my, nn);
+        gather_row_meta<U>(rdy, ldy_b, a.col, a.w, cur, gl, grp, acc);
+        cur = nxt;
+        nxt = nn;
+      } else {
+        gather_row<U, MAXM>(rdy, ldy_b, a.rowptr, a.col, a.w, row, row_ok, gl, grp, acc, deg,
+                            a.win_mask, a.slot_map);
+      }
       if (a.row_scale != nullptr && row_ok) {
         const float sc = a.row_scale[row];
 #pragma unroll

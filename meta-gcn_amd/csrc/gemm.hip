@@ -1151,7 +1151,10 @@ struct BwBank {
   uint32_t rd; // row divisor of row tid & 31
 };
 
-template <int EPI, bool DX>
+// HCS (dW only): also the column sums of dH -- the bias gradient of the
+// layer whose output gradient dH is (gcn_base_models.py:240) -- from the
+// staged rows, so that pass needs no second read of dH.
+template <int EPI, bool DX, bool HCS = false>
 __global__ __launch_bounds__(kBwThreads, 1) void gemm_bwd_kernel(
     const float *__restrict__ X, int64_t ldx, const float *__restrict__ dH, int64_t lddh,
     const float *__restrict__ W, int64_t ldw, int64_t M, float *__restrict__ dX, int64_t lddx,
@@ -1215,11 +1218,22 @@ __global__ __launch_bounds__(kBwThreads, 1) void gemm_bwd_kernel(
   // the mask / divisor words with the last part; called in pieces between the
   // MFMA steps of the previous chunk so the split VALU work and the LDS
   // writes run under them
+  float hc[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // HCS: dH column sums of float4 tid & 31
   auto stage_part = [&](const BwBank &b, char *buf, int m) {
     const int c4 = tid & 31;
     const int row = 16 * (m & 1) + (tid >> 5);
     const int off = img_off(row, c4 >> 1) + 8 * (c4 & 1);
     const float4 v = __builtin_bit_cast(float4, b.v[m]);
+    if constexpr (HCS) {
+      // every chunk is staged once (chunks past the end as zeros), rows q
+      // then 16 + q: a fixed summation order
+      if (m >= 2) {
+        hc[0] = __fadd_rn(hc[0], v.x);
+        hc[1] = __fadd_rn(hc[1], v.y);
+        hc[2] = __fadd_rn(hc[2], v.z);
+        hc[3] = __fadd_rn(hc[3], v.w);
+      }
+    }
     uint32_t hi[2], mid[2], lo[2];
 #ifdef BW_NO_SPLIT
     hi[0] = b.v[m][0]; hi[1] = b.v[m][1]; mid[0] = b.v[m][2]; mid[1] = b.v[m][3];
@@ -1374,6 +1388,19 @@ __global__ __launch_bounds__(kBwThreads, 1) void gemm_bwd_kernel(
       const int row = 32 * ti + (r & 3) + 8 * (r >> 2) + 4 * h;
       slab[row * kBwF + 32 * (tj0 + s) + lc] = accw[s][r];
     }
+  if constexpr (HCS) {
+    // fold the 16 row groups (tid >> 5) of each column in fixed order; the
+    // loop's last barrier has retired every read of the LDS images
+    float *red = reinterpret_cast<float *>(lds);
+    *reinterpret_cast<float4 *>(red + 4 * tid) = make_float4(hc[0], hc[1], hc[2], hc[3]);
+    __syncthreads();
+    if (tid < kBwF) {
+      float c = 0.0f;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) c = __fadd_rn(c, red[4 * (32 * g + (tid >> 2)) + (tid & 3)]);
+      colsum_partial[(int64_t)blockIdx.x * kBwF + tid] = c;
+    }
+  }
   if constexpr (DX && EPI != EPI_STORE) {
     // fold the four row groups of each column in fixed order
     const float a = __fadd_rn(csum, __shfl_xor(csum, 16, 64));
@@ -1382,11 +1409,11 @@ __global__ __launch_bounds__(kBwThreads, 1) void gemm_bwd_kernel(
   }
 }
 
-template <int EPI, bool DX>
+template <int EPI, bool DX, bool HCS = false>
 int launch_bwd(int grid, const float *X, int64_t ldx, const float *dH, int64_t lddh,
                const float *W, int64_t ldw, int64_t M, float *dX, int64_t lddx,
                const uint32_t *mask, const float *rd, float *dwp, float *csp, hipStream_t s) {
-  hipLaunchKernelGGL((gemm_bwd_kernel<EPI, DX>), dim3(grid), dim3(kBwThreads), 0, s, X, ldx, dH,
+  hipLaunchKernelGGL((gemm_bwd_kernel<EPI, DX, HCS>), dim3(grid), dim3(kBwThreads), 0, s, X, ldx, dH,
                      lddh, W, ldw, M, dX, lddx, mask, rd, dwp, csp);
   return check_launch("gemm_bwd_kernel");
 }
@@ -1419,11 +1446,13 @@ extern "C" int mgcn_gemm_bwd(int64_t M, int32_t F_in, int32_t F_out, const float
                "mgcn_gemm_bwd: relu_mask needs dX and colsum");
   MGCN_REQUIRE(row_div == nullptr || relu_mask != nullptr, "mgcn_gemm_bwd: row_div needs relu_mask");
   hipStream_t s = as_stream(stream);
+  // dW only with colsum: colsum = the column sums of dH (F_out entries)
+  const bool hcs = dX == nullptr && colsum != nullptr;
   if (M == 0) {
     if (!accumulate)
       for (int32_t r = 0; r < F_in; ++r)
         MGCN_HIP_TRY(hipMemsetAsync(dW + r * lddw, 0, sizeof(float) * F_out, s));
-    if (colsum) MGCN_HIP_TRY(hipMemsetAsync(colsum, 0, sizeof(float) * F_in, s));
+    if (colsum) MGCN_HIP_TRY(hipMemsetAsync(colsum, 0, sizeof(float) * (hcs ? F_out : F_in), s));
     return MGCN_OK;
   }
   MGCN_REQUIRE(X && dH && ldx >= F_in && lddh >= F_out && ldx % 4 == 0 && lddh % 4 == 0 &&
@@ -1442,7 +1471,10 @@ extern "C" int mgcn_gemm_bwd(int64_t M, int32_t F_in, int32_t F_out, const float
   const int64_t n_chunks = (M + kBwRows - 1) / kBwRows;
   const int grid = (int)(n_chunks < kBwGrid ? n_chunks : kBwGrid);
   int rc;
-  if (dX == nullptr)
+  if (dX == nullptr && hcs)
+    rc = launch_bwd<EPI_STORE, false, true>(grid, X, ldx, dH, lddh, W, ldw, M, dX, lddx,
+                                            relu_mask, row_div, dwp, csp, s);
+  else if (dX == nullptr)
     rc = launch_bwd<EPI_STORE, false>(grid, X, ldx, dH, lddh, W, ldw, M, dX, lddx, relu_mask,
                                       row_div, dwp, csp, s);
   else if (epi == EPI_RELU_DIV)
@@ -1457,6 +1489,7 @@ extern "C" int mgcn_gemm_bwd(int64_t M, int32_t F_in, int32_t F_out, const float
   if (rc) return rc;
   const int64_t MN = (int64_t)F_in * F_out;
   if (int rc2 = launch_fold(dwp, grid, MN, F_out, dW, lddw, accumulate, s)) return rc2;
+  if (hcs) return launch_colsum_fold(csp, grid, F_out, colsum, s);
   if (epi == EPI_STORE) return MGCN_OK;
   return launch_colsum_fold(csp, grid, F_in, colsum, s);
 }

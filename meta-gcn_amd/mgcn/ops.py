@@ -393,11 +393,14 @@ def gemm_bwd_supported(F_in: int, F_out: int) -> bool:
 
 def gemm_bwd(x: torch.Tensor, dH: torch.Tensor, W: torch.Tensor, want_dx: bool = True,
              relu_mask: torch.Tensor | None = None, row_div: torch.Tensor | None = None,
-             dW_out: torch.Tensor | None = None, accumulate: bool = False):
+             dW_out: torch.Tensor | None = None, accumulate: bool = False,
+             dh_colsum: bool = False):
     """Both adjoints of H = x @ W in one pass (``mgcn_gemm_bwd``, F_in = F_out
     = 128): dW = x^T dH and dX = dH W^T -- with ``relu_mask`` the lower
     layer's ReLU backward and bias-gradient column sums fused as in
-    :func:`gemm_nn`.  Returns (dW, dX or None, colsum or None)."""
+    :func:`gemm_nn`.  ``dh_colsum`` (dW only): colsum = the column sums of dH
+    (a bias gradient) from the same pass.  Returns (dW, dX or None, colsum or
+    None)."""
     lib = L.load()
     x = _contig_f32(x, "x")
     dH = _contig_f32(dH, "dH")
@@ -415,6 +418,10 @@ def gemm_bwd(x: torch.Tensor, dH: torch.Tensor, W: torch.Tensor, want_dx: bool =
                                                        device=dev)
     dX = torch.empty(M, F_in, dtype=torch.float32, device=dev) if want_dx else None
     colsum = None
+    if dh_colsum:
+        if want_dx or relu_mask is not None:
+            raise ValueError("gemm_bwd: dh_colsum is the dW-only form's")
+        colsum = torch.empty(F_out, dtype=torch.float32, device=dev)
     if relu_mask is not None:
         if not want_dx:
             raise ValueError("gemm_bwd: relu_mask needs want_dx")
@@ -606,22 +613,41 @@ class _LayerXW(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, W, bias, plan: GraphPlan, norm: NormPlan, reduce: int, relu: bool):
-        Y = spmm_xw_fwd(plan.fwd, norm.w_fwd, x, W, reduce, bias, relu)
+        # Z = the aggregate before W: dW = Z^T dY needs no second gather
+        want_z = bool(ctx.needs_input_grad[1]) and gemm_bwd_supported(W.size(0), W.size(1))
+        Y = spmm_xw_fwd(plan.fwd, norm.w_fwd, x, W, reduce, bias, relu, want_z=want_z)
+        Y, Z = Y if want_z else (Y, None)
         ctx.plan, ctx.norm, ctx.reduce, ctx.relu = plan, norm, reduce, relu
         ctx.has_bias = bias is not None
-        ctx.save_for_backward(x, W, Y if relu else None)
+        ctx.save_for_backward(x, W, Y if relu else None, Z)
         return Y
 
     @staticmethod
     def backward(ctx, dZ):
-        x, W, Y = ctx.saved_tensors
+        x, W, Y, Z = ctx.saved_tensors
         plan, norm = ctx.plan, ctx.norm
         need_b = ctx.has_bias and ctx.needs_input_grad[2]
         mean = ctx.reduce == L.REDUCE_MEAN
-        dY, db = relu_bwd_colsum(dZ.contiguous(), Y, ctx.relu, need_b,
-                                 row_div=plan.in_cnt if mean else None)
-        dW, dx, _ = spmm_xw_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, x, W,
-                                want_dx=ctx.needs_input_grad[0])
+        if Z is None:
+            dY, db = relu_bwd_colsum(dZ.contiguous(), Y, ctx.relu, need_b,
+                                     row_div=plan.in_cnt if mean else None)
+            dW, dx, _ = spmm_xw_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, x, W,
+                                    want_dx=ctx.needs_input_grad[0])
+            return dx, dW, db, None, None, None, None
+        # reassociated: dW = Z^T dY (mean: undivided Z, dY / count) on the
+        # dense dW pass, the gather only for dx
+        hcs = need_b and not ctx.relu and not mean  # db from the dW pass
+        if hcs:
+            dY, db = dZ.contiguous(), None
+        else:
+            dY, db = relu_bwd_colsum(dZ.contiguous(), Y, ctx.relu, need_b,
+                                     row_div=plan.in_cnt if mean else None)
+        dW, _, cs = gemm_bwd(Z, dY, W, want_dx=False, dh_colsum=hcs)
+        if hcs:
+            db = cs
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = spmm_xw_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, None, W)[1]
         return dx, dW, db, None, None, None, None
 
 
@@ -705,21 +731,36 @@ class _GCNStack(torch.autograd.Function):
         mean = reduce == L.REDUCE_MEAN
         rd = plan.in_cnt if mean else None
         adj = L.REDUCE_SUM if mean else reduce
-        dY, db = relu_bwd_colsum(dZ.contiguous(), outs[top], relus[top], ctx.has_bias[top],
-                                 row_div=rd)
-        gb[top] = db
+
+        def z_path(l):  # dW = Z^T dY from the forward's aggregate (below)
+            fused = l > 0 and relus[l - 1] and rmasks[l - 1].numel() > 0
+            return bool(zs[l].numel() and (fused or l == 0) and
+                        gemm_bwd_supported(Ws[l].size(0), Ws[l].size(1)))
+
+        top_z = z_path(top) and not relus[top] and rd is None
+        if top_z:
+            # dY = dZ as it is: its column sums (the top bias gradient) come
+            # from the dW = Z^T dY pass below, no separate read of dZ
+            dY = dZ.contiguous()
+        else:
+            dY, db = relu_bwd_colsum(dZ.contiguous(), outs[top], relus[top], ctx.has_bias[top],
+                                     row_div=rd)
+            gb[top] = db
         dx = None
         for l in range(top, -1, -1):
             am = args[l] if args[l].numel() else None
             W = Ws[l]
             fused = l > 0 and relus[l - 1] and rmasks[l - 1].numel() > 0
-            if zs[l].numel() and (fused or l == 0) and gemm_bwd_supported(W.size(0), W.size(1)):
+            if z_path(l):
                 # dW = Z^T dY from the forward's aggregate Z = A h (a dense
                 # pass over Z and dY, no gather); mean: Z is the undivided sum
                 # and dY arrives divided by the counts, so Z^T dY is the same
                 # product.  The gather runs only for dX (+ the lower layer's
                 # ReLU / bias gradient); the bottom layer needs no gather at all.
-                gW[l] = gemm_bwd(zs[l], dY, W, want_dx=False)[0]
+                hcs = bool(top_z and l == top and ctx.has_bias[top])
+                gW[l], _, cs = gemm_bwd(zs[l], dY, W, want_dx=False, dh_colsum=hcs)
+                if hcs:
+                    gb[top] = cs
                 if fused:
                     _, dY, db = spmm_xw_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, None,
                                             W, relu_mask=rmasks[l - 1], row_div=rd)

@@ -358,6 +358,10 @@ def test_z_dw_and_dx_only_backward(cuda, oracle, N, E, hub, deg_norm, aggr, epi)
     bound = X.double().abs().t() @ dH.double().abs()
     # two fp32-rounded association orders of the same product
     assert ((dW.double() - ref).abs() <= 4e-5 * bound + 1e-6).all()
+    # the dW-only pass with dH's column sums (the top layer's bias gradient)
+    dW2, dX2, cs = ops.gemm_bwd(Z, dYp, W, want_dx=False, dh_colsum=True)
+    assert dX2 is None and torch.equal(dW2, dW)
+    torch.testing.assert_close(cs.double(), dYp.double().sum(0), rtol=1e-5, atol=1e-4)
     rm = ops.make_relu_mask(torch.randn(N, F, device=cuda, generator=g))
     rd = plan.in_cnt if epi == "relu_div" else None
     mask = rm if epi in ("relu", "relu_div") else None
