@@ -375,6 +375,10 @@ def main():
                 if name == "spmm_xw_bwd":
                     b += 4 * rows_local * F
                     fl *= 2
+                elif name == "spmm_xw_fwd_z":
+                    b += 4 * rows_local * F  # the aggregate Z written beside Y
+                elif name == "spmm_xw_bwd_dx":
+                    b += 16 * rows_local  # dX only: the lower layer's ReLU mask words
                 elif name == "spmm_xw_bwd_dw":
                     pass  # X read instead of the output write: the same count
                 kern[name] = dict(s, bytes=b, gbs=b / (s["avg_ms"] * 1e-3) / 1e9, flop=fl,

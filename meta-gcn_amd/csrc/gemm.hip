@@ -1154,6 +1154,9 @@ struct BwBank {
 // HCS (dW only): also the column sums of dH -- the bias gradient of the
 // layer whose output gradient dH is (gcn_base_models.py:240) -- from the
 // staged rows, so that pass needs no second read of dH.
+#ifndef MGCN_BW_DEPTH_DW
+#define MGCN_BW_DEPTH_DW 2
+#endif
 template <int EPI, bool DX, bool HCS = false>
 __global__ __launch_bounds__(kBwThreads, 1) void gemm_bwd_kernel(
     const float *__restrict__ X, int64_t ldx, const float *__restrict__ dH, int64_t lddh,
@@ -1359,25 +1362,37 @@ __global__ __launch_bounds__(kBwThreads, 1) void gemm_bwd_kernel(
     }
   };
 
-  BwBank b0, b1;
+  // D register banks (dW only: 4, so three chunks are in flight under each
+  // chunk's MFMAs; with dX: 2, the registers of the dX pass)
+  constexpr int D = DX ? 2 : MGCN_BW_DEPTH_DW;
+  static_assert(D % 2 == 0, "chunk i reads LDS buffer i & 1: the bank count must be even");
+  BwBank bk[D];
   const int64_t c0 = blockIdx.x;
   const int64_t G = gridDim.x;
-  load(c0, b0);
-  load(c0 + G, b1);
-  if (c0 < n_chunks) stage(b0, lds);
+#pragma unroll
+  for (int j = 0; j < D; ++j) load(c0 + j * G, bk[j]);
+  stage(bk[0], lds);  // the grid never exceeds the chunk count
   __syncthreads();
-  // iteration m: compute chunk c0 + m G from buffer m & 1, prefetch chunk
-  // m + 2 into the bank chunk m came from, stage chunk m + 1 into the other buffer
+  // chunk i (= c0 + i G, bank i % D, LDS buffer i & 1): its bank was staged
+  // during chunk i - 1, so it takes the prefetch of chunk i + D; the MFMAs
+  // read buffer i & 1 while chunk i + 1 is staged into the other buffer
   // (a chunk past the end stages zeros that are never read: no branches)
-  for (int64_t c = c0; c < n_chunks; c += 2 * G) {
-    load(c + 2 * G, b0);
-    compute(c, lds, b1, lds + kBwBuf);
-    __syncthreads();
-    if (c + G >= n_chunks) break;
-    load(c + 3 * G, b1);
-    compute(c + G, lds + kBwBuf, b0, lds);
-    __syncthreads();
+  // 32-bit chunk counters: the loop tests stay scalar (a 64-bit compare
+  // takes a VGPR temporary, whose reuse made the latch wait for every load)
+  const int n_my = c0 < n_chunks ? (int)((n_chunks - 1 - c0) / G) + 1 : 0;
+  for (int i = 0; i < n_my; i += D) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      // leave both loops at once: a break into the latch would merge the
+      // partial iterations' load counts into the back edge (vmcnt(4) waits)
+      if (j > 0 && i + j >= n_my) goto chunks_done;
+      const int64_t ci = c0 + (int64_t)(i + j) * G;
+      load(ci + D * G, bk[j]);
+      compute(ci, lds + (j & 1) * kBwBuf, bk[(j + 1) % D], lds + ((j + 1) & 1) * kBwBuf);
+      __syncthreads();
+    }
   }
+chunks_done:
 
   // dW partial slab of this workgroup; C map: col = lc, row = (r & 3) + 8 (r >> 2) + 4 h
   float *slab = dw_partial + (int64_t)blockIdx.x * kBwF * kBwF;

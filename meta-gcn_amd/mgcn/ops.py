@@ -131,8 +131,9 @@ def spmm_xw_fwd(view: CSRView, w: torch.Tensor | None, X: torch.Tensor, W: torch
             raise ValueError(f"bias has {bias.numel()} entries, expected {F_out}")
     Y = torch.empty(view.n_rows, F_out, dtype=torch.float32, device=dev)
     Z = torch.empty(view.n_rows, F_in, dtype=torch.float32, device=dev) if want_z else None
+    tname = "spmm_xw_fwd_z" if want_z else "spmm_xw_fwd"
     if _TIMER is not None:
-        _TIMER("spmm_xw_fwd", True)
+        _TIMER(tname, True)
     with L.device_guard(dev):
         rc = lib.mgcn_spmm_xw_fwd(view.n_rows, view.n_cols, F_in, F_out, L.ptr(view.rowptr),
                                   L.ptr(view.col), L.ptr(w), L.ptr(X), X.stride(0), L.ptr(W),
@@ -140,7 +141,7 @@ def spmm_xw_fwd(view: CSRView, w: torch.Tensor | None, X: torch.Tensor, W: torch
                                   int(bool(relu)), L.ptr(relu_mask), L.ptr(Z),
                                   Z.stride(0) if Z is not None else 0, L.stream_of(dev))
     if _TIMER is not None:
-        _TIMER("spmm_xw_fwd", False)
+        _TIMER(tname, False)
     L.check(rc, "mgcn_spmm_xw_fwd")
     return (Y, Z) if want_z else Y
 

@@ -20,7 +20,9 @@ sys.path.insert(0, ROOT)
 from bench import spmm_bytes  # noqa: E402
 
 N, NNZ, F = 1_000_000, 11_000_000, 128
-KERNELS = {"fwd": "spmm_xw_fwd_kernel", "bwd": "spmm_xw_bwd_kernel", "bwd_dw": "spmm_xw_bwd_kernel"}
+KERNELS = {"fwd": "spmm_xw_fwd_kernel", "fwd_z": "spmm_xw_fwd_kernel",
+           "bwd": "spmm_xw_bwd_kernel", "bwd_dw": "spmm_xw_bwd_kernel",
+           "bwd_dx": "spmm_xw_bwd_kernel", "gemm_dw": "gemm_bwd_kernel"}
 
 
 def per_kernel(d, counter):
@@ -68,13 +70,22 @@ def main():
             continue
         alg = spmm_bytes(N, NNZ, F)
         streamed = 0.0
-        if kind.startswith("bwd"):
+        if kind in ("bwd", "bwd_dw"):
             streamed = 4.0 * N * F  # X rows, read once
-        # the streamed part reported at 1 / copy_factor, the rest at 1 / gather_factor
-        read = streamed + gather_factor * max(fk - streamed / copy_factor, 0.0)
-        name = {"fwd": "spmm_xw_fwd", "bwd": "spmm_xw_bwd", "bwd_dw": "spmm_xw_bwd_dw"}[kind]
+        name = {"fwd": "spmm_xw_fwd", "fwd_z": "spmm_xw_fwd_z", "bwd": "spmm_xw_bwd",
+                "bwd_dw": "spmm_xw_bwd_dw", "bwd_dx": "spmm_xw_bwd_dx",
+                "gemm_dw": "gemm_bwd_dw"}[kind]
         if kind == "bwd":
             alg += 4 * N * F
+        elif kind == "fwd_z":
+            alg += 4 * N * F
+        elif kind == "bwd_dx":
+            alg += 16 * N
+        elif kind == "gemm_dw":  # a dense pass: X and dY streamed, 128 x 128 partials written
+            alg = 8 * N * F
+            streamed = float(alg)
+        # the streamed part reported at 1 / copy_factor, the rest at 1 / gather_factor
+        read = streamed + gather_factor * max(fk - streamed / copy_factor, 0.0)
         res["kernels"][name] = {"FETCH_SIZE_bytes": fk, "WRITE_SIZE_bytes": wk,
                                 "read_bytes_corrected": read, "traffic_bytes": read + wk,
                                 "algorithmic_bytes": alg}

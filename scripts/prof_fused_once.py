@@ -1,5 +1,6 @@
 """Run one fused layer kernel a few times on the config-2 graph for
-rocprofv3 PMC passes:  python scripts/prof_fused_once.py {fwd,bwd,bwd_dw} [reps]"""
+rocprofv3 PMC passes:
+    python scripts/prof_fused_once.py {fwd,fwd_z,bwd,bwd_dw,bwd_dx,gemm_dw,spmm} [reps]"""
 import os
 import sys
 
@@ -29,6 +30,10 @@ fn = {"fwd": lambda: ops.spmm_xw_fwd(plan.fwd, norm.w_fwd, X, W, L.REDUCE_SUM, b
                                      relu_mask=rm),
       "bwd": lambda: ops.spmm_xw_bwd(plan.bwd, norm.w_bwd, None, dY, X, W, relu_mask=rm),
       "bwd_dw": lambda: ops.spmm_xw_bwd(plan.bwd, norm.w_bwd, None, dY, X, W, want_dx=False),
+      "fwd_z": lambda: ops.spmm_xw_fwd(plan.fwd, norm.w_fwd, X, W, L.REDUCE_SUM, b, True,
+                                       relu_mask=rm, want_z=True),
+      "bwd_dx": lambda: ops.spmm_xw_bwd(plan.bwd, norm.w_bwd, None, dY, None, W, relu_mask=rm),
+      "gemm_dw": lambda: ops.gemm_bwd(X, dY, W, want_dx=False, dh_colsum=True),
       "spmm": lambda: ops.spmm_bwd(plan.bwd, norm.w_bwd, None, dY, L.REDUCE_SUM)}[kind]
 for _ in range(reps):
     fn()
