@@ -870,6 +870,7 @@ int launch_relu_mask(int64_t n, int F, const float *Y, int64_t ldy, const int32_
 
 int g_force_vec = 0;  // tuning knobs (mgcn_set_option)
 int g_unroll = 8;
+bool g_unroll_set = false;  // spmm_unroll given explicitly: every mode takes it
 int g_heavy_side = 1;  // heavy-row launch on a side stream (concurrent)
 
 template <int VEC, int G, int U, int MODE>
@@ -894,7 +895,9 @@ int launch_g(const SpmmArgs &a, hipStream_t stream) {
   }
   if (lanes > 16) {
     if (g_unroll == 16) return launch_one<VEC, 32, 16, MODE>(a, stream);
-    if (g_unroll == 4) return launch_one<VEC, 32, 4, MODE>(a, stream);
+    // the forward max at U = 8 holds 113 VGPRs (4 waves per SIMD); at U = 4
+    // it fits 93 (5 waves), the sum kernel's occupancy
+    if (g_unroll == 4 || (MODE == FWD_MAX && !g_unroll_set)) return launch_one<VEC, 32, 4, MODE>(a, stream);
     return launch_one<VEC, 32, 8, MODE>(a, stream);
   }
   if (lanes > 8) return launch_one<VEC, 16, 8, MODE>(a, stream);
@@ -1053,6 +1056,7 @@ extern "C" int mgcn_set_option(const char *name, int value) {
   if (n == "spmm_unroll") {
     MGCN_REQUIRE(value == 4 || value == 8 || value == 16, "spmm_unroll must be 4, 8 or 16");
     g_unroll = value;
+    g_unroll_set = true;
     return MGCN_OK;
   }
   if (n == "heavy_lds_kb") {
