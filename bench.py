@@ -351,8 +351,10 @@ def main():
         "arithmetic": ("aggregation fp32 (bitwise = reference); dense x@W / dW / dX products as "
                        "bf16x6 (exact 3-term bf16 split of each fp32 operand, 6 MFMA products, "
                        "fp32 accumulate; error at fp32 level, tests/test_gpu_parity.py); "
-                       "layers fused as (A x) W in one launch per direction "
-                       "(mgcn_spmm_xw_fwd / _bwd; tests/test_gpu_fused.py)"),
+                       "forward fused as (A x) W in one launch per layer, keeping Z = A x; "
+                       "backward dW = Z^T dY in one dense pass (mgcn_gemm_bwd) and dX from a "
+                       "gather of A^T dY (mgcn_spmm_xw_bwd, dX only); the bottom layer runs "
+                       "no gather (tests/test_gpu_fused.py)"),
         "config": {"workload": workload, "nodes": N, "edges": n_edges, "nnz": nnz, "feat": F,
                    "layers": L, "global_batch": world if do_replica else 1,
                    "parallelism": parallelism},

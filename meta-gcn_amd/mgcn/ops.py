@@ -676,7 +676,12 @@ class _GCNStack(torch.autograd.Function):
     layer l's dX GEMM (mgcn_gemm_nn with Z), instead of a separate pass.
     Per layer: GEMM -> SpMM(+bias, ReLU) forward; SpMM^T, dW (split-K), dX
     (+ fused ReLU/bias of the layer below) backward.  Same math and the same
-    per-edge summation order as the layer-by-layer modules."""
+    per-edge summation order as the layer-by-layer modules.
+    128 -> 128 sum / mean layers run fused: the forward aggregates then
+    multiplies ((A h) W, one launch) and keeps Z = A h; the backward forms
+    dW = Z^T dY in one dense pass (the top layer's bias gradient from the
+    same pass) and gathers A^T dY only for dX, so the bottom layer runs no
+    gather.  Max keeps the GEMM + SpMM launches (max does not commute with W)."""
 
     @staticmethod
     def forward(ctx, x, plan, norm, reduce, relus, *params):
