@@ -235,8 +235,9 @@ __device__ __forceinline__ void gather_row_meta(const __amdgpu_buffer_rsrc_t rx,
 
 // The row sequence of one lane group in the chunk loop: row k is slot
 // 16 (k & 1) + 2 wave + grp of the workgroup's chunk k >> 1 (chunks
-// blockIdx.x + i gridDim.x).  Used by the forward (-2.5 %); the backward has
-// no registers to spare for the extra state (its spills cost more).
+// blockIdx.x + i gridDim.x).  Used by the forward (-2.5 %) and the dX-only
+// backward (-0.5 %); the dW + dX backward has no registers to spare for the
+// extra state (its spills cost more).
 struct RowSeq {
   int64_t base;  // blockIdx.x * 32 + 2 wave + grp
   int64_t step;  // gridDim.x * 32
@@ -438,7 +439,8 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_fwd_kernel(c
 // chunk), the chunk's mask / divisor words, the dX staging tile.  dX: wave w
 // owns columns 16 w .. +15; its W^T fragments are re-read from L2 (W is
 // 64 KB) and split per chunk -- held for the whole kernel they would take 48
-// VGPRs beside the gather's and dW's.
+// VGPRs beside the gather's and dW's (the dX-only form, DW = false, holds
+// them: it has no dW accumulators).
 constexpr int kXbHOff = 3 * kXwImg;
 constexpr int kXbMaskOff = 6 * kXwImg;                 // [32][4] mask words
 constexpr int kXbDivOff = kXbMaskOff + kXwRows * 16;   // [32] row divisors
