@@ -30,6 +30,14 @@ _TIMER = None  # optional callable(name, start: bool), e.g. bench.py's HIP-event
 _FUSE_XW = os.environ.get("MGCN_FUSE_XW", "1") != "0"
 
 
+# Middle layers of a stack (dX wanted, a ReLU mask below) keep the dW + dX
+# gather kernel: Z write + dW pass + dX-only gather cost 1.18 ms there
+# against 1.15 for the one kernel; the top layer (its bias gradient rides in
+# the dW pass) and the bottom layer (no gather at all) take the Z form.
+# MGCN_Z_MIDDLE=1 sends the middle layers through Z as well.
+_Z_MIDDLE = os.environ.get("MGCN_Z_MIDDLE", "0") != "0"
+
+
 def set_fused_layers(enabled: bool) -> None:
     """Use (True, the default) or bypass the fused aggregate+transform layer
     kernels (mgcn_spmm_xw_fwd / _bwd) where they apply."""
@@ -699,7 +707,9 @@ class _GCNStack(torch.autograd.Function):
             if _FUSE_XW and spmm_xw_supported(plan.fwd, W.size(0), W.size(1), reduce):
                 # (A h) W in one launch: h @ W is never written (sum / mean);
                 # the aggregate A h is kept for dW = (A h)^T dY
-                want_z = bool(ctx.needs_input_grad[5 + 2 * i])
+                # middle layers keep the dW + dX gather kernel (_Z_MIDDLE)
+                middle = 0 < i < len(Ws) - 1 and relus[i - 1]
+                want_z = bool(ctx.needs_input_grad[5 + 2 * i]) and (_Z_MIDDLE or not middle)
                 h, am = spmm_xw_fwd(plan.fwd, norm.w_fwd, h, W, reduce, b, relu,
                                     relu_mask=rm, want_z=want_z), None
                 if want_z:
