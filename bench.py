@@ -178,10 +178,9 @@ class KernelTimer:
 
 
 # ------------------------------------------------------------ main
-def build_stack(dev, ei_cpu, X, Ws, bs, dY):
-    """Single-GPU config-2 model (GCNStack of GCNLayers, the fused libmgcn
-    path) on one graph; returns (step, params).  The step is fwd + bwd to
-    every weight and bias against the fixed upstream gradient dY."""
+def make_stack(dev, Ws, bs):
+    """The config-2 model: GCNStack of GCNLayers (NodeModelAdditive 'sm' /
+    'add' + bias, ReLU between layers) holding the given weights."""
     from mgcn.models import GCNLayer, GCNStack
     L = len(Ws)
     F = Ws[0].shape[0]
@@ -194,7 +193,14 @@ def build_stack(dev, ei_cpu, X, Ws, bs, dY):
             nm.weight_node.copy_(Ws[i])
             nm.bias.copy_(bs[i])
         layers.append(layer)
-    stack = GCNStack(layers)
+    return GCNStack(layers)
+
+
+def build_stack(dev, ei_cpu, X, Ws, bs, dY):
+    """Single-GPU config-2 model (:func:`make_stack`, the fused libmgcn path)
+    on one graph; returns (step, params).  The step is fwd + bwd to every
+    weight and bias against the fixed upstream gradient dY."""
+    stack = make_stack(dev, Ws, bs)
     params = list(stack.parameters())
     ei = ei_cpu.to(dev)
     Xd = X.to(dev)

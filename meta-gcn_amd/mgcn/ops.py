@@ -45,6 +45,14 @@ def set_fused_layers(enabled: bool) -> None:
     _FUSE_XW = bool(enabled)
 
 
+def set_z_middle(enabled: bool) -> None:
+    """Send the middle layers of a fused stack through the Z^T dY + dX-only
+    backward too (True; env MGCN_Z_MIDDLE=1) or keep them on the one dW + dX
+    gather kernel (False, the default)."""
+    global _Z_MIDDLE
+    _Z_MIDDLE = bool(enabled)
+
+
 def set_kernel_timer(timer) -> None:
     """Install (or clear with None) a hook called right before and after each
     libmgcn launch, on the launch stream -- used to time kernels with events."""
@@ -105,11 +113,34 @@ def spmm_fwd(view: CSRView, w: torch.Tensor | None, H: torch.Tensor, reduce: int
     return Y, (mask if mask is not None else argmax)
 
 
-def spmm_xw_supported(view: CSRView, F_in: int, F_out: int, reduce: int) -> bool:
-    """True when :func:`spmm_xw_fwd` takes this layer: 128 -> 128, sum or mean,
-    and no heavy rows (skewed graphs keep the GEMM + heavy-row SpMM path)."""
-    return (view.n_heavy == 0 and
+# The fused kernels address the gathered table (X forward, dY backward) with
+# 32-bit byte offsets: mgcn_spmm_xw_fwd / _bwd reject a table of more than
+# 4 GiB - 16 bytes (fused.hip, the n_cols * ld * 4 checks), i.e. more than
+# 8,388,607 rows at F = 128.  Larger graphs take the two-launch path, whose
+# SpMM indexes with 64-bit offsets.
+XW_MAX_TABLE_BYTES = 0xfffffff0
+
+
+def spmm_xw_supported(view: CSRView, F_in: int, F_out: int, reduce: int,
+                      ld: int | None = None) -> bool:
+    """True when :func:`spmm_xw_fwd` (``view`` the fwd view, gathering [n_cols,
+    F_in] rows of leading dimension ``ld``) or :func:`spmm_xw_bwd` (``view``
+    the bwd view, gathering dY, F_in / F_out swapped) takes this layer:
+    128 -> 128, sum or mean, no heavy rows (skewed graphs keep the GEMM +
+    heavy-row SpMM path) and a gathered table within the kernels' 32-bit
+    offsets (:data:`XW_MAX_TABLE_BYTES`)."""
+    ld = int(F_in) if ld is None else max(int(ld), int(F_in))
+    return (view.n_heavy == 0 and 0 < view.n_cols * ld * 4 <= XW_MAX_TABLE_BYTES and
             bool(L.load().mgcn_spmm_xw_supported(int(F_in), int(F_out), int(reduce))))
+
+
+def layer_fusable(plan: GraphPlan, x: torch.Tensor, W: torch.Tensor, reduce: int) -> bool:
+    """Both directions of a layer on ``plan`` fit the fused kernels: the
+    forward gathers x over the fwd view, the backward dY over the bwd view."""
+    return (x.dim() == 2 and x.dtype == torch.float32 and W.dtype == torch.float32 and
+            x.is_cuda and x.size(0) == plan.fwd.n_cols == plan.fwd.n_rows and
+            spmm_xw_supported(plan.fwd, W.size(0), W.size(1), reduce, x.stride(0)) and
+            spmm_xw_supported(plan.bwd, W.size(1), W.size(0), L.REDUCE_SUM))
 
 
 def spmm_xw_fwd(view: CSRView, w: torch.Tensor | None, X: torch.Tensor, W: torch.Tensor,
@@ -137,6 +168,14 @@ def spmm_xw_fwd(view: CSRView, w: torch.Tensor | None, X: torch.Tensor, W: torch
         bias = bias.detach().to(torch.float32).contiguous()
         if bias.numel() != F_out:
             raise ValueError(f"bias has {bias.numel()} entries, expected {F_out}")
+    if relu_mask is not None:
+        # the kernel writes n_rows x 16 B of mask words through this pointer
+        if not relu:
+            raise ValueError("spmm_xw_fwd: relu_mask needs relu")
+        if (relu_mask.shape != (view.n_rows, 4) or relu_mask.dtype != torch.int32 or
+                not relu_mask.is_contiguous() or relu_mask.data_ptr() % 16):
+            raise ValueError(f"spmm_xw_fwd: relu_mask must be a contiguous, 16-byte aligned "
+                             f"int32 [{view.n_rows}, 4] tensor")
     Y = torch.empty(view.n_rows, F_out, dtype=torch.float32, device=dev)
     Z = torch.empty(view.n_rows, F_in, dtype=torch.float32, device=dev) if want_z else None
     tname = "spmm_xw_fwd_z" if want_z else "spmm_xw_fwd"
@@ -662,18 +701,23 @@ class _LayerXW(torch.autograd.Function):
 
 def gcn_layer(x: torch.Tensor, W: torch.Tensor, plan: GraphPlan, norm: NormPlan,
               aggr: str = "add", bias: torch.Tensor | None = None,
-              relu: bool = False) -> torch.Tensor:
+              relu: bool = False, aggregate_first: bool = False) -> torch.Tensor:
     """``aggregate_plan(x @ W, plan, norm, aggr, bias, relu)`` -- the
     reference's ``x @ weight_node`` then gather / scale / scatter (+ bias,
     ReLU) (gcn_base_models.py:201-241) -- as one fused launch per direction
-    where the kernels apply (128 -> 128, sum / mean, no heavy rows); otherwise
-    the GEMM and the aggregation run as separate launches."""
+    where the kernels apply (128 -> 128, sum / mean, no heavy rows in either
+    view, gathered tables within 4 GiB); otherwise the GEMM and the
+    aggregation run as separate launches, in the order the caller's
+    reference uses: ``aggregate_first`` (PyG SAGEConv: mean_j x_j, then
+    @ W + b) or x @ W first (the default)."""
     reduce = L.REDUCE_CODES[aggr]
-    if (_FUSE_XW and x.dim() == 2 and x.dtype == torch.float32 and W.dtype == torch.float32
-            and x.is_cuda and x.size(0) == plan.fwd.n_cols == plan.fwd.n_rows
-            and spmm_xw_supported(plan.fwd, W.size(0), W.size(1), reduce)
-            and plan.bwd.n_heavy == 0):
+    if _FUSE_XW and layer_fusable(plan, x, W, reduce):
         return _LayerXW.apply(x, W, bias, plan, norm, reduce, bool(relu))
+    if aggregate_first:
+        out = linear(aggregate_plan(x, plan, norm, aggr), W)
+        if bias is not None:
+            out = out + bias
+        return torch.relu(out) if relu else out
     return aggregate_plan(linear(x, W), plan, norm, aggr, bias, relu)
 
 
@@ -704,12 +748,20 @@ class _GCNStack(torch.autograd.Function):
             rm = None
             if relu and nxt is not None and gemm_nn_supported(nxt.size(1), nxt.size(0)):
                 rm = torch.empty(plan.fwd.n_rows, 4, dtype=torch.int32, device=h.device)
-            if _FUSE_XW and spmm_xw_supported(plan.fwd, W.size(0), W.size(1), reduce):
+            if _FUSE_XW and spmm_xw_supported(plan.fwd, W.size(0), W.size(1), reduce,
+                                              h.stride(0)):
                 # (A h) W in one launch: h @ W is never written (sum / mean);
-                # the aggregate A h is kept for dW = (A h)^T dY
+                # the aggregate A h is kept for dW = (A h)^T dY when the
+                # backward takes that form (same predicate as its z_path):
+                # the bottom layer, or one whose lower layer left a ReLU
+                # mask, with the dX-only gather possible on the bwd view;
                 # middle layers keep the dW + dX gather kernel (_Z_MIDDLE)
+                below = i == 0 or (relus[i - 1] and rmasks[i - 1] is not None)
                 middle = 0 < i < len(Ws) - 1 and relus[i - 1]
-                want_z = bool(ctx.needs_input_grad[5 + 2 * i]) and (_Z_MIDDLE or not middle)
+                want_z = (bool(ctx.needs_input_grad[5 + 2 * i]) and below and
+                          (_Z_MIDDLE or not middle) and
+                          gemm_bwd_supported(W.size(0), W.size(1)) and
+                          spmm_xw_supported(plan.bwd, W.size(1), W.size(0), L.REDUCE_SUM))
                 h, am = spmm_xw_fwd(plan.fwd, norm.w_fwd, h, W, reduce, b, relu,
                                     relu_mask=rm, want_z=want_z), None
                 if want_z:
@@ -751,7 +803,9 @@ class _GCNStack(torch.autograd.Function):
         def z_path(l):  # dW = Z^T dY from the forward's aggregate (below)
             fused = l > 0 and relus[l - 1] and rmasks[l - 1].numel() > 0
             return bool(zs[l].numel() and (fused or l == 0) and
-                        gemm_bwd_supported(Ws[l].size(0), Ws[l].size(1)))
+                        gemm_bwd_supported(Ws[l].size(0), Ws[l].size(1)) and
+                        spmm_xw_supported(plan.bwd, Ws[l].size(1), Ws[l].size(0),
+                                          L.REDUCE_SUM))
 
         top_z = z_path(top) and not relus[top] and rd is None
         if top_z:

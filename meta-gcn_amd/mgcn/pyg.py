@@ -34,7 +34,7 @@ from torch.nn import Parameter
 
 from .graph import cache_key, plan_for
 from .models import glorot, zeros
-from .ops import aggregate_plan, gcn_layer, scatter_
+from .ops import aggregate_plan, gcn_layer, linear, scatter_
 
 
 def uniform(size, tensor):
@@ -96,7 +96,16 @@ def add_remaining_self_loops(edge_index, edge_weight=None, fill_value=1, num_nod
                                  device=edge_weight.device)
         remaining = edge_weight[inv_mask]
         if remaining.numel() > 0:
-            loop_weight[row[inv_mask]] = remaining
+            # PyG's ``loop_weight[row[inv_mask]] = remaining`` on the CPU:
+            # with several loops on one node the last one in COO order wins.
+            # A device index_put picks an arbitrary one, so take the last
+            # position per node explicitly.
+            loops_at = row[inv_mask]
+            pos = torch.arange(loops_at.numel(), device=row.device)
+            last = torch.full((N,), -1, dtype=pos.dtype, device=row.device)
+            last.scatter_reduce_(0, loops_at, pos, reduce='amax')
+            has = last >= 0
+            loop_weight[has] = remaining[last[has]]
         edge_weight = torch.cat([edge_weight[mask], loop_weight], dim=0)
     edge_index = torch.cat([edge_index[:, mask], loop_index], dim=1)
     return edge_index, edge_weight
@@ -221,12 +230,14 @@ class SAGEConv(nn.Module):
         if self.concat:
             out = aggregate_plan(x, plan, norm, 'mean')
             out = torch.cat([x, out], dim=-1)
-            out = torch.matmul(out, self.weight)
+            out = linear(out, self.weight)
             if self.bias is not None:
                 out = out + self.bias
         else:
-            # mean of the neighbourhood, then @ W + b: the fused kernel's own order
-            out = gcn_layer(x, self.weight, plan, norm, 'mean', self.bias)
+            # mean of the neighbourhood, then @ W + b (PyG 1.3's order): one
+            # fused launch where it applies, else the aggregation and the GEMM
+            # in that order
+            out = gcn_layer(x, self.weight, plan, norm, 'mean', self.bias, aggregate_first=True)
         if self.normalize:
             out = F.normalize(out, p=2, dim=-1)
         return out
@@ -258,7 +269,8 @@ class GraphConv(nn.Module):
         plan = plan_for(edge_index, x.size(0))
         norm = plan.norm(None, edge_weight=edge_weight)
         if self.aggr == 'max':
-            agg = aggregate_plan(torch.matmul(x, self.weight), plan, norm, 'max')
+            # max does not commute with W: x @ W on the MFMA GEMM, then the max
+            agg = aggregate_plan(linear(x, self.weight), plan, norm, 'max')
         else:
             agg = gcn_layer(x, self.weight, plan, norm, self.aggr)
         return agg + self.lin(x)

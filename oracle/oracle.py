@@ -144,6 +144,51 @@ def layer_fwd_bwd(x, edge_index, W, b, dZ, deg_norm="sm", aggr="add", relu=False
     return {"H": H, "Z": Z, "dH": dH, "dx": dH @ W.T, "dW": x.T @ dH, "db": db, "argmax": am}
 
 
+# ------------------------------------------------- PyG 1.3 conv restatements
+def add_remaining_self_loops(edge_index, edge_weight=None, fill=1.0, num_nodes=None):
+    """PyG 1.3 ``add_remaining_self_loops`` (not vendored in the reference;
+    used by GCNConv / SAGEConv as kernel/gcn.py:10 and graph_sage.py:10 call
+    them): existing self-loops are dropped, one loop per node is appended, a
+    node that had a loop keeps that loop's weight (last in COO order), the
+    others get ``fill``.  Returns (edge_index, edge_weight or None)."""
+    ei = np.asarray(edge_index, np.int64)
+    N = int(num_nodes if num_nodes is not None else ei.max() + 1)
+    mask = ei[0] != ei[1]
+    loops = np.arange(N, dtype=np.int64)
+    ei2 = np.concatenate([ei[:, mask], np.stack([loops, loops])], 1)
+    if edge_weight is None:
+        return ei2, None
+    ew = np.asarray(edge_weight, np.float32)
+    lw = np.full(N, fill, np.float32)
+    inv = ~mask
+    lw[ei[0][inv]] = ew[inv]
+    return ei2, np.concatenate([ew[mask], lw]).astype(np.float32)
+
+
+def remove_self_loops(edge_index):
+    """PyG 1.3 ``remove_self_loops`` (GINConv, kernel/gin.py:10)."""
+    ei = np.asarray(edge_index, np.int64)
+    return ei[:, ei[0] != ei[1]]
+
+
+def gcnconv_fwd_bwd(x, edge_index, W, b, dZ, edge_weight=None, improved=False):
+    """PyG 1.3 GCNConv forward + backward with the oracle aggregation:
+    add_remaining_self_loops with unit (or given) weights, 'sm' norm over
+    edge_index[0] with the weights, sum, + b.  The
+    matmuls are fp32 numpy, so only W = I results are bit-comparable."""
+    N = x.shape[0]
+    ew = edge_weight
+    if ew is None:
+        ew = np.ones(np.asarray(edge_index).shape[1], np.float32)
+    ei2, ew2 = add_remaining_self_loops(edge_index, ew, 2.0 if improved else 1.0, N)
+    H = (x.astype(np.float32) @ W.astype(np.float32)).astype(np.float32)
+    _, _, norm = degnorm(ei2, N, None, ew2, "sm")
+    Y, _ = aggr_fwd(ei2, H, norm, "add", b)
+    dH, db = aggr_bwd(ei2, dZ, norm, None, "add", want_db=b is not None)
+    return {"y": Y, "dH": dH, "dx": dH @ W.T, "dW": x.T @ dH, "db": db, "edge_index": ei2,
+            "norm": norm}
+
+
 # ---------------------------------------------------------------- torch CPU
 def torch_layer_reference(x, edge_index, W, b, deg_norm="sm", aggr="add", deg=None):
     """The reference's op sequence (gcn_base_models.py:199-243, common.py:37-66)

@@ -2,7 +2,9 @@
 
 Run in the build container (needs /root/reference, read-only):
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py            # gcn_meta cases
+    python tests/golden/make_golden.py hardpool   # HardPooling cases
+    python tests/golden/make_golden.py conv       # GCNConv cases
 
 It imports the reference's own gcn_meta modules
 (/root/reference/src/gcn_meta/models/{gcn_base_models,common,gcn_multi_kernel,
@@ -332,6 +334,72 @@ def main_hardpool():
     print("wrote 4 hardpool fixtures to", OUT_DIR)
 
 
+def add_remaining_self_loops(ei, ew, fill, N):
+    """PyG 1.3 torch_geometric.utils.add_remaining_self_loops (published
+    algorithm; PyG is not vendored in the reference): drop every existing
+    self-loop, append one loop per node at the end; a node that had a loop
+    keeps that loop's weight (the last one in COO order), the others get
+    ``fill``."""
+    mask = ei[0] != ei[1]
+    loops = np.arange(N, dtype=np.int64)
+    ei2 = np.concatenate([ei[:, mask], np.stack([loops, loops])], 1)
+    lw = np.full(N, fill, np.float32)
+    inv = ~mask
+    lw[ei[0][inv]] = ew[inv]  # numpy fancy assignment: the last write wins
+    ew2 = np.concatenate([ew[mask], lw]).astype(np.float32)
+    return ei2, ew2
+
+
+def gcnconv_case(gbm, name, rng, N, E, F, use_ew, improved, identity, isolated=0):
+    """PyG GCNConv(F, F, improved) as kernel/gcn.py uses it, pinned through the
+    reference's own NodeModelAdditive(deg_norm='sm', aggr='add', bias=True):
+    GCNConv.norm + propagate('add') is gcn_base_models.py:199-243 with
+    edge_weight = the unit (or given) weights after add_remaining_self_loops
+    -- the same formula the in-repo copy src/gcn_meta/models/gcn.py:57-86
+    writes (deg over row, dinv[row] * w * dinv[col], message norm * x_j,
+    scatter_add over col, + bias).  The raw graph keeps random self-pairs in
+    the middle of the edge list (the loop handling is part of what is
+    pinned)."""
+    ei = make_graph(rng, N, E, self_loops=False, isolated=isolated)
+    # a few explicit self-pairs mid-list (dropped and re-added as tail loops)
+    k = max(1, N // 25)
+    v = rng.integers(0, N - isolated, k)
+    at = np.sort(rng.integers(0, ei.shape[1], k))
+    ei = np.insert(ei, at, np.stack([v, v]), axis=1).astype(np.int64)
+    ew = rng.uniform(0.1, 2.0, ei.shape[1]).astype(np.float32) if use_ew else None
+    # GCNConv.norm: unit weights first when none are given, THEN the loops
+    # (an existing loop keeps its weight 1, new loops get the fill value)
+    ew_in = ew if ew is not None else np.ones(ei.shape[1], np.float32)
+    ei2, ew2 = add_remaining_self_loops(ei, ew_in, 2.0 if improved else 1.0, N)
+    x = rng.standard_normal((N, F)).astype(np.float32)
+    dZ = rng.standard_normal((N, F)).astype(np.float32)
+    torch.manual_seed(int(rng.integers(0, 2**31)))
+    nm = gbm.NodeModelAdditive(F, F, deg_norm='sm', aggr='add', bias=True)
+    with torch.no_grad():
+        if identity:
+            nm.weight_node.copy_(torch.eye(F))
+        nm.bias.uniform_(-0.5, 0.5)
+    xt = _t(x).requires_grad_(True)
+    y = nm(xt, _t(ei2), edge_weight=_t(ew2))
+    y.backward(_t(dZ))
+    save(name, edge_index=ei, edge_weight=ew, x=x, W=nm.weight_node.detach(), b=nm.bias.detach(),
+         dZ=dZ, y=y, dx=xt.grad, dW=nm.weight_node.grad, db=nm.bias.grad,
+         meta=np.array([int(improved), int(identity), int(use_ew)]))
+
+
+def main_conv():
+    """Only the GCNConv fixtures (``python make_golden.py conv``)."""
+    _, gbm, _ = _import_reference()
+    rng = np.random.default_rng(20261017)
+    gcnconv_case(gbm, "gcnconv_id", rng, 500, 4000, 16, False, False, True, isolated=20)
+    gcnconv_case(gbm, "gcnconv_ew_id", rng, 400, 3000, 32, True, False, True)
+    gcnconv_case(gbm, "gcnconv_improved_id", rng, 400, 3000, 16, False, True, True, isolated=10)
+    gcnconv_case(gbm, "gcnconv_f128_id", rng, 600, 6000, 128, False, False, True)
+    gcnconv_case(gbm, "gcnconv_f128", rng, 600, 6000, 128, False, False, False)
+    gcnconv_case(gbm, "gcnconv_ew_f128", rng, 500, 5000, 128, True, True, False)
+    print("wrote 6 gcnconv fixtures to", OUT_DIR)
+
+
 def main():
     common, gbm, gm = _import_reference()
     rng = np.random.default_rng(20250824)
@@ -386,5 +454,7 @@ def main():
 if __name__ == "__main__":
     if sys.argv[1:] == ["hardpool"]:
         main_hardpool()
+    elif sys.argv[1:] == ["conv"]:
+        main_conv()
     else:
         main()

@@ -232,20 +232,37 @@ def test_fused_kernels_reject_unsupported(cuda):
                         torch.randn(128, 128, device=cuda), L.REDUCE_MAX)
 
 
+def _hub_src_graph(rng, N, E, hub):
+    """Uniform in-degrees, but source 1 has `hub` extra out-edges: the fwd
+    view has no heavy row, the bwd view (the adjoint's rows) has one."""
+    s = np.concatenate([rng.integers(0, N, E), np.ones(hub, np.int64), np.arange(N)])
+    d = np.concatenate([rng.integers(0, N, E), rng.integers(0, N, hub), np.arange(N)])
+    return np.stack([s, d]).astype(np.int64)
+
+
+@pytest.mark.parametrize("z_middle", [False, True], ids=["zmid0", "zmid1"])
+@pytest.mark.parametrize("graph", ["er", "hub_src"])
 @pytest.mark.parametrize("aggr,deg_norm,x_grad", [("add", "sm", True), ("mean", "rw", True),
                                                   ("max", None, True), ("max", "sm", True),
                                                   ("add", "sm", False), ("mean", None, False)])
-def test_gcn_stack_fused_vs_two_launch(cuda, aggr, deg_norm, x_grad):
+def test_gcn_stack_fused_vs_two_launch(cuda, aggr, deg_norm, x_grad, graph, z_middle):
     """The stack with the fused kernels against the same stack on the
     GEMM + SpMM launches: outputs within fp32 association tolerance, dx
     bitwise below the top layer's first adjoint (same dH, same products) up
-    to the forward's differences, all gradients within tolerance."""
+    to the forward's differences, all gradients within tolerance.  'hub_src'
+    has a heavy row in the bwd view only: the fused forward applies, the
+    dX-only gather must not (it falls back to spmm_bwd + gemm_bwd); z_middle
+    sends the middle layer through the Z^T dY form as well."""
     from mgcn import ops
+    from mgcn.graph import plan_for
     from mgcn.models import GCNLayer, GCNStack
     torch.manual_seed(0)
     rng = np.random.default_rng(13)
     N, F = 20000, 128
-    ei = _t(_graph(rng, N, 200000), cuda)
+    ei = _t(_graph(rng, N, 200000) if graph == "er" else _hub_src_graph(rng, N, 200000, 3000),
+            cuda)
+    plan = plan_for(ei, N)
+    assert plan.fwd.n_heavy == 0 and (plan.bwd.n_heavy > 0) == (graph == "hub_src")
     layers = [GCNLayer(F, F, deg_norm=deg_norm, aggr=aggr, bias=True,
                        non_linear='relu' if i < 2 else 'none').to(cuda) for i in range(3)]
     for layer in layers:
@@ -258,6 +275,7 @@ def test_gcn_stack_fused_vs_two_launch(cuda, aggr, deg_norm, x_grad):
     outs = []
     for fused in (True, False):
         ops.set_fused_layers(fused)
+        ops.set_z_middle(z_middle)
         try:
             for p in stack.parameters():
                 p.grad = None
@@ -268,6 +286,7 @@ def test_gcn_stack_fused_vs_two_launch(cuda, aggr, deg_norm, x_grad):
                          [p.grad.clone() for p in stack.parameters()]))
         finally:
             ops.set_fused_layers(True)
+            ops.set_z_middle(False)
     (ya, xa, ga), (yb, xb, gb) = outs
     torch.testing.assert_close(ya, yb, rtol=1e-5, atol=1e-5)
     if x_grad:
@@ -379,3 +398,144 @@ def test_z_dw_and_dx_only_backward(cuda, oracle, N, E, hub, deg_norm, aggr, epi)
         assert torch.equal(csa, csb)
     with pytest.raises(ValueError, match="dX only"):
         ops.spmm_xw_bwd(plan.bwd, norm.w_bwd, None, dYp, None, W, want_dx=False)
+
+
+@pytest.mark.parametrize("acts", [("none", "none"), ("relu", "none"), ("none", "relu", "none")])
+def test_gcn_stack_keeps_z_only_where_the_backward_reads_it(cuda, acts):
+    """The forward stores the aggregate Z of a layer only when the backward
+    forms that layer's dW as Z^T dY: the bottom layer, or a layer whose lower
+    layer ends in a ReLU (its mask feeds the dX-only gather's epilogue).  A
+    layer above a 'none' layer keeps no N x F Z (and its gradients still
+    match the two-launch stack)."""
+    from mgcn import ops
+    from mgcn.models import GCNLayer, GCNStack
+    torch.manual_seed(1)
+    rng = np.random.default_rng(17)
+    N, F = 6000, 128
+    ei = _t(_graph(rng, N, 60000), cuda)
+    n = len(acts)
+    stack = GCNStack([GCNLayer(F, F, deg_norm='sm', aggr='add', bias=True,
+                               non_linear=a).to(cuda) for a in acts])
+    x = torch.randn(N, F, device=cuda, requires_grad=True)
+    dZ = torch.randn(N, F, device=cuda)
+    y = stack(x, ei)
+    zs = y.grad_fn.saved_tensors[5 * n:6 * n]
+    for i in range(n):
+        want = i == 0 or (acts[i - 1] == "relu" and i == n - 1)
+        assert (zs[i].numel() > 0) == want, (i, acts)
+    y.backward(dZ)
+    got = [x.grad.clone()] + [p.grad.clone() for p in stack.parameters()]
+    ops.set_fused_layers(False)
+    try:
+        x.grad = None
+        for p in stack.parameters():
+            p.grad = None
+        stack(x, ei).backward(dZ)
+    finally:
+        ops.set_fused_layers(True)
+    ref = [x.grad] + [p.grad for p in stack.parameters()]
+    for a, b in zip(got, ref):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-3)
+
+
+def test_spmm_xw_fwd_validates_relu_mask(cuda):
+    """A wrongly shaped / typed mask would be an out-of-bounds device write."""
+    from mgcn import _lib as L
+    from mgcn import ops
+    rng = np.random.default_rng(2)
+    N = 300
+    plan, norm = _plan(cuda, _graph(rng, N, 2000), N, "sm")
+    X = torch.randn(N, 128, device=cuda)
+    W = torch.randn(128, 128, device=cuda)
+    for bad in (torch.empty(N - 1, 4, dtype=torch.int32, device=cuda),
+                torch.empty(N, 4, dtype=torch.int64, device=cuda),
+                torch.empty(4, N, dtype=torch.int32, device=cuda).t()):
+        with pytest.raises(ValueError, match="relu_mask"):
+            ops.spmm_xw_fwd(plan.fwd, norm.w_fwd, X, W, L.REDUCE_SUM, relu=True, relu_mask=bad)
+    with pytest.raises(ValueError, match="needs relu"):
+        ops.spmm_xw_fwd(plan.fwd, norm.w_fwd, X, W, L.REDUCE_SUM, relu=False,
+                        relu_mask=torch.empty(N, 4, dtype=torch.int32, device=cuda))
+
+
+def test_fused_gating_beyond_32bit_offsets(cuda):
+    """N = 8.5M nodes at F = 128: the gathered tables (X forward, dY
+    backward) are 4.35 GB, past the fused kernels' 32-bit offsets
+    (mgcn_spmm_xw_fwd / _bwd reject them).  GCNStack and GCNConv must route
+    such graphs to the two-launch path (64-bit offsets) instead of raising;
+    sampled output rows of a GCNConv layer against fp64 (|err| <= 1e-5 *
+    the |.|-weighted sum), and the stack's output and dx equal to the same
+    stack with the fused kernels switched off."""
+    from mgcn import _lib as L
+    from mgcn import ops
+    from mgcn.graph import plan_for
+    from mgcn.models import GCNLayer, GCNStack
+    from mgcn.pyg import GCNConv
+    N, F, E = 8_500_000, 128, 25_000_000
+    g = torch.Generator(device=cuda).manual_seed(0)
+    s = torch.randint(0, N, (E,), device=cuda, generator=g)
+    d = torch.randint(0, N, (E,), device=cuda, generator=g)
+    loops = torch.arange(N, device=cuda)
+    ei = torch.stack([torch.cat([s, loops]), torch.cat([d, loops])])
+    del s, d
+    x = torch.randn(N, F, device=cuda, generator=g)
+    plan = plan_for(ei, N)
+    W = torch.randn(F, F, device=cuda, generator=g) * 0.1
+    assert plan.fwd.n_heavy == 0 and plan.bwd.n_heavy == 0
+    assert not ops.spmm_xw_supported(plan.fwd, F, F, L.REDUCE_SUM)
+    assert not ops.layer_fusable(plan, x, W, L.REDUCE_SUM)
+    from mgcn.graph import CSRView
+    edge = CSRView(rowptr=plan.fwd.rowptr, col=plan.fwd.col, eid=plan.fwd.eid, n_rows=N,
+                   n_cols=8_388_607)  # the largest table the kernels take at F = 128
+    assert ops.spmm_xw_supported(edge, F, F, L.REDUCE_SUM)
+    edge.n_cols += 1
+    assert not ops.spmm_xw_supported(edge, F, F, L.REDUCE_SUM)
+
+    conv = GCNConv(F, F).to(cuda)
+    with torch.no_grad():
+        conv.weight.copy_(W)
+        conv.bias.uniform_(-0.1, 0.1)
+    y = conv(x, ei)
+    torch.cuda.synchronize()
+    rows = torch.from_numpy(np.random.default_rng(1).choice(N, 512, replace=False)).to(cuda)
+    # GCNConv drops the graph's own loops and appends one per node: every
+    # random self-pair is dropped, so the edges are the non-loop pairs + loops
+    src, dst = ei
+    keep = src != dst
+    keep[E:] = True
+    src, dst = src[keep], dst[keep]
+    deg = torch.bincount(src, minlength=N).double()
+    dinv = deg.pow(-0.5)
+    sel = torch.isin(dst, rows)
+    es, ed = src[sel], dst[sel]
+    w = dinv[es] * dinv[ed]
+    H = x[es].double() @ W.double()
+    Hm = x[es].double().abs() @ W.double().abs()
+    pos = torch.searchsorted(rows.sort().values, ed)
+    ref = torch.zeros(rows.numel(), F, dtype=torch.float64, device=cuda)
+    bnd = torch.zeros_like(ref)
+    ref.index_add_(0, pos, H * w[:, None])
+    bnd.index_add_(0, pos, Hm * w[:, None])
+    rs = rows.sort().values
+    ref += conv.bias.double()
+    bnd += conv.bias.double().abs()
+    err = (y[rs].double() - ref).abs()
+    assert bool((err <= 1e-5 * bnd + 1e-6).all()), float((err / bnd).max())
+    del y, conv
+
+    torch.manual_seed(2)
+    stack = GCNStack([GCNLayer(F, F, deg_norm='sm', aggr='add', bias=True,
+                               non_linear=a).to(cuda) for a in ("relu", "none")])
+    xg = x.requires_grad_(True)
+    dZ = torch.randn(N, F, device=cuda, generator=g)
+    outs = []
+    for fused in (True, False):
+        ops.set_fused_layers(fused)
+        try:
+            xg.grad = None
+            yy = stack(xg, ei)
+            yy.backward(dZ)
+            outs.append((yy.detach()[rs], xg.grad[rs].clone()))
+            del yy
+        finally:
+            ops.set_fused_layers(True)
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])

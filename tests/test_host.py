@@ -169,3 +169,28 @@ def test_norm_rejects_grad_requiring_edge_weight_and_deg():
         plan.norm("rw", deg=torch.ones(3, requires_grad=True))
     with pytest.raises(NotImplementedError, match="edge_weight"):
         plan.norm(None, edge_weight=ew)
+
+
+def test_pyg_loop_helpers_match_oracle_restatement(oracle):
+    """mgcn.pyg.add_remaining_self_loops / remove_self_loops (PyG 1.3, torch
+    index bookkeeping) against the oracle's numpy restatement, including
+    several loops on one node (the last one's weight is carried)."""
+    import numpy as np
+    import torch
+    from mgcn.pyg import add_remaining_self_loops, remove_self_loops
+    rng = np.random.default_rng(4)
+    N = 60
+    ei = rng.integers(0, N, (2, 400))
+    ei[1, ::7] = ei[0, ::7]  # many self-pairs, several per node
+    ew = rng.uniform(0.1, 2.0, 400).astype(np.float32)
+    for w in (ew, None):
+        a, aw = add_remaining_self_loops(torch.from_numpy(ei),
+                                         None if w is None else torch.from_numpy(w), 2.0, N)
+        b, bw = oracle.add_remaining_self_loops(ei, w, 2.0, N)
+        np.testing.assert_array_equal(a.numpy(), b)
+        if w is None:
+            assert aw is None and bw is None
+        else:
+            np.testing.assert_array_equal(aw.numpy(), bw)
+    np.testing.assert_array_equal(remove_self_loops(torch.from_numpy(ei))[0].numpy(),
+                                  oracle.remove_self_loops(ei))
