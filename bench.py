@@ -17,11 +17,13 @@ backward to every weight and bias (no optimizer step, as the metric defines).
     edges/s = E * L / t_step          (E = 10M graph edges, loops not counted)
 
 N > 1 GPUs (torch.distributed.run, one rank per GPU, RCCL): `value` is the
-whole job's edges/s of data-parallel replicas (every rank its own config-2
-graph, one bucketed gradient all-reduce per step; `scaling` "weak"); the same
-run also times ONE graph sharded by destination-node range (mgcn.dist) and
-reports it under `sharded` (`scaling` "strong").  `--mode replica|shard`
-measures one of them.
+edges/s of ONE config-2 graph sharded by destination-node range over the N
+ranks (mgcn.dist: the north star's partitioning, chunked RCCL all-gathers of
+the layer activations and upstream gradients over xGMI overlapped with the
+fused layer kernels; `scaling` "strong").  The same run also times
+data-parallel replicas (every rank its own config-2 graph, one bucketed
+gradient all-reduce per step) and reports them under `replicas` (`scaling`
+"weak").  `--mode shard|replica` measures one of them as `value`.
 """
 from __future__ import annotations
 
@@ -155,26 +157,53 @@ def cpu_baseline(ei_cpu, X, W, b, n_edges: int, reps: int = 3):
 
 # ------------------------------------------------------------ kernel timers
 class KernelTimer:
-    """HIP events around every SpMM launch, recorded on the launch stream
-    (mgcn.ops launches on torch's current stream)."""
+    """HIP events around every libmgcn launch, recorded on the launch stream
+    (mgcn.ops launches on torch's current stream), with each launch's row and
+    edge counts for its algorithmic bytes."""
 
     def __init__(self):
         self.events = {}
 
-    def __call__(self, name, start: bool):
+    def __call__(self, name, start: bool, rows=None, edges=None):
         ev = torch.cuda.Event(enable_timing=True)
         ev.record()
         if start:
-            self.events.setdefault(name, []).append([ev, None])
+            self.events.setdefault(name, []).append([ev, None, rows, edges])
         else:
             self.events[name][-1][1] = ev
 
     def summary(self):
         out = {}
-        for name, pairs in self.events.items():
-            ms = [a.elapsed_time(b) for a, b in pairs]
-            out[name] = {"launches": len(ms), "avg_ms": sum(ms) / len(ms)}
+        for name, recs in self.events.items():
+            ms = [a.elapsed_time(b) for a, b, _, _ in recs]
+            out[name] = {"launches": len(ms), "avg_ms": sum(ms) / len(ms), "total_ms": sum(ms),
+                         "sizes": [(r, e) for _, _, r, e in recs]}
         return out
+
+
+def launch_bytes(name: str, rows: int, edges: int, F: int):
+    """(algorithmic HBM bytes, flops) of one libmgcn launch:
+    the SpMM's B_spmm for every gathering kernel, plus the fused kernels'
+    extra streams (Z written, X read, ReLU mask words); the dense dW / dX
+    passes read and write whole [rows, F] tensors."""
+    if name.startswith("spmm_xw"):
+        b = spmm_bytes(rows, edges, F)
+        fl = 2.0 * rows * F * F
+        if name == "spmm_xw_bwd":
+            b += 4 * rows * F     # X rows read beside the gathered dY
+            fl *= 2
+        elif name == "spmm_xw_fwd_z":
+            b += 4 * rows * F     # the aggregate Z written beside Y
+        elif name == "spmm_xw_bwd_dx":
+            b += 16 * rows        # the lower layer's ReLU mask words
+        return b, fl
+    if name.startswith("spmm"):
+        return spmm_bytes(rows, edges, F), 0.0
+    if name == "gemm_bwd":        # dW and dX: X, dH read, dX + mask
+        return (12 * F + 16) * rows, 4.0 * rows * F * F
+    if name == "gemm_bwd_dw":     # dW alone: X (or Z), dH read
+        return 8 * F * rows, 2.0 * rows * F * F
+    return 8 * F * rows, 2.0 * rows * F * F  # F x F transforms: read + write [rows, F]
 
 
 # ------------------------------------------------------------ main
@@ -270,9 +299,12 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timers", action="store_true")
     ap.add_argument("--mode", choices=["auto", "replica", "shard"], default="auto",
-                    help="N > 1: 'auto' measures data-parallel replicas (value, weak "
-                         "scaling) and the dst-range sharded graph (the 'sharded' field, "
-                         "strong scaling); 'replica' / 'shard' measure one of them")
+                    help="N > 1: 'auto' measures the dst-range sharded graph (value, strong "
+                         "scaling) and data-parallel replicas (the 'replicas' field, weak "
+                         "scaling); 'shard' / 'replica' measure one of them as value")
+    ap.add_argument("--chunks", type=int, default=4,
+                    help="N > 1 sharded path: row chunks per layer output (all-gathers "
+                         "pipelined behind the compute)")
     ap.add_argument("--dist-backend", default="nccl", help=argparse.SUPPRESS)  # gloo: tests
     ap.add_argument("--one-device", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
@@ -300,59 +332,61 @@ def main():
     n_edges = 2 * args.pairs          # graph edges, self-loops not counted
     X, Ws, bs, dY = make_inputs(args.nodes, F, L)
     timer = None if args.no_kernel_timers else KernelTimer()
+    mode = args.mode if world > 1 else "replica"
+    if mode == "auto":
+        mode = "shard"
+    do_shard = world > 1 and (args.mode in ("auto", "shard"))
     do_replica = world == 1 or args.mode in ("auto", "replica")
-    do_shard = world > 1 and args.mode in ("auto", "shard")
-    sharded = None
-    prep_ms = None
-    elapsed = None
+    sharded = replicas = None
     N = args.nodes
+    ei_cpu = None
     if do_shard:
         from mgcn.dist import ShardedGCN
         ei_cpu, N = make_er_graph(args.nodes, args.pairs)
-        model = ShardedGCN(ei_cpu, N, Ws, bs, device=dev)
+        model = ShardedGCN(ei_cpu, N, Ws, bs, device=dev, chunks=args.chunks)
         nnz = ei_cpu.shape[1]
         t_sh, prep_sh = timed(model.step_fn(X, dY), args.steps, args.warmup, world, dev,
-                              None if do_replica else timer)
+                              timer if mode == "shard" else None)
         sharded = {"value": n_edges * L / (t_sh / args.steps), "unit": "edges/s",
                    "ms_per_step": t_sh / args.steps * 1e3, "scaling": "strong",
-                   "parallelism": f"dst-range x{world} (RCCL all-gathers of H and dY)",
+                   "parallelism": f"dst-range x{world}",
+                   "path": ("fused layer kernels, chunked RCCL all-gathers (x%d per layer and "
+                            "direction) overlapped with compute" % model.shard.chunks
+                            if model.fused else "per-layer GEMM + SpMM, RCCL all-gathers"),
                    "workload": "config 2 (one 10M-edge graph) sharded by destination range",
-                   "graph_prep_plus_first_step_ms": prep_sh}
+                   "graph_prep_plus_first_step_ms": prep_sh,
+                   "rows_per_rank": model.shard.rows}
         del model
         torch.cuda.empty_cache()
-        if not do_replica:
-            elapsed, prep_ms = t_sh, prep_sh
     if do_replica:
         from mgcn.dist import allreduce_grads
         # data-parallel replicas: rank r trains its own config-2 graph (seed r)
         # with the shared weights; one bucketed gradient all-reduce per step
-        ei_cpu, N = make_er_graph(args.nodes, args.pairs, seed=rank)
-        nnz = ei_cpu.shape[1]
-        step, params = build_stack(dev, ei_cpu, X, Ws, bs, dY)
+        ei_r, N = make_er_graph(args.nodes, args.pairs, seed=rank)
+        if ei_cpu is None:
+            ei_cpu = ei_r
+        nnz = ei_r.shape[1]
+        step, params = build_stack(dev, ei_r, X, Ws, bs, dY)
 
         def run_step():
             step()
             allreduce_grads(params)
-        elapsed, prep_ms = timed(run_step, args.steps, args.warmup, world, dev, timer)
-    ms_per_step = elapsed / args.steps * 1e3
-    if do_replica:
-        value = world * n_edges * L / (elapsed / args.steps)
-        scaling = "weak"
-        parallelism = f"dp{world}" if world > 1 else "single"
-        workload = ("config2: Erdos-Renyi N=1M, E=10M (+1M self-loops), F=128, 3-layer GCN "
-                    "(sm, add, bias, ReLU) fwd+bwd" + (
-                        f"; one graph per GPU (seed = rank), gradient all-reduce"
-                        if world > 1 else ""))
-    else:
-        value = sharded["value"]
-        scaling = "strong"
-        parallelism = f"dst-range x{world}"
-        workload = sharded["workload"]
-
+        t_r, prep_r = timed(run_step, args.steps, args.warmup, world, dev,
+                            timer if mode == "replica" else None)
+        replicas = {"value": world * n_edges * L / (t_r / args.steps), "unit": "edges/s",
+                    "ms_per_step": t_r / args.steps * 1e3, "scaling": "weak",
+                    "parallelism": f"dp{world}" if world > 1 else "single",
+                    "workload": ("config2: Erdos-Renyi N=1M, E=10M (+1M self-loops), F=128, "
+                                 "3-layer GCN (sm, add, bias, ReLU) fwd+bwd" + (
+                                     "; one graph per GPU (seed = rank), gradient all-reduce"
+                                     if world > 1 else "")),
+                    "graph_prep_plus_first_step_ms": prep_r}
+    head = sharded if mode == "shard" else replicas
+    value, ms_per_step = head["value"], head["ms_per_step"]
     result = {
         "metric": METRIC, "value": value, "unit": "edges/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
-        "higher_is_better": True, "scaling": scaling,
+        "higher_is_better": True, "scaling": head["scaling"],
         "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "arithmetic": ("aggregation fp32 (bitwise = reference); dense x@W / dW / dX products as "
                        "bf16x6 (exact 3-term bf16 split of each fp32 operand, 6 MFMA products, "
@@ -360,62 +394,39 @@ def main():
                        "forward fused as (A x) W in one launch per layer, keeping Z = A x; "
                        "backward dW = Z^T dY in one dense pass (mgcn_gemm_bwd) and dX from a "
                        "gather of A^T dY (mgcn_spmm_xw_bwd, dX only); the bottom layer runs "
-                       "no gather (tests/test_gpu_fused.py)"),
-        "config": {"workload": workload, "nodes": N, "edges": n_edges, "nnz": nnz, "feat": F,
-                   "layers": L, "global_batch": world if do_replica else 1,
-                   "parallelism": parallelism},
-        "graph_prep_plus_first_step_ms": prep_ms,
+                       "no gather (tests/test_gpu_fused.py, tests/test_gpu_headline.py)"),
+        "config": {"workload": head["workload"], "nodes": N, "edges": n_edges, "nnz": nnz,
+                   "feat": F, "layers": L, "global_batch": world if mode == "replica" else 1,
+                   "parallelism": head["parallelism"]},
+        "graph_prep_plus_first_step_ms": head["graph_prep_plus_first_step_ms"],
     }
-    if sharded is not None and do_replica:
-        result["sharded"] = sharded
+    if world > 1:
+        if mode == "shard" and replicas is not None:
+            result["replicas"] = replicas
+        if mode == "replica" and sharded is not None:
+            result["sharded"] = sharded
     if timer is not None:
         ks = timer.summary()
-        shard_only = not do_replica
-        rows_local = N // world if shard_only else N
-        nnz_local = nnz // world if shard_only else nnz
         kern = {}
-        for name, s in ks.items():
-            if name.startswith("spmm_xw"):
-                # fused layer kernels: the SpMM's bytes (gathered rows + output rows);
-                # the adjoint also reads X (4 N F) -- the dW-only form writes no dX
-                b = spmm_bytes(rows_local, nnz_local, F)
-                fl = 2.0 * rows_local * F * F
-                if name == "spmm_xw_bwd":
-                    b += 4 * rows_local * F
-                    fl *= 2
-                elif name == "spmm_xw_fwd_z":
-                    b += 4 * rows_local * F  # the aggregate Z written beside Y
-                elif name == "spmm_xw_bwd_dx":
-                    b += 16 * rows_local  # dX only: the lower layer's ReLU mask words
-                elif name == "spmm_xw_bwd_dw":
-                    pass  # X read instead of the output write: the same count
-                kern[name] = dict(s, bytes=b, gbs=b / (s["avg_ms"] * 1e-3) / 1e9, flop=fl,
-                                  tflops=fl / (s["avg_ms"] * 1e-3) / 1e12)
-            elif name.startswith("spmm"):
-                b = spmm_bytes(rows_local, nnz_local, F)
-                kern[name] = dict(s, bytes=b, gbs=b / (s["avg_ms"] * 1e-3) / 1e9)
-            elif name == "gemm_bwd":  # dW and dX: 4 rows F F flop; X, dH read, dX + mask
-                fl = 4.0 * rows_local * F * F
-                b = (12 * F + 16) * rows_local
-                kern[name] = dict(s, flop=fl, tflops=fl / (s["avg_ms"] * 1e-3) / 1e12, bytes=b,
-                                  gbs=b / (s["avg_ms"] * 1e-3) / 1e9)
-            elif name == "gemm_bwd_dw":  # dW alone: 2 rows F F flop; X, dH read
-                fl = 2.0 * rows_local * F * F
-                b = 8 * F * rows_local
-                kern[name] = dict(s, flop=fl, tflops=fl / (s["avg_ms"] * 1e-3) / 1e12, bytes=b,
-                                  gbs=b / (s["avg_ms"] * 1e-3) / 1e9)
-            else:  # F x F feature transforms on MFMA: 2 rows F F flop per launch
-                fl = 2.0 * rows_local * F * F
-                kern[name] = dict(s, flop=fl, tflops=fl / (s["avg_ms"] * 1e-3) / 1e12)
-        dom = max((k for k in kern if k.startswith("spmm")),
-                  key=lambda k: kern[k]["avg_ms"] * kern[k]["launches"])
+        for name, s_ in ks.items():
+            bytes_ = flops = 0.0
+            for r, e in s_.pop("sizes"):
+                b, fl = launch_bytes(name, r or 0, e or 0, F)
+                bytes_ += b
+                flops += fl
+            t = s_["total_ms"] * 1e-3
+            kern[name] = dict(s_, bytes=bytes_ / s_["launches"], gbs=bytes_ / t / 1e9,
+                              flop=flops / s_["launches"], tflops=flops / t / 1e12)
+        dom = max((k for k in kern if k.startswith("spmm")), key=lambda k: kern[k]["total_ms"])
         a = kern[dom]["gbs"]
         result["kernels"] = kern
         result["kernels_note"] = ("HIP events on the launch stream around every libmgcn launch, in a "
                                   "separate instrumented pass of min(K, 10) steps after the timed "
-                                  "loop; heavy-row launches on the side stream are not included "
+                                  "loop (per rank: rank 0's); bytes = algorithmic bytes per launch "
+                                  "(bench.launch_bytes), gbs = their sum over the summed launch "
+                                  "times; heavy-row launches on the side stream are not included "
                                   "(config 2 has none)")
-        traffic, src = pmc_traffic(dom, args, world if shard_only else 1)
+        traffic, src = pmc_traffic(dom, args, world)
         result["roofline"] = {"bound": "hbm", "kernel": dom, "achieved": a, "peak": HBM_PEAK_GBS,
                               "unit": "GB/s", "frac": a / HBM_PEAK_GBS, "traffic": traffic,
                               "traffic_source": src}

@@ -2,31 +2,44 @@
 
 The reference is single-device; north_star asks for the
 edge list to be sharded by destination-node range across the GPUs of a node
-with an RCCL exchange of node embeddings over xGMI.  Design:
+with an RCCL exchange of node embeddings over xGMI.  Design (SURVEY.md §8(e),
+DESIGN.md §7):
 
-* nodes are split into P contiguous ranges balanced on (in-edges + rows);
-  rank k owns rows [lo_k, hi_k) of X, of every layer's output and of dX;
-* forward, per layer:  H_k = X_k W  ->  all_gather(H_k)  ->  local SpMM over
-  the rank's destination rows (every in-edge of a destination is local, in COO
-  order, so the forward stays bit-identical to one device);
-* backward, per layer: dY_k (ReLU mask, bias partial) -> all_gather(dY_k) ->
-  local adjoint SpMM over the rank's SOURCE rows (the src-grouped view restricted
-  to [lo_k, hi_k), all of their out-edges, in COO order) -> dH_k, again
-  bit-identical to one device.  Gathering dY (instead of reduce-scattering
-  partial dH, the "all-reduce of partial embeddings" form) moves the same bytes
-  and keeps the per-edge summation order;
-* replicated parameters: one bucketed all_reduce of every weight/bias gradient
-  per step (the DP part of the step).
+* nodes are split into P contiguous ranges balanced on (in-edges + rows),
+  from a global in-degree count (no sort of the global graph); rank k owns
+  rows [lo_k, hi_k) of X, of every layer's output and of dX;
+* every rank filters the COO list once for the edges INTO its rows (the fwd
+  view, rows = its destinations) and OUT OF its rows (the bwd view, rows = its
+  sources) and sorts only those (stable, so each row keeps COO order and the
+  sums stay bit-identical to one device); degrees of its sources are summed
+  locally and the inverse degrees all-gathered once;
+* exchange layout: row i of rank k lives at ``c*P*cr + k*cr + (i - c*cr)``
+  of a [C*P*cr, F] table, c = i // cr (C row chunks of cr rows).  A layer's
+  output is produced chunk by chunk and each chunk's all-gather
+  (``all_gather_into_tensor`` of cr rows, RCCL over xGMI) is issued as soon as
+  the chunk is written, so it runs while the next chunk is computed; the
+  column indices of both views are remapped once to table positions, so the
+  kernels read the gathered table in place;
+* forward, per layer: the fused aggregate-then-transform kernel
+  (mgcn_spmm_xw_fwd) over the rank's destinations reads the table of the
+  layer's input (layer 0: the replicated input features, no exchange);
+* backward, per layer: the upstream dY rows are all-gathered (chunked, as
+  they are produced by the layer above) while dW = Z_k^T dY_k runs on local
+  data (the forward kept Z_k = the rank's aggregate); then the dX-only gather
+  kernel (mgcn_spmm_xw_bwd, X = NULL) over the rank's sources, with the lower
+  layer's ReLU mask / mean divisor / bias column sums in its epilogue;
+* replicated parameters: one bucketed all_reduce of every weight / bias
+  gradient per step.
 
-All-gathers use a padded layout [P * max_rows, F]; CSR column indices are
-remapped once to those padded positions so the SpMM reads the gathered buffer
-in place (no unpack copy).  One all_gather of 4 N F (P-1)/P bytes per rank
-per layer per direction; on MI355X's point-to-point xGMI each peer slice has
-its own link (~153 GB/s), SURVEY.md §8(e) gives the arithmetic.
+Layers the fused kernels do not take (max, F != 128, heavy rows, tables past
+4 GiB) run per layer: H_k = X_k W, all-gather H, the aggregation SpMM over the
+rank's destinations; adjoint: all-gather dY (and argmax for max), the adjoint
+SpMM over the rank's sources.
 
-The local compute goes through a backend object (default :class:`HipBackend`,
-i.e. libmgcn); tests substitute a CPU double to exercise the partitioning and
-collective logic under the gloo backend.
+Forward rows and dX rows are bitwise equal to one device; parameter
+gradients are all-reduced partial sums (fp32 tolerance).  The local compute
+goes through a backend object (default :class:`HipBackend`, libmgcn); tests
+substitute a CPU double (tests/cpu_backend.py) under gloo.
 """
 from __future__ import annotations
 
@@ -42,16 +55,43 @@ from .graph import CSRView
 class HipBackend:
     """Local compute on libmgcn (the only production backend)."""
 
-    def build_plan(self, edge_index, num_nodes):
-        from .graph import build_plan
-        return build_plan(edge_index, num_nodes)
+    def build_view(self, key, other, n_key, n_other):
+        from .graph import build_view
+        return build_view(key, other, n_key, n_other, schedule=False)
 
-    def norm(self, plan, method, deg=None, edge_weight=None):
-        return plan.norm(method, deg=deg, edge_weight=edge_weight)
+    def degree_norm(self, n, bwd, deg, ew, code):
+        from .graph import degree_norm
+        return degree_norm(n, bwd, deg, ew, code)
+
+    def edge_norm(self, view, rows_are_dst, dinv, ew, code):
+        from .graph import edge_norm
+        return edge_norm(view, rows_are_dst, dinv, ew, code)
 
     def finalize_view(self, view):
         from .graph import schedule_rows
         return schedule_rows(view)
+
+    def fused_ok(self, shard, F_in, F_out, reduce):
+        from .ops import gemm_bwd_supported, spmm_xw_supported
+        return (spmm_xw_supported(shard.fwd, F_in, F_out, reduce) and
+                spmm_xw_supported(shard.bwd, F_out, F_in, L.REDUCE_SUM) and
+                gemm_bwd_supported(F_in, F_out))
+
+    def spmm_xw_fwd(self, *a, **k):
+        from .ops import spmm_xw_fwd
+        return spmm_xw_fwd(*a, **k)
+
+    def spmm_xw_bwd_dx(self, view_t, w_t, row_scale, dY, W, relu_mask=None, row_div=None,
+                       out=None):
+        """dX only (X = NULL): returns the lower layer's bias column sums or None."""
+        from .ops import spmm_xw_bwd
+        return spmm_xw_bwd(view_t, w_t, row_scale, dY, None, W, relu_mask=relu_mask,
+                           row_div=row_div, dx_out=out)[2]
+
+    def gemm_bwd_dw(self, Z, dY, W, dh_colsum=False):
+        from .ops import gemm_bwd
+        dW, _, cs = gemm_bwd(Z, dY, W, want_dx=False, dh_colsum=dh_colsum)
+        return dW, cs
 
     def spmm_fwd(self, *a, **k):
         from .ops import spmm_fwd
@@ -71,7 +111,8 @@ class HipBackend:
 
 
 def partition_nodes(rowptr: torch.Tensor, parts: int) -> list[int]:
-    """Contiguous node ranges with ~equal (in-edges + rows) per part."""
+    """Contiguous node ranges with ~equal (in-edges + rows) per part;
+    ``rowptr`` is the cumulative in-degree ([N + 1], rowptr[0] = 0)."""
     rp = rowptr.to("cpu", torch.int64)
     n = rp.numel() - 1
     cost = rp + torch.arange(n + 1, dtype=torch.int64)  # cumulative cost up to row i
@@ -85,6 +126,17 @@ def partition_nodes(rowptr: torch.Tensor, parts: int) -> list[int]:
     return bounds
 
 
+def table_positions(ids: torch.Tensor, bounds, chunk_rows: int) -> torch.Tensor:
+    """Global node id -> row of the exchange table (module docstring)."""
+    world = len(bounds) - 1
+    b = torch.tensor(bounds, dtype=torch.int64, device=ids.device)
+    g = ids.to(torch.int64)
+    owner = torch.bucketize(g, b[1:], right=True)
+    i = g - b[owner]
+    c = torch.div(i, chunk_rows, rounding_mode="floor")
+    return c * (world * chunk_rows) + owner * chunk_rows + (i - c * chunk_rows)
+
+
 @dataclass
 class Shard:
     rank: int
@@ -93,87 +145,184 @@ class Shard:
     lo: int
     hi: int
     max_rows: int
-    fwd: CSRView        # rows = my destinations, col = padded source positions
-    bwd: CSRView        # rows = my sources, col = padded destination positions
+    chunks: int          # C
+    chunk_rows: int      # cr
+    fwd: CSRView         # rows = my destinations, col = table positions of the sources
+    bwd: CSRView         # rows = my sources, col = table positions of the destinations
     w_fwd: torch.Tensor | None
     w_bwd: torch.Tensor | None
-    row_scale: torch.Tensor | None
-    cnt_pad: torch.Tensor  # max(in-degree, 1) at padded positions (MEAN adjoint)
+    row_scale: torch.Tensor | None   # RW without edge weights: dinv of my sources
+    in_cnt: torch.Tensor             # max(in-degree, 1) of my rows (MEAN)
+    cnt_table: torch.Tensor          # the same for every node, table layout (MEAN adjoint)
+    chunk_edges_fwd: list            # edges of each row chunk (host ints, byte accounting)
+    chunk_edges_bwd: list
 
     @property
     def rows(self) -> int:
         return self.hi - self.lo
 
+    @property
+    def table_rows(self) -> int:
+        return self.chunks * self.world * self.chunk_rows
 
-def _remap(col: torch.Tensor, bounds: list, max_rows: int) -> torch.Tensor:
-    """Global node id -> row of the padded all-gather buffer."""
-    b = torch.tensor(bounds, dtype=torch.int64, device=col.device)
-    c = col.to(torch.int64)
-    owner = torch.bucketize(c, b[1:], right=True)
-    return (c + owner * max_rows - b[owner]).to(torch.int32)
+    @property
+    def pad_rows(self) -> int:
+        return self.chunks * self.chunk_rows
+
+    def chunk(self, c: int):
+        a = c * self.chunk_rows
+        return a, max(a, min(a + self.chunk_rows, self.rows))
+
+    def to_table(self, full: torch.Tensor) -> torch.Tensor:
+        """A replicated [N, ...] tensor in the exchange layout (setup only)."""
+        n = self.bounds[-1]
+        pos = table_positions(torch.arange(n, device=full.device), self.bounds, self.chunk_rows)
+        out = torch.zeros((self.table_rows,) + tuple(full.shape[1:]), dtype=full.dtype,
+                          device=full.device)
+        out[pos] = full
+        return out
+
+    def local_rows(self, full: torch.Tensor) -> torch.Tensor:
+        return full[self.lo:self.hi]
 
 
-def _slice_view(view: CSRView, lo: int, hi: int, bounds, max_rows, world):
-    rp = view.rowptr[lo:hi + 1]
-    beg = int(rp[0]) if hi >= lo else 0
-    end = int(rp[-1])
-    return CSRView(rowptr=(rp - beg).contiguous(),
-                   col=_remap(view.col[beg:end], bounds, max_rows).contiguous(),
-                   eid=view.eid[beg:end].contiguous(), n_rows=hi - lo,
-                   n_cols=world * max_rows), beg, end
+def _all_gather_flat(local: torch.Tensor, n_pad: int, world: int, group=None) -> torch.Tensor:
+    """[n, ...] per rank (n <= n_pad) -> [world * n_pad, ...] rank-major."""
+    buf = torch.zeros((n_pad,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    buf[:local.size(0)] = local
+    if world == 1:
+        return buf
+    out = torch.empty((world * n_pad,) + tuple(local.shape[1:]), dtype=local.dtype,
+                      device=local.device)
+    _gather_into(out, buf, world, group, False)
+    return out
+
+
+def _gather_into(out, inp, world, group, async_op):
+    if world == 1:
+        out.copy_(inp)
+        return None
+    if dist.get_backend(group) == "nccl":
+        return dist.all_gather_into_tensor(out, inp, group=group, async_op=async_op)
+    return dist.all_gather(list(out.chunk(world)), inp, group=group, async_op=async_op)
+
+
+def _gather_chunk(shard: Shard, c: int, local_pad: torch.Tensor, table: torch.Tensor, group):
+    """Issue the all-gather of row chunk c (async); returns the work or None."""
+    cr, P = shard.chunk_rows, shard.world
+    return _gather_into(table[c * P * cr:(c + 1) * P * cr], local_pad[c * cr:(c + 1) * cr], P,
+                        group, True)
+
+
+def _wait(works):
+    for w in works:
+        if w is not None:
+            w.wait()
+
+
+def gather_table(shard: Shard, local: torch.Tensor, group=None) -> torch.Tensor:
+    """My rows [rows, F] -> the exchange table [C*P*cr, F] on every rank."""
+    pad = torch.empty((shard.pad_rows,) + tuple(local.shape[1:]), dtype=local.dtype,
+                      device=local.device)
+    pad[:shard.rows] = local
+    if shard.pad_rows > shard.rows:
+        pad[shard.rows:].zero_()
+    table = torch.empty((shard.table_rows,) + tuple(local.shape[1:]), dtype=local.dtype,
+                        device=local.device)
+    _wait([_gather_chunk(shard, c, pad, table, group) for c in range(shard.chunks)])
+    return table
+
+
+def _local_view(backend, key, other, sel, lo, hi, n_other, bounds, cr, T):
+    """CSR of the selected edges over global rows [0, hi) (rows < lo empty),
+    eid = global COO ids; returned with the global columns (for the norms) and
+    the finishing step that slices rows [lo, hi) and remaps the columns."""
+    v = backend.build_view(key[sel], other[sel], hi, n_other)
+    v.eid = sel[v.eid.long()].to(torch.int32)
+
+    def finish():
+        col = table_positions(v.col, bounds, cr).to(torch.int32)
+        return CSRView(rowptr=v.rowptr[lo:].contiguous(), col=col, eid=v.eid, n_rows=hi - lo,
+                       n_cols=T)
+    return v, finish
 
 
 def build_shard(edge_index: torch.Tensor, num_nodes: int, deg_norm="sm", deg=None,
-                edge_weight=None, group=None, backend=None, device=None) -> Shard:
-    """Every rank builds the global CSR views on its own device (one-time),
-    then keeps its slice.  ``edge_index`` is the full graph on every rank."""
+                edge_weight=None, group=None, backend=None, device=None, chunks: int = 4) -> Shard:
+    """One-time setup of this rank's part of the graph (module docstring).
+    ``edge_index`` (and ``deg`` / ``edge_weight``) is the full graph on every
+    rank; only the rank's own edges are sorted."""
     backend = backend or HipBackend()
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     if device is not None:
         edge_index = edge_index.to(device)
-    plan = backend.build_plan(edge_index, num_nodes)
-    norm = backend.norm(plan, deg_norm, deg, edge_weight)
-    bounds = partition_nodes(plan.fwd.rowptr, world)
-    max_rows = max(bounds[k + 1] - bounds[k] for k in range(world)) if world else 0
-    max_rows = max(max_rows, 1)
+        deg = None if deg is None else deg.to(device)
+        edge_weight = None if edge_weight is None else edge_weight.to(device)
+    N = int(num_nodes)
+    src, dst = edge_index[0].to(torch.int64), edge_index[1].to(torch.int64)
+    dev = src.device
+    in_deg = torch.bincount(dst, minlength=N)
+    rowptr = torch.zeros(N + 1, dtype=torch.int64, device=dev)
+    rowptr[1:] = torch.cumsum(in_deg, 0)
+    bounds = partition_nodes(rowptr, world)
     lo, hi = bounds[rank], bounds[rank + 1]
-    fwd, fb, fe = _slice_view(plan.fwd, lo, hi, bounds, max_rows, world)
-    bwd, bb, be = _slice_view(plan.bwd, lo, hi, bounds, max_rows, world)
-    fwd, bwd = backend.finalize_view(fwd), backend.finalize_view(bwd)
-    w_fwd = None if norm.w_fwd is None else norm.w_fwd[fb:fe].contiguous()
-    w_bwd = None if norm.w_bwd is None else norm.w_bwd[bb:be].contiguous()
-    row_scale = None if norm.row_scale_bwd is None else norm.row_scale_bwd[lo:hi].contiguous()
-    cnt_pad = torch.ones(world * max_rows, dtype=torch.float32, device=plan.in_cnt.device)
-    for k in range(world):
-        a, b = bounds[k], bounds[k + 1]
-        cnt_pad[k * max_rows:k * max_rows + (b - a)] = plan.in_cnt[a:b]
-    return Shard(rank, world, bounds, lo, hi, max_rows, fwd, bwd, w_fwd, w_bwd, row_scale,
-                 cnt_pad)
-
-
-def _all_gather_rows(local: torch.Tensor, shard: Shard, group=None) -> torch.Tensor:
-    """[rows, F] per rank -> padded [world * max_rows, F] on every rank."""
-    F = local.size(1)
-    buf = torch.empty(shard.max_rows, F, dtype=local.dtype, device=local.device)
-    buf[:local.size(0)].copy_(local)
-    if shard.max_rows > local.size(0):
-        buf[local.size(0):].zero_()
-    out = torch.empty(shard.world * shard.max_rows, F, dtype=local.dtype, device=local.device)
-    if shard.world == 1:
-        out.copy_(buf)
-    elif dist.get_backend(group) == "nccl":
-        dist.all_gather_into_tensor(out, buf, group=group)
+    max_rows = max(max(bounds[k + 1] - bounds[k] for k in range(world)), 1)
+    C = max(1, min(int(chunks), max_rows))
+    cr = -(-max_rows // C)
+    T = C * world * cr
+    code = L.NORM_CODES[deg_norm]
+    ew = None if edge_weight is None else edge_weight.reshape(-1).to(torch.float32).contiguous()
+    if code == L.NORM_NONE or ew is not None:
+        deg = None
+    sel_f = torch.nonzero((dst >= lo) & (dst < hi)).view(-1)
+    sel_b = torch.nonzero((src >= lo) & (src < hi)).view(-1)
+    fwd_g, fwd_finish = _local_view(backend, dst, src, sel_f, lo, hi, N, bounds, cr, T)
+    bwd_g, bwd_finish = _local_view(backend, src, dst, sel_b, lo, hi, N, bounds, cr, T)
+    dinv = None
+    if code != L.NORM_NONE:
+        if deg is not None:  # given degrees (gcn_base_models.py:119-121): no exchange
+            _, dinv = backend.degree_norm(N, None, deg.reshape(-1).to(torch.float32).contiguous(),
+                                          None, code)
+        else:  # out-degree of my sources over their complete rows, then all-gathered
+            _, dl = backend.degree_norm(hi, bwd_g, None, ew, code)
+            mine = _all_gather_flat(dl[lo:hi], max_rows, world, group)
+            dinv = torch.cat([mine[k * max_rows:k * max_rows + bounds[k + 1] - bounds[k]]
+                              for k in range(world)])
+    row_scale = w_bwd = None
+    if code == L.NORM_NONE and ew is None:
+        w_fwd = None
+    elif code == L.NORM_RW and ew is None:
+        # x * dinv before the gather (gcn_base_models.py:217-220); the adjoint
+        # post-scales by dinv of the source
+        w_fwd = backend.edge_norm(fwd_g, True, dinv, None, code)
+        row_scale = dinv[lo:hi].contiguous()
     else:
-        dist.all_gather(list(out.chunk(shard.world)), buf, group=group)
-    return out
+        w_fwd = backend.edge_norm(fwd_g, True, dinv, ew, code)
+        w_bwd = backend.edge_norm(bwd_g, False, dinv, ew, code)
+    fwd = backend.finalize_view(fwd_finish())
+    bwd = backend.finalize_view(bwd_finish())
+    cnt = in_deg.clamp(min=1).to(torch.float32)
+    rp_f = fwd.rowptr.to("cpu")
+    rp_b = bwd.rowptr.to("cpu")
+    ce_f, ce_b = [], []
+    for c in range(C):
+        a = c * cr
+        b = max(a, min(a + cr, hi - lo))
+        ce_f.append(int(rp_f[b] - rp_f[a]) if b > a else 0)
+        ce_b.append(int(rp_b[b] - rp_b[a]) if b > a else 0)
+    sh = Shard(rank, world, bounds, lo, hi, max_rows, C, cr, fwd, bwd, w_fwd, w_bwd, row_scale,
+               cnt[lo:hi].contiguous(), None, ce_f, ce_b)
+    sh.cnt_table = sh.to_table(cnt)
+    return sh
 
 
+# ------------------------------------------------------------ per-layer path
 class _ShardedAggregate(torch.autograd.Function):
     @staticmethod
     def forward(ctx, H_local, bias, shard: Shard, reduce: int, relu: bool, backend, group):
-        Hpad = _all_gather_rows(H_local.contiguous(), shard, group)
-        Y, argmax = backend.spmm_fwd(shard.fwd, shard.w_fwd, Hpad, reduce, bias, relu)
+        Htab = gather_table(shard, H_local.contiguous(), group)
+        Y, argmax = backend.spmm_fwd(shard.fwd, shard.w_fwd, Htab, reduce, bias, relu)
         ctx.shard, ctx.reduce, ctx.relu, ctx.backend, ctx.group = shard, reduce, relu, backend, group
         ctx.has_bias = bias is not None
         ctx.save_for_backward(Y if relu else None, argmax)
@@ -185,12 +334,12 @@ class _ShardedAggregate(torch.autograd.Function):
         sh, be = ctx.shard, ctx.backend
         need_b = ctx.has_bias and ctx.needs_input_grad[1]
         dY, db = be.relu_bwd_colsum(dZ.contiguous(), Y, ctx.relu, need_b)
-        dYpad = _all_gather_rows(dY, sh, ctx.group)
-        argpad = None
+        dYtab = gather_table(sh, dY, ctx.group)
+        argtab = None
         if ctx.reduce == L.REDUCE_MAX:
-            argpad = _all_gather_rows(argmax, sh, ctx.group)
-        dH = be.spmm_bwd(sh.bwd, sh.w_bwd, sh.row_scale, dYpad, ctx.reduce,
-                         cnt=sh.cnt_pad if ctx.reduce == L.REDUCE_MEAN else None, argmax=argpad)
+            argtab = gather_table(sh, argmax, ctx.group)
+        dH = be.spmm_bwd(sh.bwd, sh.w_bwd, sh.row_scale, dYtab, ctx.reduce,
+                         cnt=sh.cnt_table if ctx.reduce == L.REDUCE_MEAN else None, argmax=argtab)
         return dH, db, None, None, None, None, None
 
 
@@ -199,6 +348,201 @@ def sharded_aggregate(H_local, shard: Shard, aggr="add", bias=None, relu=False, 
     """Aggregation of the rank's destination rows; H_local = this rank's rows."""
     return _ShardedAggregate.apply(H_local, bias, shard, L.REDUCE_CODES[aggr], bool(relu),
                                    backend or HipBackend(), group)
+
+
+# --------------------------------------------------------- fused stack path
+class _ShardedStack(torch.autograd.Function):
+    """Sum / mean 128 -> 128 layers with ReLU between them, on the fused
+    kernels, with chunked all-gathers overlapping the compute (module
+    docstring).  ``x`` is the input either as the exchange table (replicated
+    input features, ``x_is_table``) or as this rank's rows."""
+
+    @staticmethod
+    def forward(ctx, x, shard: Shard, reduce, relus, backend, group, x_is_table, *params):
+        Ws, bs = params[0::2], params[1::2]
+        if not all(relus[:-1]):
+            raise ValueError("_ShardedStack: every layer below the top needs its ReLU (its mask "
+                             "feeds the adjoint's epilogue)")
+        sh, be = shard, backend
+        rows, C = sh.rows, sh.chunks
+        dev = x.device
+        tab = x if x_is_table else gather_table(sh, x, group)
+        zs, rms, outs = [], [], []
+        n = len(Ws)
+        for i, (W, b) in enumerate(zip(Ws, bs)):
+            F_in, F_out = W.shape
+            last = i == n - 1
+            out = torch.empty(sh.pad_rows, F_out, dtype=torch.float32, device=dev)
+            want_z = bool(ctx.needs_input_grad[7 + 2 * i])
+            z = torch.empty(sh.pad_rows, F_in, dtype=torch.float32, device=dev) if want_z else None
+            rm = None
+            if relus[i] and not last:
+                rm = torch.empty(sh.pad_rows, 4, dtype=torch.int32, device=dev)
+            nxt = None if last else torch.empty(sh.table_rows, F_out, dtype=torch.float32,
+                                                device=dev)
+            works = []
+            for c in range(C):
+                a, e = sh.chunk(c)
+                if e > a:
+                    be.spmm_xw_fwd(sh.fwd.rows(a, e, sh.chunk_edges_fwd[c]), sh.w_fwd, tab, W,
+                                   reduce, b, relus[i], relu_mask=None if rm is None else rm[a:e],
+                                   want_z=want_z, out=out[a:e],
+                                   z_out=None if z is None else z[a:e])
+                if nxt is not None:
+                    works.append(_gather_chunk(sh, c, out, nxt, group))
+            _wait(works)
+            outs.append(out)
+            zs.append(z)
+            rms.append(rm)
+            tab = nxt
+        ctx.shard, ctx.reduce, ctx.relus, ctx.backend, ctx.group = sh, reduce, relus, be, group
+        ctx.n = n
+        ctx.x_is_table = x_is_table
+        ctx.has_bias = [b is not None for b in bs]
+        ctx.save_for_backward(*Ws, outs[-1], *[t if t is not None else torch.empty(0)
+                                               for t in zs + rms])
+        return outs[-1][:rows]
+
+    @staticmethod
+    def backward(ctx, dZ):
+        sh, be, group, n = ctx.shard, ctx.backend, ctx.group, ctx.n
+        saved = ctx.saved_tensors
+        Ws, top_out = saved[:n], saved[n]
+        zs, rms = saved[n + 1:2 * n + 1], saved[2 * n + 1:3 * n + 1]
+        relus = ctx.relus
+        rows, C = sh.rows, sh.chunks
+        dev = dZ.device
+        mean = ctx.reduce == L.REDUCE_MEAN
+        rd = sh.in_cnt if mean else None
+        gW, gb = [None] * n, [None] * n
+        top = n - 1
+        dY = torch.empty(sh.pad_rows, Ws[top].size(1), dtype=torch.float32, device=dev)
+        # the top bias gradient from the dW pass over dY (no separate read)
+        top_cs = not relus[top] and rd is None and ctx.has_bias[top] and zs[top].numel() > 0
+        if relus[top] or rd is not None or (ctx.has_bias[top] and not top_cs):
+            d, gb[top] = be.relu_bwd_colsum(dZ.contiguous(), top_out[:rows], relus[top],
+                                            ctx.has_bias[top], row_div=rd)
+            dY[:rows] = d
+        else:
+            dY[:rows] = dZ
+        need_x = ctx.needs_input_grad[0] and not ctx.x_is_table
+
+        def wants_dx(l):  # layer l's adjoint gather runs (and its dY is exchanged)
+            return l > 0 or need_x
+
+        # top layer's dY: all of it is local already; gather it in chunks
+        tab = works = None
+        if wants_dx(top):
+            tab = torch.empty(sh.table_rows, dY.size(1), dtype=torch.float32, device=dev)
+            works = [_gather_chunk(sh, c, dY, tab, group) for c in range(C)]
+        dx = None
+        for l in range(top, -1, -1):
+            W = Ws[l]
+            # dW = Z^T dY on local rows, while the dY chunks travel
+            if zs[l].numel():
+                gW[l], cs = be.gemm_bwd_dw(zs[l][:rows], dY[:rows], W,
+                                           dh_colsum=bool(top_cs and l == top))
+                if top_cs and l == top:
+                    gb[top] = cs
+            if not wants_dx(l):
+                break
+            _wait(works)
+            dX = torch.empty(sh.pad_rows, W.size(0), dtype=torch.float32, device=dev)
+            ntab = None
+            if l > 0 and wants_dx(l - 1):
+                ntab = torch.empty(sh.table_rows, W.size(0), dtype=torch.float32, device=dev)
+            works, sums = [], []
+            for c in range(C):
+                a, e = sh.chunk(c)
+                if e > a:
+                    cs = be.spmm_xw_bwd_dx(
+                        sh.bwd.rows(a, e, sh.chunk_edges_bwd[c]), sh.w_bwd,
+                        None if sh.row_scale is None else sh.row_scale[a:e], tab, W,
+                        relu_mask=rms[l - 1][a:e] if l > 0 else None,
+                        row_div=rd[a:e] if (l > 0 and rd is not None) else None, out=dX[a:e])
+                    if cs is not None:
+                        sums.append(cs)
+                if ntab is not None:
+                    works.append(_gather_chunk(sh, c, dX, ntab, group))
+            if l > 0:
+                if ctx.has_bias[l - 1]:
+                    gb[l - 1] = (torch.stack(sums).sum(0) if sums else
+                                 torch.zeros(W.size(0), dtype=torch.float32, device=dev))
+                dY, tab = dX, ntab
+            else:
+                dx = dX[:rows]
+        grads = []
+        for w, b in zip(gW, gb):
+            grads += [w, b]
+        return (dx, None, None, None, None, None, None, *grads)
+
+
+class ShardedGCN:
+    """Stack of GCN layers (NodeModelAdditive deg_norm / aggr + bias, ReLU
+    between layers) over a destination-range sharded graph: the bench's N > 1
+    model.  Sum / mean 128-wide stacks run on :class:`_ShardedStack`; other
+    stacks layer by layer (:func:`sharded_aggregate`)."""
+
+    def __init__(self, edge_index, num_nodes, Ws, bs, device, deg_norm="sm", aggr="add",
+                 group=None, backend=None, chunks: int = 4, fused: bool = True):
+        self.backend = backend or HipBackend()
+        self.group = group
+        self.device = device
+        self.shard = build_shard(edge_index, num_nodes, deg_norm, group=group,
+                                 backend=self.backend, device=device, chunks=chunks)
+        self.aggr = aggr
+        self.reduce = L.REDUCE_CODES[aggr]
+        self.W = [w.to(device).clone().requires_grad_(True) for w in Ws]
+        self.b = [b.to(device).clone().requires_grad_(True) for b in bs]
+        self.fused = bool(fused) and self.reduce != L.REDUCE_MAX and all(
+            self.backend.fused_ok(self.shard, w.size(0), w.size(1), self.reduce) for w in self.W)
+
+    def params(self):
+        return self.W + self.b
+
+    def local_rows(self, full: torch.Tensor) -> torch.Tensor:
+        return full[self.shard.lo:self.shard.hi].to(self.device)
+
+    def input_table(self, full: torch.Tensor) -> torch.Tensor:
+        """Replicated input features in the exchange layout (setup, untimed):
+        the first layer then reads them in place, with no exchange."""
+        return self.shard.to_table(full.to(self.device))
+
+    def _relus(self):
+        return tuple(i < len(self.W) - 1 for i in range(len(self.W)))
+
+    def forward(self, X_local=None, X_table=None):
+        if self.fused:
+            params = []
+            for w, b in zip(self.W, self.b):
+                params += [w, b]
+            x, is_tab = (X_table, True) if X_table is not None else (X_local, False)
+            return _ShardedStack.apply(x, self.shard, self.reduce, self._relus(), self.backend,
+                                       self.group, is_tab, *params)
+        h = X_local if X_local is not None else X_table[
+            table_positions(torch.arange(self.shard.lo, self.shard.hi, device=X_table.device),
+                            self.shard.bounds, self.shard.chunk_rows)]
+        L_ = len(self.W)
+        for i in range(L_):
+            H = self.backend.linear(h, self.W[i])
+            h = sharded_aggregate(H, self.shard, self.aggr, self.b[i], relu=i < L_ - 1,
+                                  backend=self.backend, group=self.group)
+        return h
+
+    def step_fn(self, X, dY):
+        """fwd + bwd to every weight and bias + the gradient all-reduce, with
+        the replicated input features resident in the exchange layout."""
+        Xt = self.input_table(X)
+        dYl = self.local_rows(dY)
+        params = self.params()
+
+        def step():
+            for p in params:
+                p.grad = None
+            out = self.forward(X_table=Xt)
+            out.backward(dYl)
+            allreduce_grads(params, self.group)
+        return step
 
 
 def allreduce_grads(params, group=None) -> None:
@@ -213,47 +557,3 @@ def allreduce_grads(params, group=None) -> None:
         n = g.numel()
         g.copy_(flat[off:off + n].view_as(g))
         off += n
-
-
-class ShardedGCN:
-    """Stack of GCN layers (NodeModelAdditive 'sm'/'add' + bias, ReLU between
-    layers) over a destination-range sharded graph; the bench's N > 1 model."""
-
-    def __init__(self, edge_index, num_nodes, Ws, bs, device, deg_norm="sm", aggr="add",
-                 group=None, backend=None):
-        self.backend = backend or HipBackend()
-        self.group = group
-        self.device = device
-        self.shard = build_shard(edge_index, num_nodes, deg_norm, group=group,
-                                 backend=self.backend, device=device)
-        self.aggr = aggr
-        self.W = [w.to(device).clone().requires_grad_(True) for w in Ws]
-        self.b = [b.to(device).clone().requires_grad_(True) for b in bs]
-
-    def params(self):
-        return self.W + self.b
-
-    def local_rows(self, full: torch.Tensor) -> torch.Tensor:
-        return full[self.shard.lo:self.shard.hi].to(self.device)
-
-    def forward(self, X_local):
-        h = X_local
-        L_ = len(self.W)
-        for i in range(L_):
-            H = self.backend.linear(h, self.W[i])
-            h = sharded_aggregate(H, self.shard, self.aggr, self.b[i], relu=i < L_ - 1,
-                                  backend=self.backend, group=self.group)
-        return h
-
-    def step_fn(self, X, dY):
-        Xl = self.local_rows(X)
-        dYl = self.local_rows(dY)
-        params = self.params()
-
-        def step():
-            for p in params:
-                p.grad = None
-            out = self.forward(Xl)
-            out.backward(dYl)
-            allreduce_grads(params, self.group)
-        return step

@@ -54,10 +54,28 @@ class CSRView:
     n_heavy: int = 0
     n_giant: int = 0
     heavy_thr: int = HEAVY_THRESHOLD
+    # edges of this view when it is a row range of a larger one (``col`` /
+    # ``eid`` then hold the whole array, rowptr indexes into it): host-side
+    # bookkeeping only (byte counts of a launch), None = all of ``col``
+    n_edges: int | None = None
 
     @property
     def nnz(self) -> int:
         return int(self.col.numel())
+
+    @property
+    def edges(self) -> int:
+        return self.nnz if self.n_edges is None else int(self.n_edges)
+
+    def rows(self, a: int, b: int, n_edges: int | None = None) -> "CSRView":
+        """Rows [a, b) as a view over the same col / eid arrays (the kernels
+        take rowptr entries as absolute slot indices), in natural row order
+        (no schedule: for the fused layer kernels, which never read one; a
+        view with heavy rows cannot be split)."""
+        if self.n_heavy:
+            raise ValueError("CSRView.rows: a view with heavy rows cannot be split by rows")
+        return CSRView(rowptr=self.rowptr[a:b + 1], col=self.col, eid=self.eid, n_rows=b - a,
+                       n_cols=self.n_cols, n_edges=n_edges)
 
     @property
     def heavy(self) -> torch.Tensor | None:
@@ -211,8 +229,10 @@ def _f32(t: torch.Tensor | None, n: int, name: str, device) -> torch.Tensor | No
     return t.to(torch.float32).contiguous()
 
 
-def build_view(key: torch.Tensor, other: torch.Tensor, n_key: int, n_other: int) -> CSRView:
-    """CSR over ``key`` (libmgcn ``mgcn_csr_build``); stable in COO order."""
+def build_view(key: torch.Tensor, other: torch.Tensor, n_key: int, n_other: int,
+               schedule: bool = True) -> CSRView:
+    """CSR over ``key`` (libmgcn ``mgcn_csr_build``); stable in COO order;
+    ``schedule`` fills the row schedule (:func:`schedule_rows`)."""
     lib = L.load()
     dev = L.require_device(key, other)
     key = key.to(torch.int64).contiguous()
@@ -227,7 +247,8 @@ def build_view(key: torch.Tensor, other: torch.Tensor, n_key: int, n_other: int)
         rc = lib.mgcn_csr_build(L.ptr(key), L.ptr(other), nnz, n_key, n_other, L.ptr(rowptr),
                                 L.ptr(col), L.ptr(eid), L.ptr(ws), ws_bytes, L.stream_of(dev))
     L.check(rc, "mgcn_csr_build")
-    return schedule_rows(CSRView(rowptr=rowptr, col=col, eid=eid, n_rows=n_key, n_cols=n_other))
+    view = CSRView(rowptr=rowptr, col=col, eid=eid, n_rows=n_key, n_cols=n_other)
+    return schedule_rows(view) if schedule else view
 
 
 def build_plan(edge_index: torch.Tensor, num_nodes: int) -> GraphPlan:
@@ -268,6 +289,28 @@ def _build_norm(g: GraphPlan, code: int, deg, edge_weight) -> NormPlan:
     w_fwd = _edge_norm(g.fwd, True, dinv, ew, code)
     w_bwd = _edge_norm(g.bwd, False, dinv, ew, code)
     return NormPlan(code, w_fwd, w_bwd, None, dg, dinv)
+
+
+def degree_norm(n: int, bwd: CSRView | None, deg, ew, code: int):
+    """(deg, dinv) of rows [0, n) (libmgcn ``mgcn_degree_norm``,
+    gcn_base_models.py:112-135): ``deg`` given -> used as is; else the
+    (weighted) out-degree summed over each row of the source-grouped ``bwd``
+    view in COO order."""
+    lib = L.load()
+    dev = (deg if deg is not None else bwd.rowptr).device
+    dg = torch.empty(n, dtype=torch.float32, device=dev)
+    dinv = torch.empty(n, dtype=torch.float32, device=dev)
+    with L.device_guard(dev):
+        rc = lib.mgcn_degree_norm(n, None if bwd is None else L.ptr(bwd.rowptr),
+                                  None if bwd is None else L.ptr(bwd.eid), L.ptr(deg), L.ptr(ew),
+                                  code, L.ptr(dg), L.ptr(dinv), L.stream_of(dev))
+    L.check(rc, "mgcn_degree_norm")
+    return dg, dinv
+
+
+def edge_norm(view: CSRView, rows_are_dst: bool, dinv, ew, code) -> torch.Tensor:
+    """Per-slot weights of ``view`` (libmgcn ``mgcn_edge_norm``)."""
+    return _edge_norm(view, rows_are_dst, dinv, ew, code)
 
 
 def _edge_norm(view: CSRView, rows_are_dst: bool, dinv, ew, code) -> torch.Tensor:

@@ -24,7 +24,10 @@ from . import _lib as L
 from .graph import CSRView, GraphPlan, NormPlan, plan_for
 
 
-_TIMER = None  # optional callable(name, start: bool), e.g. bench.py's HIP-event timer
+# optional callable(name, start: bool, rows=None, edges=None) called right
+# before / after each libmgcn launch on its stream (bench.py's HIP-event timer);
+# the start call carries the launch's row and edge counts for byte accounting
+_TIMER = None
 # fused aggregate-then-transform forward for 128 -> 128 sum / mean layers
 # (mgcn_spmm_xw_fwd); MGCN_FUSE_XW=0 selects the GEMM + SpMM launches
 _FUSE_XW = os.environ.get("MGCN_FUSE_XW", "1") != "0"
@@ -100,7 +103,7 @@ def spmm_fwd(view: CSRView, w: torch.Tensor | None, H: torch.Tensor, reduce: int
         if bias.numel() != F:
             raise ValueError(f"bias has {bias.numel()} entries, expected {F}")
     if _TIMER is not None:
-        _TIMER("spmm_fwd", True)
+        _TIMER("spmm_fwd", True, view.n_rows, view.edges)
     with L.device_guard(dev):
         rc = lib.mgcn_spmm_fwd(view.n_rows, F, L.ptr(view.rowptr), L.ptr(view.col),
                                L.ptr(view.eid), L.ptr(w), L.ptr(H), H.stride(0), L.ptr(Y),
@@ -145,12 +148,15 @@ def layer_fusable(plan: GraphPlan, x: torch.Tensor, W: torch.Tensor, reduce: int
 
 def spmm_xw_fwd(view: CSRView, w: torch.Tensor | None, X: torch.Tensor, W: torch.Tensor,
                 reduce: int, bias: torch.Tensor | None = None, relu: bool = False,
-                relu_mask: torch.Tensor | None = None, want_z: bool = False):
+                relu_mask: torch.Tensor | None = None, want_z: bool = False,
+                out: torch.Tensor | None = None, z_out: torch.Tensor | None = None):
     """Y = epi((reduce_k X[col_k] * w_k) @ W + bias) in one launch
     (``mgcn_spmm_xw_fwd``): the layer's GEMM fused behind its aggregation, so
     X @ W is never written.  Sum / mean only (they commute with W).  With
     ``want_z`` returns (Y, Z): Z = the aggregated rows before W (for mean
-    before the division), from which the backward forms dW = Z^T dY."""
+    before the division), from which the backward forms dW = Z^T dY.
+    ``out`` / ``z_out``: [n_rows, F] row-major buffers (16-byte aligned rows)
+    to write Y / Z into instead of new tensors."""
     lib = L.load()
     X = _contig_f32(X, "X")
     if X.stride(0) % 4 or X.data_ptr() % 16:
@@ -176,11 +182,21 @@ def spmm_xw_fwd(view: CSRView, w: torch.Tensor | None, X: torch.Tensor, W: torch
                 not relu_mask.is_contiguous() or relu_mask.data_ptr() % 16):
             raise ValueError(f"spmm_xw_fwd: relu_mask must be a contiguous, 16-byte aligned "
                              f"int32 [{view.n_rows}, 4] tensor")
-    Y = torch.empty(view.n_rows, F_out, dtype=torch.float32, device=dev)
-    Z = torch.empty(view.n_rows, F_in, dtype=torch.float32, device=dev) if want_z else None
+    Y = out if out is not None else torch.empty(view.n_rows, F_out, dtype=torch.float32,
+                                                device=dev)
+    Z = None
+    if want_z:
+        Z = z_out if z_out is not None else torch.empty(view.n_rows, F_in, dtype=torch.float32,
+                                                        device=dev)
+    for name, t, f in (("out", Y, F_out), ("z_out", Z, F_in)):
+        if t is not None and (t.dtype != torch.float32 or t.dim() != 2 or t.size(0) != view.n_rows
+                              or t.size(1) != f or t.stride(1) != 1 or t.stride(0) % 4
+                              or t.data_ptr() % 16):
+            raise ValueError(f"spmm_xw_fwd: {name} must be float32 [{view.n_rows}, {f}] with "
+                             f"16-byte aligned rows")
     tname = "spmm_xw_fwd_z" if want_z else "spmm_xw_fwd"
     if _TIMER is not None:
-        _TIMER(tname, True)
+        _TIMER(tname, True, view.n_rows, view.edges)
     with L.device_guard(dev):
         rc = lib.mgcn_spmm_xw_fwd(view.n_rows, view.n_cols, F_in, F_out, L.ptr(view.rowptr),
                                   L.ptr(view.col), L.ptr(w), L.ptr(X), X.stride(0), L.ptr(W),
@@ -196,7 +212,8 @@ def spmm_xw_fwd(view: CSRView, w: torch.Tensor | None, X: torch.Tensor, W: torch
 def spmm_xw_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tensor | None,
                 dY: torch.Tensor, X: torch.Tensor, W: torch.Tensor, want_dx: bool = True,
                 relu_mask: torch.Tensor | None = None, row_div: torch.Tensor | None = None,
-                win_mask: torch.Tensor | None = None, slot_map: torch.Tensor | None = None):
+                win_mask: torch.Tensor | None = None, slot_map: torch.Tensor | None = None,
+                dx_out: torch.Tensor | None = None):
     """Both adjoints of a 128 -> 128 layer from one pass (``mgcn_spmm_xw_bwd``):
     dH = A^T dY [* row_scale] stays on chip, and dW = X^T dH, dX = dH W^T
     (with the lower layer's ReLU mask / row divisor / bias column sums, as
@@ -232,7 +249,13 @@ def spmm_xw_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tens
                                  or win_mask.size(1) != (F_out + 31) // 32):
         raise ValueError("spmm_xw_bwd: win_mask must be int32 [nnz, ceil(F/32)]")
     dW = None if dx_only else torch.empty(F_in, F_out, dtype=torch.float32, device=dev)
-    dX = torch.empty(M, F_in, dtype=torch.float32, device=dev) if want_dx else None
+    dX = None
+    if want_dx:
+        dX = dx_out if dx_out is not None else torch.empty(M, F_in, dtype=torch.float32,
+                                                           device=dev)
+        if (dX.dtype != torch.float32 or dX.dim() != 2 or tuple(dX.shape) != (M, F_in) or
+                dX.stride(1) != 1 or dX.stride(0) < F_in):
+            raise ValueError(f"spmm_xw_bwd: dx_out must be float32 [{M}, {F_in}], row-major")
     colsum = None
     if relu_mask is not None:
         if not want_dx:
@@ -245,7 +268,7 @@ def spmm_xw_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tens
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
     tname = "spmm_xw_bwd_dx" if dx_only else "spmm_xw_bwd" if want_dx else "spmm_xw_bwd_dw"
     if _TIMER is not None:
-        _TIMER(tname, True)
+        _TIMER(tname, True, view_t.n_rows, view_t.edges)
     with L.device_guard(dev):
         rc = lib.mgcn_spmm_xw_bwd(M, view_t.n_cols, F_in, F_out, L.ptr(view_t.rowptr),
                                   L.ptr(view_t.col), L.ptr(w_t), L.ptr(row_scale), L.ptr(dY),
@@ -274,7 +297,7 @@ def spmm_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tensor 
     dH = out if out is not None else torch.empty(view_t.n_rows, F, dtype=torch.float32,
                                                  device=dev)
     if _TIMER is not None:
-        _TIMER("spmm_bwd", True)
+        _TIMER("spmm_bwd", True, view_t.n_rows, view_t.edges)
     with L.device_guard(dev):
         rc = lib.mgcn_spmm_bwd(view_t.n_rows, F, L.ptr(view_t.rowptr), L.ptr(view_t.col),
                                L.ptr(view_t.eid), L.ptr(w_t), L.ptr(row_scale), L.ptr(dY),
@@ -329,7 +352,7 @@ def gemm_tn(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor | None = None,
     ws_bytes = int(lib.mgcn_gemm_tn_workspace_bytes(K, M, N))
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
     if _TIMER is not None:
-        _TIMER("gemm_tn", True)
+        _TIMER("gemm_tn", True, K)
     with L.device_guard(dev):
         rc = lib.mgcn_gemm_tn(K, M, N, L.ptr(A), A.stride(0), L.ptr(B), B.stride(0), L.ptr(C),
                               C.stride(0), int(bool(accumulate)), L.ptr(ws), ws_bytes,
@@ -358,7 +381,7 @@ def gemm_tn_split(A: torch.Tensor, B: torch.Tensor, n1: int):
     ws_bytes = int(lib.mgcn_gemm_tn_workspace_bytes(K, M, N))
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
     if _TIMER is not None:
-        _TIMER("gemm_tn", True)
+        _TIMER("gemm_tn", True, K)
     with L.device_guard(dev):
         rc = lib.mgcn_gemm_tn_split(K, M, N, n1, L.ptr(A), A.stride(0), L.ptr(B), B.stride(0),
                                     L.ptr(C1), max(n1, 1), L.ptr(C2), max(M, 1), 0, L.ptr(ws),
@@ -423,7 +446,7 @@ def gemm_nn(A: torch.Tensor, W: torch.Tensor, transpose_w: bool = False,
         ws_bytes = int(lib.mgcn_gemm_nn_workspace_bytes(M, N))
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
     if _TIMER is not None:
-        _TIMER("gemm_nn", True)
+        _TIMER("gemm_nn", True, M)
     with L.device_guard(dev):
         rc = lib.mgcn_gemm_nn(M, K, N, L.ptr(A), A.stride(0), L.ptr(W), sbk, sbn, L.ptr(C),
                               C.stride(0), L.ptr(relu_mask),
@@ -480,7 +503,7 @@ def gemm_bwd(x: torch.Tensor, dH: torch.Tensor, W: torch.Tensor, want_dx: bool =
     ws_bytes = int(lib.mgcn_gemm_bwd_workspace_bytes(M, F_in, F_out))
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
     if _TIMER is not None:
-        _TIMER("gemm_bwd" if want_dx else "gemm_bwd_dw", True)
+        _TIMER("gemm_bwd" if want_dx else "gemm_bwd_dw", True, M)
     with L.device_guard(dev):
         rc = lib.mgcn_gemm_bwd(M, F_in, F_out, L.ptr(x), x.stride(0), L.ptr(dH), dH.stride(0),
                                L.ptr(W), W.stride(0), L.ptr(dW), dW.stride(0),

@@ -36,7 +36,7 @@ def _problem(N=300, pairs=1500, F=16, L=3, seed=0):
     return ei, N, X, Ws, bs, dY
 
 
-def _run(rank, world, port, aggr, out_q):
+def _run(rank, world, port, aggr, out_q, F=16, fused=True, chunks=4):
     sys.path[:0] = [os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "meta-gcn_amd"),
                     HERE]
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -46,9 +46,10 @@ def _run(rank, world, port, aggr, out_q):
         torch.set_num_threads(1)
         from cpu_backend import CpuBackend
         from mgcn.dist import ShardedGCN
-        ei, N, X, Ws, bs, dY = _problem()
+        ei, N, X, Ws, bs, dY = _problem(F=F)
         m = ShardedGCN(ei, N, Ws, bs, device=torch.device("cpu"), aggr=aggr,
-                       backend=CpuBackend())
+                       backend=CpuBackend(), fused=fused, chunks=chunks)
+        assert m.fused == (fused and aggr != "max")
         Xl = m.local_rows(X).requires_grad_(True)
         out = m.forward(Xl)
         out.backward(m.local_rows(dY))
@@ -56,16 +57,25 @@ def _run(rank, world, port, aggr, out_q):
         allreduce_grads(m.params())
         res = {"rank": rank, "lo": m.shard.lo, "hi": m.shard.hi, "out": out.detach().numpy(),
                "dX": Xl.grad.numpy(), "grads": [p.grad.numpy() for p in m.params()]}
+        # the bench's form: replicated input in the exchange layout, no x grad
+        for p in m.params():
+            p.grad = None
+        out2 = m.forward(X_table=m.input_table(X))
+        out2.backward(m.local_rows(dY))
+        allreduce_grads(m.params())
+        res["out_table"] = out2.detach().numpy()
+        res["grads_table"] = [p.grad.numpy() for p in m.params()]
         out_q.put(res)
     finally:
         dist.destroy_process_group()
 
 
-def _launch(world, aggr):
+def _launch(world, aggr, F=16, fused=True, chunks=4):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_run, args=(r, world, port, aggr, q)) for r in range(world)]
+    procs = [ctx.Process(target=_run, args=(r, world, port, aggr, q, F, fused, chunks))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in range(world)]
@@ -76,17 +86,39 @@ def _launch(world, aggr):
     return res
 
 
-@pytest.mark.parametrize("world,aggr", [(2, "add"), (2, "mean"), (4, "add"), (2, "max")])
-def test_sharded_matches_single_process(world, aggr):
-    single = _launch(1, aggr)[0]
-    shards = _launch(world, aggr)
+@pytest.mark.parametrize("world,aggr,F,fused,chunks", [
+    (2, "add", 16, True, 4), (2, "mean", 16, True, 3), (4, "add", 16, True, 4),
+    (4, "mean", 16, True, 1), (2, "max", 16, True, 4), (4, "max", 16, True, 4),
+    (2, "add", 16, False, 4), (4, "add", 256, True, 4), (4, "mean", 256, False, 2),
+    (2, "max", 256, True, 3)])
+def test_sharded_matches_single_process(world, aggr, F, fused, chunks):
+    """World P against world 1 of the same path: fused stack (sum / mean,
+    chunked all-gathers) or per-layer path (max, or fused=False), F = 16 and
+    256, local input rows (with dX) and the replicated input table."""
+    single = _launch(1, aggr, F, fused, chunks)[0]
+    shards = _launch(world, aggr, F, fused, chunks)
     assert shards[0]["lo"] == 0 and shards[-1]["hi"] == single["out"].shape[0]
     for r in shards:
         lo, hi = r["lo"], r["hi"]
         np.testing.assert_array_equal(r["out"], single["out"][lo:hi])   # forward: bitwise
         np.testing.assert_array_equal(r["dX"], single["dX"][lo:hi])     # adjoint rows: bitwise
-        for g, g1 in zip(r["grads"], single["grads"]):                  # all-reduced partials
-            np.testing.assert_allclose(g, g1, rtol=1e-5, atol=1e-5)
+        np.testing.assert_array_equal(r["out_table"], single["out"][lo:hi])
+        for key in ("grads", "grads_table"):                            # all-reduced partials
+            for g, g1 in zip(r[key], single[key]):
+                np.testing.assert_allclose(g, g1, rtol=1e-5, atol=1e-5 * max(1, np.abs(g1).max()))
+
+
+def test_fused_and_per_layer_paths_agree():
+    """The fused sharded stack and the per-layer sharded path compute the
+    same layers: outputs within fp32 association tolerance ((A x) W against
+    A (x W)), dX and gradients within tolerance."""
+    a = _launch(2, "add", 16, True)
+    b = _launch(2, "add", 16, False)
+    for ra, rb in zip(a, b):
+        np.testing.assert_allclose(ra["out"], rb["out"], rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(ra["dX"], rb["dX"], rtol=1e-4, atol=1e-5)
+        for g, g1 in zip(ra["grads"], rb["grads"]):
+            np.testing.assert_allclose(g, g1, rtol=1e-4, atol=1e-4 * max(1, np.abs(g1).max()))
 
 
 def test_single_process_double_matches_oracle(oracle):
@@ -105,6 +137,19 @@ def test_single_process_double_matches_oracle(oracle):
     np.testing.assert_array_equal(y.detach().numpy(), y_ref)
     dH, _ = oracle.aggr_bwd(ei.numpy(), dY.numpy(), wb, rs, "add", y_ref, True, None)
     np.testing.assert_array_equal(x.grad.numpy(), dH)
+
+
+def test_table_positions_layout():
+    """Row i of rank k sits at c*P*cr + k*cr + (i - c*cr), c = i // cr: each
+    chunk's all-gather fills one contiguous block."""
+    from mgcn.dist import table_positions
+    bounds = [0, 5, 9, 14]
+    pos = table_positions(torch.arange(14), bounds, 2).tolist()
+    # rank 0 rows 0..4, rank 1 rows 5..8, rank 2 rows 9..13, cr = 2, P = 3
+    assert pos[:5] == [0, 1, 6, 7, 12]
+    assert pos[5:9] == [2, 3, 8, 9]
+    assert pos[9:] == [4, 5, 10, 11, 16]
+    assert len(set(pos)) == 14
 
 
 def test_partition_balances_edges():
