@@ -65,10 +65,7 @@ constexpr int kXwStageLd = kXwF + 8;           // backward staging row: 128 valu
                                                // 4 ReLU mask words, its divisor, padding
 constexpr int kXwStage = kXwRows * kXwStageLd * 4;
 constexpr int kXfStage = kXwRows * kXwF * 4;   // forward staging tile (unpadded: 2 fit)
-#ifndef MGCN_XW_PER_CU
-#define MGCN_XW_PER_CU 2
-#endif
-constexpr int kXwPerCU = MGCN_XW_PER_CU;  // resident workgroups per CU the grid is sized for
+constexpr int kXwPerCU = 2;  // resident workgroups per CU the grid is sized for
 
 constexpr int EPI_STORE = 0, EPI_RELU = 1, EPI_RELU_DIV = 2;
 
@@ -486,9 +483,6 @@ __device__ unsigned long long g_xprof[2][64][6];
 // DW = false: dX only (X == NULL) -- the caller forms dW = Z^T dY from the
 // forward's aggregate (mgcn_gemm_bwd, dW-only), so the chunk's X rows, their
 // images and the dW MFMAs drop out.
-#ifndef XB_META
-#define XB_META 1
-#endif
 template <int U, bool DX, int EPI, bool MAXM, bool DW = true>
 __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(const XbArgs a) {
   __shared__ __attribute__((aligned(16))) char lds[kXbLds];
@@ -595,7 +589,7 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
   const RowSeq seq{(int64_t)blockIdx.x * kXwRows + 2 * wave + grp, (int64_t)gridDim.x * kXwRows,
                    a.n_rows};
   RowMeta cur{}, nxt{};
-  if constexpr (!DW && !MAXM && XB_META) {
+  if constexpr (!DW && !MAXM) {
     meta_rowptr(a.rowptr, seq.row(0), seq.row(0) < a.n_rows, cur);
     meta_first(a.col, a.w, gl, cur);
     meta_rowptr(a.rowptr, seq.row(1), seq.row(1) < a.n_rows, nxt);
@@ -638,7 +632,7 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
       const bool row_ok = row < a.n_rows;
       int deg;
       float acc[4];
-      if constexpr (!DW && !MAXM && XB_META) {
+      if constexpr (!DW && !MAXM) {
         const int64_t k = 2 * it + p;
         meta_first(a.col, a.w, gl, nxt);
         RowMeta nn;

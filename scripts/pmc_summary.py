@@ -1,4 +1,4 @@
-"""Summarise the PMC passes of scripts/r02_profiles.sh into profiles/<round>/pmc_fused.json.
+"""Summarise the PMC passes of scripts/profile_round.sh into profiles/<round>/pmc_fused.json.
 
     python scripts/pmc_summary.py gpurun_out/r02 profiles/r02/pmc_fused.json
 
