@@ -342,20 +342,27 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(const SpmmArgs a) {
             // lane gl writes record gl out: 512 contiguous bytes per group.
             // One wave's LDS operations execute in order, so the zeroing,
             // the ORs and the read-back of a window need no barrier.
-            uint32_t *rec = win_rec + ((int)(threadIdx.x >> 6) * 2 + grp) * 32 * 4;
+            // the lane constants below are derived from an opaque copy of the
+            // lane id: hoisted out of the edge loop they would stay live
+            // through it (+21 VGPRs: 4 instead of 5 waves per SIMD)
+            int tl = (int)threadIdx.x;
+            asm volatile("" : "+v"(tl));
+            const int gl2 = tl & (G - 1);
+            uint32_t *rec = win_rec + ((tl >> 6) * 2 + ((tl & 63) / G)) * 32 * 4;
+            const int sh = (gl2 & 7) << 2;
             for (int64_t w0 = 0; w0 < maxdeg; w0 += 32) {
-              *reinterpret_cast<uint4 *>(rec + 4 * gl) = make_uint4(0u, 0u, 0u, 0u);
+              *reinterpret_cast<uint4 *>(rec + 4 * gl2) = make_uint4(0u, 0u, 0u, 0u);
               __builtin_amdgcn_wave_barrier();
 #pragma unroll
               for (int j = 0; j < VEC; ++j) {
                 const int64_t p = winner[j] - w0;
                 if (winner[j] >= 0 && p >= 0 && p < 32)
-                  atomicOr(rec + 4 * p + (gl >> 3), 1u << (((gl & 7) << 2) + j));
+                  atomicOr(rec + 4 * p + (gl2 >> 3), 1u << (sh + j));
               }
               __builtin_amdgcn_wave_barrier();
-              const uint4 r = *reinterpret_cast<const uint4 *>(rec + 4 * gl);
-              if (w0 + gl < deg)
-                *reinterpret_cast<uint4 *>(a.win_mask_out + (beg + w0 + gl) * W + 4 * c) = r;
+              const uint4 r = *reinterpret_cast<const uint4 *>(rec + 4 * gl2);
+              if (w0 + gl2 < deg)
+                *reinterpret_cast<uint4 *>(a.win_mask_out + (beg + w0 + gl2) * W + 4 * c) = r;
               __builtin_amdgcn_wave_barrier();
             }
           } else {
@@ -895,9 +902,11 @@ int launch_g(const SpmmArgs &a, hipStream_t stream) {
   }
   if (lanes > 16) {
     if (g_unroll == 16) return launch_one<VEC, 32, 16, MODE>(a, stream);
-    // the forward max at U = 8 holds 113 VGPRs (4 waves per SIMD); at U = 4
-    // it fits 93 (5 waves), the sum kernel's occupancy
-    if (g_unroll == 4 || (MODE == FWD_MAX && !g_unroll_set)) return launch_one<VEC, 32, 4, MODE>(a, stream);
+    // the forward max at U = 8 holds 104 VGPRs (4 waves per SIMD); at U = 6
+    // it fits 93 (5 waves, the sum kernel's occupancy, 30 rows in flight per
+    // SIMD lane slot against U = 4's 20)
+    if (g_unroll == 6 || (MODE == FWD_MAX && !g_unroll_set)) return launch_one<VEC, 32, 6, MODE>(a, stream);
+    if (g_unroll == 4) return launch_one<VEC, 32, 4, MODE>(a, stream);
     return launch_one<VEC, 32, 8, MODE>(a, stream);
   }
   if (lanes > 8) return launch_one<VEC, 16, 8, MODE>(a, stream);
@@ -1054,7 +1063,8 @@ extern "C" int mgcn_set_option(const char *name, int value) {
     return MGCN_OK;
   }
   if (n == "spmm_unroll") {
-    MGCN_REQUIRE(value == 4 || value == 8 || value == 16, "spmm_unroll must be 4, 8 or 16");
+    MGCN_REQUIRE(value == 4 || value == 6 || value == 8 || value == 16,
+                 "spmm_unroll must be 4, 6, 8 or 16");
     g_unroll = value;
     g_unroll_set = true;
     return MGCN_OK;

@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--feat", type=int, default=128)
     ap.add_argument("--variants", action="store_true")
+    ap.add_argument("--max", action="store_true",
+                    help="the max aggregation (winner bits forward, MAXM adjoint) at every unroll")
     ap.add_argument("--once", action="store_true", help="one fwd + one bwd launch (for PMC runs)")
     ap.add_argument("--calibrate", action="store_true",
                     help="known-byte launches for PMC calibration: a 2 GiB copy, and the SpMM "
@@ -75,6 +77,23 @@ def main():
         torch.cuda.synchronize()
         return
     B = spmm_bytes(N, nnz, F)
+    if args.max:
+        from mgcn import _lib as L
+        sm = plan.slot_map()
+        _, win = ops.spmm_fwd(plan.fwd, None, H, L.REDUCE_MAX, mask_plan=plan)
+        Bm = B + 16 * nnz  # + the winner record of every edge (written / read)
+        for u in (4, 6, 8):
+            mgcn.set_option("spmm_unroll", u)
+            f_med, f_min = time_it(lambda: ops.spmm_fwd(plan.fwd, None, H, L.REDUCE_MAX,
+                                                        mask_plan=plan), args.reps)
+            b_med, b_min = time_it(lambda: ops.spmm_bwd(plan.bwd, None, None, H, L.REDUCE_MAX,
+                                                        win_mask=win, slot_map=sm), args.reps)
+            s_med, _ = time_it(lambda: ops.spmm_fwd(plan.fwd, None, H, 0), args.reps)
+            print(json.dumps({"variant": f"max_u{u}", "fwd_ms": f_med, "fwd_gbs": Bm / f_med / 1e6,
+                              "bwd_ms": b_med, "bwd_gbs": Bm / b_med / 1e6, "sum_fwd_ms": s_med}),
+                  flush=True)
+        mgcn.set_option("spmm_unroll", 8)
+        return
     variants = [("default", {})]
     if args.variants:
         variants += [(f"vec{v}_u{u}", {"spmm_vec": v, "spmm_unroll": u})
@@ -89,19 +108,6 @@ def main():
                           "bwd_gbs": B / b_med / 1e6, "bytes": B}), flush=True)
     mgcn.set_option("spmm_vec", 0)
     mgcn.set_option("spmm_unroll", 8)
-    # feature-chunked passes: each pass gathers a column slice whose working
-    # set (N x chunk x 4 B) may stay resident in the 256 MiB Infinity Cache
-    Y = torch.empty(N, F, device=dev)
-    for chunks in (2, 4, 8):
-        w = F // chunks
-
-        def run(chunks=chunks, w=w):
-            for c in range(chunks):
-                ops.spmm_fwd(plan.fwd, norm.w_fwd, H[:, c * w:(c + 1) * w], 0,
-                             out=Y[:, c * w:(c + 1) * w])
-        f_med, f_min = time_it(run, args.reps)
-        print(json.dumps({"variant": f"chunks{chunks}", "fwd_ms": f_med, "fwd_min_ms": f_min,
-                          "fwd_gbs": B / f_med / 1e6}), flush=True)
 
 
 if __name__ == "__main__":
