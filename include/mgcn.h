@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define MGCN_ABI_VERSION 10
+#define MGCN_ABI_VERSION 11
 
 /* return codes */
 #define MGCN_OK 0
@@ -417,6 +417,50 @@ int mgcn_residual_act_bwd(int64_t n_rows, int32_t F, const float *dZ, int64_t ld
                           int64_t ldz1, int relu1, const float *row_div, float *dA,
                           int64_t ldda, float *dS, int64_t ldds, float *colsums,
                           void *workspace, size_t workspace_bytes, void *stream);
+
+/*
+ * One GCNModel layer with its residual Linear, F = 32 (the botnet stack of
+ * config 3: GCNLayer + residuals[n] + the join, gcn_model.py:89-105 with
+ * residual_hop = 1; NodeModelAdditive.forward gcn_base_models.py:199-243):
+ *   Z1 = relu1((A X) W + bias),  Z = relu2(Z1 + (X Wr^T + rbias))
+ * in one pass over the rows (fwd view: rows = destinations; order / n_heavy /
+ * n_giant its row schedule, as mgcn_spmm_fwd).  W is [F][F] (H = X W), Wr
+ * the Linear weight [out][in]; bias / rbias may be NULL; reduce SUM or MEAN.
+ * masks[2 i] / masks[2 i + 1]: bit c <=> Z1[i][c] > 0 / Z[i][c] > 0
+ * (the activations the backward needs).  Z must not alias X.  Replaces the
+ * reference's x @ W, gather / scale / scatter_add, + b, ReLU, the residual
+ * Linear, `xo + xr` and the join's ReLU.
+ */
+int mgcn_residual_layer_supported(int32_t F_in, int32_t F_out, int reduce);
+int mgcn_residual_layer_fwd(int64_t n_rows, int32_t F, const int64_t *rowptr,
+                            const int32_t *col, const int32_t *eid, const float *w,
+                            const float *X, int64_t ldx, const float *W, int64_t ldw,
+                            const float *bias, const float *Wr, int64_t ldwr,
+                            const float *rbias, int reduce, int relu1, int relu2,
+                            float *Z, int64_t ldz, uint32_t *masks, const int32_t *order,
+                            int64_t n_heavy, int64_t n_giant, void *stream);
+
+/* Bytes of scratch mgcn_residual_layer_bwd needs (dA rows + column sums). */
+size_t mgcn_residual_layer_bwd_workspace_bytes(int64_t n_rows, int32_t F);
+
+/*
+ * Its adjoint (bwd view: rows = sources; row_scale the 'rw' post-scale,
+ * row_div the in-degree divisor for MEAN, both nullable):
+ *   dS = relu2' dZ,  dA = relu1' dS [/ row_div]        (from masks)
+ *   DH[:, 0:F] = dH = A^T dA,  DH[:, F:2F] = dS         (lddh >= 2F)
+ *   dX = dH W^T + dS Wr
+ *   colsums[0:F] = sum_i dA (undivided: the bias gradient), [F:2F] = sum_i dS
+ * [dW | dWr^T] = X^T DH is then one mgcn_gemm_tn_split.  dH is bit for bit
+ * mgcn_spmm_bwd's of dA.
+ */
+int mgcn_residual_layer_bwd(int64_t n_rows, int32_t F, const int64_t *rowptr_t,
+                            const int32_t *col_t, const int32_t *eid_t, const float *w_t,
+                            const float *row_scale, const float *row_div, const float *dZ,
+                            int64_t lddz, const uint32_t *masks, int relu1, int relu2,
+                            const float *W, int64_t ldw, const float *Wr, int64_t ldwr,
+                            float *dX, int64_t lddx, float *DH, int64_t lddh, float *colsums,
+                            const int32_t *order, int64_t n_heavy, int64_t n_giant,
+                            void *workspace, size_t workspace_bytes, void *stream);
 
 /*
  * Segment mean over contiguous node ranges (PyG global_mean_pool on a

@@ -70,5 +70,11 @@ int launch_fold_split(const float *partial, int64_t splits, int64_t MN, int N, f
 int launch_split_reduce(const float *partial, int splits, int64_t MN, int N, float *C,
                         int64_t ldc, int accumulate, hipStream_t s);
 int launch_colsum_fold(const float *partial, int64_t nparts, int N, float *out, hipStream_t s);
+// heavy rows of a view alone (spmm.hip), for the fused layer kernels of residual.hip
+int heavy_rows(int bwd, int64_t n_rows, int32_t F, const int64_t *rowptr, const int32_t *col,
+               const int32_t *eid, const float *w, const float *X, int64_t ldx, float *Y,
+               int64_t ldy, const float *row_scale, int mean, const int32_t *order,
+               int64_t n_heavy, int64_t n_giant, hipStream_t stream, bool *side_used);
+int heavy_rows_join(hipStream_t stream);
 
 }  // namespace mgcn

@@ -1041,6 +1041,67 @@ int launch_mode(SpmmArgs a, int vec, hipStream_t stream) {
 }
 
 }  // namespace
+
+// Heavy rows only (residual.hip's fused layer kernels aggregate the light
+// rows themselves): the giant rows on the side stream, the other heavy rows
+// on `stream`.  Forward (bwd = 0): Y[row] = sum / mean of the row's gathered
+// X rows; backward (bwd = 1): Y[row] = the adjoint sum (* row_scale).
+// *side_used: the caller must heavy_rows_join(stream) before reading the
+// giant rows' results.
+int heavy_rows(int bwd, int64_t n_rows, int32_t F, const int64_t *rowptr, const int32_t *col,
+               const int32_t *eid, const float *w, const float *X, int64_t ldx, float *Y,
+               int64_t ldy, const float *row_scale, int mean, const int32_t *order,
+               int64_t n_heavy, int64_t n_giant, hipStream_t stream, bool *side_used) {
+  *side_used = false;
+  if (order == nullptr || n_heavy <= 0) return MGCN_OK;
+  SpmmArgs a{};
+  a.n_rows = n_rows;
+  a.F = F;
+  a.n_chunks = 1;
+  a.rowptr = rowptr;
+  a.col = col;
+  a.eid = eid;
+  a.w = w;
+  a.X = X;
+  a.ldx = ldx;
+  a.Y = Y;
+  a.ldy = ldy;
+  a.row_scale = row_scale;
+  a.mean = mean;
+  a.order = order;
+  a.n_heavy = n_heavy;
+  a.n_giant = n_giant;
+  const int vec = pick_vec(F, X, ldx, Y, ldy);
+  if (n_giant > 0) {
+    SideStream *side = nullptr;
+    if (g_heavy_side) {
+      if (int rc = side_stream(&side)) return rc;
+      MGCN_HIP_TRY(hipEventRecord(side->fork, stream));
+      MGCN_HIP_TRY(hipStreamWaitEvent(side->stream, side->fork, 0));
+      const int rc = bwd ? launch_heavy_v<BWD_SUM>(a, vec, true, side->stream)
+                         : launch_heavy_v<FWD_SUM>(a, vec, true, side->stream);
+      if (rc) return rc;
+      MGCN_HIP_TRY(hipEventRecord(side->join, side->stream));
+      *side_used = true;
+    } else {
+      const int rc = bwd ? launch_heavy_v<BWD_SUM>(a, vec, true, stream)
+                         : launch_heavy_v<FWD_SUM>(a, vec, true, stream);
+      if (rc) return rc;
+    }
+  }
+  if (n_heavy > n_giant)
+    return bwd ? launch_heavy_v<BWD_SUM>(a, vec, false, stream)
+               : launch_heavy_v<FWD_SUM>(a, vec, false, stream);
+  return MGCN_OK;
+}
+
+int heavy_rows_join(hipStream_t stream) {
+  SideStream *side = nullptr;
+  if (int rc = side_stream(&side)) return rc;
+  MGCN_HIP_TRY(hipStreamWaitEvent(stream, side->join, 0));
+  return MGCN_OK;
+}
+
 }  // namespace mgcn
 
 using namespace mgcn;

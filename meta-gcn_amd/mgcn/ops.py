@@ -1004,11 +1004,111 @@ class _ResidualGCNLayer(torch.autograd.Function):
         return (dx, None, None, None, None, None, dW, db, dWr, dbr)
 
 
+def _aligned_rows(t: torch.Tensor) -> torch.Tensor:
+    """Contiguous fp32 with 16-byte aligned rows (the fused kernels' float4 accesses)."""
+    t = _contig_f32(t, "x")
+    if t.stride(0) % 4 or t.data_ptr() % 16 or t.stride(1) != 1:
+        t = t.contiguous()
+    return t
+
+
+def residual_layer_supported(plan: GraphPlan, x: torch.Tensor, W: torch.Tensor, Wr: torch.Tensor,
+                             reduce: int) -> bool:
+    """True when :class:`_ResidualLayerFused` takes this layer: 32 -> 32 with a
+    32 -> 32 residual Linear, sum or mean, fp32, on a square graph plan."""
+    return (_FUSE_XW and x.dim() == 2 and x.dtype == torch.float32 and x.is_cuda and
+            W.dtype == torch.float32 and Wr.dtype == torch.float32 and
+            tuple(W.shape) == (x.size(1), x.size(1)) and tuple(Wr.shape) == tuple(W.shape) and
+            x.size(0) == plan.fwd.n_rows == plan.fwd.n_cols and
+            bool(L.load().mgcn_residual_layer_supported(x.size(1), W.size(1), int(reduce))))
+
+
+class _ResidualLayerFused(torch.autograd.Function):
+    """One GCNModel layer with its residual Linear (gcn_model.py:89-105,
+    residual_hop = 1), F = 32, on libmgcn's fused residual-layer kernels
+    (residual.hip): the forward is one pass over the rows (aggregation of x,
+    both 32 x 32 products, bias, ReLU, join, ReLU; ReLU masks kept instead of
+    the activations), the backward one mask pass + one pass that gathers the
+    adjoint and forms dX = dH W^T + dS Wr, then [dW | dWr^T] = x^T [dH | dS]
+    as one GEMM.  (A x) W instead of A (x W): the same layer to fp32
+    rounding; the adjoint dH is the SpMM's bit for bit."""
+
+    @staticmethod
+    def forward(ctx, x, plan, norm, reduce, relu1, relu2, W, b, Wr, br):
+        lib = L.load()
+        x = _aligned_rows(x)
+        dev = L.require_device(x, W, Wr, b, br)
+        n, F = x.shape
+        Wd = W.detach().to(torch.float32).contiguous()
+        Wrd = Wr.detach().to(torch.float32).contiguous()
+        bd = None if b is None else b.detach().to(torch.float32).contiguous()
+        brd = None if br is None else br.detach().to(torch.float32).contiguous()
+        Z = torch.empty(n, F, dtype=torch.float32, device=dev)
+        masks = torch.empty(n, 2, dtype=torch.int32, device=dev)
+        v = plan.fwd
+        if _TIMER is not None:
+            _TIMER("residual_layer_fwd", True, v.n_rows, v.edges)
+        with L.device_guard(dev):
+            rc = lib.mgcn_residual_layer_fwd(n, F, L.ptr(v.rowptr), L.ptr(v.col), L.ptr(v.eid),
+                                             L.ptr(norm.w_fwd), L.ptr(x), x.stride(0), L.ptr(Wd),
+                                             F, L.ptr(bd), L.ptr(Wrd), F, L.ptr(brd), int(reduce),
+                                             int(bool(relu1)), int(bool(relu2)), L.ptr(Z), F,
+                                             L.ptr(masks), L.ptr(v.order), v.n_heavy, v.n_giant,
+                                             L.stream_of(dev))
+        if _TIMER is not None:
+            _TIMER("residual_layer_fwd", False)
+        L.check(rc, "mgcn_residual_layer_fwd")
+        ctx.plan, ctx.norm, ctx.reduce, ctx.relu1, ctx.relu2 = plan, norm, reduce, relu1, relu2
+        ctx.has_b, ctx.has_br = b is not None, br is not None
+        ctx.save_for_backward(x, Wd, Wrd, masks)
+        return Z
+
+    @staticmethod
+    def backward(ctx, dZ):
+        lib = L.load()
+        x, Wd, Wrd, masks = ctx.saved_tensors
+        plan, norm = ctx.plan, ctx.norm
+        dZ = _aligned_rows(dZ)
+        dev = dZ.device
+        n, F = x.shape
+        dX = torch.empty(n, F, dtype=torch.float32, device=dev)
+        DH = torch.empty(n, 2 * F, dtype=torch.float32, device=dev)
+        sums = torch.empty(2 * F, dtype=torch.float32, device=dev)
+        ws_bytes = int(lib.mgcn_residual_layer_bwd_workspace_bytes(n, F))
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+        v = plan.bwd
+        rd = plan.in_cnt if ctx.reduce == L.REDUCE_MEAN else None
+        if _TIMER is not None:
+            _TIMER("residual_layer_bwd", True, v.n_rows, v.edges)
+        with L.device_guard(dev):
+            rc = lib.mgcn_residual_layer_bwd(n, F, L.ptr(v.rowptr), L.ptr(v.col), L.ptr(v.eid),
+                                             L.ptr(norm.w_bwd), L.ptr(norm.row_scale_bwd),
+                                             L.ptr(rd), L.ptr(dZ), dZ.stride(0), L.ptr(masks),
+                                             int(bool(ctx.relu1)), int(bool(ctx.relu2)),
+                                             L.ptr(Wd), F, L.ptr(Wrd), F, L.ptr(dX), F,
+                                             L.ptr(DH), 2 * F, L.ptr(sums), L.ptr(v.order),
+                                             v.n_heavy, v.n_giant, L.ptr(ws), ws_bytes,
+                                             L.stream_of(dev))
+        if _TIMER is not None:
+            _TIMER("residual_layer_bwd", False)
+        L.check(rc, "mgcn_residual_layer_bwd")
+        # [dW | dWr^T] = x^T [dH | dS] in one pass, dWr written transposed
+        dW, dWr = gemm_tn_split(x, DH, F)
+        db = sums[:F] if ctx.has_b else None
+        dbr = sums[F:] if ctx.has_br else None
+        dx = dX if ctx.needs_input_grad[0] else None
+        return (dx, None, None, None, None, None, dW, db, dWr, dbr)
+
+
 def residual_gcn_layer(x, plan: GraphPlan, norm: NormPlan, aggr: str, relu1: bool, relu2: bool,
                        W, b, Wr, br):
-    """See :class:`_ResidualGCNLayer`."""
-    return _ResidualGCNLayer.apply(x, plan, norm, L.REDUCE_CODES[aggr], bool(relu1), bool(relu2),
-                                   W, b, Wr, br)
+    """One GCNModel layer + residual join: :class:`_ResidualLayerFused` where
+    it applies (32 -> 32, sum / mean), else :class:`_ResidualGCNLayer`."""
+    reduce = L.REDUCE_CODES[aggr]
+    if residual_layer_supported(plan, x, W, Wr, reduce):
+        return _ResidualLayerFused.apply(x, plan, norm, reduce, bool(relu1), bool(relu2), W, b,
+                                         Wr, br)
+    return _ResidualGCNLayer.apply(x, plan, norm, reduce, bool(relu1), bool(relu2), W, b, Wr, br)
 
 
 # ---------------------------------------------------------------- scatter_

@@ -649,9 +649,12 @@ def test_linear_matches_torch(cuda, M, fin, fout):
 @pytest.mark.parametrize("aggr,deg_norm,bias", [("add", "sm", False), ("mean", "rw", True),
                                                 ("max", None, True)])
 def test_gcn_model_residual_fused_matches_step_by_step(cuda, aggr, deg_norm, bias):
-    """GCNModel(residual_hop=1) through the fused residual layer node equals
-    the step-for-step path (gcn_model.py:86-125): forward bitwise, gradients
-    within fp32 GEMM tolerance; includes a skewed (heavy-row) graph."""
+    """GCNModel(residual_hop=1) through the fused residual layer nodes equals
+    the step-for-step path (gcn_model.py:86-125): forward bitwise where the
+    layer keeps the reference's association (max, and the first 1 -> 32
+    layer), within fp32 tolerance where the 32 -> 32 layers run
+    (A x) W on the fused residual-layer kernels (add, mean); gradients within
+    fp32 GEMM tolerance; includes a skewed (heavy-row) graph."""
     from mgcn.models import GCNModel
     rng = np.random.default_rng(21)
     N = 4000
@@ -675,7 +678,11 @@ def test_gcn_model_residual_fused_matches_step_by_step(cuda, aggr, deg_norm, bia
                           {k: p.grad.clone() for k, p in model.named_parameters()})
         finally:
             GCNModel.fuse_residual = True
-    assert torch.equal(res[True][0], res[False][0])
+    if aggr == "max":
+        assert torch.equal(res[True][0], res[False][0])
+    else:
+        torch.testing.assert_close(res[True][0], res[False][0], rtol=1e-4,
+                                   atol=1e-5 * max(1.0, float(res[False][0].abs().max())))
     for k, g in res[False][1].items():
         scale = max(1.0, float(g.abs().max()))
         torch.testing.assert_close(res[True][1][k], g, rtol=1e-4, atol=1e-5 * scale, msg=k)

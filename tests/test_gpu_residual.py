@@ -1,0 +1,140 @@
+"""The fused residual-layer kernels (libmgcn mgcn_residual_layer_fwd / _bwd,
+residual.hip): one GCNModel layer with its residual Linear at F = 32 (the
+botnet stack of config 3, gcn_model.py:89-105 with residual_hop = 1), on
+skewed graphs whose rows take every path (light rows in the fused kernel,
+heavy and giant rows through the SpMM's workgroup kernels then the fused
+epilogue).
+
+Bars:
+  * W = I, Wr = 0, no biases: every product is exact, so Z = relu(A x) equals
+    the oracle's aggregation BIT FOR BIT, and the masks are its ReLU bits;
+  * backward with W = I, Wr = 0: dX = dH = A^T (relu' dZ) bit for bit the
+    oracle adjoint; with W = 0, Wr = I: dX = dS = relu2' dZ exactly;
+  * random weights: forward, dx and all four parameter gradients against the
+    two-launch layer (ops._ResidualGCNLayer: x @ [W | Wr^T], SpMM, join) within
+    fp32 tolerance (the fused layer associates (A x) W).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _t(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def _skewed(rng, N, E, hubs=((0, 2000), (1, 300), (2, 700))):
+    """Random graph + hub nodes (in- and out-edges) + self-loops: heavy rows
+    above 128 edges, giant ones above 512, in both views."""
+    s, d = [rng.integers(0, N, E)], [rng.integers(0, N, E)]
+    for h, k in hubs:
+        s += [rng.integers(0, N, k), np.full(k, h)]
+        d += [np.full(k, h), rng.integers(0, N, k)]
+    s.append(np.arange(N))
+    d.append(np.arange(N))
+    return np.stack([np.concatenate(s), np.concatenate(d)]).astype(np.int64)
+
+
+def _plan(cuda, ei, N, deg_norm):
+    from mgcn.graph import plan_for
+    plan = plan_for(_t(ei, cuda), N)
+    return plan, plan.norm(deg_norm)
+
+
+@pytest.mark.parametrize("deg_norm,aggr", [("sm", "add"), ("rw", "mean"), (None, "add")])
+@pytest.mark.parametrize("relu1,relu2", [(True, True), (True, False), (False, True)])
+def test_residual_layer_identity_bitwise(cuda, oracle, deg_norm, aggr, relu1, relu2):
+    from mgcn import _lib as L
+    from mgcn import ops
+    rng = np.random.default_rng(7 + relu1 + 2 * relu2 + len(aggr))
+    N, F = 6000, 32
+    ei = _skewed(rng, N, 40000)
+    plan, norm = _plan(cuda, ei, N, deg_norm)
+    assert plan.fwd.n_heavy > 0 and plan.fwd.n_giant > 0 and plan.bwd.n_giant > 0
+    x = rng.standard_normal((N, F)).astype(np.float32)
+    dZ = rng.standard_normal((N, F)).astype(np.float32)
+    reduce = L.REDUCE_CODES[aggr]
+    xt = _t(x, cuda).requires_grad_(True)
+    eye, zero = torch.eye(F, device=cuda), torch.zeros(F, F, device=cuda)
+    Wt, Wrt = eye.clone().requires_grad_(True), zero.clone().requires_grad_(True)
+    assert ops.residual_layer_supported(plan, xt, Wt, Wrt, reduce)
+    Z = ops._ResidualLayerFused.apply(xt, plan, norm, reduce, relu1, relu2, Wt, None, Wrt, None)
+    wf, wb, rs = oracle.edge_factors(ei, N, deg_norm)
+    agg, _ = oracle.aggr_fwd(ei, x, wf, aggr, None, relu1)
+    ref = np.maximum(agg, 0) if relu2 else agg
+    np.testing.assert_array_equal(Z.detach().cpu().numpy(), ref)
+    Z.backward(_t(dZ, cuda))
+    # Wr = 0: dX = dH = A^T (relu1' relu2' dZ) [/ count], the oracle adjoint
+    g = np.where(ref > 0, dZ, 0) if relu2 else dZ
+    dH, _ = oracle.aggr_bwd(ei, g, wb, rs, aggr, agg, relu1, None)
+    np.testing.assert_array_equal(xt.grad.cpu().numpy(), dH)
+    # W = 0, Wr = I: dX = dS exactly
+    xt.grad = None
+    Z = ops._ResidualLayerFused.apply(xt, plan, norm, reduce, relu1, relu2, zero, None, eye, None)
+    Z.backward(_t(dZ, cuda))
+    z = x.copy()
+    zz = np.maximum(np.maximum(0, 0) + z, 0) if relu2 else z  # relu1(0) + x
+    np.testing.assert_array_equal(Z.detach().cpu().numpy(), zz)
+    np.testing.assert_array_equal(xt.grad.cpu().numpy(), np.where(zz > 0, dZ, 0) if relu2 else dZ)
+
+
+@pytest.mark.parametrize("deg_norm,aggr,bias", [("sm", "add", False), ("sm", "add", True),
+                                                ("rw", "mean", True), (None, "mean", False)])
+@pytest.mark.parametrize("relu2", [True, False])
+def test_residual_layer_vs_two_launch(cuda, deg_norm, aggr, bias, relu2):
+    from mgcn import _lib as L
+    from mgcn import ops
+    rng = np.random.default_rng(11 + bias + 2 * relu2)
+    N, F = 8000, 32
+    ei = _skewed(rng, N, 60000)
+    plan, norm = _plan(cuda, ei, N, deg_norm)
+    reduce = L.REDUCE_CODES[aggr]
+    g = torch.Generator(device=cuda).manual_seed(5)
+    x = torch.randn(N, F, device=cuda, generator=g)
+    dZ = torch.randn(N, F, device=cuda, generator=g)
+    params = [torch.randn(F, F, device=cuda, generator=g) * 0.2,
+              torch.randn(F, device=cuda, generator=g) * 0.1 if bias else None,
+              torch.randn(F, F, device=cuda, generator=g) * 0.2,
+              torch.randn(F, device=cuda, generator=g) * 0.1]
+    outs = []
+    for fn in (ops._ResidualLayerFused, ops._ResidualGCNLayer):
+        xi = x.clone().requires_grad_(True)
+        ps = [None if p is None else p.clone().requires_grad_(True) for p in params]
+        Z = fn.apply(xi, plan, norm, reduce, True, relu2, *ps)
+        Z.backward(dZ)
+        outs.append([Z.detach(), xi.grad] + [None if p is None else p.grad for p in ps])
+    for a, b in zip(*outs):
+        if b is None:
+            assert a is None
+            continue
+        scale = float(b.abs().max())
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=2e-5 * max(1.0, scale))
+
+
+def test_residual_layer_deterministic_and_first_layer_fallback(cuda):
+    """Repeated runs are bitwise identical (fixed summation orders, no
+    atomics); a 1 -> 32 first layer (F_in != 32) keeps the two-launch path."""
+    from mgcn import _lib as L
+    from mgcn import ops
+    rng = np.random.default_rng(3)
+    N, F = 5000, 32
+    plan, norm = _plan(cuda, _skewed(rng, N, 30000), N, "sm")
+    g = torch.Generator(device=cuda).manual_seed(1)
+    x = torch.randn(N, F, device=cuda, generator=g)
+    W, Wr = torch.randn(F, F, device=cuda, generator=g), torch.randn(F, F, device=cuda, generator=g)
+    b = torch.randn(F, device=cuda, generator=g)
+    dZ = torch.randn(N, F, device=cuda, generator=g)
+    res = []
+    for _ in range(2):
+        xi = x.clone().requires_grad_(True)
+        ps = [p.clone().requires_grad_(True) for p in (W, b, Wr, b)]
+        Z = ops._ResidualLayerFused.apply(xi, plan, norm, L.REDUCE_SUM, True, True, *ps)
+        Z.backward(dZ)
+        res.append([Z.detach(), xi.grad] + [p.grad for p in ps])
+    for a, c in zip(*res):
+        assert torch.equal(a, c)
+    x1 = torch.randn(N, 1, device=cuda)
+    assert not ops.residual_layer_supported(plan, x1, torch.randn(1, F, device=cuda),
+                                            torch.randn(F, 1, device=cuda), L.REDUCE_SUM)
