@@ -463,6 +463,34 @@ int mgcn_residual_layer_bwd(int64_t n_rows, int32_t F, const int64_t *rowptr_t,
                             void *workspace, size_t workspace_bytes, void *stream);
 
 /*
+ * A stack of n_layers such layers in one call (GCNModel's 32 -> 32 layers):
+ * layer l reads X0 (l = 0) or Z[l - 1] and writes Z[l] = Z + l n_rows F and
+ * masks + 2 l n_rows; W / bias / Wr / rbias / relu1 / relu2 are host arrays
+ * with one entry per layer (device pointers; bias / rbias arrays or entries
+ * may be NULL).  The backward runs the layers top-down: dZ the top layer's
+ * upstream gradient, dW[l] ([F][F]) and dWr[l] ([F][F], the Linear layout)
+ * written per layer, sums + 2 F l = (bias | rbias gradient) of layer l, dX0
+ * (nullable) the gradient of X0.  Bitwise the layer-by-layer calls.
+ */
+int mgcn_residual_stack_fwd(int64_t n_rows, int32_t F, int32_t n_layers, const int64_t *rowptr,
+                            const int32_t *col, const int32_t *eid, const float *w,
+                            const float *X0, int64_t ldx, const float *const *W,
+                            const float *const *bias, const float *const *Wr,
+                            const float *const *rbias, int reduce, const int32_t *relu1,
+                            const int32_t *relu2, float *Z, uint32_t *masks,
+                            const int32_t *order, int64_t n_heavy, int64_t n_giant, void *stream);
+size_t mgcn_residual_stack_bwd_workspace_bytes(int64_t n_rows, int32_t F);
+int mgcn_residual_stack_bwd(int64_t n_rows, int32_t F, int32_t n_layers, const int64_t *rowptr_t,
+                            const int32_t *col_t, const int32_t *eid_t, const float *w_t,
+                            const float *row_scale, const float *row_div, const float *dZ,
+                            int64_t lddz, const float *X0, int64_t ldx, const float *Z,
+                            const uint32_t *masks, const int32_t *relu1, const int32_t *relu2,
+                            const float *const *W, const float *const *Wr, float *dX0,
+                            float *const *dW, float *const *dWr, float *sums,
+                            const int32_t *order, int64_t n_heavy, int64_t n_giant,
+                            void *workspace, size_t workspace_bytes, void *stream);
+
+/*
  * Segment mean over contiguous node ranges (PyG global_mean_pool on a
  * collated Batch, kernel/gcn.py:29; GCNModel pred_on='graph',
  * gcn_model.py:112-123):  out[g, :] = sum_{i in [ptr[g], ptr[g+1])} x[i, :]

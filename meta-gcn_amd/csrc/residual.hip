@@ -508,3 +508,101 @@ extern "C" int mgcn_residual_layer_bwd(int64_t n_rows, int32_t F, const int64_t 
   a.n_items = n_heavy;
   return launch_rl<true>(a, s);
 }
+
+// ---------------------------------------------------------------------------
+// A whole stack of such layers per call (GCNModel's 32 -> 32 layers, config 3):
+// one host call per direction instead of one (forward) / two (backward) per
+// layer -- the host's issue time, not the GPU, bounded the 12-layer step.
+
+extern "C" int mgcn_residual_stack_fwd(int64_t n_rows, int32_t F, int32_t n_layers,
+                                       const int64_t *rowptr, const int32_t *col,
+                                       const int32_t *eid, const float *w, const float *X0,
+                                       int64_t ldx, const float *const *W,
+                                       const float *const *bias, const float *const *Wr,
+                                       const float *const *rbias, int reduce,
+                                       const int32_t *relu1, const int32_t *relu2, float *Z,
+                                       uint32_t *masks, const int32_t *order, int64_t n_heavy,
+                                       int64_t n_giant, void *stream) {
+  clear_error();
+  MGCN_REQUIRE(n_rows >= 0 && n_layers >= 0, "mgcn_residual_stack_fwd: negative size");
+  MGCN_REQUIRE(n_layers == 0 || (W && Wr && relu1 && relu2 && Z && masks),
+               "mgcn_residual_stack_fwd: null array");
+  for (int32_t l = 0; l < n_layers; ++l) {
+    const float *xin = l == 0 ? X0 : Z + (int64_t)(l - 1) * n_rows * F;
+    const int64_t ldin = l == 0 ? ldx : F;
+    if (int rc = mgcn_residual_layer_fwd(n_rows, F, rowptr, col, eid, w, xin, ldin, W[l], F,
+                                         bias ? bias[l] : nullptr, Wr[l], F,
+                                         rbias ? rbias[l] : nullptr, reduce, relu1[l], relu2[l],
+                                         Z + (int64_t)l * n_rows * F, F,
+                                         masks + (int64_t)l * n_rows * 2, order, n_heavy, n_giant,
+                                         stream))
+      return rc;
+  }
+  return MGCN_OK;
+}
+
+namespace {
+struct StackScratch {
+  size_t layer, dh, dx, gemm, total;
+};
+StackScratch stack_scratch(int64_t n_rows, int32_t F) {
+  StackScratch s{};
+  const int64_t n = n_rows > 0 ? n_rows : 1;
+  s.layer = 0;
+  s.dh = align_up(mgcn_residual_layer_bwd_workspace_bytes(n_rows, F), 256);
+  s.dx = s.dh + align_up((size_t)n * 2 * F * sizeof(float), 256);
+  s.gemm = s.dx + 2 * align_up((size_t)n * F * sizeof(float), 256);
+  s.total = s.gemm + align_up(mgcn_gemm_tn_workspace_bytes(n_rows, F, 2 * F), 256);
+  return s;
+}
+}  // namespace
+
+extern "C" size_t mgcn_residual_stack_bwd_workspace_bytes(int64_t n_rows, int32_t F) {
+  return stack_scratch(n_rows, F).total;
+}
+
+extern "C" int mgcn_residual_stack_bwd(int64_t n_rows, int32_t F, int32_t n_layers,
+                                       const int64_t *rowptr_t, const int32_t *col_t,
+                                       const int32_t *eid_t, const float *w_t,
+                                       const float *row_scale, const float *row_div,
+                                       const float *dZ, int64_t lddz, const float *X0,
+                                       int64_t ldx, const float *Z, const uint32_t *masks,
+                                       const int32_t *relu1, const int32_t *relu2,
+                                       const float *const *W, const float *const *Wr, float *dX0,
+                                       float *const *dW, float *const *dWr, float *sums,
+                                       const int32_t *order, int64_t n_heavy, int64_t n_giant,
+                                       void *workspace, size_t workspace_bytes, void *stream) {
+  clear_error();
+  MGCN_REQUIRE(n_rows >= 0 && n_layers >= 0, "mgcn_residual_stack_bwd: negative size");
+  if (n_layers == 0) return MGCN_OK;
+  MGCN_REQUIRE(W && Wr && dW && dWr && sums && relu1 && relu2 && masks && Z && dZ && X0,
+               "mgcn_residual_stack_bwd: null array");
+  const StackScratch sc = stack_scratch(n_rows, F);
+  if (workspace == nullptr || workspace_bytes < sc.total) {
+    set_error("mgcn_residual_stack_bwd: workspace %zu < %zu", workspace_bytes, sc.total);
+    return MGCN_EWORKSPACE;
+  }
+  char *ws = static_cast<char *>(workspace);
+  float *DH = reinterpret_cast<float *>(ws + sc.dh);
+  float *dxb[2] = {reinterpret_cast<float *>(ws + sc.dx),
+                   reinterpret_cast<float *>(ws + sc.dx +
+                                             align_up((size_t)(n_rows > 0 ? n_rows : 1) * F * 4, 256))};
+  const size_t gemm_bytes = sc.total - sc.gemm;
+  for (int32_t l = n_layers - 1; l >= 0; --l) {
+    const float *dz = l == n_layers - 1 ? dZ : dxb[(l + 1) & 1];
+    const int64_t ldz = l == n_layers - 1 ? lddz : F;
+    float *dx = (l == 0 && dX0 != nullptr) ? dX0 : dxb[l & 1];
+    if (int rc = mgcn_residual_layer_bwd(n_rows, F, rowptr_t, col_t, eid_t, w_t, row_scale, row_div,
+                                         dz, ldz, masks + (int64_t)l * n_rows * 2, relu1[l],
+                                         relu2[l], W[l], F, Wr[l], F, dx, F, DH, 2 * F,
+                                         sums + (int64_t)l * 2 * F, order, n_heavy, n_giant,
+                                         ws + sc.layer, sc.dh - sc.layer, stream))
+      return rc;
+    // [dW | dWr^T] = X_l^T [dH | dS]
+    const float *xin = l == 0 ? X0 : Z + (int64_t)(l - 1) * n_rows * F;
+    if (int rc = mgcn_gemm_tn_split(n_rows, F, 2 * F, F, xin, l == 0 ? ldx : F, DH, 2 * F, dW[l], F,
+                                    dWr[l], F, 0, ws + sc.gemm, gemm_bytes, stream))
+      return rc;
+  }
+  return MGCN_OK;
+}

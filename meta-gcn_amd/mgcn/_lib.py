@@ -82,6 +82,12 @@ SIGNATURES = {
     "mgcn_residual_layer_fwd": (_int, [_i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp,
                                        _vp, _i64, _vp, _int, _int, _int, _vp, _i64, _vp, _vp,
                                        _i64, _i64, _vp]),
+    "mgcn_residual_stack_fwd": (_int, [_i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp,
+                                       _vp, _vp, _int, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp]),
+    "mgcn_residual_stack_bwd_workspace_bytes": (_sz, [_i64, _i32]),
+    "mgcn_residual_stack_bwd": (_int, [_i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64,
+                                       _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                       _vp, _vp, _i64, _i64, _vp, _sz, _vp]),
     "mgcn_residual_layer_bwd_workspace_bytes": (_sz, [_i64, _i32]),
     "mgcn_residual_layer_bwd": (_int, [_i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp,
                                        _int, _int, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp,

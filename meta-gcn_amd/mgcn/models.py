@@ -29,7 +29,7 @@ from torch.nn.utils.rnn import pad_sequence
 from . import _lib as L
 from .graph import plan_for
 from .ops import (aggregate_plan, gcn_layer, gcn_stack, linear, linear_bias,  # noqa: F401
-                  residual_gcn_layer,  # noqa: F401
+                  residual_gcn_layer, residual_layer_supported, residual_stack,  # noqa: F401
                   scatter_)
 
 
@@ -435,12 +435,32 @@ class GCNModel(nn.Module):
             edge_weight = edge_weight[0]
         plan = plan_for(edge_index, x.size(0))
         last = self.num_layers - 1
+        items = []
         for n, (layer, res) in enumerate(zip(self.gcn_net, self.residuals)):
             nm = layer.gcn.node_models[0]
             norm = plan.norm(nm.deg_norm, deg=deg,
                              edge_weight=edge_weight if nm.deg_norm is not None else None)
-            x = residual_gcn_layer(x, plan, norm, nm.aggr, layer.non_linear_name == 'relu',
-                                   n < last, nm.weight_node, nm.bias, res.weight, res.bias)
+            items.append((nm, norm, layer.non_linear_name == 'relu', n < last, res))
+        n = 0
+        while n < len(items):
+            nm, norm, relu1, relu2, res = items[n]
+            # a run of 32 -> 32 layers on the same normalisation and aggregator:
+            # one fused stack node (one host call per direction)
+            m = n
+            while (m < len(items) and items[m][1] is norm and items[m][0].aggr == nm.aggr and
+                   residual_layer_supported(plan, x, items[m][0].weight_node,
+                                            items[m][4].weight, L.REDUCE_CODES[nm.aggr])):
+                m += 1
+            if m - n >= 2:
+                x = residual_stack(x, plan, norm, nm.aggr, [it[2] for it in items[n:m]],
+                                   [it[3] for it in items[n:m]],
+                                   [(it[0].weight_node, it[0].bias, it[4].weight, it[4].bias)
+                                    for it in items[n:m]])
+                n = m
+                continue
+            x = residual_gcn_layer(x, plan, norm, nm.aggr, relu1, relu2, nm.weight_node, nm.bias,
+                                   res.weight, res.bias)
+            n += 1
         return x
 
     def _readout(self, x, **kwargs):

@@ -1100,6 +1100,127 @@ class _ResidualLayerFused(torch.autograd.Function):
         return (dx, None, None, None, None, None, dW, db, dWr, dbr)
 
 
+def _ptr_array(ts):
+    """Host array of device pointers (NULL for None) for the stack entry points."""
+    import ctypes
+    arr = (ctypes.c_void_p * max(len(ts), 1))(*[None if t is None else t.data_ptr() for t in ts])
+    return ctypes.cast(arr, ctypes.c_void_p), arr
+
+
+def _int_array(vals):
+    import ctypes
+    arr = (ctypes.c_int32 * max(len(vals), 1))(*[int(bool(v)) for v in vals])
+    return ctypes.cast(arr, ctypes.c_void_p), arr
+
+
+def _param_f32(t):
+    if t is None:
+        return None
+    t = t.detach()
+    return t if (t.dtype == torch.float32 and t.is_contiguous()) else t.to(torch.float32).contiguous()
+
+
+class _ResidualStack(torch.autograd.Function):
+    """Consecutive 32 -> 32 GCNModel layers with their residual Linears
+    (:class:`_ResidualLayerFused` each) as ONE autograd node and one host call
+    per direction (``mgcn_residual_stack_fwd`` / ``_bwd``): bitwise the
+    layer-by-layer fused path, without ~40 us of Python and ctypes work per
+    layer and direction (the 12-layer config-3 step was bound by host issue).
+    params = (W, b, Wr, br) per layer."""
+
+    @staticmethod
+    def forward(ctx, x0, plan, norm, reduce, relu1s, relu2s, *params):
+        lib = L.load()
+        nl = len(relu1s)
+        x0 = _aligned_rows(x0)
+        dev = x0.device
+        n, F = x0.shape
+        Ws = [_param_f32(p) for p in params[0::4]]
+        bs = [_param_f32(p) for p in params[1::4]]
+        Wrs = [_param_f32(p) for p in params[2::4]]
+        brs = [_param_f32(p) for p in params[3::4]]
+        Z = torch.empty(nl, n, F, dtype=torch.float32, device=dev)
+        masks = torch.empty(nl, n, 2, dtype=torch.int32, device=dev)
+        pw, aw = _ptr_array(Ws)
+        pb, ab = _ptr_array(bs)
+        pwr, awr = _ptr_array(Wrs)
+        pbr, abr = _ptr_array(brs)
+        pr1, ar1 = _int_array(relu1s)
+        pr2, ar2 = _int_array(relu2s)
+        v = plan.fwd
+        if _TIMER is not None:
+            _TIMER("residual_stack_fwd", True, v.n_rows, v.edges)
+        with L.device_guard(dev):
+            rc = lib.mgcn_residual_stack_fwd(n, F, nl, L.ptr(v.rowptr), L.ptr(v.col), L.ptr(v.eid),
+                                             L.ptr(norm.w_fwd), L.ptr(x0), x0.stride(0), pw, pb,
+                                             pwr, pbr, int(reduce), pr1, pr2, L.ptr(Z),
+                                             L.ptr(masks), L.ptr(v.order), v.n_heavy, v.n_giant,
+                                             L.stream_of(dev))
+        if _TIMER is not None:
+            _TIMER("residual_stack_fwd", False)
+        L.check(rc, "mgcn_residual_stack_fwd")
+        ctx.plan, ctx.norm, ctx.reduce = plan, norm, reduce
+        ctx.relu1s, ctx.relu2s = relu1s, relu2s
+        ctx.has_b = [b is not None for b in bs]
+        ctx.has_br = [b is not None for b in brs]
+        ctx.save_for_backward(x0, Z, masks, *Ws, *Wrs)
+        return Z[nl - 1]
+
+    @staticmethod
+    def backward(ctx, dZ):
+        lib = L.load()
+        nl = len(ctx.relu1s)
+        saved = ctx.saved_tensors
+        x0, Z, masks = saved[:3]
+        Ws, Wrs = saved[3:3 + nl], saved[3 + nl:3 + 2 * nl]
+        plan, norm = ctx.plan, ctx.norm
+        dZ = _aligned_rows(dZ)
+        dev = dZ.device
+        n, F = x0.shape
+        G = torch.empty(nl, 2, F, F, dtype=torch.float32, device=dev)  # dW[l] | dWr[l]
+        sums = torch.empty(nl, 2 * F, dtype=torch.float32, device=dev)
+        dX0 = torch.empty(n, F, dtype=torch.float32, device=dev) if ctx.needs_input_grad[0] \
+            else None
+        ws_bytes = int(lib.mgcn_residual_stack_bwd_workspace_bytes(n, F))
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+        pw, aw = _ptr_array(Ws)
+        pwr, awr = _ptr_array(Wrs)
+        pdw, adw = _ptr_array([G[l, 0] for l in range(nl)])
+        pdwr, adwr = _ptr_array([G[l, 1] for l in range(nl)])
+        pr1, ar1 = _int_array(ctx.relu1s)
+        pr2, ar2 = _int_array(ctx.relu2s)
+        v = plan.bwd
+        rd = plan.in_cnt if ctx.reduce == L.REDUCE_MEAN else None
+        if _TIMER is not None:
+            _TIMER("residual_stack_bwd", True, v.n_rows, v.edges)
+        with L.device_guard(dev):
+            rc = lib.mgcn_residual_stack_bwd(n, F, nl, L.ptr(v.rowptr), L.ptr(v.col), L.ptr(v.eid),
+                                             L.ptr(norm.w_bwd), L.ptr(norm.row_scale_bwd),
+                                             L.ptr(rd), L.ptr(dZ), dZ.stride(0), L.ptr(x0),
+                                             x0.stride(0), L.ptr(Z), L.ptr(masks), pr1, pr2, pw,
+                                             pwr, L.ptr(dX0), pdw, pdwr, L.ptr(sums),
+                                             L.ptr(v.order), v.n_heavy, v.n_giant, L.ptr(ws),
+                                             ws_bytes, L.stream_of(dev))
+        if _TIMER is not None:
+            _TIMER("residual_stack_bwd", False)
+        L.check(rc, "mgcn_residual_stack_bwd")
+        grads = []
+        for l in range(nl):
+            grads += [G[l, 0], sums[l, :F] if ctx.has_b[l] else None, G[l, 1],
+                      sums[l, F:] if ctx.has_br[l] else None]
+        return (dX0, None, None, None, None, None, *grads)
+
+
+def residual_stack(x, plan: GraphPlan, norm: NormPlan, aggr: str, relu1s, relu2s, params):
+    """Layers of :class:`_ResidualStack`; params = [(W, b, Wr, br), ...]."""
+    flat = []
+    for p in params:
+        flat += list(p)
+    return _ResidualStack.apply(x, plan, norm, L.REDUCE_CODES[aggr],
+                                tuple(bool(r) for r in relu1s), tuple(bool(r) for r in relu2s),
+                                *flat)
+
+
 def residual_gcn_layer(x, plan: GraphPlan, norm: NormPlan, aggr: str, relu1: bool, relu2: bool,
                        W, b, Wr, br):
     """One GCNModel layer + residual join: :class:`_ResidualLayerFused` where

@@ -138,3 +138,41 @@ def test_residual_layer_deterministic_and_first_layer_fallback(cuda):
     x1 = torch.randn(N, 1, device=cuda)
     assert not ops.residual_layer_supported(plan, x1, torch.randn(1, F, device=cuda),
                                             torch.randn(F, 1, device=cuda), L.REDUCE_SUM)
+
+
+@pytest.mark.parametrize("aggr,deg_norm,bias", [("add", "sm", False), ("mean", "rw", True)])
+def test_residual_stack_matches_layer_by_layer(cuda, aggr, deg_norm, bias):
+    """mgcn_residual_stack_fwd / _bwd (one host call per direction for a run
+    of 32 -> 32 layers) against the same layers as separate fused nodes:
+    outputs, dx and every parameter gradient bit for bit (same kernels, same
+    order), on a skewed graph; and GCNModel routes its 32 -> 32 run there."""
+    from mgcn import _lib as L
+    from mgcn import ops
+    rng = np.random.default_rng(17 + bias)
+    N, F, nl = 5000, 32, 4
+    plan, norm = _plan(cuda, _skewed(rng, N, 30000), N, deg_norm)
+    reduce = L.REDUCE_CODES[aggr]
+    g = torch.Generator(device=cuda).manual_seed(9)
+    x = torch.randn(N, F, device=cuda, generator=g)
+    dZ = torch.randn(N, F, device=cuda, generator=g)
+    params = [(torch.randn(F, F, device=cuda, generator=g) * 0.3,
+               torch.randn(F, device=cuda, generator=g) * 0.1 if bias else None,
+               torch.randn(F, F, device=cuda, generator=g) * 0.3,
+               torch.randn(F, device=cuda, generator=g) * 0.1) for _ in range(nl)]
+    relu1s = [True] * nl
+    relu2s = [True] * (nl - 1) + [False]
+    outs = []
+    for stacked in (True, False):
+        xi = x.clone().requires_grad_(True)
+        ps = [tuple(None if p is None else p.clone().requires_grad_(True) for p in q)
+              for q in params]
+        if stacked:
+            y = ops.residual_stack(xi, plan, norm, aggr, relu1s, relu2s, ps)
+        else:
+            y = xi
+            for q, r1, r2 in zip(ps, relu1s, relu2s):
+                y = ops._ResidualLayerFused.apply(y, plan, norm, reduce, r1, r2, *q)
+        y.backward(dZ)
+        outs.append([y.detach(), xi.grad] + [p.grad for q in ps for p in q if p is not None])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
