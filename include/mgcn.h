@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define MGCN_ABI_VERSION 11
+#define MGCN_ABI_VERSION 12
 
 /* return codes */
 #define MGCN_OK 0
@@ -370,6 +370,27 @@ int mgcn_spmm_xw_bwd(int64_t n_rows, int64_t n_cols, int32_t F_in, int32_t F_out
                      const float *row_div, float *colsum, const uint32_t *win_mask,
                      const int32_t *slot_map, void *workspace, size_t workspace_bytes,
                      void *stream);
+
+/* ---------------------------------------------------- edge weight adjoint */
+
+/*
+ * Gradient of the per-edge message weights (the SDDMM of the aggregation's
+ * adjoint): over the fwd view (rowptr / col: rows = destinations, col =
+ * sources), for every slot k of row d
+ *   dw[k] = sum_f dY[d, f] * H[col[k], f]   (MAX: only the features f whose
+ *           winner slot k is, bit f of win_mask[k * ceil(F/32) + f/32])
+ * in fwd slot order; dY as the SpMM adjoint receives it (mean: divided by the
+ * in-degree).  This is what autograd of the reference's
+ * `index_select(x, 0, src) * norm.view(-1, 1)` gives the norm
+ * (gcn_base_models.py:217-224), from which degnorm_const's edge_weight / deg
+ * gradients follow (gcn_base_models.py:102-140; chained by the host).
+ * Deterministic; fp32 products, a fixed butterfly sum over features (the
+ * reference's CPU sum order differs: equal to fp32 rounding, not bitwise).
+ * 1 <= F <= 1024; H rows stride ldh, dY rows lddy.
+ */
+int mgcn_edge_weight_grad(int64_t n_rows, int32_t F, const int64_t *rowptr, const int32_t *col,
+                          const float *H, int64_t ldh, const float *dY, int64_t lddy,
+                          const uint32_t *win_mask, float *dw, void *stream);
 
 /* ----------------------------------------------------------- elementwise */
 

@@ -73,6 +73,18 @@ struct RlArgs {
   const float *b, *br;
   int mean, relu1, relu2;
   int gather;  // 0: the aggregate is already in agg (heavy rows)
+  // backward inside a stack: the mask pass of the layer below fused into the
+  // store of dX (= that layer's dZ): instead of dX the kernel writes its dS
+  // (mds) and dA (mda, / mrow_div for mean) and per-block column sums of both
+  // ([gridDim.x][2F]: dA | dS) -- residual_mask_bwd_kernel's outputs
+  const uint32_t *mmask;  // the lower layer's [row][2] masks; NULL: write dX
+  int mrelu1, mrelu2;
+  const float *mrow_div;
+  float *mds;
+  int64_t ldmds;
+  float *mda;
+  int64_t ldmda;
+  float *mpart;
 };
 
 __device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
@@ -117,6 +129,8 @@ __global__ __launch_bounds__(kRBlock) void residual_layer_kernel(const RlArgs a)
   const int r16 = lane & 15, kk = lane >> 4;  // MFMA roles
   float(*T)[kTileLd] = tile[wib];
   const bool has_w = a.w != nullptr;
+  const bool fmask = BWD && a.mmask != nullptr;
+  float msa[4] = {0.f, 0.f, 0.f, 0.f}, mss[4] = {0.f, 0.f, 0.f, 0.f};  // fmask column sums
   const int64_t n_tiles = (a.n_items + kTileRows - 1) / kTileRows;
   for (int64_t wv = (int64_t)blockIdx.x * kRWaves + wib; wv < n_tiles;
        wv += (int64_t)gridDim.x * kRWaves) {
@@ -274,9 +288,49 @@ __global__ __launch_bounds__(kRBlock) void residual_layer_kernel(const RlArgs a)
     for (int st = 0; st < 2; ++st) {
       const int tr = 8 * st + grp;
       const int64_t row = tile_row[wib][tr];
-      if (row >= 0) st4(a.out + row * a.ldout + f0, ld4(&T[tr][f0]));
+      if (row < 0) continue;
+      if (!fmask) {
+        st4(a.out + row * a.ldout + f0, ld4(&T[tr][f0]));
+        continue;
+      }
+      // the lower layer's mask pass on this dZ row (residual_mask_bwd_kernel's
+      // arithmetic): dS = relu2'(dZ), dA = relu1'(dS) [/ in-degree]
+      const float4 g4 = ld4(&T[tr][f0]);
+      const uint2 mk = *reinterpret_cast<const uint2 *>(a.mmask + 2 * row);
+      const float dv = a.mrow_div != nullptr ? a.mrow_div[row] : 1.0f;
+      float g[4] = {g4.x, g4.y, g4.z, g4.w}, av[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int bit = f0 + j;
+        if (a.mrelu2 && !((mk.y >> bit) & 1u)) g[j] = 0.0f;
+        av[j] = (a.mrelu1 && !((mk.x >> bit) & 1u)) ? 0.0f : g[j];
+        mss[j] = __fadd_rn(mss[j], g[j]);
+        msa[j] = __fadd_rn(msa[j], av[j]);
+        if (a.mrow_div != nullptr) av[j] = __fdiv_rn(av[j], dv);
+      }
+      st4(a.mds + row * a.ldmds + f0, make_float4(g[0], g[1], g[2], g[3]));
+      st4(a.mda + row * a.ldmda + f0, make_float4(av[0], av[1], av[2], av[3]));
     }
     __builtin_amdgcn_wave_barrier();  // the tile is restaged by the next 16 rows
+  }
+  if (fmask) {
+    // block partial of the column sums: the 32 lane groups of the block in a
+    // fixed order (every block writes one, zeros where it had no rows)
+    __syncthreads();
+    float *red = &tile[0][0][0];  // 4 x 16 x 68 floats >= 256 threads x 8
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      red[tid * 8 + j] = msa[j];
+      red[tid * 8 + 4 + j] = mss[j];
+    }
+    __syncthreads();
+    if (tid < 2 * kRF) {
+      const int which = tid / kRF, f = tid % kRF;
+      const int q = f >> 2, j = f & 3;
+      float x = 0.0f;
+      for (int g = 0; g < kRBlock / kRG; ++g) x = __fadd_rn(x, red[(g * kRG + q) * 8 + 4 * which + j]);
+      a.mpart[(int64_t)blockIdx.x * 2 * kRF + tid] = x;
+    }
   }
 }
 
@@ -286,6 +340,7 @@ __global__ __launch_bounds__(kRBlock) void residual_layer_kernel(const RlArgs a)
 // partials [block][2F] in a fixed row order (launch_colsum_fold folds them).
 // Thread (t_row, q): features 4 q .. 4 q + 3 of rows t_row, t_row + R, ...
 constexpr int kMaxParts = 1024;
+constexpr int kMaxRlParts = 2048;  // fused mask pass: partials per residual_layer_kernel launch
 
 __global__ __launch_bounds__(256) void residual_mask_bwd_kernel(
     int64_t n, const float *__restrict__ dZ, int64_t lddz, const uint32_t *__restrict__ masks,
@@ -341,12 +396,20 @@ int mask_parts(int64_t n) {
   return (int)b;
 }
 
+// blocks of one launch: grid-stride beyond (W / Wr^T staged once per block);
+// with the fused mask pass, each block also writes one partial of the sums
+int64_t rl_blocks(int64_t n_items, bool fused_mask) {
+  if (n_items <= 0) return 0;
+  const int64_t waves = (n_items + kTileRows - 1) / kTileRows;
+  int64_t blocks = (waves + kRWaves - 1) / kRWaves;
+  const int64_t cap = fused_mask ? kMaxRlParts : 8192;
+  return blocks > cap ? cap : blocks;
+}
+
 template <bool BWD>
 int launch_rl(const RlArgs &a, hipStream_t s) {
   if (a.n_items <= 0) return MGCN_OK;
-  const int64_t waves = (a.n_items + kTileRows - 1) / kTileRows;
-  int64_t blocks = (waves + kRWaves - 1) / kRWaves;
-  if (blocks > 8192) blocks = 8192;  // grid-stride beyond: W / Wr^T loaded once per block
+  const int64_t blocks = rl_blocks(a.n_items, BWD && a.mmask != nullptr);
   hipLaunchKernelGGL((residual_layer_kernel<8, BWD>), dim3((unsigned)blocks), dim3(kRBlock), 0, s, a);
   return check_launch("residual_layer_kernel");
 }
@@ -428,6 +491,89 @@ extern "C" int mgcn_residual_layer_fwd(int64_t n_rows, int32_t F, const int64_t 
   return launch_rl<false>(a, s);
 }
 
+namespace mgcn {
+int g_fused_mask = 1;  // mgcn_set_option("residual_fused_mask")
+namespace {
+// The mask pass of the layer below, fused into this layer's dX store (stack
+// backward): its masks / flags / mean divisor, where dS and dA go, the block
+// partials of the column sums ([2 kMaxRlParts][2F]) and their fold.
+struct LowerMask {
+  const uint32_t *masks;
+  int relu1, relu2;
+  const float *row_div;
+  float *dS;
+  int64_t ldds;
+  float *dA;
+  int64_t ldda;
+  float *partial;
+  float *colsums;
+};
+
+// Heavy rows (workgroup kernels into DH), the light rows' fused pass, the
+// heavy rows' transform: dA gathered into dH = DH[:, :F], dS = DH[:, F:]
+// read as the own operand, dX = dH W^T + dS Wr (or, with lm, the lower
+// layer's dS / dA and column sums).
+int residual_bwd_core(int64_t n_rows, const int64_t *rowptr_t, const int32_t *col_t,
+                      const int32_t *eid_t, const float *w_t, const float *row_scale,
+                      const float *dA, const float *W, int64_t ldw, const float *Wr, int64_t ldwr,
+                      float *dX, int64_t lddx, float *DH, int64_t lddh, const int32_t *order,
+                      int64_t n_heavy, int64_t n_giant, const LowerMask *lm, hipStream_t s) {
+  const int F = kRF;
+  if (order == nullptr) n_heavy = n_giant = 0;
+  bool side = false;
+  if (n_heavy > 0)
+    if (int rc = heavy_rows(1, n_rows, F, rowptr_t, col_t, eid_t, w_t, dA, F, DH, lddh, row_scale,
+                            0, order, n_heavy, n_giant, s, &side))
+      return rc;
+  RlArgs a{};
+  a.rowptr = rowptr_t;
+  a.col = col_t;
+  a.w = w_t;
+  a.row_scale = row_scale;
+  a.T = dA;
+  a.ldt = F;
+  a.own = DH + F;
+  a.ldo = lddh;
+  a.agg = DH;
+  a.ldagg = lddh;
+  a.out = dX;
+  a.ldout = lddx;
+  a.W = W;
+  a.ldw = ldw;
+  a.Wr = Wr;
+  a.ldwr = ldwr;
+  if (lm != nullptr) {
+    a.mmask = lm->masks;
+    a.mrelu1 = lm->relu1;
+    a.mrelu2 = lm->relu2;
+    a.mrow_div = lm->row_div;
+    a.mds = lm->dS;
+    a.ldmds = lm->ldds;
+    a.mda = lm->dA;
+    a.ldmda = lm->ldda;
+    a.mpart = lm->partial;
+  }
+  a.gather = 1;
+  a.items = order != nullptr ? order + n_heavy : nullptr;
+  a.n_items = n_rows - n_heavy;
+  if (int rc = launch_rl<true>(a, s)) return rc;
+  int64_t parts = rl_blocks(a.n_items, lm != nullptr);
+  if (n_heavy > 0) {
+    if (side)
+      if (int rc = heavy_rows_join(s)) return rc;
+    a.gather = 0;
+    a.items = order;
+    a.n_items = n_heavy;
+    if (lm != nullptr) a.mpart = lm->partial + parts * 2 * F;
+    if (int rc = launch_rl<true>(a, s)) return rc;
+    parts += rl_blocks(n_heavy, lm != nullptr);
+  }
+  if (lm == nullptr) return MGCN_OK;
+  return launch_colsum_fold(lm->partial, parts, 2 * F, lm->colsums, s);
+}
+}  // namespace
+}  // namespace mgcn
+
 extern "C" size_t mgcn_residual_layer_bwd_workspace_bytes(int64_t n_rows, int32_t F) {
   const int64_t n = n_rows > 0 ? n_rows : 1;
   const int32_t f = F > 0 ? F : 1;
@@ -473,40 +619,8 @@ extern "C" int mgcn_residual_layer_bwd(int64_t n_rows, int32_t F, const int64_t 
                      masks, relu1, relu2, row_div, dA, (int64_t)F, DH + F, lddh, partial);
   if (int rc = check_launch("residual_mask_bwd_kernel")) return rc;
   if (int rc = launch_colsum_fold(partial, nparts, 2 * F, colsums, s)) return rc;
-  if (order == nullptr) n_heavy = n_giant = 0;
-  bool side = false;
-  if (n_heavy > 0)
-    if (int rc = heavy_rows(1, n_rows, F, rowptr_t, col_t, eid_t, w_t, dA, F, DH, lddh, row_scale,
-                            0, order, n_heavy, n_giant, s, &side))
-      return rc;
-  RlArgs a{};
-  a.rowptr = rowptr_t;
-  a.col = col_t;
-  a.w = w_t;
-  a.row_scale = row_scale;
-  a.T = dA;
-  a.ldt = F;
-  a.own = DH + F;
-  a.ldo = lddh;
-  a.agg = DH;
-  a.ldagg = lddh;
-  a.out = dX;
-  a.ldout = lddx;
-  a.W = W;
-  a.ldw = ldw;
-  a.Wr = Wr;
-  a.ldwr = ldwr;
-  a.gather = 1;
-  a.items = order != nullptr ? order + n_heavy : nullptr;
-  a.n_items = n_rows - n_heavy;
-  if (int rc = launch_rl<true>(a, s)) return rc;
-  if (n_heavy == 0) return MGCN_OK;
-  if (side)
-    if (int rc = heavy_rows_join(s)) return rc;
-  a.gather = 0;
-  a.items = order;
-  a.n_items = n_heavy;
-  return launch_rl<true>(a, s);
+  return residual_bwd_core(n_rows, rowptr_t, col_t, eid_t, w_t, row_scale, dA, W, ldw, Wr, ldwr,
+                           dX, lddx, DH, lddh, order, n_heavy, n_giant, nullptr, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -542,16 +656,23 @@ extern "C" int mgcn_residual_stack_fwd(int64_t n_rows, int32_t F, int32_t n_laye
 }
 
 namespace {
+// [mask partials of the top layer's pass] [dA x 2] [DH x 2] [dX of layer 0]
+// [fused-mask partials] [gemm_tn_split workspace]
 struct StackScratch {
-  size_t layer, dh, dx, gemm, total;
+  size_t mpart, da, dh, dx, fpart, gemm, total;
+  size_t nf, n2f;  // bytes of one [n, F] / [n, 2F] buffer
 };
 StackScratch stack_scratch(int64_t n_rows, int32_t F) {
   StackScratch s{};
   const int64_t n = n_rows > 0 ? n_rows : 1;
-  s.layer = 0;
-  s.dh = align_up(mgcn_residual_layer_bwd_workspace_bytes(n_rows, F), 256);
-  s.dx = s.dh + align_up((size_t)n * 2 * F * sizeof(float), 256);
-  s.gemm = s.dx + 2 * align_up((size_t)n * F * sizeof(float), 256);
+  s.nf = align_up((size_t)n * F * sizeof(float), 256);
+  s.n2f = align_up((size_t)n * 2 * F * sizeof(float), 256);
+  s.mpart = 0;
+  s.da = align_up((size_t)mask_parts(n) * 2 * F * sizeof(float), 256);
+  s.dh = s.da + 2 * s.nf;
+  s.dx = s.dh + 2 * s.n2f;
+  s.fpart = s.dx + s.nf;
+  s.gemm = s.fpart + align_up((size_t)2 * kMaxRlParts * 2 * F * sizeof(float), 256);
   s.total = s.gemm + align_up(mgcn_gemm_tn_workspace_bytes(n_rows, F, 2 * F), 256);
   return s;
 }
@@ -583,25 +704,65 @@ extern "C" int mgcn_residual_stack_bwd(int64_t n_rows, int32_t F, int32_t n_laye
     return MGCN_EWORKSPACE;
   }
   char *ws = static_cast<char *>(workspace);
-  float *DH = reinterpret_cast<float *>(ws + sc.dh);
-  float *dxb[2] = {reinterpret_cast<float *>(ws + sc.dx),
-                   reinterpret_cast<float *>(ws + sc.dx +
-                                             align_up((size_t)(n_rows > 0 ? n_rows : 1) * F * 4, 256))};
+  float *dAb[2] = {reinterpret_cast<float *>(ws + sc.da), reinterpret_cast<float *>(ws + sc.da + sc.nf)};
+  float *DHb[2] = {reinterpret_cast<float *>(ws + sc.dh), reinterpret_cast<float *>(ws + sc.dh + sc.n2f)};
+  float *mpart = reinterpret_cast<float *>(ws + sc.mpart);
+  float *fpart = reinterpret_cast<float *>(ws + sc.fpart);
   const size_t gemm_bytes = sc.total - sc.gemm;
-  for (int32_t l = n_layers - 1; l >= 0; --l) {
-    const float *dz = l == n_layers - 1 ? dZ : dxb[(l + 1) & 1];
-    const int64_t ldz = l == n_layers - 1 ? lddz : F;
-    float *dx = (l == 0 && dX0 != nullptr) ? dX0 : dxb[l & 1];
-    if (int rc = mgcn_residual_layer_bwd(n_rows, F, rowptr_t, col_t, eid_t, w_t, row_scale, row_div,
-                                         dz, ldz, masks + (int64_t)l * n_rows * 2, relu1[l],
-                                         relu2[l], W[l], F, Wr[l], F, dx, F, DH, 2 * F,
-                                         sums + (int64_t)l * 2 * F, order, n_heavy, n_giant,
-                                         ws + sc.layer, sc.dh - sc.layer, stream))
+  hipStream_t s = as_stream(stream);
+  const int64_t nl = n_rows;
+  if (n_rows == 0) {
+    // no rows: every weight and bias gradient is zero
+    for (int32_t l = 0; l < n_layers; ++l) {
+      MGCN_HIP_TRY(hipMemsetAsync(dW[l], 0, sizeof(float) * F * F, s));
+      MGCN_HIP_TRY(hipMemsetAsync(dWr[l], 0, sizeof(float) * F * F, s));
+    }
+    MGCN_HIP_TRY(hipMemsetAsync(sums, 0, sizeof(float) * 2 * F * n_layers, s));
+    return MGCN_OK;
+  }
+  MGCN_REQUIRE(F == kRF && al16(dZ, lddz) && lddz >= F && al16(X0, ldx) && ldx >= F,
+               "mgcn_residual_stack_bwd: F must be 32, dZ / X0 16-byte aligned rows");
+  // the top layer's mask pass reads dZ; every lower layer's runs fused in the
+  // store of the layer above's dX (its dS / dA / column sums straight from there)
+  const int32_t top = n_layers - 1;
+  const int nparts = mask_parts(n_rows);
+  hipLaunchKernelGGL(residual_mask_bwd_kernel, dim3(nparts), dim3(256), 0, s, n_rows, dZ, lddz,
+                     masks + (int64_t)top * nl * 2, relu1[top], relu2[top], row_div, dAb[top & 1],
+                     (int64_t)F, DHb[top & 1] + F, (int64_t)2 * F, mpart);
+  if (int rc = check_launch("residual_mask_bwd_kernel")) return rc;
+  if (int rc = launch_colsum_fold(mpart, nparts, 2 * F, sums + (int64_t)top * 2 * F, s)) return rc;
+  for (int32_t l = top; l >= 0; --l) {
+    const int c = l & 1, o = c ^ 1;
+    float *dx = (l == 0 && dX0 != nullptr) ? dX0 : reinterpret_cast<float *>(ws + sc.dx);
+    LowerMask lm{};
+    if (l > 0) {
+      lm.masks = masks + (int64_t)(l - 1) * nl * 2;
+      lm.relu1 = relu1[l - 1];
+      lm.relu2 = relu2[l - 1];
+      lm.row_div = row_div;
+      lm.dS = DHb[o] + F;
+      lm.ldds = 2 * F;
+      lm.dA = dAb[o];
+      lm.ldda = F;
+      lm.partial = fpart;
+      lm.colsums = sums + (int64_t)(l - 1) * 2 * F;
+    }
+    const bool fuse = l > 0 && g_fused_mask;
+    if (int rc = residual_bwd_core(n_rows, rowptr_t, col_t, eid_t, w_t, row_scale, dAb[c], W[l], F,
+                                   Wr[l], F, dx, F, DHb[c], 2 * F, order, n_heavy, n_giant,
+                                   fuse ? &lm : nullptr, s))
       return rc;
+    if (l > 0 && !fuse) {  // the lower layer's mask pass as its own kernel
+      hipLaunchKernelGGL(residual_mask_bwd_kernel, dim3(nparts), dim3(256), 0, s, n_rows, dx,
+                         (int64_t)F, lm.masks, lm.relu1, lm.relu2, row_div, dAb[o], (int64_t)F,
+                         DHb[o] + F, (int64_t)2 * F, mpart);
+      if (int rc = check_launch("residual_mask_bwd_kernel")) return rc;
+      if (int rc = launch_colsum_fold(mpart, nparts, 2 * F, lm.colsums, s)) return rc;
+    }
     // [dW | dWr^T] = X_l^T [dH | dS]
     const float *xin = l == 0 ? X0 : Z + (int64_t)(l - 1) * n_rows * F;
-    if (int rc = mgcn_gemm_tn_split(n_rows, F, 2 * F, F, xin, l == 0 ? ldx : F, DH, 2 * F, dW[l], F,
-                                    dWr[l], F, 0, ws + sc.gemm, gemm_bytes, stream))
+    if (int rc = mgcn_gemm_tn_split(n_rows, F, 2 * F, F, xin, l == 0 ? ldx : F, DHb[c], 2 * F,
+                                    dW[l], F, dWr[l], F, 0, ws + sc.gemm, gemm_bytes, stream))
       return rc;
   }
   return MGCN_OK;

@@ -1159,6 +1159,11 @@ extern "C" int mgcn_set_option(const char *name, int value) {
     return gemm_set_precision(value);
   }
   if (n == "spmm_xw_unroll") return xw_set_unroll(value);
+  if (n == "residual_fused_mask") {
+    MGCN_REQUIRE(value == 0 || value == 1, "residual_fused_mask must be 0 or 1");
+    g_fused_mask = value;
+    return MGCN_OK;
+  }
   if (n == "heavy_side_stream") {
     MGCN_REQUIRE(value == 0 || value == 1, "heavy_side_stream must be 0 or 1");
     g_heavy_side = value;

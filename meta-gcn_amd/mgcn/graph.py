@@ -130,6 +130,11 @@ class NormPlan:
     row_scale_bwd: torch.Tensor | None  # RW without edge weights: dinv post-scale
     deg: torch.Tensor | None
     dinv: torch.Tensor | None
+    # True: w_fwd (or, for 'rw' without edge weights, the per-slot dinv in
+    # w_fwd) carries autograd history back to edge_weight / deg -- the
+    # aggregation then takes the weights as an input (ops._AggregateW) and
+    # returns their gradient (libmgcn mgcn_edge_weight_grad); never cached.
+    grad: bool = False
 
 
 @dataclass
@@ -143,6 +148,7 @@ class GraphPlan:
     norms: dict = field(default_factory=dict)
     _key_refs: list = field(default_factory=list)
     _slot_map: torch.Tensor | None = None
+    _coo: tuple | None = None
 
     def slot_map(self) -> torch.Tensor:
         """int32 [nnz]: the fwd-view slot of every bwd-view slot (mgcn_slot_map),
@@ -161,6 +167,20 @@ class GraphPlan:
         return self._slot_map
 
     # ------------------------------------------------------------------ norms
+    def coo(self) -> tuple[torch.Tensor, torch.Tensor]:
+        """(src, dst) int64 [nnz] in COO (edge id) order, rebuilt from the fwd
+        view on first use (the differentiable norm of :func:`_grad_norm`)."""
+        if self._coo is None:
+            eid = self.fwd.eid.long()
+            src = torch.empty(self.nnz, dtype=torch.int64, device=self.device)
+            dst = torch.empty(self.nnz, dtype=torch.int64, device=self.device)
+            src[eid] = self.fwd.col.long()
+            cnt = self.fwd.rowptr[1:] - self.fwd.rowptr[:-1]
+            dst[eid] = torch.repeat_interleave(
+                torch.arange(self.num_nodes, device=self.device), cnt, output_size=self.nnz)
+            self._coo = (src, dst)
+        return self._coo
+
     def norm(self, method: str | None, deg: torch.Tensor | None = None,
              edge_weight: torch.Tensor | None = None) -> NormPlan:
         """Normalisation weights, as NodeModelBase.degnorm_const computes them
@@ -176,16 +196,11 @@ class GraphPlan:
         code = L.NORM_CODES[method]
         if edge_weight is not None:
             deg = None
-        if torch.is_grad_enabled():
-            # The per-slot weights are built outside autograd: no gradient
-            # flows back into edge_weight / deg.  The reference's degnorm_const
-            # (gcn_base_models.py:102-140) is differentiable in them, so a
-            # caller that wants that gradient must not get a silent zero.
-            for name, t in (("edge_weight", edge_weight), ("deg", deg)):
-                if t is not None and t.requires_grad:
-                    raise NotImplementedError(
-                        f"mgcn: gradient with respect to {name} is not implemented; pass "
-                        f"{name}.detach() (or run under torch.no_grad())")
+        if torch.is_grad_enabled() and any(t is not None and t.requires_grad
+                                           for t in (edge_weight, deg)):
+            # degnorm_const is differentiable in edge_weight / deg
+            # (gcn_base_models.py:102-140): build the weights through autograd
+            return _grad_norm(self, code, deg, edge_weight)
         key = (code, _tkey(deg), _tkey(edge_weight))
         hit = self.norms.get(key)
         if hit is not None and _alive(hit[1]):
@@ -289,6 +304,70 @@ def _build_norm(g: GraphPlan, code: int, deg, edge_weight) -> NormPlan:
     w_fwd = _edge_norm(g.fwd, True, dinv, ew, code)
     w_bwd = _edge_norm(g.bwd, False, dinv, ew, code)
     return NormPlan(code, w_fwd, w_bwd, None, dg, dinv)
+
+
+class _DegNorm(torch.autograd.Function):
+    """dinv = deg^-1/2 ('sm') or deg^-1 ('rw'), inf -> 0, with deg the given
+    one or the weighted out-degree sum_{e: src_e = n} edge_weight_e
+    (gcn_base_models.py:112-135; forward = libmgcn mgcn_degree_norm, bit for
+    bit).  Backward = autograd of the reference's ops: pow's derivative,
+    zeroed where the in-place ``deg_inv_sqrt[... == inf] = 0`` overwrote the
+    entry (as there, 0 * the derivative's inf is NaN at deg = 0), then the
+    degree sum's adjoint, a gather over the edges' sources."""
+
+    @staticmethod
+    def forward(ctx, ew, deg, g, code):
+        dg, dinv = degree_norm(g.num_nodes, g.bwd, None if deg is None else deg.detach(),
+                               None if ew is None else ew.detach(), code)
+        ctx.g, ctx.code, ctx.has_ew = g, code, ew is not None
+        ctx.save_for_backward(dg)
+        return dinv
+
+    @staticmethod
+    def backward(ctx, grad):
+        (dg,) = ctx.saved_tensors
+        e, c = (-1.5, -0.5) if ctx.code == L.NORM_SM else (-2.0, -1.0)
+        gdeg = grad.masked_fill(dg == 0, 0.0) * (c * dg.pow(e))
+        if ctx.has_ew:
+            src, _ = ctx.g.coo()
+            return gdeg[src], None, None, None
+        return None, gdeg, None, None
+
+
+def _grad_norm(g: GraphPlan, code: int, deg, edge_weight) -> NormPlan:
+    """:meth:`GraphPlan.norm` when edge_weight or deg requires grad: the same
+    weights (bit for bit), formed by differentiable ops in COO order exactly
+    as degnorm_const writes them (``deg_inv_sqrt[row] * edge_weight *
+    deg_inv_sqrt[col]``, gcn_base_models.py:137-142), then gathered into the
+    views' slot orders.  Only the fwd weights keep the history; the adjoint's
+    copies are detached (their gradient comes through the fwd ones)."""
+    dev = g.device
+    ew = None
+    if edge_weight is not None:
+        ew = edge_weight.reshape(-1)
+        if ew.numel() != g.nnz:
+            raise ValueError(f"edge_weight has {ew.numel()} entries, expected {g.nnz}")
+        if ew.device != dev:
+            raise L.MgcnError(f"edge_weight is on {ew.device}, graph is on {dev}")
+        ew = ew.to(torch.float32)
+    if deg is not None:
+        deg = deg.reshape(-1).to(torch.float32)
+        if deg.numel() != g.num_nodes:
+            raise ValueError(f"deg has {deg.numel()} entries, expected {g.num_nodes}")
+    feid, beid = g.fwd.eid.long(), g.bwd.eid.long()
+    if code == L.NORM_NONE:  # plain message weights (PyG GraphConv / SAGEConv)
+        return NormPlan(code, ew[feid], ew.detach()[beid], None, None, None, grad=True)
+    src, dst = g.coo()
+    dinv = _DegNorm.apply(ew, deg, g, code)
+    if code == L.NORM_RW and ew is None:
+        # x * dinv before the gather (gcn_base_models.py:217-220): per fwd slot
+        # dinv[src]; the adjoint post-scales by dinv
+        return NormPlan(code, dinv[g.fwd.col.long()], None, dinv.detach(), None, dinv, grad=True)
+    if code == L.NORM_SM:
+        w = dinv[src] * ew * dinv[dst] if ew is not None else dinv[src] * dinv[dst]
+    else:
+        w = dinv[src] * ew
+    return NormPlan(code, w[feid], w.detach()[beid], None, None, dinv.detach(), grad=True)
 
 
 def degree_norm(n: int, bwd: CSRView | None, deg, ew, code: int):

@@ -34,6 +34,16 @@ from .ops import (aggregate_plan, gcn_layer, gcn_stack, linear, linear_bias,  # 
 
 
 # --------------------------------------------------------------- inits (PyG)
+def _wants_norm_grad(deg, edge_weight) -> bool:
+    """A gradient is asked of deg / edge_weight (lists: the K kernels')."""
+    if not torch.is_grad_enabled():
+        return False
+    ts = []
+    for t in (deg, edge_weight):
+        ts += list(t) if isinstance(t, (list, tuple)) else [t]
+    return any(isinstance(t, torch.Tensor) and t.requires_grad for t in ts)
+
+
 def glorot(tensor):
     """torch_geometric.nn.inits.glorot (used at gcn_base_models.py:193)."""
     if tensor is not None:
@@ -105,16 +115,20 @@ class NodeModelBase(nn.Module):
                       device=None):
         """Normalisation constants exactly as gcn_base_models.py:65-146 returns
         them (size (E,), or (N,) for 'rw' without edge weights), computed by
-        libmgcn (mgcn_degree_norm / mgcn_edge_norm) and returned in COO order."""
+        libmgcn (mgcn_degree_norm / mgcn_edge_norm) and returned in COO order;
+        differentiable in edge_weight / deg when they require grad."""
         assert method in ['sm', 'rw']
         if edge_weight is None and deg is None:
             assert edge_index is not None and num_nodes is not None
         plan = plan_for(edge_index, int(num_nodes if num_nodes is not None else deg.numel()))
         norm = plan.norm(method, deg=deg, edge_weight=edge_weight)
         if method == 'rw' and edge_weight is None:
-            return norm.dinv
+            return norm.dinv  # (with its autograd history when deg requires grad)
+        eid = plan.fwd.eid.long()
+        if norm.grad:
+            return torch.zeros_like(norm.w_fwd).index_put((eid,), norm.w_fwd)
         out = torch.empty_like(norm.w_fwd)
-        out[plan.fwd.eid.long()] = norm.w_fwd
+        out[eid] = norm.w_fwd
         return out
 
     def forward(self, x, edge_index, edge_attr=None, deg=None, *args, **kwargs):
@@ -407,7 +421,8 @@ class GCNModel(nn.Module):
 
     def forward(self, x, edge_index_K, edge_attr_K=None, deg_K=None, edge_weight_K=None,
                 **kwargs):
-        if self._residual_fusable(x, edge_index_K, edge_attr_K):
+        if (self._residual_fusable(x, edge_index_K, edge_attr_K) and
+                not _wants_norm_grad(deg_K, edge_weight_K)):
             x = self._forward_residual_fused(x, edge_index_K, deg_K, edge_weight_K)
             return self._readout(x, **kwargs)
         # gcn_model.py:86-125, step for step

@@ -666,12 +666,75 @@ def aggregate(H: torch.Tensor, edge_index: torch.Tensor, aggr: str = "add",
     n = H.size(0) if num_nodes is None else int(num_nodes)
     plan = plan_for(edge_index, n)
     norm = plan.norm(deg_norm, deg=deg, edge_weight=edge_weight)
-    return _Aggregate.apply(H, bias, plan, norm, L.REDUCE_CODES[aggr], bool(relu))
+    return aggregate_plan(H, plan, norm, aggr, bias, relu)
+
+
+def edge_weight_grad(view: CSRView, H: torch.Tensor, dY: torch.Tensor,
+                     win_mask: torch.Tensor | None = None) -> torch.Tensor:
+    """dw[k] = sum_f dY[row(k), f] * H[col[k], f] for every slot k of the fwd
+    view (``mgcn_edge_weight_grad``; max: the features slot k won), in slot
+    order: the gradient of the aggregation with respect to its per-slot edge
+    weights (the reference's ``x_j * norm.view(-1, 1)`` adjoint,
+    gcn_base_models.py:217-224)."""
+    lib = L.load()
+    H = _contig_f32(H, "H")
+    dY = _contig_f32(dY, "dY")
+    dev = L.require_device(H, dY, view.rowptr)
+    F = H.size(1)
+    if dY.size(1) != F or H.size(0) != view.n_cols or dY.size(0) != view.n_rows:
+        raise ValueError(f"edge_weight_grad: H {tuple(H.shape)}, dY {tuple(dY.shape)} do not fit "
+                         f"the view ({view.n_rows} rows, {view.n_cols} columns)")
+    dw = torch.empty(view.nnz, dtype=torch.float32, device=dev)
+    with L.device_guard(dev):
+        rc = lib.mgcn_edge_weight_grad(view.n_rows, F, L.ptr(view.rowptr), L.ptr(view.col),
+                                       L.ptr(H), H.stride(0), L.ptr(dY), dY.stride(0),
+                                       L.ptr(win_mask), L.ptr(dw), L.stream_of(dev))
+    L.check(rc, "mgcn_edge_weight_grad")
+    return dw
+
+
+class _AggregateW(torch.autograd.Function):
+    """:class:`_Aggregate` with the fwd per-slot weights as an autograd input
+    (a :class:`NormPlan` built with ``grad``): the backward also returns their
+    gradient, from which autograd reaches edge_weight / deg through the
+    differentiable degnorm_const of graph._grad_norm."""
+
+    @staticmethod
+    def forward(ctx, H, w_fwd, bias, plan: GraphPlan, norm: NormPlan, reduce: int, relu: bool):
+        Y, mask = spmm_fwd(plan.fwd, w_fwd.detach(), H, reduce, bias, relu, mask_plan=plan)
+        ctx.plan, ctx.norm, ctx.reduce, ctx.relu = plan, norm, reduce, relu
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(H, Y if relu else None, mask)
+        return Y
+
+    @staticmethod
+    def backward(ctx, dZ):
+        H, Y, mask = ctx.saved_tensors
+        plan, norm = ctx.plan, ctx.norm
+        need_h = ctx.needs_input_grad[0]
+        need_w = ctx.needs_input_grad[1]
+        need_b = ctx.has_bias and ctx.needs_input_grad[2]
+        mean = ctx.reduce == L.REDUCE_MEAN
+        # mean: dY divided by the counts once, for the adjoint gather and for
+        # the weights' gradient alike (scatter_mean's backward, common.py:59)
+        dY, db = relu_bwd_colsum(dZ, Y, ctx.relu, need_b,
+                                 row_div=plan.in_cnt if (mean and (need_h or need_w)) else None)
+        dH = dw = None
+        if need_h:
+            dH = spmm_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY,
+                          L.REDUCE_SUM if mean else ctx.reduce, win_mask=mask,
+                          slot_map=plan.slot_map() if mask is not None else None)
+        if need_w:
+            dw = edge_weight_grad(plan.fwd, H, dY, win_mask=mask)
+        return dH, dw, db, None, None, None, None
 
 
 def aggregate_plan(H: torch.Tensor, plan: GraphPlan, norm: NormPlan, aggr: str = "add",
                    bias: torch.Tensor | None = None, relu: bool = False) -> torch.Tensor:
     """:func:`aggregate` on an already-built plan (no cache lookup)."""
+    if norm.grad:
+        return _AggregateW.apply(H, norm.w_fwd, bias, plan, norm, L.REDUCE_CODES[aggr],
+                                 bool(relu))
     return _Aggregate.apply(H, bias, plan, norm, L.REDUCE_CODES[aggr], bool(relu))
 
 
@@ -734,7 +797,7 @@ def gcn_layer(x: torch.Tensor, W: torch.Tensor, plan: GraphPlan, norm: NormPlan,
     reference uses: ``aggregate_first`` (PyG SAGEConv: mean_j x_j, then
     @ W + b) or x @ W first (the default)."""
     reduce = L.REDUCE_CODES[aggr]
-    if _FUSE_XW and layer_fusable(plan, x, W, reduce):
+    if _FUSE_XW and not norm.grad and layer_fusable(plan, x, W, reduce):
         return _LayerXW.apply(x, W, bias, plan, norm, reduce, bool(relu))
     if aggregate_first:
         out = linear(aggregate_plan(x, plan, norm, aggr), W)
@@ -911,6 +974,10 @@ class _GCNStack(torch.autograd.Function):
 def gcn_stack(x: torch.Tensor, plan: GraphPlan, norm: NormPlan, Ws, bs, relus,
               aggr: str = "add") -> torch.Tensor:
     """Run len(Ws) fused GCN layers (see :class:`_GCNStack`)."""
+    if norm.grad:  # weights with autograd history: layer by layer (_AggregateW)
+        for W, b, r in zip(Ws, bs, relus):
+            x = aggregate_plan(linear(x, W), plan, norm, aggr, b, bool(r))
+        return x
     params = []
     for W, b in zip(Ws, bs):
         params += [W, b]

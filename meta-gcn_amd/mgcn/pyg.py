@@ -119,6 +119,12 @@ def remove_self_loops(edge_index, edge_attr=None):
 
 
 def _with_loops(edge_index, edge_weight, num_nodes, fill):
+    if edge_weight is not None and edge_weight.requires_grad and torch.is_grad_enabled():
+        # the weights carry this call's autograd graph: derive them afresh
+        # (the loop-augmented edge list itself stays cached for the plan cache)
+        ei = _derived("loops", edge_index, None, num_nodes, fill,
+                      lambda: add_remaining_self_loops(edge_index, None, fill, num_nodes))[0]
+        return ei, add_remaining_self_loops(edge_index, edge_weight, fill, num_nodes)[1]
     return _derived("loops", edge_index, edge_weight, num_nodes, fill,
                     lambda: add_remaining_self_loops(edge_index, edge_weight, fill, num_nodes))
 

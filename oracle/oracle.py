@@ -190,22 +190,32 @@ def gcnconv_fwd_bwd(x, edge_index, W, b, dZ, edge_weight=None, improved=False):
 
 
 # ---------------------------------------------------------------- torch CPU
-def torch_layer_reference(x, edge_index, W, b, deg_norm="sm", aggr="add", deg=None):
+def torch_layer_reference(x, edge_index, W, b, deg_norm="sm", aggr="add", deg=None,
+                          edge_weight=None):
     """The reference's op sequence (gcn_base_models.py:199-243, common.py:37-66)
     in torch CPU ops, autograd-capable; ``aggr`` 'add' only (the timed CPU
-    baseline of bench.py).  Returns the layer output tensor."""
+    baseline of bench.py).  ``edge_weight``: degnorm_const's weighted form
+    (:102-142: degree = scatter_add of the weights over edge_index[0]; norm =
+    dinv[row] * w * dinv[col] ('sm') or dinv[row] * w ('rw')), differentiable
+    in the weights.  Returns the layer output tensor."""
     import torch
     src, dst = edge_index[0], edge_index[1]
     h = torch.matmul(x, W)
     if deg_norm is None:
         x_j = torch.index_select(h, 0, src)
     else:
-        if deg is None:
+        if edge_weight is not None:
+            deg = torch.zeros(x.size(0), dtype=h.dtype).scatter_add(0, src, edge_weight)
+        elif deg is None:
             deg = torch.zeros(x.size(0), dtype=h.dtype).scatter_add_(
                 0, src, torch.ones(src.numel(), dtype=h.dtype))
         dinv = deg.pow(-0.5) if deg_norm == "sm" else deg.pow(-1)
         dinv = dinv.masked_fill(dinv == float("inf"), 0)
-        if deg_norm == "rw":
+        if edge_weight is not None:
+            norm = (dinv[src] * edge_weight * dinv[dst] if deg_norm == "sm"
+                    else dinv[src] * edge_weight)
+            x_j = torch.index_select(h, 0, src) * norm.view(-1, 1)
+        elif deg_norm == "rw":
             x_j = torch.index_select(h * dinv.view(-1, 1), 0, src)
         else:
             norm = dinv[src] * dinv[dst]

@@ -5,6 +5,7 @@ Run in the build container (needs /root/reference, read-only):
     python tests/golden/make_golden.py            # gcn_meta cases
     python tests/golden/make_golden.py hardpool   # HardPooling cases
     python tests/golden/make_golden.py conv       # GCNConv cases
+    python tests/golden/make_golden.py ewgrad     # edge_weight / deg gradients
 
 It imports the reference's own gcn_meta modules
 (/root/reference/src/gcn_meta/models/{gcn_base_models,common,gcn_multi_kernel,
@@ -387,6 +388,52 @@ def gcnconv_case(gbm, name, rng, N, E, F, use_ew, improved, identity, isolated=0
          meta=np.array([int(improved), int(identity), int(use_ew)]))
 
 
+def ewgrad_case(gbm, name, rng, N, E, F, deg_norm, aggr, identity, given="ew", isolated=10):
+    """NodeModelAdditive with edge_weight (or deg) requiring grad: records the
+    gradient degnorm_const passes back to it (gcn_base_models.py:102-140)."""
+    ei = make_graph(rng, N, E, self_loops=True, isolated=isolated)
+    nnz = ei.shape[1]
+    x = rng.standard_normal((N, F)).astype(np.float32)
+    dZ = rng.standard_normal((N, F)).astype(np.float32)
+    ew = rng.uniform(0.1, 2.0, nnz).astype(np.float32)
+    deg = rng.uniform(0.5, 5.0, N).astype(np.float32)
+    deg[rng.integers(0, N, max(1, N // 20))] = 0.0  # the inf -> 0 entries
+    torch.manual_seed(int(rng.integers(0, 2**31)))
+    nm = gbm.NodeModelAdditive(F, F, deg_norm=deg_norm, aggr=aggr, bias=True)
+    with torch.no_grad():
+        if identity:
+            nm.weight_node.copy_(torch.eye(F))
+        nm.bias.uniform_(-0.5, 0.5)
+    xt = _t(x).requires_grad_(True)
+    ewt = _t(ew).requires_grad_(True) if given == "ew" else None
+    degt = _t(deg).requires_grad_(True) if given == "deg" else None
+    y = nm(xt, _t(ei), deg=degt, edge_weight=ewt)
+    y.backward(_t(dZ))
+    save(name, edge_index=ei, x=x, W=nm.weight_node.detach(), b=nm.bias.detach(),
+         edge_weight=ew if given == "ew" else None, deg=deg if given == "deg" else None, dZ=dZ,
+         y=y, dx=xt.grad, dW=nm.weight_node.grad, db=nm.bias.grad,
+         dew=None if ewt is None else ewt.grad, ddeg=None if degt is None else degt.grad,
+         meta=np.array([deg_norm, aggr, given, int(identity)]))
+
+
+def main_ewgrad():
+    """Only the edge_weight / deg gradient fixtures (``python make_golden.py ewgrad``)."""
+    _, gbm, _ = _import_reference()
+    rng = np.random.default_rng(20261018)
+    n = 0
+    for deg_norm in ["sm", "rw"]:
+        for aggr in ["add", "mean", "max"]:
+            ewgrad_case(gbm, f"ewgrad_{deg_norm}_{aggr}", rng, 400, 3000, 16, deg_norm, aggr,
+                        True)
+            n += 1
+        ewgrad_case(gbm, f"degrad_{deg_norm}_add", rng, 400, 3000, 16, deg_norm, "add", True,
+                    given="deg")
+        n += 1
+    ewgrad_case(gbm, "ewgrad_sm_add_f128", rng, 500, 5000, 128, "sm", "add", False)
+    n += 1
+    print(f"wrote {n} edge-weight gradient fixtures to", OUT_DIR)
+
+
 def main_conv():
     """Only the GCNConv fixtures (``python make_golden.py conv``)."""
     _, gbm, _ = _import_reference()
@@ -456,5 +503,7 @@ if __name__ == "__main__":
         main_hardpool()
     elif sys.argv[1:] == ["conv"]:
         main_conv()
+    elif sys.argv[1:] == ["ewgrad"]:
+        main_ewgrad()
     else:
         main()

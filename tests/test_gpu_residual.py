@@ -144,8 +144,11 @@ def test_residual_layer_deterministic_and_first_layer_fallback(cuda):
 def test_residual_stack_matches_layer_by_layer(cuda, aggr, deg_norm, bias):
     """mgcn_residual_stack_fwd / _bwd (one host call per direction for a run
     of 32 -> 32 layers) against the same layers as separate fused nodes:
-    outputs, dx and every parameter gradient bit for bit (same kernels, same
-    order), on a skewed graph; and GCNModel routes its 32 -> 32 run there."""
+    outputs, dx and the weight gradients bit for bit (same kernels, same
+    order), on a skewed graph.  The bias gradients of the layers below the
+    top come from the mask pass fused into the layer above's dX store in the
+    stack (the same dS / dA values, column-summed per block of that kernel
+    instead of the mask kernel's rows): equal to fp32 rounding."""
     from mgcn import _lib as L
     from mgcn import ops
     rng = np.random.default_rng(17 + bias)
@@ -175,4 +178,7 @@ def test_residual_stack_matches_layer_by_layer(cuda, aggr, deg_norm, bias):
         y.backward(dZ)
         outs.append([y.detach(), xi.grad] + [p.grad for q in ps for p in q if p is not None])
     for a, b in zip(*outs):
-        assert torch.equal(a, b)
+        if a.dim() == 1:  # a bias gradient
+            torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6 * max(1.0, b.abs().max().item()))
+        else:
+            assert torch.equal(a, b)

@@ -33,7 +33,7 @@ def test_library_exports_every_header_symbol():
 def test_abi_version_and_option_errors():
     import mgcn
     lib = mgcn.load()
-    assert lib.mgcn_abi_version() == mgcn._lib.ABI_VERSION == 11
+    assert lib.mgcn_abi_version() == mgcn._lib.ABI_VERSION == 12
     assert lib.mgcn_set_option(b"no_such_option", 1) == 1
     assert b"unknown option" in lib.mgcn_last_error()
     with pytest.raises(mgcn.MgcnError):
@@ -154,21 +154,62 @@ def test_oracle_is_not_imported_by_product():
                 assert "liboracle" not in text, f
 
 
-def test_norm_rejects_grad_requiring_edge_weight_and_deg():
-    """degnorm_const is differentiable in edge_weight / deg in the reference
-    (gcn_base_models.py:102-140); the per-slot weights here are built
-    outside autograd, so asking for that gradient raises instead of
-    silently returning none (checked before any device work)."""
-    from mgcn.graph import GraphPlan
-    plan = GraphPlan(num_nodes=3, nnz=4, device=torch.device("cpu"), fwd=None, bwd=None,
-                     in_cnt=torch.ones(3))
-    ew = torch.ones(4, requires_grad=True)
-    with pytest.raises(NotImplementedError, match="edge_weight"):
-        plan.norm("sm", edge_weight=ew)
-    with pytest.raises(NotImplementedError, match="deg"):
-        plan.norm("rw", deg=torch.ones(3, requires_grad=True))
-    with pytest.raises(NotImplementedError, match="edge_weight"):
-        plan.norm(None, edge_weight=ew)
+@pytest.mark.parametrize("method,given", [("sm", "ew"), ("rw", "ew"), ("sm", "deg"),
+                                          ("rw", "deg"), (None, "ew")])
+def test_grad_norm_chain_matches_reference_autograd(monkeypatch, method, given):
+    """graph._grad_norm (edge_weight / deg requiring grad) against autograd of
+    the reference's own expression (gcn_base_models.py:117-142: scatter_add
+    of the weights over edge_index[0], pow(-1/2 | -1), inf -> 0 in place,
+    dinv[row] * w * dinv[col]).  Host logic only: the degree kernel is the
+    CPU double's (tests/cpu_backend.py); the SDDMM is a GPU test."""
+    import mgcn.graph as G
+    from cpu_backend import CpuBackend
+    be = CpuBackend()
+    monkeypatch.setattr(G, "degree_norm", be.degree_norm)
+    g = torch.Generator().manual_seed(7)
+    N, E = 40, 160
+    ei = torch.randint(0, N, (2, E), generator=g)
+    ei[:, :5] = torch.tensor([[3, 3, 3, 9, 9], [1, 2, 3, 9, 0]])
+    plan = be.build_plan(ei, N)
+    ew = (torch.rand(E, generator=g) + 0.1).requires_grad_(given == "ew")
+    deg = (torch.rand(N, generator=g) * 4).requires_grad_(given == "deg")
+    with torch.no_grad():
+        deg[[5, 11]] = 0.0  # the inf -> 0 entries (gradient masked there)
+    ew_r = ew.detach().clone().requires_grad_(given == "ew")
+    deg_r = deg.detach().clone().requires_grad_(given == "deg")
+    src, dst = ei
+    if given == "ew":
+        d = torch.zeros(N).scatter_add(0, src, ew_r)
+    else:
+        d = deg_r
+    if method is None:
+        w_ref = ew_r
+    else:
+        a = d.pow(-0.5) if method == "sm" else d.pow(-1)
+        a = a.clone()
+        a[a == float("inf")] = 0
+        if method == "rw" and given == "deg":
+            w_ref = a[src]  # per-slot dinv[src]: x * dinv before the gather
+        elif method == "sm":
+            w_ref = a[src] * ew_r * a[dst] if given == "ew" else a[src] * a[dst]
+        else:
+            w_ref = a[src] * ew_r
+    nm = plan.norm(method, deg=None if given == "ew" else deg,
+                   edge_weight=ew if given == "ew" else None)
+    assert nm.grad and nm.w_fwd.requires_grad
+    eid = plan.fwd.eid.long()
+    w = torch.zeros(E).index_put((eid,), nm.w_fwd)
+    torch.testing.assert_close(w.detach(), w_ref.detach(), rtol=1e-6, atol=0)
+    gout = torch.randn(E, generator=g)
+    (w * gout).sum().backward()
+    (w_ref * gout).sum().backward()
+    got, want = (ew.grad, ew_r.grad) if given == "ew" else (deg.grad, deg_r.grad)
+    finite = torch.isfinite(want)
+    assert torch.equal(finite, torch.isfinite(got))
+    torch.testing.assert_close(got[finite], want[finite], rtol=1e-5, atol=1e-6)
+    if nm.w_bwd is not None:
+        assert not nm.w_bwd.requires_grad
+        torch.testing.assert_close(nm.w_bwd, w.detach()[plan.bwd.eid.long()], rtol=0, atol=0)
 
 
 def test_pyg_loop_helpers_match_oracle_restatement(oracle):
