@@ -110,8 +110,16 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--aggr", default="add,mean,max", help="config4: aggregators to run")
+    ap.add_argument("--opt", action="append", default=[],
+                    help="libmgcn option name=value (mgcn_set_option), repeatable")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
+    if args.opt:
+        import mgcn
+        lib = mgcn.load()
+        for kv in args.opt:
+            k, v = kv.split("=")
+            mgcn._lib.check(lib.mgcn_set_option(k.encode(), int(v)), "mgcn_set_option")
     fn = {"config3": config3, "config4": config4}[args.workload]
     print(json.dumps(fn(args, dev)), flush=True)
 
