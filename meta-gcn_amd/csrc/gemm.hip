@@ -441,12 +441,108 @@ __global__ __launch_bounds__(256) void gemm_tn_small_kernel(
   }
 }
 
+// Staged small C for M = 32, N = 32 NT with 16-byte aligned rows (the F = 32
+// weight GEMMs of config 3, [W | Wr^T] with NT = 2): the split's rows stream
+// in 64-row chunks of float4 buffer loads (one register bank of prefetch, the
+// tail past the split reads zeros), are staged in LDS and feed
+// v_mfma_f32_32x32x2f32 from there (rows of 32 / 64 floats: conflict-free
+// operand reads); the four waves take interleaved k-steps of each chunk and
+// fold through LDS in wave order.  Same partial-slab layout as
+// gemm_tn_small_kernel.  The 4-byte-per-lane loads of that kernel leave ~6
+// dependent round trips per split at config 3 (26 us per launch).
+template <int NT>
+__global__ __launch_bounds__(256) void gemm_tn_staged_kernel(
+    const float *__restrict__ A, int64_t lda, const float *__restrict__ B, int64_t ldb,
+    int64_t K, int64_t k_per_split, float *__restrict__ partial) {
+  constexpr int CK = 64;       // rows per chunk
+  constexpr int NB = 32 * NT;  // columns of B (and C)
+  constexpr int QA = CK * 32 / 4 / 256, QB = CK * NB / 4 / 256;  // float4 per thread
+  // one allocation: the final fold reuses its first 16 KB
+  __shared__ __attribute__((aligned(16))) float stage[CK * 32 + CK * NB];
+  float(*As)[32] = reinterpret_cast<float(*)[32]>(stage);
+  float(*Bs)[NB] = reinterpret_cast<float(*)[NB]>(stage + CK * 32);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lr = lane >> 5, lc = lane & 31;
+  const int64_t kb = (int64_t)blockIdx.x * k_per_split;
+  const int64_t ke = (kb + k_per_split < K) ? kb + k_per_split : K;
+  const auto ra_ = buf_rsrc(A + kb * lda, (uint32_t)((ke - kb) * lda * 4));
+  const auto rb_ = buf_rsrc(B + kb * ldb, (uint32_t)((ke - kb) * ldb * 4));
+  u32x4 ra[QA], rb[QB];
+  auto load = [&](int64_t r0) {  // chunk at split row r0 (relative)
+#pragma unroll
+    for (int j = 0; j < QA; ++j) {
+      const int i = tid + 256 * j, row = i >> 3, c4 = i & 7;
+      ra[j] = __builtin_amdgcn_raw_buffer_load_b128(
+          ra_, (int)(((r0 + row) * lda + 4 * c4) * 4), 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < QB; ++j) {
+      const int i = tid + 256 * j, row = i / (NB / 4), c4 = i % (NB / 4);
+      rb[j] = __builtin_amdgcn_raw_buffer_load_b128(
+          rb_, (int)(((r0 + row) * ldb + 4 * c4) * 4), 0, 0);
+    }
+  };
+  f32x16 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
+  const int64_t n = ke - kb;
+  if (n > 0) load(0);
+  for (int64_t r0 = 0; r0 < n; r0 += CK) {
+    __syncthreads();  // the previous chunk's operand reads are done
+#pragma unroll
+    for (int j = 0; j < QA; ++j) {
+      const int i = tid + 256 * j;
+      *reinterpret_cast<u32x4 *>(&As[i >> 3][4 * (i & 7)]) = ra[j];
+    }
+#pragma unroll
+    for (int j = 0; j < QB; ++j) {
+      const int i = tid + 256 * j;
+      *reinterpret_cast<u32x4 *>(&Bs[i / (NB / 4)][4 * (i % (NB / 4))]) = rb[j];
+    }
+    __syncthreads();
+    if (r0 + CK < n) load(r0 + CK);  // in flight under this chunk's MFMAs
+    // wave w: k-steps w, w + 4, ... of two rows each (rows past the split are 0)
+#pragma unroll
+    for (int st = 0; st < CK / 8; ++st) {
+      const int k = 2 * (wave + 4 * st) + lr;
+      const float a = As[k][lc];
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, Bs[k][32 * t + lc], acc[t], 0, 0, 0);
+    }
+  }
+  // fold the four waves' accumulators in wave order (4 x 16 x 64 floats =
+  // 16 KB of the staging allocation, 16 or 24 KB)
+  float(*red)[16][64] = reinterpret_cast<float(*)[16][64]>(stage);
+  float *slab = partial + (int64_t)blockIdx.x * 32 * NB;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[wave][r][lane] = acc[t][r];
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float v = __fadd_rn(__fadd_rn(red[0][r][lane], red[1][r][lane]),
+                                  __fadd_rn(red[2][r][lane], red[3][r][lane]));
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * lr;
+        slab[row * NB + 32 * t + lc] = v;
+      }
+    }
+  }
+}
+
 bool tn_lds(int M, int N) { return M % kTile == 0 && N % kTile == 0; }
 
 // LDS-staged dW variants (mgcn_set_option "gemm_tn_variant"; measured at
 // K = 1M, M = N = 128: 0.321 / 0.335 / 0.337 ms): 0 = BK 64, one workgroup
 // per CU; 1 = BK 32, two; 2 = BK 16, three
 int g_tn_lds_variant = 0;
+int g_tn_staged = 1;  // M = 32, N = 32 / 64: gemm_tn_staged_kernel (0: gemm_tn_small_kernel)
 int tn_lds_wgs() { return g_tn_lds_variant == 1 ? 2 : g_tn_lds_variant == 2 ? 3 : 1; }
 
 int gemm_splits(int64_t K, int M, int N) {
@@ -467,6 +563,12 @@ int gemm_splits(int64_t K, int M, int N) {
 int gemm_set_tn_variant(int value) {
   if (value < 0 || value > 2) return MGCN_EINVAL;
   g_tn_lds_variant = value;
+  return MGCN_OK;
+}
+
+int gemm_set_tn_staged(int value) {
+  if (value < 0 || value > 1) return MGCN_EINVAL;
+  g_tn_staged = value;
   return MGCN_OK;
 }
 
@@ -504,6 +606,26 @@ int gemm_tn_impl(int64_t K, int32_t M, int32_t N, const float *A, int64_t lda, c
   kps = (kps + 63) / 64 * 64;  // whole chunks of every variant (and whole kU groups)
   const int used = (int)((K + kps - 1) / kps);
   float *partial = static_cast<float *>(workspace);
+  if (M == 32 && (N == 32 || N == 64) && reinterpret_cast<uintptr_t>(A) % 16 == 0 &&
+      reinterpret_cast<uintptr_t>(B) % 16 == 0 && lda % 4 == 0 && ldb % 4 == 0 &&
+      g_tn_staged) {
+    // at most `splits` (the workspace's count) workgroups of >= 256 rows
+    int64_t s2 = (K + 255) / 256;
+    if (s2 > 512) s2 = 512;
+    if (s2 > splits) s2 = splits;
+    int64_t kps2 = (K + s2 - 1) / s2;
+    kps2 = (kps2 + 63) / 64 * 64;
+    const int used2 = (int)((K + kps2 - 1) / kps2);
+    if (N == 32)
+      hipLaunchKernelGGL(gemm_tn_staged_kernel<1>, dim3(used2), dim3(256), 0, s, A, lda, B, ldb,
+                         K, kps2, partial);
+    else
+      hipLaunchKernelGGL(gemm_tn_staged_kernel<2>, dim3(used2), dim3(256), 0, s, A, lda, B, ldb,
+                         K, kps2, partial);
+    if (int rc = check_launch("gemm_tn_staged_kernel")) return rc;
+    return launch_fold_split(partial, used2, (int64_t)M * N, N, C, ldc, N1, C2, ldc2, accumulate,
+                             s);
+  }
   if (M <= 32 && N <= 64) {
     if (N <= 32)
       hipLaunchKernelGGL(gemm_tn_small_kernel<1>, dim3(used), dim3(256), 0, s, A, lda, B, ldb, K,

@@ -1154,6 +1154,10 @@ extern "C" int mgcn_set_option(const char *name, int value) {
     MGCN_REQUIRE(value >= 0 && value <= 2, "gemm_tn_variant must be 0, 1 or 2");
     return gemm_set_tn_variant(value);
   }
+  if (n == "gemm_tn_staged") {
+    MGCN_REQUIRE(value == 0 || value == 1, "gemm_tn_staged must be 0 or 1");
+    return gemm_set_tn_staged(value);
+  }
   if (n == "gemm_precision") {
     MGCN_REQUIRE(value == 0 || value == 1, "gemm_precision must be 0 (f32) or 1 (bf16x6)");
     return gemm_set_precision(value);

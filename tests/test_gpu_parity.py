@@ -252,7 +252,10 @@ def gemm_precision(request):
 
 @pytest.mark.parametrize("K,M,N", [(1_000_000, 128, 128), (4097, 128, 128), (3000, 7, 130),
                                    (50, 32, 2), (0, 4, 4), (286_214, 32, 32), (286_214, 2, 32),
-                                   (1001, 17, 5), (77, 128, 256), (1_000_003, 128, 128)])
+                                   (1001, 17, 5), (77, 128, 256), (1_000_003, 128, 128),
+                                   # M = 32, N = 32 / 64: the staged kernel (config 3's
+                                   # [dW | dWr^T]), whole and ragged 64-row chunks
+                                   (286_214, 32, 64), (100, 32, 64), (64, 32, 32), (65, 32, 64)])
 def test_gemm_tn_matches_fp64(cuda, K, M, N, gemm_precision):
     """dW = A^T B (f32 MFMA: exact f32 products; bf16x6: the exact three-term
     bf16 split, six products on bf16 MFMA; f32 accumulation in a different
