@@ -606,15 +606,16 @@ int gemm_tn_impl(int64_t K, int32_t M, int32_t N, const float *A, int64_t lda, c
   kps = (kps + 63) / 64 * 64;  // whole chunks of every variant (and whole kU groups)
   const int used = (int)((K + kps - 1) / kps);
   float *partial = static_cast<float *>(workspace);
+  // the staged kernel: at most `splits` (the workspace's count) workgroups
+  // of >= 256 rows, each split's byte offsets within 32 bits (buffer loads)
+  int64_t s2 = (K + 255) / 256;
+  if (s2 > 512) s2 = 512;
+  if (s2 > splits) s2 = splits;
+  int64_t kps2 = (K + s2 - 1) / s2;
+  kps2 = (kps2 + 63) / 64 * 64;
   if (M == 32 && (N == 32 || N == 64) && reinterpret_cast<uintptr_t>(A) % 16 == 0 &&
       reinterpret_cast<uintptr_t>(B) % 16 == 0 && lda % 4 == 0 && ldb % 4 == 0 &&
-      g_tn_staged) {
-    // at most `splits` (the workspace's count) workgroups of >= 256 rows
-    int64_t s2 = (K + 255) / 256;
-    if (s2 > 512) s2 = 512;
-    if (s2 > splits) s2 = splits;
-    int64_t kps2 = (K + s2 - 1) / s2;
-    kps2 = (kps2 + 63) / 64 * 64;
+      (kps2 + 64) * (lda > ldb ? lda : ldb) * 4 < (int64_t(1) << 31) && g_tn_staged) {
     const int used2 = (int)((K + kps2 - 1) / kps2);
     if (N == 32)
       hipLaunchKernelGGL(gemm_tn_staged_kernel<1>, dim3(used2), dim3(256), 0, s, A, lda, B, ldb,
