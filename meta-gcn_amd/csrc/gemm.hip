@@ -453,7 +453,27 @@ __global__ __launch_bounds__(256) void gemm_tn_small_kernel(
 template <int NT>
 __global__ __launch_bounds__(256) void gemm_tn_staged_kernel(
     const float *__restrict__ A, int64_t lda, const float *__restrict__ B, int64_t ldb,
-    int64_t K, int64_t k_per_split, float *__restrict__ partial) {
+    int64_t K, int64_t k_per_split, float *__restrict__ partial, SideFold sf) {
+  if (blockIdx.x >= gridDim.x - (unsigned)sf.n) {
+    // a side job riding in the same launch: column j of an independent fold
+    // of [sf.parts][sf.n] partials (the residual stack's bias-gradient column
+    // sums), 256 strided partial sums then a fixed tree -- as
+    // fold_partials_kernel with one element per block
+    __shared__ float red[256];
+    const int j = (int)(blockIdx.x - (gridDim.x - (unsigned)sf.n));
+    float acc = 0.0f;
+#pragma unroll 4
+    for (int64_t sp = threadIdx.x; sp < sf.parts; sp += 256)
+      acc = __fadd_rn(acc, sf.partial[sp * sf.n + j]);
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int h = 128; h >= 1; h >>= 1) {
+      if ((int)threadIdx.x < h) red[threadIdx.x] = __fadd_rn(red[threadIdx.x], red[threadIdx.x + h]);
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) sf.out[j] = red[0];
+    return;
+  }
   constexpr int CK = 64;       // rows per chunk
   constexpr int NB = 32 * NT;  // columns of B (and C)
   constexpr int QA = CK * 32 / 4 / 256, QB = CK * NB / 4 / 256;  // float4 per thread
@@ -582,9 +602,10 @@ extern "C" size_t mgcn_gemm_tn_workspace_bytes(int64_t K, int32_t M, int32_t N) 
 
 namespace {
 // C = A^T B; columns [N1, N) go transposed to C2 (N1 == N: plain C)
-int gemm_tn_impl(int64_t K, int32_t M, int32_t N, const float *A, int64_t lda, const float *B,
+int gemm_tn_core(int64_t K, int32_t M, int32_t N, const float *A, int64_t lda, const float *B,
                  int64_t ldb, float *C, int64_t ldc, int32_t N1, float *C2, int64_t ldc2,
-                 int accumulate, void *workspace, size_t workspace_bytes, hipStream_t s) {
+                 int accumulate, void *workspace, size_t workspace_bytes, hipStream_t s,
+                 const SideFold *side, bool *side_done) {
   if (M == 0 || N == 0) return MGCN_OK;
   if (K == 0) {
     if (!accumulate) {
@@ -617,12 +638,18 @@ int gemm_tn_impl(int64_t K, int32_t M, int32_t N, const float *A, int64_t lda, c
       reinterpret_cast<uintptr_t>(B) % 16 == 0 && lda % 4 == 0 && ldb % 4 == 0 &&
       (kps2 + 64) * (lda > ldb ? lda : ldb) * 4 < (int64_t(1) << 31) && g_tn_staged) {
     const int used2 = (int)((K + kps2 - 1) / kps2);
+    SideFold sf{};
+    if (side != nullptr && side->parts > 0 && side->n > 0) {
+      sf = *side;
+      *side_done = true;
+    }
+    const dim3 grid((unsigned)(used2 + sf.n));
     if (N == 32)
-      hipLaunchKernelGGL(gemm_tn_staged_kernel<1>, dim3(used2), dim3(256), 0, s, A, lda, B, ldb,
-                         K, kps2, partial);
+      hipLaunchKernelGGL(gemm_tn_staged_kernel<1>, grid, dim3(256), 0, s, A, lda, B, ldb, K,
+                         kps2, partial, sf);
     else
-      hipLaunchKernelGGL(gemm_tn_staged_kernel<2>, dim3(used2), dim3(256), 0, s, A, lda, B, ldb,
-                         K, kps2, partial);
+      hipLaunchKernelGGL(gemm_tn_staged_kernel<2>, grid, dim3(256), 0, s, A, lda, B, ldb, K,
+                         kps2, partial, sf);
     if (int rc = check_launch("gemm_tn_staged_kernel")) return rc;
     return launch_fold_split(partial, used2, (int64_t)M * N, N, C, ldc, N1, C2, ldc2, accumulate,
                              s);
@@ -659,6 +686,18 @@ int gemm_tn_impl(int64_t K, int32_t M, int32_t N, const float *A, int64_t lda, c
   const int64_t MN = (int64_t)M * N;
   return launch_fold_split(partial, used, MN, N, C, ldc, N1, C2, ldc2, accumulate, s);
 }
+
+int gemm_tn_impl(int64_t K, int32_t M, int32_t N, const float *A, int64_t lda, const float *B,
+                 int64_t ldb, float *C, int64_t ldc, int32_t N1, float *C2, int64_t ldc2,
+                 int accumulate, void *workspace, size_t workspace_bytes, hipStream_t s,
+                 const SideFold *side = nullptr) {
+  bool done = false;
+  if (int rc = gemm_tn_core(K, M, N, A, lda, B, ldb, C, ldc, N1, C2, ldc2, accumulate, workspace,
+                            workspace_bytes, s, side, &done))
+    return rc;
+  if (side == nullptr || done || side->n <= 0) return MGCN_OK;
+  return launch_colsum_fold(side->partial, side->parts, side->n, side->out, s);
+}
 }  // namespace
 
 extern "C" int mgcn_gemm_tn(int64_t K, int32_t M, int32_t N, const float *A, int64_t lda,
@@ -672,6 +711,16 @@ extern "C" int mgcn_gemm_tn(int64_t K, int32_t M, int32_t N, const float *A, int
   return gemm_tn_impl(K, M, N, A, lda, B, ldb, C, ldc, N, nullptr, 0, accumulate, workspace,
                       workspace_bytes, as_stream(stream));
 }
+
+namespace mgcn {
+int gemm_tn_split_fold(int64_t K, int32_t M, int32_t N, int32_t N1, const float *A, int64_t lda,
+                       const float *B, int64_t ldb, float *C1, int64_t ldc1, float *C2t,
+                       int64_t ldc2t, void *workspace, size_t workspace_bytes,
+                       const SideFold &side, hipStream_t s) {
+  return gemm_tn_impl(K, M, N, A, lda, B, ldb, C1, ldc1, N1, C2t, ldc2t, 0, workspace,
+                      workspace_bytes, s, &side);
+}
+}  // namespace mgcn
 
 extern "C" int mgcn_gemm_tn_split(int64_t K, int32_t M, int32_t N, int32_t N1, const float *A,
                                   int64_t lda, const float *B, int64_t ldb, float *C1,

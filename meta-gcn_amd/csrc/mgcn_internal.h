@@ -72,6 +72,20 @@ int launch_fold_split(const float *partial, int64_t splits, int64_t MN, int N, f
 int launch_split_reduce(const float *partial, int splits, int64_t MN, int N, float *C,
                         int64_t ldc, int accumulate, hipStream_t s);
 int launch_colsum_fold(const float *partial, int64_t nparts, int N, float *out, hipStream_t s);
+// an independent fold of [parts][n] partials into out[n], run by extra
+// workgroups of a launch that has other work (gemm_tn_split_fold)
+struct SideFold {
+  const float *partial;
+  int64_t parts;
+  int n;
+  float *out;
+};
+// mgcn_gemm_tn_split (accumulate = 0) plus `side`'s fold, in the same launch
+// where the staged kernel takes the shape (else a separate fold launch)
+int gemm_tn_split_fold(int64_t K, int32_t M, int32_t N, int32_t N1, const float *A, int64_t lda,
+                       const float *B, int64_t ldb, float *C1, int64_t ldc1, float *C2t,
+                       int64_t ldc2t, void *workspace, size_t workspace_bytes,
+                       const SideFold &side, hipStream_t s);
 // heavy rows of a view alone (spmm.hip), for the fused layer kernels of residual.hip
 int heavy_rows(int bwd, int64_t n_rows, int32_t F, const int64_t *rowptr, const int32_t *col,
                const int32_t *eid, const float *w, const float *X, int64_t ldx, float *Y,

@@ -517,7 +517,8 @@ int residual_bwd_core(int64_t n_rows, const int64_t *rowptr_t, const int32_t *co
                       const int32_t *eid_t, const float *w_t, const float *row_scale,
                       const float *dA, const float *W, int64_t ldw, const float *Wr, int64_t ldwr,
                       float *dX, int64_t lddx, float *DH, int64_t lddh, const int32_t *order,
-                      int64_t n_heavy, int64_t n_giant, const LowerMask *lm, hipStream_t s) {
+                      int64_t n_heavy, int64_t n_giant, const LowerMask *lm, hipStream_t s,
+                      int64_t *defer_parts = nullptr) {
   const int F = kRF;
   if (order == nullptr) n_heavy = n_giant = 0;
   bool side = false;
@@ -569,6 +570,10 @@ int residual_bwd_core(int64_t n_rows, const int64_t *rowptr_t, const int32_t *co
     parts += rl_blocks(n_heavy, lm != nullptr);
   }
   if (lm == nullptr) return MGCN_OK;
+  if (defer_parts != nullptr) {  // the caller folds them (in its weight-GEMM launch)
+    *defer_parts = parts;
+    return MGCN_OK;
+  }
   return launch_colsum_fold(lm->partial, parts, 2 * F, lm->colsums, s);
 }
 }  // namespace
@@ -748,9 +753,10 @@ extern "C" int mgcn_residual_stack_bwd(int64_t n_rows, int32_t F, int32_t n_laye
       lm.colsums = sums + (int64_t)(l - 1) * 2 * F;
     }
     const bool fuse = l > 0 && g_fused_mask;
+    int64_t parts = 0;
     if (int rc = residual_bwd_core(n_rows, rowptr_t, col_t, eid_t, w_t, row_scale, dAb[c], W[l], F,
                                    Wr[l], F, dx, F, DHb[c], 2 * F, order, n_heavy, n_giant,
-                                   fuse ? &lm : nullptr, s))
+                                   fuse ? &lm : nullptr, s, fuse ? &parts : nullptr))
       return rc;
     if (l > 0 && !fuse) {  // the lower layer's mask pass as its own kernel
       hipLaunchKernelGGL(residual_mask_bwd_kernel, dim3(nparts), dim3(256), 0, s, n_rows, dx,
@@ -759,10 +765,13 @@ extern "C" int mgcn_residual_stack_bwd(int64_t n_rows, int32_t F, int32_t n_laye
       if (int rc = check_launch("residual_mask_bwd_kernel")) return rc;
       if (int rc = launch_colsum_fold(mpart, nparts, 2 * F, lm.colsums, s)) return rc;
     }
-    // [dW | dWr^T] = X_l^T [dH | dS]
+    // [dW | dWr^T] = X_l^T [dH | dS]; with the fused mask pass, the lower
+    // layer's bias-gradient column sums are folded in the same launch
     const float *xin = l == 0 ? X0 : Z + (int64_t)(l - 1) * n_rows * F;
-    if (int rc = mgcn_gemm_tn_split(n_rows, F, 2 * F, F, xin, l == 0 ? ldx : F, DHb[c], 2 * F,
-                                    dW[l], F, dWr[l], F, 0, ws + sc.gemm, gemm_bytes, stream))
+    SideFold side{};
+    if (fuse) side = SideFold{lm.partial, parts, 2 * F, lm.colsums};
+    if (int rc = gemm_tn_split_fold(n_rows, F, 2 * F, F, xin, l == 0 ? ldx : F, DHb[c], 2 * F,
+                                    dW[l], F, dWr[l], F, ws + sc.gemm, gemm_bytes, side, s))
       return rc;
   }
   return MGCN_OK;
