@@ -454,24 +454,11 @@ template <int NT>
 __global__ __launch_bounds__(256) void gemm_tn_staged_kernel(
     const float *__restrict__ A, int64_t lda, const float *__restrict__ B, int64_t ldb,
     int64_t K, int64_t k_per_split, float *__restrict__ partial, SideFold sf) {
-  if (blockIdx.x >= gridDim.x - (unsigned)sf.n) {
-    // a side job riding in the same launch: column j of an independent fold
-    // of [sf.parts][sf.n] partials (the residual stack's bias-gradient column
-    // sums), 256 strided partial sums then a fixed tree -- as
-    // fold_partials_kernel with one element per block
+  if (blockIdx.x >= gridDim.x - (unsigned)sf.blocks) {
+    // a side job riding in the same launch (the residual stack's bias-gradient
+    // column sums, an independent fold)
     __shared__ float red[256];
-    const int j = (int)(blockIdx.x - (gridDim.x - (unsigned)sf.n));
-    float acc = 0.0f;
-#pragma unroll 4
-    for (int64_t sp = threadIdx.x; sp < sf.parts; sp += 256)
-      acc = __fadd_rn(acc, sf.partial[sp * sf.n + j]);
-    red[threadIdx.x] = acc;
-    __syncthreads();
-    for (int h = 128; h >= 1; h >>= 1) {
-      if ((int)threadIdx.x < h) red[threadIdx.x] = __fadd_rn(red[threadIdx.x], red[threadIdx.x + h]);
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) sf.out[j] = red[0];
+    side_fold_block(sf, (int)(blockIdx.x - (gridDim.x - (unsigned)sf.blocks)), red);
     return;
   }
   constexpr int CK = 64;       // rows per chunk
@@ -605,7 +592,7 @@ namespace {
 int gemm_tn_core(int64_t K, int32_t M, int32_t N, const float *A, int64_t lda, const float *B,
                  int64_t ldb, float *C, int64_t ldc, int32_t N1, float *C2, int64_t ldc2,
                  int accumulate, void *workspace, size_t workspace_bytes, hipStream_t s,
-                 const SideFold *side, bool *side_done) {
+                 const SideFold *side, bool *side_done, SideFold *defer) {
   if (M == 0 || N == 0) return MGCN_OK;
   if (K == 0) {
     if (!accumulate) {
@@ -639,11 +626,11 @@ int gemm_tn_core(int64_t K, int32_t M, int32_t N, const float *A, int64_t lda, c
       (kps2 + 64) * (lda > ldb ? lda : ldb) * 4 < (int64_t(1) << 31) && g_tn_staged) {
     const int used2 = (int)((K + kps2 - 1) / kps2);
     SideFold sf{};
-    if (side != nullptr && side->parts > 0 && side->n > 0) {
+    if (side != nullptr && side->blocks > 0) {
       sf = *side;
       *side_done = true;
     }
-    const dim3 grid((unsigned)(used2 + sf.n));
+    const dim3 grid((unsigned)(used2 + sf.blocks));
     if (N == 32)
       hipLaunchKernelGGL(gemm_tn_staged_kernel<1>, grid, dim3(256), 0, s, A, lda, B, ldb, K,
                          kps2, partial, sf);
@@ -651,6 +638,10 @@ int gemm_tn_core(int64_t K, int32_t M, int32_t N, const float *A, int64_t lda, c
       hipLaunchKernelGGL(gemm_tn_staged_kernel<2>, grid, dim3(256), 0, s, A, lda, B, ldb, K,
                          kps2, partial, sf);
     if (int rc = check_launch("gemm_tn_staged_kernel")) return rc;
+    if (defer != nullptr && !accumulate) {
+      *defer = make_side_fold(partial, used2, (int64_t)M * N, N, C, ldc, N1, C2, ldc2);
+      return MGCN_OK;
+    }
     return launch_fold_split(partial, used2, (int64_t)M * N, N, C, ldc, N1, C2, ldc2, accumulate,
                              s);
   }
@@ -690,13 +681,14 @@ int gemm_tn_core(int64_t K, int32_t M, int32_t N, const float *A, int64_t lda, c
 int gemm_tn_impl(int64_t K, int32_t M, int32_t N, const float *A, int64_t lda, const float *B,
                  int64_t ldb, float *C, int64_t ldc, int32_t N1, float *C2, int64_t ldc2,
                  int accumulate, void *workspace, size_t workspace_bytes, hipStream_t s,
-                 const SideFold *side = nullptr) {
+                 const SideFold *side = nullptr, SideFold *defer = nullptr) {
   bool done = false;
+  if (defer != nullptr) *defer = SideFold{};
   if (int rc = gemm_tn_core(K, M, N, A, lda, B, ldb, C, ldc, N1, C2, ldc2, accumulate, workspace,
-                            workspace_bytes, s, side, &done))
+                            workspace_bytes, s, side, &done, defer))
     return rc;
-  if (side == nullptr || done || side->n <= 0) return MGCN_OK;
-  return launch_colsum_fold(side->partial, side->parts, side->n, side->out, s);
+  if (side == nullptr || done) return MGCN_OK;
+  return launch_side_fold(*side, s);
 }
 }  // namespace
 
@@ -716,9 +708,9 @@ namespace mgcn {
 int gemm_tn_split_fold(int64_t K, int32_t M, int32_t N, int32_t N1, const float *A, int64_t lda,
                        const float *B, int64_t ldb, float *C1, int64_t ldc1, float *C2t,
                        int64_t ldc2t, void *workspace, size_t workspace_bytes,
-                       const SideFold &side, hipStream_t s) {
+                       const SideFold &side, hipStream_t s, SideFold *defer) {
   return gemm_tn_impl(K, M, N, A, lda, B, ldb, C1, ldc1, N1, C2t, ldc2t, 0, workspace,
-                      workspace_bytes, s, &side);
+                      workspace_bytes, s, &side, defer);
 }
 }  // namespace mgcn
 
@@ -1193,6 +1185,33 @@ int launch_fold_split(const float *partial, int64_t splits, int64_t MN, int N, f
   const int64_t blocks = (MN + (1 << log_eb) - 1) >> log_eb;
   hipLaunchKernelGGL(fold_partials_kernel, dim3((unsigned)blocks), dim3(256), 0, s, partial,
                      splits, MN, N, C, ldc, accumulate, log_eb, N1, C2, ldc2);
+  return check_launch("fold_partials_kernel");
+}
+
+SideFold make_side_fold(const float *partial, int64_t parts, int64_t MN, int N, float *C,
+                        int64_t ldc, int N1, float *C2, int64_t ldc2) {
+  SideFold f{};
+  if (MN <= 0) return f;
+  int log_eb = 0;  // as launch_fold_split
+  while (log_eb < 4 && (MN >> (log_eb + 9)) > 0) ++log_eb;
+  f.partial = partial;
+  f.parts = parts;
+  f.MN = MN;
+  f.N = N;
+  f.N1 = N1;
+  f.log_eb = log_eb;
+  f.blocks = (int)((MN + (1 << log_eb) - 1) >> log_eb);
+  f.C = C;
+  f.C2 = C2;
+  f.ldc = ldc;
+  f.ldc2 = ldc2;
+  return f;
+}
+
+int launch_side_fold(const SideFold &f, hipStream_t s) {
+  if (f.blocks <= 0) return MGCN_OK;
+  hipLaunchKernelGGL(fold_partials_kernel, dim3((unsigned)f.blocks), dim3(256), 0, s, f.partial,
+                     f.parts, f.MN, f.N, f.C, f.ldc, 0, f.log_eb, f.N1, f.C2, f.ldc2);
   return check_launch("fold_partials_kernel");
 }
 

@@ -72,20 +72,54 @@ int launch_fold_split(const float *partial, int64_t splits, int64_t MN, int N, f
 int launch_split_reduce(const float *partial, int splits, int64_t MN, int N, float *C,
                         int64_t ldc, int accumulate, hipStream_t s);
 int launch_colsum_fold(const float *partial, int64_t nparts, int N, float *out, hipStream_t s);
-// an independent fold of [parts][n] partials into out[n], run by extra
-// workgroups of a launch that has other work (gemm_tn_split_fold)
+// A fold of split partials (launch_fold_split's job: C[e] = sum_sp
+// partial[sp * MN + e], columns [N1, N) of the [MN / N, N] result to C2
+// transposed) run by `blocks` extra 256-thread workgroups of a launch that
+// has other work; a workgroup b < blocks calls side_fold_block(f, b, red).
 struct SideFold {
   const float *partial;
-  int64_t parts;
-  int n;
-  float *out;
+  int64_t parts, MN;
+  int N, N1, log_eb, blocks;
+  float *C, *C2;
+  int64_t ldc, ldc2;
 };
-// mgcn_gemm_tn_split (accumulate = 0) plus `side`'s fold, in the same launch
-// where the staged kernel takes the shape (else a separate fold launch)
+SideFold make_side_fold(const float *partial, int64_t parts, int64_t MN, int N, float *C,
+                        int64_t ldc, int N1, float *C2, int64_t ldc2);
+int launch_side_fold(const SideFold &f, hipStream_t s);  // on its own (nothing to ride in)
+
+// the same fixed order as fold_partials_kernel (strided partial sums of EB
+// elements per workgroup, then a tree over the 256 / EB groups); red: 256
+// floats of LDS; every thread of the workgroup calls it
+__device__ inline void side_fold_block(const SideFold &f, int b, float *red) {
+  const int EB = 1 << f.log_eb, T = 256 >> f.log_eb;
+  const int el = threadIdx.x & (EB - 1), g = threadIdx.x >> f.log_eb;
+  const int64_t e = (int64_t)b * EB + el;
+  float acc = 0.0f;
+  if (e < f.MN) {
+#pragma unroll 4
+    for (int64_t sp = g; sp < f.parts; sp += T) acc = __fadd_rn(acc, f.partial[sp * f.MN + e]);
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int h = T >> 1; h >= 1; h >>= 1) {
+    if (g < h) red[threadIdx.x] = __fadd_rn(red[threadIdx.x], red[threadIdx.x + h * EB]);
+    __syncthreads();
+  }
+  if (g == 0 && e < f.MN) {
+    const int64_t row = e / f.N, col = e % f.N;
+    float *dst = col < f.N1 ? f.C + row * f.ldc + col : f.C2 + (col - f.N1) * f.ldc2 + row;
+    *dst = red[el];
+  }
+}
+
+// mgcn_gemm_tn_split (accumulate = 0) with `side` folded by extra workgroups
+// of the same launch; where the staged kernel takes the shape and `defer` is
+// given, its own split-K fold is left to the caller (*defer, to ride in a
+// later launch: launch_side_fold if none does), else folded here
 int gemm_tn_split_fold(int64_t K, int32_t M, int32_t N, int32_t N1, const float *A, int64_t lda,
                        const float *B, int64_t ldb, float *C1, int64_t ldc1, float *C2t,
                        int64_t ldc2t, void *workspace, size_t workspace_bytes,
-                       const SideFold &side, hipStream_t s);
+                       const SideFold &side, hipStream_t s, SideFold *defer = nullptr);
 // heavy rows of a view alone (spmm.hip), for the fused layer kernels of residual.hip
 int heavy_rows(int bwd, int64_t n_rows, int32_t F, const int64_t *rowptr, const int32_t *col,
                const int32_t *eid, const float *w, const float *X, int64_t ldx, float *Y,

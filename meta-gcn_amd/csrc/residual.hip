@@ -85,6 +85,9 @@ struct RlArgs {
   float *mda;
   int64_t ldmda;
   float *mpart;
+  // an independent fold riding in this launch: its workgroups are the last
+  // side.blocks of the grid (the weight-GEMM split-K fold of the layer above)
+  SideFold side;
 };
 
 __device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
@@ -99,6 +102,12 @@ constexpr int kTileLd = 2 * kRF + 4;
 
 template <int U, bool BWD>
 __global__ __launch_bounds__(kRBlock) void residual_layer_kernel(const RlArgs a) {
+  __shared__ __attribute__((aligned(16))) float tile[kRWaves][kTileRows][kTileLd];
+  if (blockIdx.x >= gridDim.x - (unsigned)a.side.blocks) {
+    side_fold_block(a.side, (int)(blockIdx.x - (gridDim.x - (unsigned)a.side.blocks)),
+                    &tile[0][0][0]);
+    return;
+  }
   // B operands of v_mfma_f32_16x16x4_f32 (lane l: B[k][16 cb + (l & 15)]);
   // the k-steps are permuted so that step s of lane group kk = l >> 4 is
   // k = 8 kk + s: a lane's A operands are then 8 contiguous floats of its
@@ -107,7 +116,6 @@ __global__ __launch_bounds__(kRBlock) void residual_layer_kernel(const RlArgs a)
   //   backward: B1[k][n] = W[n][k],  B2[k][n] = Wr[k][n]   (dX = dH W^T + dS Wr)
   __shared__ __attribute__((aligned(16))) float B1[2][64][8];
   __shared__ __attribute__((aligned(16))) float B2[2][64][8];
-  __shared__ __attribute__((aligned(16))) float tile[kRWaves][kTileRows][kTileLd];
   __shared__ int64_t tile_row[kRWaves][kTileRows];
   const int tid = threadIdx.x;
   for (int e = tid; e < 2 * 64 * 8; e += kRBlock) {
@@ -408,8 +416,8 @@ int64_t rl_blocks(int64_t n_items, bool fused_mask) {
 
 template <bool BWD>
 int launch_rl(const RlArgs &a, hipStream_t s) {
-  if (a.n_items <= 0) return MGCN_OK;
-  const int64_t blocks = rl_blocks(a.n_items, BWD && a.mmask != nullptr);
+  if (a.n_items <= 0) return launch_side_fold(a.side, s);  // nothing to ride in
+  const int64_t blocks = rl_blocks(a.n_items, BWD && a.mmask != nullptr) + a.side.blocks;
   hipLaunchKernelGGL((residual_layer_kernel<8, BWD>), dim3((unsigned)blocks), dim3(kRBlock), 0, s, a);
   return check_launch("residual_layer_kernel");
 }
@@ -518,7 +526,7 @@ int residual_bwd_core(int64_t n_rows, const int64_t *rowptr_t, const int32_t *co
                       const float *dA, const float *W, int64_t ldw, const float *Wr, int64_t ldwr,
                       float *dX, int64_t lddx, float *DH, int64_t lddh, const int32_t *order,
                       int64_t n_heavy, int64_t n_giant, const LowerMask *lm, hipStream_t s,
-                      int64_t *defer_parts = nullptr) {
+                      int64_t *defer_parts = nullptr, const SideFold *ride = nullptr) {
   const int F = kRF;
   if (order == nullptr) n_heavy = n_giant = 0;
   bool side = false;
@@ -557,7 +565,9 @@ int residual_bwd_core(int64_t n_rows, const int64_t *rowptr_t, const int32_t *co
   a.gather = 1;
   a.items = order != nullptr ? order + n_heavy : nullptr;
   a.n_items = n_rows - n_heavy;
+  if (ride != nullptr) a.side = *ride;
   if (int rc = launch_rl<true>(a, s)) return rc;
+  a.side = SideFold{};
   int64_t parts = rl_blocks(a.n_items, lm != nullptr);
   if (n_heavy > 0) {
     if (side)
@@ -736,6 +746,7 @@ extern "C" int mgcn_residual_stack_bwd(int64_t n_rows, int32_t F, int32_t n_laye
                      (int64_t)F, DHb[top & 1] + F, (int64_t)2 * F, mpart);
   if (int rc = check_launch("residual_mask_bwd_kernel")) return rc;
   if (int rc = launch_colsum_fold(mpart, nparts, 2 * F, sums + (int64_t)top * 2 * F, s)) return rc;
+  SideFold pending{};  // the weight-GEMM fold of the layer above, riding in the next light pass
   for (int32_t l = top; l >= 0; --l) {
     const int c = l & 1, o = c ^ 1;
     float *dx = (l == 0 && dX0 != nullptr) ? dX0 : reinterpret_cast<float *>(ws + sc.dx);
@@ -756,8 +767,9 @@ extern "C" int mgcn_residual_stack_bwd(int64_t n_rows, int32_t F, int32_t n_laye
     int64_t parts = 0;
     if (int rc = residual_bwd_core(n_rows, rowptr_t, col_t, eid_t, w_t, row_scale, dAb[c], W[l], F,
                                    Wr[l], F, dx, F, DHb[c], 2 * F, order, n_heavy, n_giant,
-                                   fuse ? &lm : nullptr, s, fuse ? &parts : nullptr))
+                                   fuse ? &lm : nullptr, s, fuse ? &parts : nullptr, &pending))
       return rc;
+    pending = SideFold{};
     if (l > 0 && !fuse) {  // the lower layer's mask pass as its own kernel
       hipLaunchKernelGGL(residual_mask_bwd_kernel, dim3(nparts), dim3(256), 0, s, n_rows, dx,
                          (int64_t)F, lm.masks, lm.relu1, lm.relu2, row_div, dAb[o], (int64_t)F,
@@ -769,10 +781,12 @@ extern "C" int mgcn_residual_stack_bwd(int64_t n_rows, int32_t F, int32_t n_laye
     // layer's bias-gradient column sums are folded in the same launch
     const float *xin = l == 0 ? X0 : Z + (int64_t)(l - 1) * n_rows * F;
     SideFold side{};
-    if (fuse) side = SideFold{lm.partial, parts, 2 * F, lm.colsums};
+    if (fuse) side = make_side_fold(lm.partial, parts, 2 * F, 2 * F, lm.colsums, 2 * F, 2 * F,
+                                    nullptr, 0);
     if (int rc = gemm_tn_split_fold(n_rows, F, 2 * F, F, xin, l == 0 ? ldx : F, DHb[c], 2 * F,
-                                    dW[l], F, dWr[l], F, ws + sc.gemm, gemm_bytes, side, s))
+                                    dW[l], F, dWr[l], F, ws + sc.gemm, gemm_bytes, side, s,
+                                    &pending))
       return rc;
   }
-  return MGCN_OK;
+  return launch_side_fold(pending, s);  // the bottom layer's weight-GEMM fold
 }
