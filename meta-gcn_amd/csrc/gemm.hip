@@ -20,6 +20,7 @@
 
 #include "mgcn_internal.h"
 #include "x6.h"
+#include "tn_staged.h"
 
 namespace mgcn {
 namespace {
@@ -442,105 +443,25 @@ __global__ __launch_bounds__(256) void gemm_tn_small_kernel(
 }
 
 // Staged small C for M = 32, N = 32 NT with 16-byte aligned rows (the F = 32
-// weight GEMMs of config 3, [W | Wr^T] with NT = 2): the split's rows stream
-// in 64-row chunks of float4 buffer loads (one register bank of prefetch, the
-// tail past the split reads zeros), are staged in LDS and feed
-// v_mfma_f32_32x32x2f32 from there (rows of 32 / 64 floats: conflict-free
-// operand reads); the four waves take interleaved k-steps of each chunk and
-// fold through LDS in wave order.  Same partial-slab layout as
-// gemm_tn_small_kernel.  The 4-byte-per-lane loads of that kernel leave ~6
-// dependent round trips per split at config 3 (26 us per launch).
+// weight GEMMs of config 3, [W | Wr^T] with NT = 2): tn_staged.h's split-K
+// workgroups (64-row chunks), plus the side-fold workgroups of an independent
+// job at the end of the grid.  The 4-byte-per-lane loads of
+// gemm_tn_small_kernel leave ~6 dependent round trips per split at config 3
+// (26 us per launch; this one 20 us).
 template <int NT>
 __global__ __launch_bounds__(256) void gemm_tn_staged_kernel(
     const float *__restrict__ A, int64_t lda, const float *__restrict__ B, int64_t ldb,
     int64_t K, int64_t k_per_split, float *__restrict__ partial, SideFold sf) {
+  constexpr int CK = 64;
+  __shared__ __attribute__((aligned(16))) float stage[CK * 32 + CK * 32 * NT > 4096
+                                                          ? CK * 32 + CK * 32 * NT
+                                                          : 4096];
   if (blockIdx.x >= gridDim.x - (unsigned)sf.blocks) {
-    // a side job riding in the same launch (the residual stack's bias-gradient
-    // column sums, an independent fold)
-    __shared__ float red[256];
-    side_fold_block(sf, (int)(blockIdx.x - (gridDim.x - (unsigned)sf.blocks)), red);
+    // a side job riding in the same launch (an independent fold)
+    side_fold_block(sf, (int)(blockIdx.x - (gridDim.x - (unsigned)sf.blocks)), stage);
     return;
   }
-  constexpr int CK = 64;       // rows per chunk
-  constexpr int NB = 32 * NT;  // columns of B (and C)
-  constexpr int QA = CK * 32 / 4 / 256, QB = CK * NB / 4 / 256;  // float4 per thread
-  // one allocation: the final fold reuses its first 16 KB
-  __shared__ __attribute__((aligned(16))) float stage[CK * 32 + CK * NB];
-  float(*As)[32] = reinterpret_cast<float(*)[32]>(stage);
-  float(*Bs)[NB] = reinterpret_cast<float(*)[NB]>(stage + CK * 32);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lr = lane >> 5, lc = lane & 31;
-  const int64_t kb = (int64_t)blockIdx.x * k_per_split;
-  const int64_t ke = (kb + k_per_split < K) ? kb + k_per_split : K;
-  const auto ra_ = buf_rsrc(A + kb * lda, (uint32_t)((ke - kb) * lda * 4));
-  const auto rb_ = buf_rsrc(B + kb * ldb, (uint32_t)((ke - kb) * ldb * 4));
-  u32x4 ra[QA], rb[QB];
-  auto load = [&](int64_t r0) {  // chunk at split row r0 (relative)
-#pragma unroll
-    for (int j = 0; j < QA; ++j) {
-      const int i = tid + 256 * j, row = i >> 3, c4 = i & 7;
-      ra[j] = __builtin_amdgcn_raw_buffer_load_b128(
-          ra_, (int)(((r0 + row) * lda + 4 * c4) * 4), 0, 0);
-    }
-#pragma unroll
-    for (int j = 0; j < QB; ++j) {
-      const int i = tid + 256 * j, row = i / (NB / 4), c4 = i % (NB / 4);
-      rb[j] = __builtin_amdgcn_raw_buffer_load_b128(
-          rb_, (int)(((r0 + row) * ldb + 4 * c4) * 4), 0, 0);
-    }
-  };
-  f32x16 acc[NT];
-#pragma unroll
-  for (int t = 0; t < NT; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
-  const int64_t n = ke - kb;
-  if (n > 0) load(0);
-  for (int64_t r0 = 0; r0 < n; r0 += CK) {
-    __syncthreads();  // the previous chunk's operand reads are done
-#pragma unroll
-    for (int j = 0; j < QA; ++j) {
-      const int i = tid + 256 * j;
-      *reinterpret_cast<u32x4 *>(&As[i >> 3][4 * (i & 7)]) = ra[j];
-    }
-#pragma unroll
-    for (int j = 0; j < QB; ++j) {
-      const int i = tid + 256 * j;
-      *reinterpret_cast<u32x4 *>(&Bs[i / (NB / 4)][4 * (i % (NB / 4))]) = rb[j];
-    }
-    __syncthreads();
-    if (r0 + CK < n) load(r0 + CK);  // in flight under this chunk's MFMAs
-    // wave w: k-steps w, w + 4, ... of two rows each (rows past the split are 0)
-#pragma unroll
-    for (int st = 0; st < CK / 8; ++st) {
-      const int k = 2 * (wave + 4 * st) + lr;
-      const float a = As[k][lc];
-#pragma unroll
-      for (int t = 0; t < NT; ++t)
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, Bs[k][32 * t + lc], acc[t], 0, 0, 0);
-    }
-  }
-  // fold the four waves' accumulators in wave order (4 x 16 x 64 floats =
-  // 16 KB of the staging allocation, 16 or 24 KB)
-  float(*red)[16][64] = reinterpret_cast<float(*)[16][64]>(stage);
-  float *slab = partial + (int64_t)blockIdx.x * 32 * NB;
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 16; ++r) red[wave][r][lane] = acc[t][r];
-    __syncthreads();
-    if (wave == 0) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float v = __fadd_rn(__fadd_rn(red[0][r][lane], red[1][r][lane]),
-                                  __fadd_rn(red[2][r][lane], red[3][r][lane]));
-        const int row = (r & 3) + 8 * (r >> 2) + 4 * lr;
-        slab[row * NB + 32 * t + lc] = v;
-      }
-    }
-  }
+  tn_staged_block<NT, CK>(A, lda, B, ldb, K, k_per_split, partial, (int)blockIdx.x, stage);
 }
 
 bool tn_lds(int M, int N) { return M % kTile == 0 && N % kTile == 0; }
@@ -614,17 +535,10 @@ int gemm_tn_core(int64_t K, int32_t M, int32_t N, const float *A, int64_t lda, c
   kps = (kps + 63) / 64 * 64;  // whole chunks of every variant (and whole kU groups)
   const int used = (int)((K + kps - 1) / kps);
   float *partial = static_cast<float *>(workspace);
-  // the staged kernel: at most `splits` (the workspace's count) workgroups
-  // of >= 256 rows, each split's byte offsets within 32 bits (buffer loads)
-  int64_t s2 = (K + 255) / 256;
-  if (s2 > 512) s2 = 512;
-  if (s2 > splits) s2 = splits;
-  int64_t kps2 = (K + s2 - 1) / s2;
-  kps2 = (kps2 + 63) / 64 * 64;
-  if (M == 32 && (N == 32 || N == 64) && reinterpret_cast<uintptr_t>(A) % 16 == 0 &&
-      reinterpret_cast<uintptr_t>(B) % 16 == 0 && lda % 4 == 0 && ldb % 4 == 0 &&
-      (kps2 + 64) * (lda > ldb ? lda : ldb) * 4 < (int64_t(1) << 31) && g_tn_staged) {
-    const int used2 = (int)((K + kps2 - 1) / kps2);
+  TnJob job{};
+  if (K > 0 && tn_staged_plan(K, M, N, A, lda, B, ldb, workspace, workspace_bytes, &job)) {
+    const int used2 = job.blocks;
+    const int64_t kps2 = job.kps;
     SideFold sf{};
     if (side != nullptr && side->blocks > 0) {
       sf = *side;
@@ -1665,3 +1579,27 @@ extern "C" int mgcn_gemm_bwd(int64_t M, int32_t F_in, int32_t F_out, const float
   if (epi == EPI_STORE) return MGCN_OK;
   return launch_colsum_fold(csp, grid, F_in, colsum, s);
 }
+
+namespace mgcn {
+// The staged kernel takes C = A^T B when M = 32, N = 32 / 64, rows 16-byte
+// aligned and a split's byte offsets within 32 bits: at most gemm_splits
+// (the workspace's count, K >= 64 rows each) workgroups of >= 256 rows.
+bool tn_staged_plan(int64_t K, int32_t M, int32_t N, const float *A, int64_t lda, const float *B,
+                    int64_t ldb, void *workspace, size_t workspace_bytes, TnJob *job) {
+  if (!g_tn_staged || K <= 0 || M != 32 || (N != 32 && N != 64) ||
+      reinterpret_cast<uintptr_t>(A) % 16 || reinterpret_cast<uintptr_t>(B) % 16 || lda % 4 ||
+      ldb % 4 || workspace == nullptr ||
+      workspace_bytes < mgcn_gemm_tn_workspace_bytes(K, M, N))
+    return false;
+  const int splits = gemm_splits(K, M, N);
+  int64_t s2 = (K + 255) / 256;
+  if (s2 > 512) s2 = 512;
+  if (s2 > splits) s2 = splits;
+  int64_t kps2 = (K + s2 - 1) / s2;
+  kps2 = (kps2 + 63) / 64 * 64;
+  if ((kps2 + 64) * (lda > ldb ? lda : ldb) * 4 >= (int64_t(1) << 31)) return false;
+  *job = TnJob{A, lda, B, ldb, K, kps2, static_cast<float *>(workspace),
+               (int)((K + kps2 - 1) / kps2)};
+  return true;
+}
+}  // namespace mgcn

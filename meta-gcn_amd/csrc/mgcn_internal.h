@@ -112,6 +112,21 @@ __device__ inline void side_fold_block(const SideFold &f, int b, float *red) {
   }
 }
 
+// The staged small-C GEMM C = A^T B as a job for other launches (tn_staged.h:
+// tn_staged_block over `blocks` workgroups into the split partials at
+// `partial`, folded afterwards with make_side_fold(partial, blocks, M N, ...)).
+struct TnJob {
+  const float *A;
+  int64_t lda;
+  const float *B;
+  int64_t ldb;
+  int64_t K, kps;
+  float *partial;
+  int blocks;
+};
+bool tn_staged_plan(int64_t K, int32_t M, int32_t N, const float *A, int64_t lda, const float *B,
+                    int64_t ldb, void *workspace, size_t workspace_bytes, TnJob *job);
+
 // mgcn_gemm_tn_split (accumulate = 0) with `side` folded by extra workgroups
 // of the same launch; where the staged kernel takes the shape and `defer` is
 // given, its own split-K fold is left to the caller (*defer, to ride in a

@@ -41,6 +41,7 @@
 // and the 2 x 2 N F^2 FMA flops ride under the gathers.
 
 #include "mgcn_internal.h"
+#include "tn_staged.h"
 
 namespace mgcn {
 namespace {
@@ -85,9 +86,12 @@ struct RlArgs {
   float *mda;
   int64_t ldmda;
   float *mpart;
-  // an independent fold riding in this launch: its workgroups are the last
-  // side.blocks of the grid (the weight-GEMM split-K fold of the layer above)
-  SideFold side;
+  // independent work riding in this launch, in extra workgroups after the
+  // rows' ones: the weight GEMM of the stack's layer (tn_staged.h, on the
+  // heavy-row transform launch) and up to two folds of the layer above (its
+  // GEMM's split-K partials, the lower layer's bias-gradient column sums)
+  TnJob gemm;
+  SideFold side[2];
 };
 
 __device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
@@ -103,10 +107,25 @@ constexpr int kTileLd = 2 * kRF + 4;
 template <int U, bool BWD>
 __global__ __launch_bounds__(kRBlock) void residual_layer_kernel(const RlArgs a) {
   __shared__ __attribute__((aligned(16))) float tile[kRWaves][kTileRows][kTileLd];
-  if (blockIdx.x >= gridDim.x - (unsigned)a.side.blocks) {
-    side_fold_block(a.side, (int)(blockIdx.x - (gridDim.x - (unsigned)a.side.blocks)),
-                    &tile[0][0][0]);
-    return;
+  {
+    const unsigned n_extra =
+        (unsigned)(a.gemm.blocks + a.side[0].blocks + a.side[1].blocks);
+    if (blockIdx.x >= gridDim.x - n_extra) {
+      int b = (int)(blockIdx.x - (gridDim.x - n_extra));
+      float *lds = &tile[0][0][0];  // 4352 floats >= the GEMM's 4096 / the fold's 256
+      if (b < a.gemm.blocks) {
+        tn_staged_block<2, 32>(a.gemm.A, a.gemm.lda, a.gemm.B, a.gemm.ldb, a.gemm.K, a.gemm.kps,
+                               a.gemm.partial, b, lds);
+        return;
+      }
+      b -= a.gemm.blocks;
+      if (b < a.side[0].blocks) {
+        side_fold_block(a.side[0], b, lds);
+        return;
+      }
+      side_fold_block(a.side[1], b - a.side[0].blocks, lds);
+      return;
+    }
   }
   // B operands of v_mfma_f32_16x16x4_f32 (lane l: B[k][16 cb + (l & 15)]);
   // the k-steps are permuted so that step s of lane group kk = l >> 4 is
@@ -416,8 +435,12 @@ int64_t rl_blocks(int64_t n_items, bool fused_mask) {
 
 template <bool BWD>
 int launch_rl(const RlArgs &a, hipStream_t s) {
-  if (a.n_items <= 0) return launch_side_fold(a.side, s);  // nothing to ride in
-  const int64_t blocks = rl_blocks(a.n_items, BWD && a.mmask != nullptr) + a.side.blocks;
+  if (a.n_items <= 0) {  // nothing to ride in (callers attach the GEMM only to a launch with rows)
+    if (int rc = launch_side_fold(a.side[0], s)) return rc;
+    return launch_side_fold(a.side[1], s);
+  }
+  const int64_t blocks = rl_blocks(a.n_items, BWD && a.mmask != nullptr) + a.gemm.blocks +
+                         a.side[0].blocks + a.side[1].blocks;
   hipLaunchKernelGGL((residual_layer_kernel<8, BWD>), dim3((unsigned)blocks), dim3(kRBlock), 0, s, a);
   return check_launch("residual_layer_kernel");
 }
@@ -526,7 +549,8 @@ int residual_bwd_core(int64_t n_rows, const int64_t *rowptr_t, const int32_t *co
                       const float *dA, const float *W, int64_t ldw, const float *Wr, int64_t ldwr,
                       float *dX, int64_t lddx, float *DH, int64_t lddh, const int32_t *order,
                       int64_t n_heavy, int64_t n_giant, const LowerMask *lm, hipStream_t s,
-                      int64_t *defer_parts = nullptr, const SideFold *ride = nullptr) {
+                      int64_t *defer_parts = nullptr, const SideFold *ride = nullptr,
+                      const TnJob *gemm = nullptr, bool *gemm_done = nullptr) {
   const int F = kRF;
   if (order == nullptr) n_heavy = n_giant = 0;
   bool side = false;
@@ -565,9 +589,9 @@ int residual_bwd_core(int64_t n_rows, const int64_t *rowptr_t, const int32_t *co
   a.gather = 1;
   a.items = order != nullptr ? order + n_heavy : nullptr;
   a.n_items = n_rows - n_heavy;
-  if (ride != nullptr) a.side = *ride;
+  if (ride != nullptr) a.side[0] = ride[0], a.side[1] = ride[1];
   if (int rc = launch_rl<true>(a, s)) return rc;
-  a.side = SideFold{};
+  a.side[0] = a.side[1] = SideFold{};
   int64_t parts = rl_blocks(a.n_items, lm != nullptr);
   if (n_heavy > 0) {
     if (side)
@@ -575,6 +599,10 @@ int residual_bwd_core(int64_t n_rows, const int64_t *rowptr_t, const int32_t *co
     a.gather = 0;
     a.items = order;
     a.n_items = n_heavy;
+    if (gemm != nullptr) {  // the layer's weight GEMM beside the heavy rows' transform
+      a.gemm = *gemm;
+      *gemm_done = true;
+    }
     if (lm != nullptr) a.mpart = lm->partial + parts * 2 * F;
     if (int rc = launch_rl<true>(a, s)) return rc;
     parts += rl_blocks(n_heavy, lm != nullptr);
@@ -672,9 +700,9 @@ extern "C" int mgcn_residual_stack_fwd(int64_t n_rows, int32_t F, int32_t n_laye
 
 namespace {
 // [mask partials of the top layer's pass] [dA x 2] [DH x 2] [dX of layer 0]
-// [fused-mask partials] [gemm_tn_split workspace]
+// [fused-mask partials x 2] [gemm_tn_split workspace]
 struct StackScratch {
-  size_t mpart, da, dh, dx, fpart, gemm, total;
+  size_t mpart, da, dh, dx, fpart, fpart_half, gemm, total;
   size_t nf, n2f;  // bytes of one [n, F] / [n, 2F] buffer
 };
 StackScratch stack_scratch(int64_t n_rows, int32_t F) {
@@ -687,7 +715,9 @@ StackScratch stack_scratch(int64_t n_rows, int32_t F) {
   s.dh = s.da + 2 * s.nf;
   s.dx = s.dh + 2 * s.n2f;
   s.fpart = s.dx + s.nf;
-  s.gemm = s.fpart + align_up((size_t)2 * kMaxRlParts * 2 * F * sizeof(float), 256);
+  s.fpart_half = align_up((size_t)2 * kMaxRlParts * 2 * F * sizeof(float), 256);
+  s.gemm = s.fpart + 2 * s.fpart_half;  // two buffers: a layer's partials are folded
+                                        // while the next layer writes its own
   s.total = s.gemm + align_up(mgcn_gemm_tn_workspace_bytes(n_rows, F, 2 * F), 256);
   return s;
 }
@@ -746,7 +776,10 @@ extern "C" int mgcn_residual_stack_bwd(int64_t n_rows, int32_t F, int32_t n_laye
                      (int64_t)F, DHb[top & 1] + F, (int64_t)2 * F, mpart);
   if (int rc = check_launch("residual_mask_bwd_kernel")) return rc;
   if (int rc = launch_colsum_fold(mpart, nparts, 2 * F, sums + (int64_t)top * 2 * F, s)) return rc;
-  SideFold pending{};  // the weight-GEMM fold of the layer above, riding in the next light pass
+  // folds of the layer above riding in the next layer's light-row launch:
+  // [0] its weight GEMM's split-K partials, [1] the column sums of the bias
+  // gradients its passes produced (partials double-buffered by layer parity)
+  SideFold pend[2] = {};
   for (int32_t l = top; l >= 0; --l) {
     const int c = l & 1, o = c ^ 1;
     float *dx = (l == 0 && dX0 != nullptr) ? dX0 : reinterpret_cast<float *>(ws + sc.dx);
@@ -760,16 +793,25 @@ extern "C" int mgcn_residual_stack_bwd(int64_t n_rows, int32_t F, int32_t n_laye
       lm.ldds = 2 * F;
       lm.dA = dAb[o];
       lm.ldda = F;
-      lm.partial = fpart;
+      lm.partial = fpart + (size_t)c * sc.fpart_half / sizeof(float);
       lm.colsums = sums + (int64_t)(l - 1) * 2 * F;
     }
     const bool fuse = l > 0 && g_fused_mask;
+    // [dW | dWr^T] = X_l^T [dH | dS]: on the staged GEMM's workgroups of the
+    // heavy-row transform launch where there is one, else its own launch
+    const float *xin = l == 0 ? X0 : Z + (int64_t)(l - 1) * n_rows * F;
+    const int64_t ldxin = l == 0 ? ldx : F;
+    TnJob job{};
+    const bool staged = tn_staged_plan(n_rows, F, 2 * F, xin, ldxin, DHb[c], 2 * F, ws + sc.gemm,
+                                       gemm_bytes, &job);
+    bool gemm_done = false;
     int64_t parts = 0;
     if (int rc = residual_bwd_core(n_rows, rowptr_t, col_t, eid_t, w_t, row_scale, dAb[c], W[l], F,
                                    Wr[l], F, dx, F, DHb[c], 2 * F, order, n_heavy, n_giant,
-                                   fuse ? &lm : nullptr, s, fuse ? &parts : nullptr, &pending))
+                                   fuse ? &lm : nullptr, s, fuse ? &parts : nullptr, pend,
+                                   staged ? &job : nullptr, &gemm_done))
       return rc;
-    pending = SideFold{};
+    pend[0] = pend[1] = SideFold{};
     if (l > 0 && !fuse) {  // the lower layer's mask pass as its own kernel
       hipLaunchKernelGGL(residual_mask_bwd_kernel, dim3(nparts), dim3(256), 0, s, n_rows, dx,
                          (int64_t)F, lm.masks, lm.relu1, lm.relu2, row_div, dAb[o], (int64_t)F,
@@ -777,16 +819,19 @@ extern "C" int mgcn_residual_stack_bwd(int64_t n_rows, int32_t F, int32_t n_laye
       if (int rc = check_launch("residual_mask_bwd_kernel")) return rc;
       if (int rc = launch_colsum_fold(mpart, nparts, 2 * F, lm.colsums, s)) return rc;
     }
-    // [dW | dWr^T] = X_l^T [dH | dS]; with the fused mask pass, the lower
-    // layer's bias-gradient column sums are folded in the same launch
-    const float *xin = l == 0 ? X0 : Z + (int64_t)(l - 1) * n_rows * F;
-    SideFold side{};
-    if (fuse) side = make_side_fold(lm.partial, parts, 2 * F, 2 * F, lm.colsums, 2 * F, 2 * F,
-                                    nullptr, 0);
-    if (int rc = gemm_tn_split_fold(n_rows, F, 2 * F, F, xin, l == 0 ? ldx : F, DHb[c], 2 * F,
-                                    dW[l], F, dWr[l], F, ws + sc.gemm, gemm_bytes, side, s,
-                                    &pending))
+    if (gemm_done) {
+      pend[0] = make_side_fold(job.partial, job.blocks, (int64_t)F * 2 * F, 2 * F, dW[l], F, F,
+                               dWr[l], F);
+    } else if (int rc = gemm_tn_split_fold(n_rows, F, 2 * F, F, xin, ldxin, DHb[c], 2 * F, dW[l],
+                                           F, dWr[l], F, ws + sc.gemm, gemm_bytes, SideFold{}, s,
+                                           &pend[0])) {
       return rc;
+    }
+    if (fuse)
+      pend[1] = make_side_fold(lm.partial, parts, 2 * F, 2 * F, lm.colsums, 2 * F, 2 * F,
+                               nullptr, 0);
   }
-  return launch_side_fold(pending, s);  // the bottom layer's weight-GEMM fold
+  // the bottom layer's folds: nothing left to ride in
+  if (int rc = launch_side_fold(pend[0], s)) return rc;
+  return launch_side_fold(pend[1], s);
 }
