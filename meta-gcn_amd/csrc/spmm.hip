@@ -977,8 +977,10 @@ int launch_heavy_v(const SpmmArgs &a, int vec, bool giant, hipStream_t stream) {
 // unchanged: everything after the call on `stream` waits for both launches).
 struct SideStream {
   hipStream_t stream = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;   // device-scope release (same-GPU streams)
+  hipEvent_t fork_sys = nullptr, join_sys = nullptr;  // with the system-scope fence
 };
+int g_side_fence = 0;  // mgcn_set_option("heavy_side_fence"): 1 = system-scope events
 
 int side_stream(SideStream **out) {
   static thread_local SideStream per_dev[64];  // per host thread: events never shared
@@ -988,10 +990,18 @@ int side_stream(SideStream **out) {
   SideStream &s = per_dev[dev];
   if (s.stream == nullptr) {
     MGCN_HIP_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
-    MGCN_HIP_TRY(hipEventCreateWithFlags(&s.fork, hipEventDisableTiming));
-    MGCN_HIP_TRY(hipEventCreateWithFlags(&s.join, hipEventDisableTiming));
+    // the fork / join only order two streams of one GPU: no system-scope
+    // fence (an L2 writeback for host / peer visibility) at each record
+    const unsigned fl = hipEventDisableTiming | hipEventDisableSystemFence;
+    MGCN_HIP_TRY(hipEventCreateWithFlags(&s.fork, fl));
+    MGCN_HIP_TRY(hipEventCreateWithFlags(&s.join, fl));
+    MGCN_HIP_TRY(hipEventCreateWithFlags(&s.fork_sys, hipEventDisableTiming));
+    MGCN_HIP_TRY(hipEventCreateWithFlags(&s.join_sys, hipEventDisableTiming));
   }
-  *out = &s;
+  static thread_local SideStream view[64];
+  view[dev] = s;
+  if (g_side_fence) view[dev].fork = s.fork_sys, view[dev].join = s.join_sys;
+  *out = &view[dev];
   return MGCN_OK;
 }
 
@@ -1166,6 +1176,11 @@ extern "C" int mgcn_set_option(const char *name, int value) {
   if (n == "residual_fused_mask") {
     MGCN_REQUIRE(value == 0 || value == 1, "residual_fused_mask must be 0 or 1");
     g_fused_mask = value;
+    return MGCN_OK;
+  }
+  if (n == "heavy_side_fence") {
+    MGCN_REQUIRE(value == 0 || value == 1, "heavy_side_fence must be 0 or 1");
+    g_side_fence = value;
     return MGCN_OK;
   }
   if (n == "heavy_side_stream") {
