@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define MGCN_ABI_VERSION 12
+#define MGCN_ABI_VERSION 13
 
 /* return codes */
 #define MGCN_OK 0
@@ -256,6 +256,16 @@ int mgcn_gemm_tn_split(int64_t K, int32_t M, int32_t N, int32_t N1, const float 
                        const float *B, int64_t ldb, float *C1, int64_t ldc1, float *C2t,
                        int64_t ldc2t, int accumulate, void *workspace, size_t workspace_bytes,
                        void *stream);
+
+/*
+ * C[M, N] = A[M, K] . B[K, N] for 1 <= K <= 8, N <= 128, B addressed as B[k * sbk +
+ * n * sbn] (W or W^T): the products accumulated in k order on fma.  Replaces
+ * `torch.matmul` where the contraction is a handful of features (a 1 -> F
+ * input layer, gcn_model.py:64-66; the F -> 2 projection's input gradient).
+ */
+int mgcn_gemm_small_k(int64_t M, int32_t K, int32_t N, const float *A, int64_t lda,
+                      const float *B, int64_t sbk, int64_t sbn, float *C, int64_t ldc,
+                      void *stream);
 
 /* 1 if mgcn_gemm_nn handles this (K, N): K in {32, 64, 128}, 1 <= N <= 128. */
 int mgcn_gemm_nn_supported(int32_t K, int32_t N);

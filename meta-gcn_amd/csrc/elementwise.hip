@@ -288,6 +288,81 @@ extern "C" int mgcn_relu_bwd_colsum(int64_t n_rows, int32_t F, const float *dZ, 
   return MGCN_OK;
 }
 
+namespace mgcn {
+namespace {
+// C = A . B for a handful of K (the 1 -> 32 input layer x @ [W | Wr^T] and
+// the 32 -> 2 projection's dX = dY W of config 3): one thread per 4 outputs
+// of a row, the K products accumulated in k order on fma (a BLAS's order for
+// K <= 8); HBM-bound: 4 M (K + N) bytes.  hipBLASLt spends 35-38 us on
+// these shapes at config 3, this ~8.
+constexpr int kSmallK = 8;
+constexpr int kSmallN = 128;
+__global__ __launch_bounds__(256) void gemm_small_k_kernel(int64_t M, int K, int N,
+                                                           const float *__restrict__ A,
+                                                           int64_t lda,
+                                                           const float *__restrict__ B,
+                                                           int64_t sbk, int64_t sbn,
+                                                           float *__restrict__ C, int64_t ldc) {
+  // B staged once per workgroup as [k][n] (zeros past K / N)
+  __shared__ __attribute__((aligned(16))) float Bs[kSmallK][kSmallN];
+  for (int e = threadIdx.x; e < kSmallK * kSmallN; e += 256) {
+    const int k = e / kSmallN, n = e % kSmallN;
+    Bs[k][n] = (k < K && n < N) ? B[k * sbk + n * sbn] : 0.0f;
+  }
+  __syncthreads();
+  const int nq = (N + 3) / 4;
+  const int64_t total = M * nq;
+  const bool vec = (ldc & 3) == 0 && ((uintptr_t)C & 15) == 0 && (N & 3) == 0;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * 256) {
+    const int64_t i = t / nq;
+    const int j0 = 4 * (int)(t - i * nq);
+    float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int k = 0; k < kSmallK; ++k) {
+      if (k < K) {
+        const float a = A[i * lda + k];
+        const float4 b = *reinterpret_cast<const float4 *>(&Bs[k][j0]);
+        if (k == 0) {
+          c = make_float4(__fmul_rn(a, b.x), __fmul_rn(a, b.y), __fmul_rn(a, b.z),
+                          __fmul_rn(a, b.w));
+        } else {
+          c.x = __fmaf_rn(a, b.x, c.x);
+          c.y = __fmaf_rn(a, b.y, c.y);
+          c.z = __fmaf_rn(a, b.z, c.z);
+          c.w = __fmaf_rn(a, b.w, c.w);
+        }
+      }
+    }
+    float *dst = C + i * ldc + j0;
+    if (vec) {
+      *reinterpret_cast<float4 *>(dst) = c;
+    } else {
+      const float cv[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (j0 + q < N) dst[q] = cv[q];
+    }
+  }
+}
+}  // namespace
+}  // namespace mgcn
+
+extern "C" int mgcn_gemm_small_k(int64_t M, int32_t K, int32_t N, const float *A, int64_t lda,
+                                 const float *B, int64_t sbk, int64_t sbn, float *C, int64_t ldc,
+                                 void *stream) {
+  clear_error();
+  MGCN_REQUIRE(M >= 0 && N >= 0 && K >= 1 && K <= kSmallK && N <= kSmallN,
+               "mgcn_gemm_small_k: need 1 <= K <= %d, N <= %d (K=%d, N=%d)", kSmallK, kSmallN, K,
+               N);
+  if (M == 0 || N == 0) return MGCN_OK;
+  MGCN_REQUIRE(A && B && C && lda >= K && ldc >= N, "mgcn_gemm_small_k: bad arguments");
+  const int64_t work = M * ((N + 3) / 4);
+  hipLaunchKernelGGL(gemm_small_k_kernel, dim3(grid_for(work, 256)), dim3(256), 0,
+                     as_stream(stream), M, K, N, A, lda, B, sbk, sbn, C, ldc);
+  return check_launch("gemm_small_k_kernel");
+}
+
 extern "C" int mgcn_segment_mean(int64_t n_seg, int32_t F, const int64_t *ptr, const float *x,
                                  int64_t ldx, float *out, int64_t ldo, void *stream) {
   clear_error();

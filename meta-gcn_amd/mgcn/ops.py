@@ -517,10 +517,37 @@ def gemm_bwd(x: torch.Tensor, dH: torch.Tensor, W: torch.Tensor, want_dx: bool =
     return dW, dX, colsum
 
 
+SMALL_K = 8  # mgcn_gemm_small_k: K <= 8, N <= 128
+
+
+def gemm_small_k(A: torch.Tensor, W: torch.Tensor, transpose_w: bool = False) -> torch.Tensor:
+    """A @ W (or A @ W^T) for a contraction of at most SMALL_K features
+    (``mgcn_gemm_small_k``: k-ordered fma, HBM-bound)."""
+    lib = L.load()
+    A = _contig_f32(A, "A")
+    W = W.detach().to(torch.float32)
+    dev = L.require_device(A, W)
+    K = A.size(1)
+    N = W.size(0) if transpose_w else W.size(1)
+    if (W.size(1) if transpose_w else W.size(0)) != K:
+        raise ValueError(f"gemm_small_k: A {tuple(A.shape)}, W {tuple(W.shape)}")
+    sbk, sbn = (W.stride(1), W.stride(0)) if transpose_w else (W.stride(0), W.stride(1))
+    C = torch.empty(A.size(0), N, dtype=torch.float32, device=dev)
+    with L.device_guard(dev):
+        rc = lib.mgcn_gemm_small_k(A.size(0), K, N, L.ptr(A), A.stride(0), L.ptr(W), sbk, sbn,
+                                   L.ptr(C), C.stride(0), L.stream_of(dev))
+    L.check(rc, "mgcn_gemm_small_k")
+    return C
+
+
 def _mm(x: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
-    """x @ W on libmgcn when the shape is supported, else hipBLASLt."""
+    """x @ W on libmgcn (MFMA for K in {32, 64, 128}, the small-K kernel for
+    K <= 8), else hipBLASLt."""
     if gemm_nn_supported(W.size(0), W.size(1)):
         return gemm_nn(x, W)[0]
+    if 1 <= W.size(0) <= SMALL_K and W.size(1) <= 128 and x.dim() == 2 and \
+            x.dtype == torch.float32:
+        return gemm_small_k(x, W)
     return torch.matmul(x, W.detach())
 
 
@@ -528,6 +555,9 @@ def _mm_t(dH: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
     """dH @ W^T."""
     if gemm_nn_supported(W.size(1), W.size(0)):
         return gemm_nn(dH, W, transpose_w=True)[0]
+    if 1 <= W.size(1) <= SMALL_K and W.size(0) <= 128 and dH.dim() == 2 and \
+            dH.dtype == torch.float32:
+        return gemm_small_k(dH, W, transpose_w=True)
     return torch.matmul(dH, W.detach().t())
 
 

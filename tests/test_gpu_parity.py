@@ -747,3 +747,25 @@ def test_int64_offsets_beyond_2_31_elements(cuda):
             for k in range(e - b):
                 acc = (acc + (xs[k] * ww[k]).astype(np.float32)).astype(np.float32)
             np.testing.assert_array_equal(out[r].cpu().numpy(), acc)
+
+
+@pytest.mark.parametrize("M,K,N,tw", [(286_214, 1, 64, False), (286_214, 2, 32, True),
+                                      (1000, 8, 7, False), (3, 5, 128, True), (7, 3, 5, True),
+                                      (0, 2, 4, False)])
+def test_gemm_small_k_matches_fp64(cuda, M, K, N, tw):
+    """mgcn_gemm_small_k (the 1 -> F input layer, the F -> 2 projection's dX):
+    within fp32 rounding of fp64 (k-ordered fma); K = 1 is the single product
+    bit for bit."""
+    from mgcn.ops import gemm_small_k
+    g = torch.Generator(device=cuda).manual_seed(M + K + N)
+    A = torch.randn(M, K, device=cuda, generator=g)
+    W = torch.randn(N, K, device=cuda, generator=g) if tw else \
+        torch.randn(K, N, device=cuda, generator=g)
+    C = gemm_small_k(A, W, transpose_w=tw)
+    Wm = W.t() if tw else W
+    ref = A.double() @ Wm.double()
+    bound = A.double().abs() @ Wm.double().abs()
+    assert C.shape == (M, N)
+    assert ((C.double() - ref).abs() <= 2e-7 * K * bound + 1e-30).all()
+    if K == 1:
+        assert torch.equal(C, A * Wm)
