@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define MGCN_ABI_VERSION 13
+#define MGCN_ABI_VERSION 14
 
 /* return codes */
 #define MGCN_OK 0
@@ -401,6 +401,27 @@ int mgcn_spmm_xw_bwd(int64_t n_rows, int64_t n_cols, int32_t F_in, int32_t F_out
 int mgcn_edge_weight_grad(int64_t n_rows, int32_t F, const int64_t *rowptr, const int32_t *col,
                           const float *H, int64_t ldh, const float *dY, int64_t lddy,
                           const uint32_t *win_mask, float *dw, void *stream);
+
+/* ------------------------------------------------------- pooling support */
+
+/* Bytes of scratch mgcn_edge_merge_greedy needs. */
+size_t mgcn_edge_merge_workspace_bytes(int64_t n_nodes, int64_t n_edges);
+
+/*
+ * EdgePooling's edge contraction (PyG 1.3 EdgePooling.__merge_edges__, the
+ * pool of reference kernel/edge_pool.py:19,42): walking the edges in `order`
+ * (edge ids by descending score), an edge whose endpoints are both unmatched
+ * is taken; taken edges become clusters 0..n_chosen-1 in walk order, the
+ * unmatched nodes the clusters after them in ascending node order.  Built on
+ * the device as the equivalent locally-dominant matching (same result bit for
+ * bit).  src / dst: the two rows of edge_index (int64, E each); order: a
+ * permutation of 0..E-1.  Outputs (device): cluster[N], chosen[0..n_chosen)
+ * (edge ids, walk order; E entries of room), counts = {n_chosen, n_clusters}.
+ * N, E < 2^31 - 1.
+ */
+int mgcn_edge_merge_greedy(int64_t n_nodes, int64_t n_edges, const int64_t *src, const int64_t *dst,
+                           const int64_t *order, void *workspace, size_t workspace_bytes,
+                           int64_t *cluster, int64_t *chosen, int64_t *counts, void *stream);
 
 /* ----------------------------------------------------------- elementwise */
 

@@ -1,0 +1,191 @@
+// EdgePooling's edge contraction on the device (gfx950).
+//
+// reference kernel/edge_pool.py:4,19,42 pools with PyG 1.3's EdgePooling,
+// whose __merge_edges__ walks the edges by descending score and contracts an
+// edge when both endpoints are still unmatched (a sequential greedy
+// matching), numbering the clusters in the order the edges are taken and the
+// nodes left over after them in ascending node order.
+//
+// With distinct priorities (an edge's position p in the score order) the
+// greedy matching is the unique locally-dominant matching: an edge is in it
+// iff, once the edges matched before it are removed, no available edge at
+// either endpoint comes earlier.  So it is built in rounds, every available
+// edge at once: each free node takes the earliest available edge incident to
+// it (atomicMin over positions), and an edge that both its endpoints took is
+// matched (a self loop needs its one endpoint).  The earliest available edge
+// of the whole graph always matches, so every round matches at least one edge
+// and the loop ends; a round leaves the same matched set the sequential walk
+// reaches, so the result is the sequential one bit for bit.
+//
+// Then the cluster ids: chosen edges numbered in position order (an exclusive
+// scan of the per-position flags), the free nodes after them in node order
+// (a scan of the free flags).
+//
+// One 1024-thread workgroup (rounds are separated by workgroup barriers; the
+// pooled graphs are mini-batches of small graphs).  Integer work over E and N,
+// latency-bound per round: ~(2E + 2N) x 4 B of workspace traffic per round.
+
+#include "mgcn_internal.h"
+
+namespace mgcn {
+namespace {
+
+constexpr int kMgThreads = 1024;
+constexpr int kMgWaves = kMgThreads / 64;
+
+// Workspace words shared between the workgroup's waves go through the L2
+// (agent-scope relaxed atomics: the atomicMin results are read back without
+// trusting a line the CU's L1 may hold from an earlier access); the barriers
+// order the phases.
+__device__ __forceinline__ int ld(const int32_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st(int32_t *p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// exclusive scan of v over the workgroup; returns the prefix, *total = sum
+__device__ int block_exclusive_scan(int v, int *lds_wave, int *total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) lds_wave[wave] = x;
+  __syncthreads();
+  if (wave == 0) {
+    int w = lane < kMgWaves ? lds_wave[lane] : 0;
+#pragma unroll
+    for (int off = 1; off < kMgWaves; off <<= 1) {
+      const int y = __shfl_up(w, off, 64);
+      if (lane >= off) w += y;
+    }
+    if (lane < kMgWaves) lds_wave[kMgWaves + lane] = w;  // inclusive wave totals
+  }
+  __syncthreads();
+  const int before = wave == 0 ? 0 : lds_wave[kMgWaves + wave - 1];
+  *total = lds_wave[2 * kMgWaves - 1];
+  __syncthreads();  // lds_wave is reused by the next call
+  return before + x - v;
+}
+
+__global__ __launch_bounds__(kMgThreads) void edge_merge_kernel(
+    int32_t N, int32_t E, const int64_t *__restrict__ src, const int64_t *__restrict__ dst,
+    const int64_t *__restrict__ order, int32_t *__restrict__ rank, int32_t *__restrict__ flag,
+    int32_t *__restrict__ best, int32_t *__restrict__ freen, int64_t *__restrict__ cluster,
+    int64_t *__restrict__ chosen, int64_t *__restrict__ counts) {
+  __shared__ int lds_wave[2 * kMgWaves];
+  __shared__ int matched[3];  // round r writes slot r % 3, resets slot (r + 1) % 3
+  const int tid = threadIdx.x;
+  for (int p = tid; p < E; p += kMgThreads) {
+    st(&rank[(int32_t)order[p]], p);
+    st(&flag[p], 0);
+  }
+  for (int u = tid; u < N; u += kMgThreads) st(&freen[u], 1);
+  if (tid < 3) matched[tid] = 0;
+  __syncthreads();
+
+  for (int round = 0;; ++round) {
+    for (int u = tid; u < N; u += kMgThreads)
+      if (ld(&freen[u])) st(&best[u], INT32_MAX);
+    if (tid == 0) matched[(round + 1) % 3] = 0;  // last read in round - 2
+    __syncthreads();
+    for (int e = tid; e < E; e += kMgThreads) {
+      const int32_t s = (int32_t)src[e], t = (int32_t)dst[e];
+      if (ld(&freen[s]) && ld(&freen[t])) {
+        const int r = ld(&rank[e]);
+        atomicMin(&best[s], r);
+        if (t != s) atomicMin(&best[t], r);
+      }
+    }
+    __syncthreads();
+    // best[] is final for this round: an edge matches where both its
+    // endpoints chose it; its endpoints leave the free set after a barrier
+    int any = 0;
+    for (int e = tid; e < E; e += kMgThreads) {
+      const int32_t s = (int32_t)src[e], t = (int32_t)dst[e];
+      const int r = ld(&rank[e]);
+      if (ld(&freen[s]) && ld(&freen[t]) && ld(&best[s]) == r && ld(&best[t]) == r) {
+        st(&flag[r], 1);
+        any = 1;
+      }
+    }
+    __syncthreads();
+    for (int e = tid; e < E; e += kMgThreads)
+      if (ld(&flag[ld(&rank[e])])) {
+        st(&freen[(int32_t)src[e]], 0);
+        st(&freen[(int32_t)dst[e]], 0);
+      }
+    if (any) matched[round % 3] = 1;  // plain LDS store: every writer writes 1
+    __syncthreads();
+    if (!matched[round % 3]) break;
+  }
+
+  // cluster ids: chosen edges in position order, then free nodes in node order
+  int base = 0;
+  for (int p0 = 0; p0 < E; p0 += kMgThreads) {
+    const int p = p0 + tid;
+    const int f = p < E ? ld(&flag[p]) : 0;
+    int tot;
+    const int id = base + block_exclusive_scan(f, lds_wave, &tot);
+    if (f) {
+      const int64_t e = order[p];
+      chosen[id] = e;
+      cluster[src[e]] = id;
+      cluster[dst[e]] = id;
+    }
+    base += tot;
+  }
+  const int n_chosen = base;
+  for (int u0 = 0; u0 < N; u0 += kMgThreads) {
+    const int u = u0 + tid;
+    const int f = u < N ? ld(&freen[u]) : 0;
+    int tot;
+    const int id = base + block_exclusive_scan(f, lds_wave, &tot);
+    if (f) cluster[u] = id;
+    base += tot;
+  }
+  if (tid == 0) {
+    counts[0] = n_chosen;
+    counts[1] = base;
+  }
+}
+
+}  // namespace
+}  // namespace mgcn
+
+using namespace mgcn;
+
+extern "C" size_t mgcn_edge_merge_workspace_bytes(int64_t n_nodes, int64_t n_edges) {
+  const int64_t n = n_nodes > 0 ? n_nodes : 0, e = n_edges > 0 ? n_edges : 0;
+  return align_up((size_t)(2 * e + 2 * n) * 4 + 4, 256);
+}
+
+extern "C" int mgcn_edge_merge_greedy(int64_t n_nodes, int64_t n_edges, const int64_t *src,
+                                      const int64_t *dst, const int64_t *order, void *workspace,
+                                      size_t workspace_bytes, int64_t *cluster, int64_t *chosen,
+                                      int64_t *counts, void *stream) {
+  clear_error();
+  MGCN_REQUIRE(n_nodes >= 0 && n_edges >= 0 && n_nodes < INT32_MAX && n_edges < INT32_MAX,
+               "mgcn_edge_merge_greedy: need 0 <= n_nodes, n_edges < 2^31 - 1");
+  MGCN_REQUIRE(counts != nullptr, "mgcn_edge_merge_greedy: null counts");
+  MGCN_REQUIRE(n_edges == 0 || (src && dst && order && chosen), "mgcn_edge_merge_greedy: null edges");
+  MGCN_REQUIRE(n_nodes == 0 || cluster != nullptr, "mgcn_edge_merge_greedy: null cluster");
+  MGCN_REQUIRE(n_edges == 0 || n_nodes > 0, "mgcn_edge_merge_greedy: edges without nodes");
+  const size_t need = mgcn_edge_merge_workspace_bytes(n_nodes, n_edges);
+  if (workspace == nullptr || workspace_bytes < need) {
+    set_error("mgcn_edge_merge_greedy: workspace %zu < %zu", workspace_bytes, need);
+    return MGCN_EWORKSPACE;
+  }
+  hipStream_t s = as_stream(stream);
+  int32_t *rank = static_cast<int32_t *>(workspace);
+  int32_t *flag = rank + n_edges;
+  int32_t *best = flag + n_edges;
+  int32_t *freen = best + n_nodes;
+  hipLaunchKernelGGL(edge_merge_kernel, dim3(1), dim3(kMgThreads), 0, s, (int32_t)n_nodes,
+                     (int32_t)n_edges, src, dst, order, rank, flag, best, freen, cluster, chosen,
+                     counts);
+  return check_launch("edge_merge_kernel");
+}

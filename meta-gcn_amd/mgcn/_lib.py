@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmgcn.so")
 
 # constants mirrored from include/mgcn.h
-ABI_VERSION = 13
+ABI_VERSION = 14
 OK, EINVAL, EINDEX, EHIP, EWORKSPACE = 0, 1, 2, 3, 4
 REDUCE_SUM, REDUCE_MEAN, REDUCE_MAX = 0, 1, 2
 NORM_NONE, NORM_SM, NORM_RW = 0, 1, 2
@@ -66,6 +66,8 @@ SIGNATURES = {
     "mgcn_gemm_bwd": (_int, [_i64, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _int,
                              _vp, _i64, _vp, _vp, _vp, _vp, _sz, _vp]),
     "mgcn_edge_weight_grad": (_int, [_i64, _i32, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp]),
+    "mgcn_edge_merge_workspace_bytes": (_sz, [_i64, _i64]),
+    "mgcn_edge_merge_greedy": (_int, [_i64, _i64, _vp, _vp, _vp, _vp, _sz, _vp, _vp, _vp, _vp]),
     "mgcn_spmm_xw_supported": (_int, [_i32, _i32, _int]),
     "mgcn_spmm_xw_fwd": (_int, [_i64, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp,
                                 _i64, _int, _int, _vp, _vp, _i64, _vp]),

@@ -264,6 +264,33 @@ def merge_edges_greedy(edge_index_np: np.ndarray, order: np.ndarray, num_nodes: 
     return cluster, np.asarray(chosen, dtype=np.int64), i + rest.size
 
 
+def edge_merge_greedy(edge_index: torch.Tensor, order: torch.Tensor, num_nodes: int):
+    """:func:`merge_edges_greedy` on the device (``mgcn_edge_merge_greedy``:
+    the same matching and numbering, built as the locally-dominant matching
+    in rounds).  Returns (cluster [N] int64, chosen edge ids int64, number of
+    clusters); one host sync for the two counts."""
+    lib = L.load()
+    dev = L.require_device(edge_index, order)
+    ei = edge_index.to(torch.int64).contiguous()
+    order = order.to(torch.int64).contiguous()
+    E = ei.size(1)
+    N = int(num_nodes)
+    if order.numel() != E:
+        raise ValueError(f"edge_merge_greedy: order has {order.numel()} entries for {E} edges")
+    cluster = torch.empty(N, dtype=torch.int64, device=dev)
+    chosen = torch.empty(max(E, 1), dtype=torch.int64, device=dev)
+    counts = torch.empty(2, dtype=torch.int64, device=dev)
+    ws_bytes = int(lib.mgcn_edge_merge_workspace_bytes(N, E))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    with L.device_guard(dev):
+        rc = lib.mgcn_edge_merge_greedy(N, E, L.ptr(ei[0]), L.ptr(ei[1]), L.ptr(order),
+                                        L.ptr(ws), ws_bytes, L.ptr(cluster), L.ptr(chosen),
+                                        L.ptr(counts), L.stream_of(dev))
+    L.check(rc, "mgcn_edge_merge_greedy")
+    n_chosen, C = (int(v) for v in counts.tolist())
+    return cluster, chosen[:n_chosen], C
+
+
 class EdgePooling(torch.nn.Module):
     """PyG 1.3 EdgePooling(in_channels, edge_score_method=None, dropout=0,
     add_to_edge_score=0.5); forward(x, edge_index, batch) returns
@@ -308,10 +335,7 @@ class EdgePooling(torch.nn.Module):
     def merge_edges(self, x, edge_index, batch, edge_score):
         N = x.size(0)
         order = torch.argsort(edge_score.detach(), descending=True, stable=True)
-        cluster_np, chosen_np, C = merge_edges_greedy(edge_index.cpu().numpy(),
-                                                      order.cpu().numpy(), N)
-        cluster = torch.from_numpy(cluster_np).to(x.device)
-        chosen = torch.from_numpy(chosen_np).to(x.device)
+        cluster, chosen, C = edge_merge_greedy(edge_index, order, N)
         new_x = scatter_('add', x, cluster, dim_size=C)
         new_edge_score = edge_score[chosen]
         if C > chosen.numel():
@@ -645,4 +669,4 @@ __all__ = ["TopKPooling", "SAGPooling", "EdgePooling", "HardPooling", "GlobalAtt
            "Set2Set", "DenseSAGEConv", "dense_diff_pool", "global_sort_pool", "graclus",
            "max_pool", "max_pool_x", "softmax", "topk", "filter_adj", "to_dense_batch",
            "consecutive_cluster", "pool_edge", "scatter_max_arg", "coalesce",
-           "merge_edges_greedy"]
+           "merge_edges_greedy", "edge_merge_greedy"]

@@ -198,6 +198,51 @@ def test_edge_pooling_matches_pyg_merge(cuda):
     assert ux.shape == x.shape and torch.equal(ub.cpu(), batch)
 
 
+@pytest.mark.parametrize("n,E,loops,dups", [
+    (1, 0, False, False), (5, 0, False, False), (1, 1, True, False), (12, 30, True, True),
+    (700, 2500, True, True), (3000, 1500, False, False), (5000, 40000, True, True),
+    (20000, 60000, False, True)])
+def test_edge_merge_greedy_device_matches_pyg_walk(cuda, n, E, loops, dups):
+    """mgcn_edge_merge_greedy (device, locally-dominant rounds) against PyG
+    1.3's sequential set-based walk: the same cluster of every node, the same
+    contracted edges in the same order, the same cluster count -- with self
+    loops, duplicate / reversed edges, isolated nodes and more nodes and
+    edges than one 1024-thread scan block."""
+    from mgcn.pool import edge_merge_greedy
+    rng = np.random.default_rng(n * 7 + E)
+    s = rng.integers(0, n, E)
+    d = rng.integers(0, n, E)
+    if loops and E:
+        k = max(1, E // 10)
+        d[:k] = s[:k]
+    if dups and E > 4:
+        k = E // 5
+        s[-k:], d[-k:] = d[:k], s[:k]  # reversed copies of the first edges
+    ei = torch.from_numpy(np.stack([s, d]).astype(np.int64))
+    order = torch.from_numpy(rng.permutation(E).astype(np.int64))
+    nodes_remaining = set(range(n))
+    cluster = torch.empty(n, dtype=torch.long)
+    i, chosen = 0, []
+    for e in order.tolist():
+        a, b = int(s[e]), int(d[e])
+        if a not in nodes_remaining or b not in nodes_remaining:
+            continue
+        chosen.append(e)
+        cluster[a] = i
+        nodes_remaining.remove(a)
+        if a != b:
+            cluster[b] = i
+            nodes_remaining.remove(b)
+        i += 1
+    for node in sorted(nodes_remaining):
+        cluster[node] = i
+        i += 1
+    c_dev, ch_dev, C = edge_merge_greedy(ei.to(cuda), order.to(cuda), n)
+    assert C == i
+    assert torch.equal(c_dev.cpu(), cluster)
+    assert ch_dev.cpu().tolist() == chosen
+
+
 def test_graclus_is_a_maximal_matching_and_max_pool(cuda):
     from mgcn.kernel.data import Batch
     from mgcn.pool import graclus, max_pool
