@@ -59,7 +59,8 @@ def config3(args, dev):
     model = GCNModel(1, [32] * 12, 2, non_linear='relu', non_linear_layer_wise='relu',
                      residual_hop=1, dropout=0.0, final_type='proj', pred_on='node',
                      deg_norm='sm', aggr='add', bias=False).to(dev)
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=5e-4)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=5e-4,
+                           **({"fused": True} if args.adam == "fused" else {}))
     from mgcn.botnet import CrossEntropyLoss
     crit = CrossEntropyLoss()
 
@@ -110,6 +111,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--aggr", default="add,mean,max", help="config4: aggregators to run")
+    ap.add_argument("--adam", choices=["default", "fused"], default="default",
+                    help="config3: torch Adam implementation (default = foreach)")
     ap.add_argument("--opt", action="append", default=[],
                     help="libmgcn option name=value (mgcn_set_option), repeatable")
     args = ap.parse_args()
