@@ -199,6 +199,14 @@ def launch_bytes(name: str, rows: int, edges: int, F: int):
         return b, fl
     if name.startswith("spmm"):
         return spmm_bytes(rows, edges, F), 0.0
+    if name.startswith("residual_layer"):
+        # residual.hip (F = 32 whatever the bench width): the SpMM bytes plus
+        # the row's own X and its Z / dX out, and the two ReLU mask words
+        Fr = 32
+        return (8 * (rows + 1) + edges * (8 + 4 * Fr) + 8 * rows * Fr + 8 * rows,
+                4.0 * rows * Fr * Fr)
+    if name.startswith("residual_stack"):
+        return None, None  # one launch runs a whole run of layers: no per-launch count
     if name == "gemm_bwd":        # dW and dX: X, dH read, dX + mask
         return (12 * F + 16) * rows, 4.0 * rows * F * F
     if name == "gemm_bwd_dw":     # dW alone: X (or Z), dH read
@@ -412,9 +420,15 @@ def main():
             bytes_ = flops = 0.0
             for r, e in s_.pop("sizes"):
                 b, fl = launch_bytes(name, r or 0, e or 0, F)
+                if b is None:
+                    bytes_ = flops = None
+                    break
                 bytes_ += b
                 flops += fl
             t = s_["total_ms"] * 1e-3
+            if bytes_ is None:
+                kern[name] = dict(s_, bytes=None, gbs=None, flop=None, tflops=None)
+                continue
             kern[name] = dict(s_, bytes=bytes_ / s_["launches"], gbs=bytes_ / t / 1e9,
                               flop=flops / s_["launches"], tflops=flops / t / 1e12)
         dom = max((k for k in kern if k.startswith("spmm")), key=lambda k: kern[k]["total_ms"])

@@ -24,6 +24,12 @@
 // One 1024-thread workgroup (rounds are separated by workgroup barriers; the
 // pooled graphs are mini-batches of small graphs).  Integer work over E and N,
 // latency-bound per round: ~(2E + 2N) x 4 B of workspace traffic per round.
+// Rounds: every round matches at least the globally earliest available edge,
+// so at most min(E, N) rounds; the worst case is a long monotone priority
+// chain (a path whose scores rise along it matches two edges from its ends
+// per round: ~N / 4 rounds), the typical TU mini-batch takes a handful.
+// Inputs are validated on the device (endpoints in [0, N), order a
+// permutation) before any indexed write.
 
 #include "mgcn_internal.h"
 
@@ -79,6 +85,19 @@ __global__ __launch_bounds__(kMgThreads) void edge_merge_kernel(
   __shared__ int lds_wave[2 * kMgWaves];
   __shared__ int matched[3];  // round r writes slot r % 3, resets slot (r + 1) % 3
   const int tid = threadIdx.x;
+  // malformed input (an endpoint outside [0, N), an order that is not a
+  // permutation of [0, E)) ends the kernel before any indexed write:
+  // counts = {-1, -1}, the host raises
+  int bad = 0;
+  for (int e = tid; e < E; e += kMgThreads) {
+    const int64_t s = src[e], t = dst[e], o = order[e];
+    bad |= (s < 0) | (s >= N) | (t < 0) | (t >= N) | (o < 0) | (o >= E);
+    st(&rank[e], -1);
+  }
+  if (__syncthreads_or(bad)) {
+    if (tid == 0) counts[0] = counts[1] = -1;
+    return;
+  }
   for (int p = tid; p < E; p += kMgThreads) {
     st(&rank[(int32_t)order[p]], p);
     st(&flag[p], 0);
@@ -86,6 +105,11 @@ __global__ __launch_bounds__(kMgThreads) void edge_merge_kernel(
   for (int u = tid; u < N; u += kMgThreads) st(&freen[u], 1);
   if (tid < 3) matched[tid] = 0;
   __syncthreads();
+  for (int e = tid; e < E; e += kMgThreads) bad |= ld(&rank[e]) < 0;  // a repeated position
+  if (__syncthreads_or(bad)) {
+    if (tid == 0) counts[0] = counts[1] = -1;
+    return;
+  }
 
   for (int round = 0;; ++round) {
     for (int u = tid; u < N; u += kMgThreads)

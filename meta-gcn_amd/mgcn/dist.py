@@ -253,6 +253,13 @@ def build_shard(edge_index: torch.Tensor, num_nodes: int, deg_norm="sm", deg=Non
     ``edge_index`` (and ``deg`` / ``edge_weight``) is the full graph on every
     rank; only the rank's own edges are sorted."""
     backend = backend or HipBackend()
+    if torch.is_grad_enabled() and any(t is not None and t.requires_grad
+                                       for t in (edge_weight, deg)):
+        # the shard's norms are built outside autograd (once per graph); the
+        # single-device path (GraphPlan.norm) is the differentiable one
+        raise NotImplementedError("build_shard: edge_weight / deg requiring grad is not supported "
+                                  "on the sharded path (detach them, or use the single-device "
+                                  "modules)")
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     if device is not None:

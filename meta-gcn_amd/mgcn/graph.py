@@ -194,7 +194,8 @@ class GraphPlan:
         plain message weight, PyG GraphConv/SAGEConv).
         """
         code = L.NORM_CODES[method]
-        if edge_weight is not None:
+        if edge_weight is not None or code == L.NORM_NONE:
+            # unnormalised: degnorm_const never reads deg (gcn_base_models.py:209-211)
             deg = None
         if torch.is_grad_enabled() and any(t is not None and t.requires_grad
                                            for t in (edge_weight, deg)):

@@ -27,7 +27,6 @@ from __future__ import annotations
 
 from collections import namedtuple
 
-import numpy as np
 import torch
 import torch.nn.functional as F
 from torch.nn import Parameter
@@ -237,37 +236,13 @@ UnpoolDescription = namedtuple("UnpoolDescription",
                                ["edge_index", "cluster", "batch", "new_edge_score"])
 
 
-def merge_edges_greedy(edge_index_np: np.ndarray, order: np.ndarray, num_nodes: int):
-    """PyG 1.3 EdgePooling.__merge_edges__ matching: walk edges by descending
-    score, contract an edge when both endpoints are still free; the free
-    nodes left over become singleton clusters in ascending node order (the
-    iteration order of PyG's ``set(range(N))``).  Returns (cluster [N],
-    chosen edge ids, number of clusters)."""
-    free = np.ones(num_nodes, dtype=bool)
-    cluster = np.empty(num_nodes, dtype=np.int64)
-    chosen = []
-    i = 0
-    src, dst = edge_index_np[0], edge_index_np[1]
-    for e in order.tolist():
-        s, t = int(src[e]), int(dst[e])
-        if not free[s] or not free[t]:
-            continue
-        chosen.append(e)
-        cluster[s] = i
-        free[s] = False
-        if s != t:
-            cluster[t] = i
-            free[t] = False
-        i += 1
-    rest = np.nonzero(free)[0]
-    cluster[rest] = np.arange(i, i + rest.size)
-    return cluster, np.asarray(chosen, dtype=np.int64), i + rest.size
-
-
 def edge_merge_greedy(edge_index: torch.Tensor, order: torch.Tensor, num_nodes: int):
-    """:func:`merge_edges_greedy` on the device (``mgcn_edge_merge_greedy``:
-    the same matching and numbering, built as the locally-dominant matching
-    in rounds).  Returns (cluster [N] int64, chosen edge ids int64, number of
+    """PyG 1.3 EdgePooling.__merge_edges__ matching on the device
+    (``mgcn_edge_merge_greedy``): PyG walks the edges by descending score and
+    contracts an edge when both endpoints are still free, the free nodes left
+    over becoming singleton clusters in ascending node order; the same
+    matching and numbering is built here as the locally-dominant matching in
+    rounds.  Returns (cluster [N] int64, chosen edge ids int64, number of
     clusters); one host sync for the two counts."""
     lib = L.load()
     dev = L.require_device(edge_index, order)
@@ -288,6 +263,9 @@ def edge_merge_greedy(edge_index: torch.Tensor, order: torch.Tensor, num_nodes: 
                                         L.ptr(counts), L.stream_of(dev))
     L.check(rc, "mgcn_edge_merge_greedy")
     n_chosen, C = (int(v) for v in counts.tolist())
+    if n_chosen < 0:
+        raise IndexError(f"edge_merge_greedy: edge_index outside [0, {N}) or order not a "
+                         f"permutation of [0, {E})")
     return cluster, chosen[:n_chosen], C
 
 
@@ -669,4 +647,4 @@ __all__ = ["TopKPooling", "SAGPooling", "EdgePooling", "HardPooling", "GlobalAtt
            "Set2Set", "DenseSAGEConv", "dense_diff_pool", "global_sort_pool", "graclus",
            "max_pool", "max_pool_x", "softmax", "topk", "filter_adj", "to_dense_batch",
            "consecutive_cluster", "pool_edge", "scatter_max_arg", "coalesce",
-           "merge_edges_greedy", "edge_merge_greedy"]
+           "edge_merge_greedy"]

@@ -33,7 +33,7 @@ from torch import nn
 from torch.nn import Parameter
 
 from .graph import cache_key, plan_for
-from .models import glorot, zeros
+from .models import Linear, glorot, zeros
 from .ops import aggregate_plan, gcn_layer, linear, scatter_
 
 
@@ -263,7 +263,7 @@ class GraphConv(nn.Module):
         self.out_channels = out_channels
         self.aggr = aggr
         self.weight = Parameter(torch.Tensor(in_channels, out_channels))
-        self.lin = torch.nn.Linear(in_channels, out_channels, bias=bias)
+        self.lin = Linear(in_channels, out_channels, bias=bias)  # libmgcn GEMMs, nn.Linear state_dict
         self.reset_parameters()
 
     def reset_parameters(self):
@@ -313,7 +313,7 @@ class JumpingKnowledge(torch.nn.Module):
             assert channels is not None and num_layers is not None
             self.lstm = torch.nn.LSTM(channels, (num_layers * channels) // 2, bidirectional=True,
                                       batch_first=True)
-            self.att = torch.nn.Linear(2 * ((num_layers * channels) // 2), 1)
+            self.att = torch.nn.Linear(2 * ((num_layers * channels) // 2), 1)  # on 3-D LSTM output
         self.reset_parameters()
 
     def reset_parameters(self):

@@ -1,5 +1,6 @@
 """Phase timing of the heavy-row SpMM kernel (workgroup 0) from a library built
-with -DMGCN_HEAVY_PROFILE (`make -C meta-gcn_amd/csrc prof`): per batch, the
+with -DMGCN_HEAVY_PROFILE (`make -C meta-gcn_amd/csrc prof`, a separate
+libmgcn_prof.so loaded through MGCN_LIB): per batch, the
 clock64 span of the fold wave's and the producer waves' work and the barrier
 wait, on star graphs (one destination, D sources)."""
 import ctypes
@@ -9,6 +10,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "meta-gcn_amd")]
+os.environ.setdefault("MGCN_LIB", os.path.join(ROOT, "meta-gcn_amd", "mgcn", "libmgcn_prof.so"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 

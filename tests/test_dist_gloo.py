@@ -157,3 +157,17 @@ def test_partition_balances_edges():
     rp = torch.tensor([0, 10, 10, 10, 50, 51, 60, 100])
     b = partition_nodes(rp, 3)
     assert b[0] == 0 and b[-1] == 7 and all(x <= y for x, y in zip(b, b[1:]))
+
+
+def test_build_shard_rejects_differentiable_norm_inputs():
+    """The sharded path builds its norms once, outside autograd: an
+    edge_weight / deg that requires grad raises instead of silently getting
+    no gradient (the single-device modules are the differentiable path)."""
+    import pytest
+    from mgcn.dist import build_shard
+    ei = torch.tensor([[0, 1, 2, 0, 1, 2], [1, 2, 0, 0, 1, 2]])
+    ew = torch.ones(6, requires_grad=True)
+    with pytest.raises(NotImplementedError):
+        build_shard(ei, 3, "sm", edge_weight=ew)
+    with pytest.raises(NotImplementedError):
+        build_shard(ei, 3, "sm", deg=torch.ones(3, requires_grad=True))

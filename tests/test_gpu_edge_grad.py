@@ -180,3 +180,24 @@ def test_stacks_with_edge_weight_grad_run_layer_by_layer(cuda):
     e3 = ew.clone().requires_grad_(True)
     conv(x, ei, e3).sum().backward()
     assert e3.grad is not None and torch.isfinite(e3.grad).all() and e3.grad.abs().sum() > 0
+
+
+def test_unnormalised_layer_ignores_deg_requiring_grad(cuda, oracle):
+    """deg_norm=None never reads deg (gcn_base_models.py:209-211): a deg that
+    requires grad is ignored (no gradient, no error) and the layer is the
+    plain sum bit for bit (W = I)."""
+    from mgcn.models import NodeModelAdditive
+    rng = np.random.default_rng(5)
+    N, F = 300, 16
+    s, d = rng.integers(0, N, 2000), rng.integers(0, N, 2000)
+    ei = np.stack([np.concatenate([s, np.arange(N)]), np.concatenate([d, np.arange(N)])])
+    x = rng.standard_normal((N, F)).astype(np.float32)
+    m = NodeModelAdditive(F, F, deg_norm=None, aggr='add', bias=False).to(cuda)
+    with torch.no_grad():
+        m.weight_node.copy_(torch.eye(F))
+    deg = torch.rand(N, device=cuda).add_(1.0).requires_grad_(True)
+    y = m(_t(x, cuda), _t(ei, cuda), deg=deg)
+    y.sum().backward()
+    assert deg.grad is None
+    ref, _ = oracle.aggr_fwd(ei, x, None, "add")
+    np.testing.assert_array_equal(_np(y), ref)

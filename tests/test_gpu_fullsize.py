@@ -1,0 +1,251 @@
+"""Configs 3 and 4 checked at their own timed sizes (BASELINE.json configs[2],
+configs[3]; the shapes scripts/bench_workloads.py times), so every path the
+timed steps take is exercised on the timed inputs: config 3's giant and
+mid-heavy rows (max in-degree ~6.5k), the side stream without the system
+fence, the SideFold folds riding in other launches, the fused residual stack;
+config 4's 10M-edge mean / max / sum stacks.
+
+Config 3 (src/run/run_botnet.sh:14: GCNModel(1, [32]*12, residual_hop=1,
+deg_norm='sm', bias=0, final proj 32 -> 2), gcn_model.py:86-125) on two
+botnet-shaped graphs batched (2 x 143,107 nodes), deg_K = out-degree:
+  (a) exact weights (first layer W = ones, 32 -> 32 layers W = I, residual
+      Linears and their biases 0, final Linear picking features 0 and 1):
+      every product is exact, so y must equal the C oracle's chain BIT FOR
+      BIT, and x.grad (the sum of the two live columns of the bottom dH) must
+      sit within 2^-22 of the exact sum of the oracle's dH columns;
+  (b) the same with 32 input features and no final Linear: y and x.grad bit
+      for bit the oracle chain, all 32 columns live in both directions;
+  (c) bench_workloads' seeded model and inputs (x = [1, deg]): every layer's
+      output against fp64 at its own input, and every parameter gradient
+      against the fp64 adjoint chain, within 1e-5 of the |.|-weighted chain.
+      The ReLU decisions are the kernels' own (the stack's saved masks), so
+      a value that rounds across 0 does not fork the two chains.
+Config 4 (kernel/gin.py / graph_sage.py aggregators on the config-2 graph,
+deg_norm None, F = 128, 3 layers + bias + ReLU): W = I, forward and x.grad bit
+for bit the oracle chain for add, mean and max.
+"""
+import numpy as np
+import pytest
+import torch
+from fp64_ref import A64, within
+
+pytestmark = pytest.mark.gpu
+
+L3 = 12
+
+
+@pytest.fixture(scope="module")
+def config3_graph():
+    from bench import batch_graphs, make_botnet_graph
+    g1, n1, _ = make_botnet_graph(seed=0)
+    g2, n2, _ = make_botnet_graph(seed=1)
+    ei, N = batch_graphs([(g1, n1), (g2, n2)])
+    deg = torch.bincount(ei[0], minlength=N).float()
+    return ei, N, deg
+
+
+def _model(dev, F_in, final_type):
+    from mgcn.models import GCNModel
+    return GCNModel(F_in, [32] * L3, 2, non_linear='relu', non_linear_layer_wise='relu',
+                    residual_hop=1, dropout=0.0, final_type=final_type, pred_on='node',
+                    deg_norm='sm', aggr='add', bias=False).to(dev)
+
+
+def _exact_weights(model, F_in):
+    with torch.no_grad():
+        for l, layer in enumerate(model.gcn_net):
+            W = layer.gcn.node_models[0].weight_node
+            W.copy_(torch.ones(1, 32) if (l == 0 and F_in == 1) else torch.eye(32))
+        for res in model.residuals:
+            res.weight.zero_()
+            res.bias.zero_()
+        if not isinstance(model.final, torch.nn.Identity):
+            model.final.weight.zero_()
+            model.final.weight[0, 0] = 1.0
+            model.final.weight[1, 1] = 1.0
+            model.final.bias.zero_()
+
+
+def _oracle_chain(oracle, ein, N, deg, h0, dY):
+    """relu(A h) per layer (the residual branch is 0, relu of relu is relu),
+    then the adjoint with each layer's own ReLU mask."""
+    wf, wb, rs = oracle.edge_factors(ein, N, "sm", deg=deg)
+    outs, h = [], h0
+    for _ in range(L3):
+        h, _ = oracle.aggr_fwd(ein, h, wf, "add", None, relu=True)
+        outs.append(h)
+    g = dY
+    for l in range(L3 - 1, -1, -1):
+        g, _ = oracle.aggr_bwd(ein, g, wb, rs, "add", outs[l], True, None)
+    return outs, g
+
+
+def test_config3_exact_weights_in1_bitwise(cuda, oracle, config3_graph):
+    """(a) GCNModel(1, [32]*12) as config 3 builds it, exact weights."""
+    ei, N, deg = config3_graph
+    model = _model(cuda, 1, 'proj')
+    _exact_weights(model, 1)
+    rng = np.random.default_rng(31)
+    x0 = rng.standard_normal((N, 1)).astype(np.float32)
+    dY = rng.standard_normal((N, 2)).astype(np.float32)
+    xt = torch.from_numpy(x0).to(cuda).requires_grad_(True)
+    y = model(xt, ei.to(cuda), deg_K=deg.to(cuda))
+    y.backward(torch.from_numpy(dY).to(cuda))
+    torch.cuda.synchronize()
+    ein = ei.numpy()
+    g_top = np.zeros((N, 32), np.float32)
+    g_top[:, :2] = dY
+    outs, dH1 = _oracle_chain(oracle, ein, N, deg.numpy(), np.repeat(x0, 32, axis=1), g_top)
+    np.testing.assert_array_equal(y.detach().cpu().numpy(), outs[-1][:, :2])
+    # x.grad = dH1 @ ones^T (a bf16x6 GEMM): two live columns, within a few
+    # roundings of their exact sum
+    a, b = dH1[:, 0].astype(np.float64), dH1[:, 1].astype(np.float64)
+    got = xt.grad.cpu().numpy()[:, 0].astype(np.float64)
+    assert np.all(np.abs(got - (a + b)) <= 2.0 ** -22 * (np.abs(a) + np.abs(b)))
+    assert np.count_nonzero(dH1[:, 2:]) == 0
+
+
+def test_config3_exact_weights_in32_bitwise(cuda, oracle, config3_graph):
+    """(b) 32 input features, W = I everywhere, no final Linear: all 32
+    columns live forward and backward; y and x.grad bit for bit."""
+    ei, N, deg = config3_graph
+    model = _model(cuda, 32, 'none')
+    _exact_weights(model, 32)
+    rng = np.random.default_rng(32)
+    x0 = rng.standard_normal((N, 32)).astype(np.float32)
+    dY = rng.standard_normal((N, 32)).astype(np.float32)
+    xt = torch.from_numpy(x0).to(cuda).requires_grad_(True)
+    y = model(xt, ei.to(cuda), deg_K=deg.to(cuda))
+    y.backward(torch.from_numpy(dY).to(cuda))
+    torch.cuda.synchronize()
+    outs, dX = _oracle_chain(oracle, ei.numpy(), N, deg.numpy(), x0, dY)
+    np.testing.assert_array_equal(y.detach().cpu().numpy(), outs[-1])
+    np.testing.assert_array_equal(xt.grad.cpu().numpy(), dX)
+
+
+def _find_node(fn, name):
+    seen, todo = set(), [fn]
+    while todo:
+        f = todo.pop()
+        if f is None or f in seen:
+            continue
+        seen.add(f)
+        if type(f).__name__ == name:
+            return f
+        todo += [g for g, _ in f.next_functions]
+    raise AssertionError(f"{name} not in the autograd graph")
+
+
+def _bits(words, F=32):
+    """[N] int32 mask words -> [N, F] float64 0/1 (bit c <-> feature c)."""
+    w = words.to(torch.int64) & 0xffffffff
+    sh = torch.arange(F, device=words.device)
+    return ((w[:, None] >> sh) & 1).to(torch.float64)
+
+
+def test_config3_seeded_model_vs_fp64(cuda, oracle, config3_graph):
+    """(c) the timed config-3 model (bench_workloads: torch.manual_seed(0)
+    init, x = [1, deg]) with a fixed upstream gradient on its [N, 2] output:
+    every layer's output at its own input and every parameter gradient within
+    1e-5 of the |.|-weighted fp64 chain."""
+    ei, N, deg = config3_graph
+    torch.manual_seed(0)
+    model = _model(cuda, 1, 'proj')
+    x = torch.stack([torch.ones(N), deg], 1).to(cuda)
+    eic, degc = ei.to(cuda), deg.to(cuda)
+    dY = torch.randn(N, 2, generator=torch.Generator().manual_seed(4)).to(cuda)
+    y = model(x[:, 0].view(-1, 1), eic, deg_K=degc)
+    stack = _find_node(y.grad_fn, "_ResidualStackBackward")
+    a1, Zs, masks = (t.detach().clone() for t in stack.saved_tensors[:3])
+    assert Zs.shape[0] == L3 - 1
+    y.backward(dY)
+    torch.cuda.synchronize()
+    P = [(lay.gcn.node_models[0].weight_node, res.weight, res.bias)
+         for lay, res in zip(model.gcn_net, model.residuals)]
+    Wf, bf = model.final.weight, model.final.bias
+    d64 = lambda t: t.detach().to(torch.float64)  # noqa: E731
+
+    wf, _, _ = oracle.edge_factors(ei.numpy(), N, "sm", deg=deg.numpy())
+    A = A64(ei, wf, N, cuda)
+    acts = [x[:, :1].double(), a1.double()] + [Zs[l].double() for l in range(L3 - 1)]
+    m1 = [None] + [_bits(masks[l, :, 0]) for l in range(L3 - 1)]
+    # layer 0 (1 -> 32 on the two-launch path): x = 1, so A (x W0) = W0 * (A 1)
+    # with A 1 > 0 -- its ReLU decision is sign(W0) exactly
+    W0 = d64(P[0][0])
+    m1[0] = (W0 > 0).double().expand(N, 32)
+    # ---- forward, layer by layer at the stack's own inputs (acts[l + 1] is
+    # layer l's output as the kernels wrote it; the top one has no join ReLU)
+    for l in range(L3):
+        W, Wr, br = (d64(t) for t in P[l])
+        a = acts[l]
+        z1 = A.apply(a @ W) * m1[l]
+        z1a = A.apply(a.abs() @ W.abs(), absolute=True) * m1[l]
+        s = z1 + a @ Wr.t() + br
+        sa = z1a + a.abs() @ Wr.abs().t() + br.abs()
+        ref = s.clamp_min(0) if l < L3 - 1 else s
+        ok, worst = within(acts[l + 1] - ref, sa, 1e-5)
+        assert ok, ("forward", l, worst)
+    a12 = acts[L3]
+    yr = a12 @ d64(Wf).t() + d64(bf)
+    ya = a12.abs() @ d64(Wf).abs().t() + d64(bf).abs()
+    ok, worst = within(y.detach().double() - yr, ya, 1e-5)
+    assert ok, ("y", worst)
+    # ---- backward: the fp64 adjoint chain with the kernels' masks
+    g = dY.double()
+    ga = g.abs()
+    ok, worst = within(d64(Wf.grad) - g.t() @ a12, ga.t() @ a12.abs(), 1e-5)
+    assert ok, ("dWf", worst)
+    ok, worst = within(d64(bf.grad) - g.sum(0), ga.sum(0), 1e-5)
+    assert ok, ("dbf", worst)
+    d, da = g @ d64(Wf), ga @ d64(Wf).abs()
+    for l in range(L3 - 1, -1, -1):
+        W, Wr, br = (d64(t) for t in P[l])
+        a = acts[l]
+        m2 = (acts[l + 1] > 0).double() if l < L3 - 1 else 1.0
+        ds, dsa = d * m2, da * m2
+        dz1, dz1a = ds * m1[l], dsa * m1[l]
+        dH = A.apply(dz1, transpose=True)
+        dHa = A.apply(dz1a, transpose=True, absolute=True)
+        gW, gWr, gbr = (d64(t.grad) for t in P[l])
+        for name, got, ref, bnd in [("dW", gW, a.t() @ dH, a.abs().t() @ dHa),
+                                    ("dWr", gWr, ds.t() @ a, dsa.t() @ a.abs()),
+                                    ("dbr", gbr, ds.sum(0), dsa.sum(0))]:
+            ok, worst = within(got - ref, bnd, 1e-5)
+            assert ok, (name, l, worst)
+        d = dH @ W.t() + ds @ Wr
+        da = dHa @ W.abs().t() + dsa @ Wr.abs()
+
+
+@pytest.mark.parametrize("aggr", ["add", "mean", "max"])
+def test_config4_identity_weights_bitwise(cuda, oracle, aggr):
+    """Config 4's 3-layer stacks (deg_norm None, bias, ReLU between layers)
+    on the 10M-edge graph with W = I: forward and x.grad bit for bit the
+    oracle's chain (max: the forward's winners route the adjoint)."""
+    from bench import make_er_graph, make_inputs
+    from mgcn.models import GCNLayer, GCNStack
+    ei, N = make_er_graph()
+    X, _, bs, dY = make_inputs(N, 128, 3)
+    layers = []
+    for i in range(3):
+        layer = GCNLayer(128, 128, deg_norm=None, aggr=aggr, bias=True,
+                         non_linear='relu' if i < 2 else 'none').to(cuda)
+        with torch.no_grad():
+            layer.gcn.node_models[0].weight_node.copy_(torch.eye(128))
+            layer.gcn.node_models[0].bias.copy_(bs[i])
+        layers.append(layer)
+    stack = GCNStack(layers)
+    x = X.to(cuda).requires_grad_(True)
+    y = stack(x, ei.to(cuda))
+    y.backward(dY.to(cuda))
+    torch.cuda.synchronize()
+    ein = ei.numpy()
+    h, outs, ams = X.numpy(), [], []
+    for l in range(3):
+        h, am = oracle.aggr_fwd(ein, h, None, aggr, bs[l].numpy(), relu=l < 2)
+        outs.append(h)
+        ams.append(am)
+    np.testing.assert_array_equal(y.detach().cpu().numpy(), outs[-1])
+    g = dY.numpy()
+    for l in range(2, -1, -1):
+        g, _ = oracle.aggr_bwd(ein, g, None, None, aggr, outs[l], l < 2, ams[l])
+    np.testing.assert_array_equal(x.grad.cpu().numpy(), g)

@@ -20,6 +20,7 @@ the per-edge weights are the oracle's.
 import numpy as np
 import pytest
 import torch
+from fp64_ref import A64 as _A64
 
 pytestmark = pytest.mark.gpu
 
@@ -36,27 +37,6 @@ def config2(cuda):
 
 def _np(t):
     return t.detach().cpu().numpy()
-
-
-class _A64:
-    """x -> A x (and A^T, |A|) in fp64 on the GPU with the oracle's weights."""
-
-    def __init__(self, ei, w, N, dev, chunk=1 << 21):
-        self.src = ei[0].to(dev)
-        self.dst = ei[1].to(dev)
-        self.w = torch.from_numpy(w).to(dev, torch.float64)
-        self.N, self.chunk = N, chunk
-
-    def apply(self, H, transpose=False, absolute=False):
-        out = torch.zeros(self.N, H.size(1), dtype=torch.float64, device=H.device)
-        for a in range(0, self.src.numel(), self.chunk):
-            s, d = self.src[a:a + self.chunk], self.dst[a:a + self.chunk]
-            w = self.w[a:a + self.chunk]
-            if absolute:
-                w = w.abs()
-            fr, to = (d, s) if transpose else (s, d)
-            out.index_add_(0, to, H[fr] * w[:, None])
-        return out
 
 
 def test_config2_stack_identity_weights_bitwise(cuda, oracle, config2):

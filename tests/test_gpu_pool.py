@@ -243,6 +243,25 @@ def test_edge_merge_greedy_device_matches_pyg_walk(cuda, n, E, loops, dups):
     assert ch_dev.cpu().tolist() == chosen
 
 
+def test_edge_merge_greedy_rejects_malformed_input(cuda):
+    """Endpoints outside [0, N) and an order that is not a permutation are
+    caught on the device before any indexed write (IndexError, as the host
+    walk raised)."""
+    from mgcn.pool import edge_merge_greedy
+    ei = torch.tensor([[0, 1, 2], [1, 2, 0]], dtype=torch.int64, device=cuda)
+    order = torch.tensor([2, 0, 1], dtype=torch.int64, device=cuda)
+    c, ch, C = edge_merge_greedy(ei, order, 3)
+    assert C == 2 and ch.numel() == 1
+    for bad_ei, bad_order, n in [
+            (torch.tensor([[0, 1, 5], [1, 2, 0]]), order, 3),     # endpoint >= N
+            (torch.tensor([[0, -1, 2], [1, 2, 0]]), order, 3),    # negative endpoint
+            (ei, torch.tensor([2, 0, 3]), 3),                     # order out of range
+            (ei, torch.tensor([2, 0, 0]), 3)]:                    # repeated position
+        with pytest.raises(IndexError):
+            edge_merge_greedy(bad_ei.to(cuda), bad_order.to(cuda), n)
+    torch.cuda.synchronize()
+
+
 def test_graclus_is_a_maximal_matching_and_max_pool(cuda):
     from mgcn.kernel.data import Batch
     from mgcn.pool import graclus, max_pool

@@ -6,7 +6,6 @@ import numpy as np
 import torch
 
 from mgcn.kernel.data import DenseDataLoader, ToDense, get_dataset
-from mgcn.pool import merge_edges_greedy
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
@@ -31,6 +30,31 @@ def _pyg_merge(ei, order, n):
         cluster[node] = i
         i += 1
     return np.array(cluster), np.array(chosen, dtype=np.int64), i
+
+
+def merge_edges_greedy(edge_index_np: np.ndarray, order: np.ndarray, num_nodes: int):
+    """Array restatement of the same walk (boolean free mask, the leftover
+    free nodes numbered by np.nonzero): the form the device kernel's
+    numbering step follows (csrc/pool.hip)."""
+    free = np.ones(num_nodes, dtype=bool)
+    cluster = np.empty(num_nodes, dtype=np.int64)
+    chosen = []
+    i = 0
+    src, dst = edge_index_np[0], edge_index_np[1]
+    for e in order.tolist():
+        s, t = int(src[e]), int(dst[e])
+        if not free[s] or not free[t]:
+            continue
+        chosen.append(e)
+        cluster[s] = i
+        free[s] = False
+        if s != t:
+            cluster[t] = i
+            free[t] = False
+        i += 1
+    rest = np.nonzero(free)[0]
+    cluster[rest] = np.arange(i, i + rest.size)
+    return cluster, np.asarray(chosen, dtype=np.int64), i + rest.size
 
 
 def test_merge_edges_greedy_matches_pyg_loop():
