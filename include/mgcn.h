@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define MGCN_ABI_VERSION 14
+#define MGCN_ABI_VERSION 15
 
 /* return codes */
 #define MGCN_OK 0
@@ -267,23 +267,33 @@ int mgcn_gemm_small_k(int64_t M, int32_t K, int32_t N, const float *A, int64_t l
                       const float *B, int64_t sbk, int64_t sbn, float *C, int64_t ldc,
                       void *stream);
 
-/* 1 if mgcn_gemm_nn handles this (K, N): K in {32, 64, 128}, 1 <= N <= 128. */
+/* 1 if mgcn_gemm_nn handles this (K, N): every K, N >= 1 (ABI v15). */
 int mgcn_gemm_nn_supported(int32_t K, int32_t N);
+/* 1 if (K, N) takes the tuned tall-skinny kernel (K in {32, 64, 128, 256},
+ * any N; A rows must also be 16-byte aligned): else the generic tiled one. */
+int mgcn_gemm_nn_fast(int32_t K, int32_t N);
+/* 1 if the fused ReLU-mask epilogue (relu_mask != NULL) is available for
+ * (K, N): the tuned kernel with N <= 128. */
+int mgcn_gemm_nn_epi_supported(int32_t K, int32_t N);
 /* Bytes of scratch mgcn_gemm_nn needs for its fused column sums. */
 size_t mgcn_gemm_nn_workspace_bytes(int64_t M, int32_t N);
 
 /*
  * C[M, N] = A[M, K] . B[K, N] on MFMA (gemm_precision: bf16x6 or f32); A
- * row-major (lda, 16-byte aligned rows), B addressed as B[k * sbk + n * sbn]
- * (so W or W^T).  Replaces `torch.matmul(x, self.weight_node)`
- * (gcn_base_models.py:201) and its input gradient dX = dH W^T.  If relu_mask
+ * row-major (lda), B addressed as B[k * sbk + n * sbn] (so W or W^T).
+ * K in {32, 64, 128, 256} with 16-byte aligned A rows: the tuned
+ * tall-skinny kernel (B^T split once per workgroup into LDS, A streamed;
+ * N wider than 128 (64 at K = 256) as XCD-local column groups); any other
+ * shape: a generic 64 x 64-tiled kernel.  Replaces `torch.matmul(x,
+ * self.weight_node)` (gcn_base_models.py:201), its input gradient
+ * dX = dH W^T, and the Linear layers of the module surface.  If relu_mask
  * != NULL (mgcn_spmm_fwd / mgcn_relu_mask layout, the previous layer's
  * output Z > 0) the ReLU backward and bias gradient are fused into the
  * epilogue:
  *   C = Z > 0 ? A.B : 0,  colsum[n] = sum_m C[m, n]  (deterministic)
  * (gcn_model.py:196 + gcn_base_models.py:240-241 adjoints); with row_div
  * (mean aggregation, = max(in-degree, 1)) C is stored divided by it, the
- * column sums stay undivided.
+ * column sums stay undivided (mgcn_gemm_nn_epi_supported shapes only).
  */
 int mgcn_gemm_nn(int64_t M, int32_t K, int32_t N, const float *A, int64_t lda,
                  const float *B, int64_t sbk, int64_t sbn, float *C, int64_t ldc,

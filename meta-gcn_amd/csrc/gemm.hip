@@ -683,12 +683,20 @@ constexpr int nn_lds_bytes() {
   return P == PREC_BF16X6 ? 3 * NT * 32 * (K + 8) * 2 : NT * 32 * (K + 4) * 4;
 }
 
+// Column groups (N wider than one workgroup's B^T fits in LDS: K = 256 holds
+// 64 columns, K <= 128 holds 128): workgroup b takes column group
+// (b >> 3) % n_groups of row stream ((b >> 3) / n_groups) * 8 + (b & 7).  The
+// workgroups of one row stream are 8 apart in dispatch order, so they land
+// on the same XCD (round-robin dispatch) at the same time and walk the same
+// rows in the same order: A is read from HBM once and re-read from that
+// XCD's L2 by the other groups.  The grid is a multiple of 8 n_groups
+// (n_groups = 1: any grid, b = the row stream).
 template <int K, int NT, int EPI, int P>
 __global__ __launch_bounds__(kNNThreads, P == PREC_BF16X6 ? 1 : 2) void gemm_nn_kernel(
     const float *__restrict__ A, int64_t lda, const float *__restrict__ B, int64_t sbk,
     int64_t sbn, float *__restrict__ C, int64_t ldc, int64_t M, int N,
     const uint32_t *__restrict__ relu_mask, const float *__restrict__ row_div,
-    float *__restrict__ colsum_partial) {
+    float *__restrict__ colsum_partial, int n_groups) {
   constexpr int KH = K / 2;              // k per lane half
   constexpr int S4 = KH / 4;             // float4 steps per 32-row subtile
   constexpr int GS = (K == 32) ? 2 : 1;  // subtiles per unit (>= 8 steps per unit)
@@ -702,6 +710,11 @@ __global__ __launch_bounds__(kNNThreads, P == PREC_BF16X6 ? 1 : 2) void gemm_nn_
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 5, lc = lane & 31;
+  const int bx = (int)blockIdx.x;
+  const int cg = (bx >> 3) % n_groups;                       // column group
+  const int rs = ((bx >> 3) / n_groups) * 8 + (bx & 7);      // row stream
+  const int n_streams = (int)gridDim.x / n_groups;
+  const int n0 = cg * NT * 32;                               // first column of the group
 
   if constexpr (P == PREC_BF16X6) {
     // B^T split into its three bf16 terms, 8 k per item; columns past N zero
@@ -710,7 +723,7 @@ __global__ __launch_bounds__(kNNThreads, P == PREC_BF16X6 ? 1 : 2) void gemm_nn_
       float v[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        v[j] = (n < N) ? B[(int64_t)(k8 + j) * sbk + (int64_t)n * sbn] : 0.0f;
+        v[j] = (n0 + n < N) ? B[(int64_t)(k8 + j) * sbk + (int64_t)(n0 + n) * sbn] : 0.0f;
       bf16x8 th, tm, tl;
       split3_bf16(v, th, tm, tl);
       *reinterpret_cast<bf16x8 *>(&BS[(0 * NT * 32 + n) * LDK + k8]) = th;
@@ -722,8 +735,8 @@ __global__ __launch_bounds__(kNNThreads, P == PREC_BF16X6 ? 1 : 2) void gemm_nn_
     for (int idx = tid; idx < NT * 32 * (K / 4); idx += kNNThreads) {
       const int n = idx / (K / 4), k4 = (idx % (K / 4)) * 4;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (n < N) {
-        const float *bp = B + (int64_t)k4 * sbk + (int64_t)n * sbn;
+      if (n0 + n < N) {
+        const float *bp = B + (int64_t)k4 * sbk + (int64_t)(n0 + n) * sbn;
         v.x = bp[0];
         v.y = bp[sbk];
         v.z = bp[2 * sbk];
@@ -736,11 +749,11 @@ __global__ __launch_bounds__(kNNThreads, P == PREC_BF16X6 ? 1 : 2) void gemm_nn_
 
   const int64_t n_sub = (M + 31) / 32;
   const int64_t n_units = (n_sub + GS - 1) / GS;
-  const int64_t wstride = (int64_t)gridDim.x * kNNWaves;
+  const int64_t wstride = (int64_t)n_streams * kNNWaves;
   // A is read in BURSTS of 8 float4 steps = one 128-byte line per lane,
   // issued back to back (the 8 requests of a line meet in L1), into two
   // register banks: burst t + 1 loads while burst t feeds the MFMAs.
-  constexpr int NB = S / 8;  // bursts per unit: 2 (K = 128) or 1 (K = 64; K = 32: 2 subtiles)
+  constexpr int NB = S / 8;  // bursts per unit: 4 (K = 256), 2 (K = 128), 1 (K = 64; K = 32: 2 subtiles)
   auto load_burst = [&](int64_t unit, int part, float4 (&bk)[8]) {
     const float4 *rp[GS];
 #pragma unroll
@@ -880,9 +893,9 @@ __global__ __launch_bounds__(kNNThreads, P == PREC_BF16X6 ? 1 : 2) void gemm_nn_
       const bool rows_full = r0 + 32 <= M;  // wave-uniform
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
-        const int n = j * 32 + lc;
+        const int n = n0 + j * 32 + lc;
         const bool n_ok = n < N;
-        const int bit = 8 * j + (lc >> 2);
+        const int bit = n >> 2;  // EPI_RELU*: N <= 128, one 4-word mask row
         float *cp = C + (r0 + 4 * h) * ldc + n;
         if (rows_full) {
           if constexpr (EPI != EPI_STORE) {
@@ -924,9 +937,24 @@ __global__ __launch_bounds__(kNNThreads, P == PREC_BF16X6 ? 1 : 2) void gemm_nn_
   };
 
   float4 bank0[8], bank1[8];
-  int64_t u = (int64_t)blockIdx.x * kNNWaves + wave;
+  int64_t u = (int64_t)rs * kNNWaves + wave;
   if (u < n_units) load_burst(u, 0, bank0);
-  if constexpr (NB == 2) {
+  if constexpr (NB == 4) {
+    for (; u < n_units; u += wstride) {
+      const int64_t un = (u + wstride < n_units) ? u + wstride : u;  // last: harmless reload
+      zero_acc();
+      load_mask(u);
+      load_burst(u, 1, bank1);
+      compute_burst(bank0, 0);
+      load_burst(u, 2, bank0);
+      compute_burst(bank1, 1);
+      load_burst(u, 3, bank1);
+      compute_burst(bank0, 2);
+      load_burst(un, 0, bank0);
+      compute_burst(bank1, 3);
+      epilogue(u);
+    }
+  } else if constexpr (NB == 2) {
     for (; u < n_units; u += wstride) {
       const int64_t un = (u + wstride < n_units) ? u + wstride : u;  // last: harmless reload
       zero_acc();
@@ -964,17 +992,18 @@ __global__ __launch_bounds__(kNNThreads, P == PREC_BF16X6 ? 1 : 2) void gemm_nn_
       if (h == 0) red[wave * NT * 32 + j * 32 + lc] = both;
     }
     __syncthreads();
-    for (int n = tid; n < N; n += kNNThreads) {
-      float v = red[n];
-      for (int w = 1; w < kNNWaves; ++w) v = __fadd_rn(v, red[w * NT * 32 + n]);
-      colsum_partial[(int64_t)blockIdx.x * N + n] = v;
+    for (int c = tid; c < NT * 32 && n0 + c < N; c += kNNThreads) {
+      float v = red[c];
+      for (int w = 1; w < kNNWaves; ++w) v = __fadd_rn(v, red[w * NT * 32 + c]);
+      colsum_partial[(int64_t)rs * N + n0 + c] = v;  // [row stream][N]
     }
   }
 }
 
+// Resident capacity of this instantiation (queried once), capped by work;
+// with column groups a multiple of 8 groups (module comment above the kernel).
 template <int K, int NT, int EPI, int P>
-int nn_blocks(int64_t M) {
-  // resident capacity of this instantiation (queried once), capped by work
+int nn_blocks(int64_t M, int n_groups) {
   static std::atomic<int> per_cu_cache{0};  // same code object on every device
   int per_cu = per_cu_cache.load(std::memory_order_relaxed);
   if (per_cu == 0) {
@@ -987,22 +1016,23 @@ int nn_blocks(int64_t M) {
   }
   constexpr int GS = (K == 32) ? 2 : 1;
   const int64_t units = ((M + 31) / 32 + GS - 1) / GS;
-  int64_t g = (units + kNNWaves - 1) / kNNWaves;
-  const int64_t cap = 256LL * per_cu;
-  if (g > cap) g = cap;
-  if (g > kNNMaxGrid) g = kNNMaxGrid;
-  return (int)(g > 0 ? g : 1);
+  int64_t streams = (units + kNNWaves - 1) / kNNWaves;
+  int64_t cap = 256LL * per_cu / n_groups;
+  if (cap > kNNMaxGrid) cap = kNNMaxGrid;  // colsum partial slots: one per row stream
+  if (streams > cap) streams = cap;
+  if (n_groups > 1) streams = streams < 8 ? 8 : streams / 8 * 8;
+  return (int)((streams > 0 ? streams : 1) * n_groups);
 }
-
 
 template <int K, int NT, int EPI, int P>
 int launch_nn_epi(int64_t M, int N, const float *A, int64_t lda, const float *B, int64_t sbk,
                   int64_t sbn, float *C, int64_t ldc, const uint32_t *mask,
-                  const float *row_div, float *partial, int *grid_out, hipStream_t s) {
-  const int g = nn_blocks<K, NT, EPI, P>(M);
+                  const float *row_div, float *partial, int *streams_out, hipStream_t s) {
+  const int n_groups = (N + NT * 32 - 1) / (NT * 32);
+  const int g = nn_blocks<K, NT, EPI, P>(M, n_groups);
   hipLaunchKernelGGL((gemm_nn_kernel<K, NT, EPI, P>), dim3(g), dim3(kNNThreads), 0, s, A, lda, B,
-                     sbk, sbn, C, ldc, M, N, mask, row_div, partial);
-  *grid_out = g;
+                     sbk, sbn, C, ldc, M, N, mask, row_div, partial, n_groups);
+  *streams_out = g / n_groups;
   return check_launch("gemm_nn_kernel");
 }
 
@@ -1020,18 +1050,27 @@ int launch_nn_nt(int64_t M, int N, const float *A, int64_t lda, const float *B, 
                                             grid_out, s);
 }
 
+// Column tiles per workgroup: the split B^T (3 bf16 terms, K + 8 per row)
+// must fit the 160 KB of LDS -- K = 256: 64 columns (101 KB), K <= 128: 128.
+// Wider N runs as column groups.
 template <int K, int P>
 int launch_nn_p(int64_t M, int N, const float *A, int64_t lda, const float *B, int64_t sbk,
                 int64_t sbn, float *C, int64_t ldc, int epi, const uint32_t *Z,
                 const float *rd, float *partial, int *grid_out, hipStream_t s) {
   const int nt = (N + 31) / 32;
-  if (nt == 1)
-    return launch_nn_nt<K, 1, P>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, rd, partial, grid_out, s);
-  if (nt == 2)
+  if constexpr (K == 256) {
+    if (nt == 1)
+      return launch_nn_nt<K, 1, P>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, rd, partial, grid_out, s);
     return launch_nn_nt<K, 2, P>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, rd, partial, grid_out, s);
-  if (nt == 3)
-    return launch_nn_nt<K, 3, P>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, rd, partial, grid_out, s);
-  return launch_nn_nt<K, 4, P>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, rd, partial, grid_out, s);
+  } else {
+    if (nt == 1)
+      return launch_nn_nt<K, 1, P>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, rd, partial, grid_out, s);
+    if (nt == 2)
+      return launch_nn_nt<K, 2, P>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, rd, partial, grid_out, s);
+    if (nt == 3)
+      return launch_nn_nt<K, 3, P>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, rd, partial, grid_out, s);
+    return launch_nn_nt<K, 4, P>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, rd, partial, grid_out, s);
+  }
 }
 
 template <int K>
@@ -1043,6 +1082,131 @@ int launch_nn(int64_t M, int N, const float *A, int64_t lda, const float *B, int
                                        grid_out, s);
   return launch_nn_p<K, PREC_F32>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, Z, rd, partial,
                                   grid_out, s);
+}
+
+// ---------------------------------------------------------------------------
+// Any other shape (K not in {32, 64, 128, 256}, rows not 16-byte aligned, B
+// through any strides): C[M, N] = A[M, K] B[K, N] on 64 x 64 output tiles,
+// one per 256-thread workgroup (four waves of 32 x 32), the K range in
+// chunks of 16 staged through LDS -- bounds-checked element loads, the
+// fp32 operands split into their three bf16 terms (row-major [row][16 k]
+// images, B transposed) and multiplied on v_mfma_f32_32x32x16_bf16 (bf16x6),
+// or kept fp32 for v_mfma_f32_32x32x2_f32 (gemm_precision 0).  Two LDS
+// buffers, one barrier per chunk.  Not a roofline kernel: it covers the
+// shapes of the module surface the tuned kernels do not take (TU input
+// widths such as 3 / 21 / 89, hidden 16, classifier heads) so that no
+// product GEMM runs on a vendor library.
+constexpr int kGenT = 64, kGenK = 16, kGenThreads = 256;
+
+template <int P>
+__global__ __launch_bounds__(kGenThreads) void gemm_gen_kernel(
+    const float *__restrict__ A, int64_t lda, const float *__restrict__ B, int64_t sbk,
+    int64_t sbn, float *__restrict__ C, int64_t ldc, int64_t M, int K, int N) {
+  // x6: [buf][A | B^T][term][64][16] bf16; f32: [buf][A | B^T][64][16 + 1] fp32
+  constexpr int kImg = kGenT * kGenK * 2;            // one bf16 term image (2 KB)
+  constexpr int kF32Ld = kGenK + 1;
+  constexpr int kBufBytes = P == PREC_BF16X6 ? 2 * 3 * kImg : 2 * kGenT * kF32Ld * 4;
+  __shared__ __attribute__((aligned(16))) char lds[2 * kBufBytes];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wi = wave >> 1, wj = wave & 1;
+  const int h = lane >> 5, lc = lane & 31;
+  const int64_t m0 = (int64_t)blockIdx.x * kGenT;
+  const int n0 = (int)blockIdx.y * kGenT;
+  // staging: A element (row t >> 2, k 4 (t & 3) + i), B element (k 4 (t >> 6) + i, col t & 63)
+  const int ar = tid >> 2, ak = 4 * (tid & 3);
+  const int bn = tid & 63, bk = 4 * (tid >> 6);
+  const bool a_row_ok = m0 + ar < M;
+  const bool b_col_ok = n0 + bn < N;
+  const float *ap = A + (m0 + ar) * lda;
+  const float *bp = B + (int64_t)(n0 + bn) * sbn;
+  float ra[4], rb[4];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ka = k0 + ak + i, kb = k0 + bk + i;
+      ra[i] = (a_row_ok && ka < K) ? ap[ka] : 0.0f;
+      rb[i] = (b_col_ok && kb < K) ? bp[(int64_t)kb * sbk] : 0.0f;
+    }
+  };
+  auto store = [&](char *buf) {
+    if constexpr (P == PREC_BF16X6) {
+#pragma unroll
+      for (int op = 0; op < 2; ++op) {
+        const float *v = op ? rb : ra;
+        uint32_t hi[2], mid[2], lo[2];
+        split3_pair(f32x2{v[0], v[1]}, hi[0], mid[0], lo[0]);
+        split3_pair(f32x2{v[2], v[3]}, hi[1], mid[1], lo[1]);
+        const int row = op ? bn : ar, k = op ? bk : ak;
+        char *img = buf + op * 3 * kImg + (row * kGenK + k) * 2;
+        *reinterpret_cast<uint2 *>(img) = make_uint2(hi[0], hi[1]);
+        *reinterpret_cast<uint2 *>(img + kImg) = make_uint2(mid[0], mid[1]);
+        *reinterpret_cast<uint2 *>(img + 2 * kImg) = make_uint2(lo[0], lo[1]);
+      }
+    } else {
+      float *fa = reinterpret_cast<float *>(buf);
+      float *fb = fa + kGenT * kF32Ld;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        fa[ar * kF32Ld + ak + i] = ra[i];
+        fb[bn * kF32Ld + bk + i] = rb[i];
+      }
+    }
+  };
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+  const int nk = (K + kGenK - 1) / kGenK;
+  load(0);
+  store(lds);
+  __syncthreads();
+  for (int c = 0; c < nk; ++c) {
+    const char *buf = lds + (c & 1) * kBufBytes;
+    if (c + 1 < nk) load((c + 1) * kGenK);
+    if constexpr (P == PREC_BF16X6) {
+      // lane (h, lc): row lc of the wave's 32-row A tile / column lc of its
+      // B tile, k = 8 h .. 8 h + 7 of the chunk
+      const char *pa = buf + ((32 * wi + lc) * kGenK + 8 * h) * 2;
+      const char *pb = buf + 3 * kImg + ((32 * wj + lc) * kGenK + 8 * h) * 2;
+      const bf16x8 ah = *reinterpret_cast<const bf16x8 *>(pa);
+      const bf16x8 am = *reinterpret_cast<const bf16x8 *>(pa + kImg);
+      const bf16x8 al = *reinterpret_cast<const bf16x8 *>(pa + 2 * kImg);
+      const bf16x8 bh = *reinterpret_cast<const bf16x8 *>(pb);
+      const bf16x8 bm = *reinterpret_cast<const bf16x8 *>(pb + kImg);
+      const bf16x8 bl = *reinterpret_cast<const bf16x8 *>(pb + 2 * kImg);
+      acc = mfma_x6(ah, am, al, bh, bm, bl, acc);
+    } else {
+      const float *fa = reinterpret_cast<const float *>(buf) + (32 * wi + lc) * kF32Ld;
+      const float *fb = reinterpret_cast<const float *>(buf) + kGenT * kF32Ld + (32 * wj + lc) * kF32Ld;
+#pragma unroll
+      for (int ks = 0; ks < kGenK / 2; ++ks)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[2 * ks + h], fb[2 * ks + h], acc, 0, 0, 0);
+    }
+    if (c + 1 < nk) store(lds + ((c + 1) & 1) * kBufBytes);
+    __syncthreads();
+  }
+  // C/D map: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 h
+  const int n = n0 + 32 * wj + lc;
+  if (n < N) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int64_t row = m0 + 32 * wi + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (row < M) C[row * ldc + n] = acc[r];
+    }
+  }
+}
+
+int launch_gen(int64_t M, int K, int N, const float *A, int64_t lda, const float *B, int64_t sbk,
+               int64_t sbn, float *C, int64_t ldc, hipStream_t s) {
+  const dim3 grid((unsigned)((M + kGenT - 1) / kGenT), (unsigned)((N + kGenT - 1) / kGenT));
+  if (g_gemm_precision == PREC_BF16X6)
+    hipLaunchKernelGGL(gemm_gen_kernel<PREC_BF16X6>, grid, dim3(kGenThreads), 0, s, A, lda, B, sbk,
+                       sbn, C, ldc, M, K, N);
+  else
+    hipLaunchKernelGGL(gemm_gen_kernel<PREC_F32>, grid, dim3(kGenThreads), 0, s, A, lda, B, sbk,
+                       sbn, C, ldc, M, K, N);
+  return check_launch("gemm_gen_kernel");
 }
 
 // Deterministic fold of split partial sums: C[e] (+)= sum over sp of
@@ -1148,8 +1312,25 @@ int gemm_set_precision(int value) {
 
 }  // namespace mgcn
 
+namespace {
+// the tuned tall-skinny kernel: K in {32, 64, 128, 256}, 16-byte aligned A rows
+bool nn_fast(int32_t K, const float *A, int64_t lda) {
+  return (K == 32 || K == 64 || K == 128 || K == 256) && lda % 4 == 0 &&
+         reinterpret_cast<uintptr_t>(A) % 16 == 0;
+}
+}  // namespace
+
 extern "C" int mgcn_gemm_nn_supported(int32_t K, int32_t N) {
-  return (K == 32 || K == 64 || K == 128) && N >= 1 && N <= 128;
+  return K >= 1 && N >= 1;  // every shape: the tuned kernel or gemm_gen_kernel
+}
+
+extern "C" int mgcn_gemm_nn_fast(int32_t K, int32_t N) {
+  return (K == 32 || K == 64 || K == 128 || K == 256) && N >= 1;
+}
+
+extern "C" int mgcn_gemm_nn_epi_supported(int32_t K, int32_t N) {
+  // the fused ReLU-mask epilogue: the tuned kernel, one 4-word mask row (N <= 128)
+  return mgcn_gemm_nn_fast(K, N) && N <= 128;
 }
 
 extern "C" size_t mgcn_gemm_nn_workspace_bytes(int64_t M, int32_t N) {
@@ -1163,18 +1344,21 @@ extern "C" int mgcn_gemm_nn(int64_t M, int32_t K, int32_t N, const float *A, int
                             void *workspace, size_t workspace_bytes, void *stream) {
   clear_error();
   MGCN_REQUIRE(M >= 0 && K >= 0 && N >= 0, "mgcn_gemm_nn: negative size");
-  MGCN_REQUIRE(mgcn_gemm_nn_supported(K, N), "mgcn_gemm_nn: unsupported K=%d N=%d", K, N);
+  MGCN_REQUIRE(K >= 1 && N >= 1, "mgcn_gemm_nn: unsupported K=%d N=%d", K, N);
   hipStream_t s = as_stream(stream);
+  const int epi = relu_mask == nullptr ? EPI_STORE : row_div != nullptr ? EPI_RELU_DIV : EPI_RELU;
   if (M == 0) {
     if (colsum) MGCN_HIP_TRY(hipMemsetAsync(colsum, 0, sizeof(float) * N, s));
     return MGCN_OK;
   }
   MGCN_REQUIRE(A && B && C && lda >= K && ldc >= N, "mgcn_gemm_nn: bad A/B/C");
-  MGCN_REQUIRE(lda % 4 == 0 && reinterpret_cast<uintptr_t>(A) % 16 == 0,
-               "mgcn_gemm_nn: A must be 16-byte aligned with lda % 4 == 0");
-  const int epi = relu_mask == nullptr ? EPI_STORE : row_div != nullptr ? EPI_RELU_DIV : EPI_RELU;
   MGCN_REQUIRE(epi == EPI_STORE || colsum != nullptr, "mgcn_gemm_nn: relu_mask given without colsum");
   MGCN_REQUIRE(row_div == nullptr || relu_mask != nullptr, "mgcn_gemm_nn: row_div needs relu_mask");
+  const bool fast = nn_fast(K, A, lda);
+  MGCN_REQUIRE(epi == EPI_STORE || (fast && N <= 128),
+               "mgcn_gemm_nn: the ReLU-mask epilogue needs K in {32, 64, 128, 256}, N <= 128 and "
+               "16-byte aligned A rows (K=%d N=%d)", K, N);
+  if (!fast) return launch_gen(M, K, N, A, lda, B, sbk, sbn, C, ldc, s);
   float *partial = nullptr;
   if (epi != EPI_STORE) {
     const size_t need = mgcn_gemm_nn_workspace_bytes(M, N);
@@ -1185,15 +1369,17 @@ extern "C" int mgcn_gemm_nn(int64_t M, int32_t K, int32_t N, const float *A, int
     partial = static_cast<float *>(workspace);
   }
   int rc;
-  int grid = 0;
+  int streams = 0;
   if (K == 32)
-    rc = launch_nn<32>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, relu_mask, row_div, partial, &grid, s);
+    rc = launch_nn<32>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, relu_mask, row_div, partial, &streams, s);
   else if (K == 64)
-    rc = launch_nn<64>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, relu_mask, row_div, partial, &grid, s);
+    rc = launch_nn<64>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, relu_mask, row_div, partial, &streams, s);
+  else if (K == 128)
+    rc = launch_nn<128>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, relu_mask, row_div, partial, &streams, s);
   else
-    rc = launch_nn<128>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, relu_mask, row_div, partial, &grid, s);
+    rc = launch_nn<256>(M, N, A, lda, B, sbk, sbn, C, ldc, epi, relu_mask, row_div, partial, &streams, s);
   if (rc || epi == EPI_STORE) return rc;
-  return launch_colsum_fold(partial, grid, N, colsum, s);
+  return launch_colsum_fold(partial, streams, N, colsum, s);
 }
 
 // ---------------------------------------------------------------------------

@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmgcn.so")
 
 # constants mirrored from include/mgcn.h
-ABI_VERSION = 14
+ABI_VERSION = 15
 OK, EINVAL, EINDEX, EHIP, EWORKSPACE = 0, 1, 2, 3, 4
 REDUCE_SUM, REDUCE_MEAN, REDUCE_MAX = 0, 1, 2
 NORM_NONE, NORM_SM, NORM_RW = 0, 1, 2
@@ -58,6 +58,8 @@ SIGNATURES = {
                                   _i64, _int, _vp, _sz, _vp]),
     "mgcn_gemm_small_k": (_int, [_i64, _i32, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _i64, _vp]),
     "mgcn_gemm_nn_supported": (_int, [_i32, _i32]),
+    "mgcn_gemm_nn_fast": (_int, [_i32, _i32]),
+    "mgcn_gemm_nn_epi_supported": (_int, [_i32, _i32]),
     "mgcn_gemm_nn_workspace_bytes": (_sz, [_i64, _i32]),
     "mgcn_gemm_nn": (_int, [_i64, _i32, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _i64, _vp,
                             _vp, _vp, _vp, _sz, _vp]),

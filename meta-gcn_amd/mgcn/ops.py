@@ -17,6 +17,7 @@ max routes through the saved argmax), so the adjoint is bit-identical too.
 from __future__ import annotations
 
 import os
+from collections import Counter
 
 import torch
 
@@ -396,6 +397,12 @@ def gemm_nn_supported(K: int, N: int) -> bool:
     return bool(L.load().mgcn_gemm_nn_supported(int(K), int(N)))
 
 
+def gemm_nn_epi_supported(K: int, N: int) -> bool:
+    """The fused ReLU-mask / bias-gradient epilogue of mgcn_gemm_nn (the tuned
+    kernel, N <= 128)."""
+    return bool(L.load().mgcn_gemm_nn_epi_supported(int(K), int(N)))
+
+
 def make_relu_mask(Z: torch.Tensor) -> torch.Tensor:
     """int32 [rows, 4]: bit b of word v set iff Z[i, 4 b + v] > 0 (F <= 128;
     ``mgcn_relu_mask``)."""
@@ -540,24 +547,44 @@ def gemm_small_k(A: torch.Tensor, W: torch.Tensor, transpose_w: bool = False) ->
     return C
 
 
+# Dense products that left libmgcn for torch.matmul (hipBLASLt), by shape:
+# only non-2-D or non-fp32 operands do (every 2-D fp32 shape has a libmgcn
+# kernel since ABI v15).  tests/test_host.py holds configs 2-4 to zero.
+VENDOR_GEMMS: "Counter[tuple]" = Counter()
+
+
+def mm_route(K: int, N: int, dim: int = 2, dtype=torch.float32) -> str:
+    """Which kernel takes C[M, N] = A[M, K] B[K, N]: 'nn' (mgcn_gemm_nn: the
+    tuned kernel for K in {32, 64, 128, 256}, the generic tiled one for the
+    rest), 'small_k' (mgcn_gemm_small_k: K <= SMALL_K, N <= 128, k-ordered
+    fma) or 'vendor' (torch.matmul: non-2-D / non-fp32 operands only)."""
+    if dim != 2 or dtype != torch.float32 or K < 1 or N < 1:
+        return "vendor"
+    if K <= SMALL_K and N <= 128:
+        return "small_k"
+    return "nn"
+
+
 def _mm(x: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
-    """x @ W on libmgcn (MFMA for K in {32, 64, 128}, the small-K kernel for
-    K <= 8), else hipBLASLt."""
-    if gemm_nn_supported(W.size(0), W.size(1)):
+    """x @ W on libmgcn (:func:`mm_route`)."""
+    route = mm_route(W.size(0), W.size(1), x.dim(), x.dtype if W.dtype == torch.float32 else None)
+    if route == "nn":
         return gemm_nn(x, W)[0]
-    if 1 <= W.size(0) <= SMALL_K and W.size(1) <= 128 and x.dim() == 2 and \
-            x.dtype == torch.float32:
+    if route == "small_k":
         return gemm_small_k(x, W)
+    VENDOR_GEMMS[("mm", tuple(x.shape), tuple(W.shape), str(x.dtype))] += 1
     return torch.matmul(x, W.detach())
 
 
 def _mm_t(dH: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
-    """dH @ W^T."""
-    if gemm_nn_supported(W.size(1), W.size(0)):
+    """dH @ W^T on libmgcn (:func:`mm_route`)."""
+    route = mm_route(W.size(1), W.size(0), dH.dim(),
+                     dH.dtype if W.dtype == torch.float32 else None)
+    if route == "nn":
         return gemm_nn(dH, W, transpose_w=True)[0]
-    if 1 <= W.size(1) <= SMALL_K and W.size(0) <= 128 and dH.dim() == 2 and \
-            dH.dtype == torch.float32:
+    if route == "small_k":
         return gemm_small_k(dH, W, transpose_w=True)
+    VENDOR_GEMMS[("mm_t", tuple(dH.shape), tuple(W.shape), str(dH.dtype))] += 1
     return torch.matmul(dH, W.detach().t())
 
 
@@ -619,6 +646,7 @@ def linear_bias(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None) -> tor
     F.linear on the same HIP device).  CPU tensors raise: no CPU path."""
     L.require_device(x, W, b)
     if x.dim() != 2 or x.dtype != torch.float32:
+        VENDOR_GEMMS[("linear", tuple(x.shape), tuple(W.shape), str(x.dtype))] += 1
         return torch.nn.functional.linear(x, W, b)
     return _LinearBias.apply(x, W, b)
 
@@ -628,6 +656,7 @@ def linear(x: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
     tensors raise: no CPU path."""
     L.require_device(x, W)
     if x.dim() != 2 or x.dtype != torch.float32 or W.dtype != torch.float32:
+        VENDOR_GEMMS[("matmul", tuple(x.shape), tuple(W.shape), str(x.dtype))] += 1
         return torch.matmul(x, W)
     return _Linear.apply(x, W)
 
@@ -862,7 +891,7 @@ class _GCNStack(torch.autograd.Function):
             # the ReLU mask the next layer's dX GEMM reads (16 B per row)
             nxt = Ws[i + 1] if i + 1 < len(Ws) else None
             rm = None
-            if relu and nxt is not None and gemm_nn_supported(nxt.size(1), nxt.size(0)):
+            if relu and nxt is not None and gemm_nn_epi_supported(nxt.size(1), nxt.size(0)):
                 rm = torch.empty(plan.fwd.n_rows, 4, dtype=torch.int32, device=h.device)
             if _FUSE_XW and spmm_xw_supported(plan.fwd, W.size(0), W.size(1), reduce,
                                               h.stride(0)):

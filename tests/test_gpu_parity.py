@@ -409,6 +409,61 @@ def test_gemm_nn_matches_fp64(cuda, M, K, N, trans, gemm_precision):
     assert torch.allclose(cs2.double(), ref_cs, rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("M,K,N,trans", [
+    # K = 256 (config 5's x @ W and dH W^T): 64-column groups on one XCD each
+    (1_000_003, 256, 256, False), (100_000, 256, 256, True), (70_001, 256, 100, False),
+    (5000, 256, 32, True), (33, 256, 256, False),
+    # K <= 128 with N > 128: 128-column groups
+    (300_000, 128, 256, False), (1000, 128, 300, True), (3000, 64, 200, False),
+    # the generic tiled kernel: K outside {32, 64, 128, 256} (TU inputs, hidden 16)
+    (10_000, 16, 16, False), (10_000, 89, 64, True), (3000, 21, 130, False),
+    (777, 300, 5, True), (65, 12, 33, False), (50_000, 130, 128, False), (1, 9, 1, True)])
+def test_gemm_nn_wide_and_generic_matches_fp64(cuda, M, K, N, trans, gemm_precision):
+    """mgcn_gemm_nn on every shape (ABI v15): the tuned kernel's column
+    groups (K = 256, N > 128) and the generic tiled kernel, both precisions,
+    against fp64 within 1e-5 of sum_k |a_k b_k|; deterministic; the fused
+    ReLU-mask epilogue where it applies (tuned kernel, N <= 128)."""
+    from mgcn import ops
+    g = torch.Generator(device=cuda).manual_seed(M + 3 * K + N)
+    A = torch.randn(M, K, device=cuda, generator=g)
+    W = torch.randn(N, K, device=cuda, generator=g) if trans else \
+        torch.randn(K, N, device=cuda, generator=g)
+    Wm = W.t() if trans else W
+    C, _ = ops.gemm_nn(A, W, transpose_w=trans)
+    ref = A.double() @ Wm.double()
+    bound = A.double().abs() @ Wm.double().abs()
+    err = (C.double() - ref).abs()
+    assert bool((err <= 1e-5 * bound + 1e-6).all()), float((err / (bound + 1e-6)).max())
+    assert torch.equal(C, ops.gemm_nn(A, W, transpose_w=trans)[0])
+    if ops.gemm_nn_epi_supported(K, N):
+        Z = torch.randn(M, N, device=cuda, generator=g)
+        C2, cs2 = ops.gemm_nn(A, W, transpose_w=trans, Z=Z)
+        assert torch.equal(C2, torch.where(Z > 0, C, torch.zeros_like(C)))
+        assert torch.allclose(cs2.double(), C2.double().sum(0), rtol=1e-4, atol=1e-3)
+
+
+def test_linear_layers_of_odd_widths_stay_on_libmgcn(cuda):
+    """x @ W and F.linear of the module surface at widths the tuned kernels
+    do not take run on libmgcn (no torch.matmul), forward and backward."""
+    from mgcn import ops
+    from mgcn.models import Linear
+    ops.VENDOR_GEMMS.clear()
+    g = torch.Generator(device=cuda).manual_seed(3)
+    for fin, fout in [(89, 16), (16, 6), (21, 64), (7, 130), (300, 2)]:
+        x = torch.randn(5000, fin, device=cuda, generator=g).requires_grad_(True)
+        lin = Linear(fin, fout).to(cuda)
+        W = torch.randn(fin, fout, device=cuda, generator=g).requires_grad_(True)
+        y = lin(x) + ops.linear(x, W)
+        y.backward(torch.ones_like(y))
+        ref = x.detach().double() @ lin.weight.detach().double().t() + lin.bias.detach().double() \
+            + x.detach().double() @ W.detach().double()
+        assert torch.allclose(y.detach().double(), ref, rtol=1e-5, atol=1e-4)
+        dx = torch.ones(5000, fout, device=cuda, dtype=torch.float64) @ \
+            (lin.weight.detach().double() + W.detach().double().t())
+        assert torch.allclose(x.grad.double(), dx, rtol=1e-5, atol=1e-4)
+    assert not ops.VENDOR_GEMMS, dict(ops.VENDOR_GEMMS)
+
+
 @pytest.mark.parametrize("M", [1_000_000, 1_000_003, 4097, 31, 1, 0])
 def test_gemm_bwd_matches_fp64(cuda, M):
     """Fused adjoints (mgcn_gemm_bwd): dW = X^T dH and dX = dH W^T within

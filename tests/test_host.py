@@ -235,3 +235,26 @@ def test_pyg_loop_helpers_match_oracle_restatement(oracle):
             np.testing.assert_array_equal(aw.numpy(), bw)
     np.testing.assert_array_equal(remove_self_loops(torch.from_numpy(ei))[0].numpy(),
                                   oracle.remove_self_loops(ei))
+
+
+def test_dense_products_never_route_to_a_vendor_gemm():
+    """Every 2-D fp32 product of the module surface routes to a libmgcn
+    kernel (mm_route): configs 2-5 (128 -> 128, the botnet stack's 1 -> 32,
+    32 -> 32 and 32 -> 2 heads with their transposes, 256 -> 256) and the
+    kernel/ nets' widths (TU inputs 3 / 7 / 21 / 89, hidden 16-128, 2-6
+    classes); torch.matmul is left only for non-2-D / non-fp32 operands."""
+    import torch
+    from mgcn.ops import mm_route
+    shapes = [(128, 128), (1, 32), (32, 1), (32, 32), (32, 2), (2, 32), (64, 64), (256, 256),
+              (128, 256), (256, 128)]
+    for fin in (3, 7, 21, 89):
+        for hid in (16, 32, 64, 128):
+            shapes += [(fin, hid), (hid, fin)]
+    for hid in (16, 32, 64, 128):
+        for c in (2, 6):
+            shapes += [(hid, c), (c, hid), (hid, hid), (2 * hid, hid), (hid, 2 * hid)]
+    for K, N in shapes:
+        assert mm_route(K, N) in ("nn", "small_k"), (K, N)
+    assert mm_route(32, 128) == "nn" and mm_route(1, 32) == "small_k"
+    assert mm_route(128, 128, dim=3) == "vendor"
+    assert mm_route(128, 128, dtype=torch.float16) == "vendor"
