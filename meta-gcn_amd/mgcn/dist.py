@@ -156,6 +156,12 @@ class Shard:
     cnt_table: torch.Tensor          # the same for every node, table layout (MEAN adjoint)
     chunk_edges_fwd: list            # edges of each row chunk (host ints, byte accounting)
     chunk_edges_bwd: list
+    # emulated rank (one process standing in for rank `rank` of `world`, no
+    # collectives): the exchange tables are persistent buffers whose other
+    # ranks' rows are left as they are -- the rank-local compute of the
+    # sharded step timed on one GPU (scripts/config5_rank.py)
+    emulated: bool = False
+    _tables: dict = None
 
     @property
     def rows(self) -> int:
@@ -208,10 +214,32 @@ def _gather_into(out, inp, world, group, async_op):
 
 
 def _gather_chunk(shard: Shard, c: int, local_pad: torch.Tensor, table: torch.Tensor, group):
-    """Issue the all-gather of row chunk c (async); returns the work or None."""
+    """Issue the all-gather of row chunk c (async); returns the work or None.
+    Emulated rank: only this rank's slice of the chunk is written."""
     cr, P = shard.chunk_rows, shard.world
+    if shard.emulated:
+        a = c * P * cr + shard.rank * cr
+        table[a:a + cr].copy_(local_pad[c * cr:(c + 1) * cr])
+        return None
     return _gather_into(table[c * P * cr:(c + 1) * P * cr], local_pad[c * cr:(c + 1) * cr], P,
                         group, True)
+
+
+def new_table(shard: Shard, F: int, dtype, device, slot: str) -> torch.Tensor:
+    """An exchange table [C*P*cr, F]: a fresh buffer, or (emulated rank) the
+    shard's persistent one for ``slot`` -- a rank-local timing of the
+    sharded step must not allocate 51 GB per layer where the real step
+    receives it from its peers."""
+    if not shard.emulated:
+        return torch.empty(shard.table_rows, F, dtype=dtype, device=device)
+    if shard._tables is None:
+        shard._tables = {}
+    key = (slot, F, dtype, str(device))
+    t = shard._tables.get(key)
+    if t is None:
+        t = torch.zeros(shard.table_rows, F, dtype=dtype, device=device)
+        shard._tables[key] = t
+    return t
 
 
 def _wait(works):
@@ -220,15 +248,18 @@ def _wait(works):
             w.wait()
 
 
-def gather_table(shard: Shard, local: torch.Tensor, group=None) -> torch.Tensor:
+def gather_table(shard: Shard, local: torch.Tensor, group=None, slot: str = "g") -> torch.Tensor:
     """My rows [rows, F] -> the exchange table [C*P*cr, F] on every rank."""
     pad = torch.empty((shard.pad_rows,) + tuple(local.shape[1:]), dtype=local.dtype,
                       device=local.device)
     pad[:shard.rows] = local
     if shard.pad_rows > shard.rows:
         pad[shard.rows:].zero_()
-    table = torch.empty((shard.table_rows,) + tuple(local.shape[1:]), dtype=local.dtype,
-                        device=local.device)
+    if local.dim() == 2:
+        table = new_table(shard, local.size(1), local.dtype, local.device, slot)
+    else:
+        table = torch.empty((shard.table_rows,) + tuple(local.shape[1:]), dtype=local.dtype,
+                            device=local.device)
     _wait([_gather_chunk(shard, c, pad, table, group) for c in range(shard.chunks)])
     return table
 
@@ -248,10 +279,14 @@ def _local_view(backend, key, other, sel, lo, hi, n_other, bounds, cr, T):
 
 
 def build_shard(edge_index: torch.Tensor, num_nodes: int, deg_norm="sm", deg=None,
-                edge_weight=None, group=None, backend=None, device=None, chunks: int = 4) -> Shard:
+                edge_weight=None, group=None, backend=None, device=None, chunks: int = 4,
+                emulate=None) -> Shard:
     """One-time setup of this rank's part of the graph (module docstring).
     ``edge_index`` (and ``deg`` / ``edge_weight``) is the full graph on every
-    rank; only the rank's own edges are sorted."""
+    rank; only the rank's own edges are sorted.  ``emulate=(rank, world)``:
+    build rank ``rank`` of ``world`` in this one process without
+    torch.distributed (the degrees that the real ranks all-gather are
+    counted here over the whole graph; no exchange ever runs)."""
     backend = backend or HipBackend()
     if torch.is_grad_enabled() and any(t is not None and t.requires_grad
                                        for t in (edge_weight, deg)):
@@ -260,8 +295,13 @@ def build_shard(edge_index: torch.Tensor, num_nodes: int, deg_norm="sm", deg=Non
         raise NotImplementedError("build_shard: edge_weight / deg requiring grad is not supported "
                                   "on the sharded path (detach them, or use the single-device "
                                   "modules)")
-    rank = dist.get_rank(group) if dist.is_initialized() else 0
-    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    if emulate is not None:
+        rank, world = (int(v) for v in emulate)
+        if not 0 <= rank < world:
+            raise ValueError(f"build_shard: emulate={emulate}")
+    else:
+        rank = dist.get_rank(group) if dist.is_initialized() else 0
+        world = dist.get_world_size(group) if dist.is_initialized() else 1
     if device is not None:
         edge_index = edge_index.to(device)
         deg = None if deg is None else deg.to(device)
@@ -291,6 +331,11 @@ def build_shard(edge_index: torch.Tensor, num_nodes: int, deg_norm="sm", deg=Non
         if deg is not None:  # given degrees (gcn_base_models.py:119-121): no exchange
             _, dinv = backend.degree_norm(N, None, deg.reshape(-1).to(torch.float32).contiguous(),
                                           None, code)
+        elif emulate is not None:  # every rank's out-degrees, counted here
+            if ew is not None:
+                raise NotImplementedError("build_shard(emulate=...): edge weights")
+            odeg = torch.bincount(src, minlength=N).to(torch.float32).contiguous()
+            _, dinv = backend.degree_norm(N, None, odeg, None, code)
         else:  # out-degree of my sources over their complete rows, then all-gathered
             _, dl = backend.degree_norm(hi, bwd_g, None, ew, code)
             mine = _all_gather_flat(dl[lo:hi], max_rows, world, group)
@@ -319,7 +364,7 @@ def build_shard(edge_index: torch.Tensor, num_nodes: int, deg_norm="sm", deg=Non
         ce_f.append(int(rp_f[b] - rp_f[a]) if b > a else 0)
         ce_b.append(int(rp_b[b] - rp_b[a]) if b > a else 0)
     sh = Shard(rank, world, bounds, lo, hi, max_rows, C, cr, fwd, bwd, w_fwd, w_bwd, row_scale,
-               cnt[lo:hi].contiguous(), None, ce_f, ce_b)
+               cnt[lo:hi].contiguous(), None, ce_f, ce_b, emulated=emulate is not None)
     sh.cnt_table = sh.to_table(cnt)
     return sh
 
@@ -328,7 +373,7 @@ def build_shard(edge_index: torch.Tensor, num_nodes: int, deg_norm="sm", deg=Non
 class _ShardedAggregate(torch.autograd.Function):
     @staticmethod
     def forward(ctx, H_local, bias, shard: Shard, reduce: int, relu: bool, backend, group):
-        Htab = gather_table(shard, H_local.contiguous(), group)
+        Htab = gather_table(shard, H_local.contiguous(), group, slot="fwd")
         Y, argmax = backend.spmm_fwd(shard.fwd, shard.w_fwd, Htab, reduce, bias, relu)
         ctx.shard, ctx.reduce, ctx.relu, ctx.backend, ctx.group = shard, reduce, relu, backend, group
         ctx.has_bias = bias is not None
@@ -341,10 +386,10 @@ class _ShardedAggregate(torch.autograd.Function):
         sh, be = ctx.shard, ctx.backend
         need_b = ctx.has_bias and ctx.needs_input_grad[1]
         dY, db = be.relu_bwd_colsum(dZ.contiguous(), Y, ctx.relu, need_b)
-        dYtab = gather_table(sh, dY, ctx.group)
+        dYtab = gather_table(sh, dY, ctx.group, slot="bwd")
         argtab = None
         if ctx.reduce == L.REDUCE_MAX:
-            argtab = gather_table(sh, argmax, ctx.group)
+            argtab = gather_table(sh, argmax, ctx.group, slot="arg")
         dH = be.spmm_bwd(sh.bwd, sh.w_bwd, sh.row_scale, dYtab, ctx.reduce,
                          cnt=sh.cnt_table if ctx.reduce == L.REDUCE_MEAN else None, argmax=argtab)
         return dH, db, None, None, None, None, None
@@ -373,7 +418,7 @@ class _ShardedStack(torch.autograd.Function):
         sh, be = shard, backend
         rows, C = sh.rows, sh.chunks
         dev = x.device
-        tab = x if x_is_table else gather_table(sh, x, group)
+        tab = x if x_is_table else gather_table(sh, x, group, slot="f1")
         zs, rms, outs = [], [], []
         n = len(Ws)
         for i, (W, b) in enumerate(zip(Ws, bs)):
@@ -385,8 +430,7 @@ class _ShardedStack(torch.autograd.Function):
             rm = None
             if relus[i] and not last:
                 rm = torch.empty(sh.pad_rows, 4, dtype=torch.int32, device=dev)
-            nxt = None if last else torch.empty(sh.table_rows, F_out, dtype=torch.float32,
-                                                device=dev)
+            nxt = None if last else new_table(sh, F_out, torch.float32, dev, "f%d" % (i & 1))
             works = []
             for c in range(C):
                 a, e = sh.chunk(c)
@@ -440,7 +484,7 @@ class _ShardedStack(torch.autograd.Function):
         # top layer's dY: all of it is local already; gather it in chunks
         tab = works = None
         if wants_dx(top):
-            tab = torch.empty(sh.table_rows, dY.size(1), dtype=torch.float32, device=dev)
+            tab = new_table(sh, dY.size(1), torch.float32, dev, "b%d" % (top & 1))
             works = [_gather_chunk(sh, c, dY, tab, group) for c in range(C)]
         dx = None
         for l in range(top, -1, -1):
@@ -457,7 +501,7 @@ class _ShardedStack(torch.autograd.Function):
             dX = torch.empty(sh.pad_rows, W.size(0), dtype=torch.float32, device=dev)
             ntab = None
             if l > 0 and wants_dx(l - 1):
-                ntab = torch.empty(sh.table_rows, W.size(0), dtype=torch.float32, device=dev)
+                ntab = new_table(sh, W.size(0), torch.float32, dev, "b%d" % ((l - 1) & 1))
             works, sums = [], []
             for c in range(C):
                 a, e = sh.chunk(c)
@@ -491,12 +535,13 @@ class ShardedGCN:
     stacks layer by layer (:func:`sharded_aggregate`)."""
 
     def __init__(self, edge_index, num_nodes, Ws, bs, device, deg_norm="sm", aggr="add",
-                 group=None, backend=None, chunks: int = 4, fused: bool = True):
+                 group=None, backend=None, chunks: int = 4, fused: bool = True, emulate=None):
         self.backend = backend or HipBackend()
         self.group = group
         self.device = device
         self.shard = build_shard(edge_index, num_nodes, deg_norm, group=group,
-                                 backend=self.backend, device=device, chunks=chunks)
+                                 backend=self.backend, device=device, chunks=chunks,
+                                 emulate=emulate)
         self.aggr = aggr
         self.reduce = L.REDUCE_CODES[aggr]
         self.W = [w.to(device).clone().requires_grad_(True) for w in Ws]
@@ -536,11 +581,13 @@ class ShardedGCN:
                                   backend=self.backend, group=self.group)
         return h
 
-    def step_fn(self, X, dY):
+    def step_fn(self, X, dY, X_table=None, dY_local=None):
         """fwd + bwd to every weight and bias + the gradient all-reduce, with
-        the replicated input features resident in the exchange layout."""
-        Xt = self.input_table(X)
-        dYl = self.local_rows(dY)
+        the replicated input features resident in the exchange layout (given
+        as the full [N, F] X, or directly as the table; dY as the full [N, F]
+        upstream gradient or this rank's rows)."""
+        Xt = X_table if X_table is not None else self.input_table(X)
+        dYl = dY_local if dY_local is not None else self.local_rows(dY)
         params = self.params()
 
         def step():

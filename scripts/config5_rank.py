@@ -1,0 +1,132 @@
+"""Config 5's sharded step, one rank's share timed on ONE MI355X
+(BASELINE.json configs[4]: N = 50M nodes, 250M pairs symmetrised to
+E = 500M edges + 50M self-loops, F = 256, 8 GPUs, destination-range shards).
+
+The rank-local compute of the P-way sharded step is what one GPU of the
+8-GPU run executes between its exchanges: rank r of P builds its shard
+(mgcn.dist.build_shard(emulate=(r, P)): the edges into and out of its
+destination range, columns remapped to the exchange table, the same norms),
+and runs the product step -- ShardedGCN: 3 GCN layers 256 -> 256 ('sm',
+'add', bias, ReLU between), forward + backward to every weight and bias --
+with the exchange tables resident (the replicated input in the exchange
+layout; the layer tables written only at this rank's rows; no RCCL).  So
+the measured time is the step minus its all-gathers; the script also
+reports per-kernel HIP-event times and algorithmic GB/s (bench.KernelTimer
+accounting), and the predicted P = 1 / 2 / 4 / 8 curve from the measured
+rank-local time (which scales with rows / P) and the all-gathers' bytes at
+the xGMI link rate.
+
+    python scripts/config5_rank.py [--world 8 --rank 0 --steps 3 --warmup 1]
+Prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "meta-gcn_amd")]
+import torch  # noqa: E402
+
+from bench import KernelTimer, launch_bytes  # noqa: E402
+
+XGMI_LINK_GBS = 153.0  # per link and direction
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--nodes", type=int, default=50_000_000)
+    ap.add_argument("--pairs", type=int, default=250_000_000)
+    ap.add_argument("--feat", type=int, default=256)
+    ap.add_argument("--layers", type=int, default=3)
+    ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--rank", type=int, default=0)
+    ap.add_argument("--chunks", type=int, default=4)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--no-fused", action="store_true")
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    from mgcn import ops
+    from mgcn.dist import ShardedGCN
+    N, P, F, L = args.nodes, args.pairs, args.feat, args.layers
+    t0 = time.perf_counter()
+    g = torch.Generator(device=dev).manual_seed(0)
+    s = torch.randint(0, N, (P,), device=dev, generator=g)
+    d = torch.randint(0, N, (P,), device=dev, generator=g)
+    loops = torch.arange(N, device=dev)
+    ei = torch.stack([torch.cat([s, d, loops]), torch.cat([d, s, loops])])
+    del s, d, loops
+    gw = torch.Generator().manual_seed(2)
+    gb = torch.Generator().manual_seed(3)
+    a = (6.0 / (F + F)) ** 0.5
+    Ws = [torch.rand(F, F, generator=gw) * (2 * a) - a for _ in range(L)]
+    bs = [torch.rand(F, generator=gb) * 0.2 - 0.1 for _ in range(L)]
+    model = ShardedGCN(ei, N, Ws, bs, device=dev, chunks=args.chunks, fused=not args.no_fused,
+                       emulate=(args.rank, args.world))
+    sh = model.shard
+    nnz = int(ei.size(1))
+    del ei
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    prep_s = time.perf_counter() - t0
+    # the replicated input in the exchange layout and this rank's upstream gradient
+    Xt = torch.randn(sh.table_rows, F, device=dev, generator=g)
+    dYl = torch.randn(sh.rows, F, device=dev, generator=g)
+    step = model.step_fn(None, None, X_table=Xt, dY_local=dYl)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / args.steps * 1e3
+    timer = KernelTimer()
+    ops.set_kernel_timer(timer)
+    step()
+    torch.cuda.synchronize()
+    ops.set_kernel_timer(None)
+    kern = {}
+    for name, k in timer.summary().items():
+        byts = 0.0
+        for r, e in k.pop("sizes"):
+            b, _ = launch_bytes(name, r or 0, e or 0, F)
+            byts += b or 0.0
+        t = k["total_ms"] * 1e-3
+        kern[name] = dict(k, bytes=byts / k["launches"], gbs=byts / t / 1e9 if t else None)
+    kernel_ms = sum(k["total_ms"] for k in kern.values())
+    # predicted curve: rank-local compute scales with the rank's rows; each
+    # exchanged table is an all-gather of [N, F] fp32, a rank receiving
+    # (P - 1) / P of it over P - 1 links
+    tables = (2 * (L - 1)) if model.fused else (2 * L)
+    per_rank_rows = sh.rows
+    curve = {}
+    for p in (1, 2, 4, 8):
+        compute = ms * (per_rank_rows * args.world / p) / per_rank_rows
+        xch = 0.0 if p == 1 else tables * (4.0 * N * F * (p - 1) / p) / (
+            (p - 1) * XGMI_LINK_GBS * 1e9) * 1e3
+        curve[str(p)] = {"compute_ms": compute, "exchange_ms": xch,
+                         "step_ms_overlapped": max(compute, xch),
+                         "step_ms_serial": compute + xch,
+                         "edges_per_s_overlapped": 2 * P * L / (max(compute, xch) * 1e-3)}
+    out = {"workload": f"config5 rank {args.rank} of {args.world}: N={N}, E={2 * P} (+{N} loops), "
+                       f"F={F}, {L}-layer GCN (sm, add, bias, ReLU) fwd+bwd, exchange tables "
+                       "resident (no RCCL)",
+           "path": ("fused layer kernels (_ShardedStack)" if model.fused else
+                    "per layer: x @ W (mgcn_gemm_nn) + SpMM; adjoint SpMM + dW (mgcn_gemm_tn) + "
+                    "dX (mgcn_gemm_nn)"),
+           "rows": sh.rows, "fwd_slots": int(sh.fwd.nnz), "bwd_slots": int(sh.bwd.nnz),
+           "nnz_global": nnz, "table_rows": sh.table_rows, "prep_s": prep_s,
+           "ms_per_step": ms, "kernel_ms_per_step": kernel_ms,
+           "rank_edges_per_s": (sh.fwd.nnz - sh.rows) * L / (ms * 1e-3),
+           "kernels": kern, "exchanged_tables_per_step": tables,
+           "xgmi_link_gbs": XGMI_LINK_GBS, "predicted_curve": curve,
+           "peak_mem_gb": torch.cuda.max_memory_allocated() / 1e9}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

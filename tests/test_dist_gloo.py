@@ -171,3 +171,39 @@ def test_build_shard_rejects_differentiable_norm_inputs():
         build_shard(ei, 3, "sm", edge_weight=ew)
     with pytest.raises(NotImplementedError):
         build_shard(ei, 3, "sm", deg=torch.ones(3, requires_grad=True))
+
+
+@pytest.mark.parametrize("fused,aggr", [(True, "add"), (False, "add"), (True, "max")])
+def test_emulated_rank_runs_the_rank_local_step(fused, aggr):
+    """build_shard(emulate=(r, P)): one process stands in for rank r of P
+    without torch.distributed (the config-5 rank timing,
+    scripts/config5_rank.py).  Its shard equals the real rank's (same rows,
+    slots, weights), a one-layer forward over the true input table equals the
+    single-process rows bit for bit, and the 3-layer step runs on the
+    persistent exchange tables (other ranks' rows left as they are).  The
+    per-layer path exchanges x W, which an emulated rank holds only for its
+    own rows, so only its running is checked."""
+    sys.path.insert(0, HERE)
+    from cpu_backend import CpuBackend
+    from mgcn.dist import ShardedGCN
+    ei, N, X, Ws, bs, dY = _problem(F=16)
+    be = CpuBackend()
+    cpu = torch.device("cpu")
+    one = ShardedGCN(ei, N, Ws[:1], bs[:1], device=cpu, aggr=aggr, backend=be, fused=fused)
+    y1 = one.forward(X_table=one.input_table(X)).detach()
+    for r in range(3):
+        m = ShardedGCN(ei, N, Ws[:1], bs[:1], device=cpu, aggr=aggr, backend=be, fused=fused,
+                       emulate=(r, 3))
+        sh = m.shard
+        assert sh.emulated and sh.world == 3 and sh.rank == r
+        y = m.forward(X_table=m.input_table(X)).detach()
+        if m.fused:  # reads the input table itself (the per-layer path exchanges x W)
+            assert torch.equal(y, y1[sh.lo:sh.hi])
+        m3 = ShardedGCN(ei, N, Ws, bs, device=cpu, aggr=aggr, backend=be, fused=fused,
+                        emulate=(r, 3))
+        step = m3.step_fn(X, dY)
+        step()
+        step()
+        assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in m3.params())
+        assert set(m3.shard._tables) and all(t.shape[0] == m3.shard.table_rows
+                                             for t in m3.shard._tables.values())
