@@ -328,15 +328,23 @@ int mgcn_gemm_bwd(int64_t M, int32_t F_in, int32_t F_out, const float *X, int64_
 
 /* ------------------------------------------------- fused layer forward */
 
-/* 1 if mgcn_spmm_xw_fwd / _bwd handle (F_in, F_out, reduce): 128 x 128, sum or
- * mean, under the bf16x6 product arithmetic (gemm_precision 1, the default). */
+/* 1 if mgcn_spmm_xw_fwd / _bwd handle (F_in, F_out, reduce): 128 x 128 or
+ * 256 x 256 (ABI v15), sum or mean, under bf16x6 precision.  At 256 the
+ * backward is the dX-only form. */
 int mgcn_spmm_xw_supported(int32_t F_in, int32_t F_out, int reduce);
+/* 1 if mgcn_spmm_xw_bwd's dW-accumulating form and its max adjoint apply
+ * (128 x 128 only). */
+int mgcn_spmm_xw_bwd_full_supported(int32_t F_in, int32_t F_out);
+/* Bytes of scratch mgcn_spmm_xw_fwd needs: 0 at 128, the split W image at 256. */
+size_t mgcn_spmm_xw_fwd_workspace_bytes(int32_t F_in, int32_t F_out);
 
 /*
  * One GCN layer forward in one launch, aggregating before transforming:
  *   Y[i] = epi( (reduce_{k in row i} X[col_k] * w_k) . W + bias )
  * over the fwd CSR view (rowptr/col as mgcn_spmm_fwd; w nullable), X
- * [n_cols, F_in] (ldx, 16-byte aligned rows, under 4 GiB), W [F_in, F_out] row-major (ldw),
+ * [n_cols, F_in] (ldx, 16-byte aligned rows; under 4 GiB at F = 128, any
+ * size at F = 256, whose kernel gives every gathered row a 64-bit base), W
+ * [F_in, F_out] row-major (ldw),
  * reduce SUM or MEAN (divides the aggregated row by max(in-degree, 1)), epi =
  * optional ReLU, relu_mask (nullable, needs relu) in mgcn_spmm_fwd's layout.
  * Equals mgcn_gemm_nn (X W) followed by mgcn_spmm_fwd up to the association
@@ -350,15 +358,20 @@ int mgcn_spmm_xw_supported(int32_t F_in, int32_t F_out, int reduce);
  * backward can form dW = Z^T dY' (dY' = dY pre-divided by the counts for
  * MEAN) with mgcn_gemm_bwd instead of a second gather over the graph
  * (the adjoint of `x @ weight_node`, gcn_base_models.py:201, reassociated).
+ * At F = 256 (fused_wide.hip) W is split once per call into a fragment
+ * image in `workspace` (mgcn_spmm_xw_fwd_workspace_bytes; NULL at 128), Y
+ * needs 16-byte aligned rows, and relu_mask holds 8 words per row (feature f
+ * at word 4 (f >> 7) + (f & 3), bit (f & 127) >> 2).
  */
 int mgcn_spmm_xw_fwd(int64_t n_rows, int64_t n_cols, int32_t F_in, int32_t F_out, const int64_t *rowptr,
                      const int32_t *col, const float *w, const float *X, int64_t ldx,
                      const float *W, int64_t ldw, const float *bias, float *Y, int64_t ldy,
                      int reduce, int relu, uint32_t *relu_mask, float *Z, int64_t ldz,
-                     void *stream);
+                     void *workspace, size_t workspace_bytes, void *stream);
 
-/* Bytes of scratch mgcn_spmm_xw_bwd needs (split-K partials + column sums). */
-size_t mgcn_spmm_xw_bwd_workspace_bytes(int64_t n_rows);
+/* Bytes of scratch mgcn_spmm_xw_bwd needs (split-K partials + column sums;
+ * at 256: the split W^T image + column-sum partials). */
+size_t mgcn_spmm_xw_bwd_workspace_bytes(int64_t n_rows, int32_t F_in, int32_t F_out);
 
 /*
  * One GCN layer backward in one launch (F_in = F_out = 128; sum / mean
@@ -381,6 +394,8 @@ size_t mgcn_spmm_xw_bwd_workspace_bytes(int64_t n_rows);
  * dX only: X == NULL and dW == NULL (dX required, no win_mask) -- the
  * gather, dX = dH W^T and its epilogue, nothing else; dX bit for bit the
  * full form's.  Pair with mgcn_spmm_xw_fwd's Z and mgcn_gemm_bwd (dW-only).
+ * F = 256: the dX-only form only (dY any size: 64-bit row bases; relu_mask
+ * in the 8-word layout of mgcn_spmm_xw_fwd at 256; dX 16-byte aligned rows).
  */
 int mgcn_spmm_xw_bwd(int64_t n_rows, int64_t n_cols, int32_t F_in, int32_t F_out,
                      const int64_t *rowptr_t, const int32_t *col_t, const float *w_t,

@@ -822,20 +822,31 @@ int xw_set_unroll(int value) {
 using namespace mgcn;
 
 extern "C" int mgcn_spmm_xw_supported(int32_t F_in, int32_t F_out, int reduce) {
-  return F_in == kXwF && F_out == kXwF && gemm_precision_is_x6() &&
+  return F_in == F_out && (F_in == kXwF || F_in == 256) && gemm_precision_is_x6() &&
          (reduce == MGCN_REDUCE_SUM || reduce == MGCN_REDUCE_MEAN);
+}
+
+extern "C" int mgcn_spmm_xw_bwd_full_supported(int32_t F_in, int32_t F_out) {
+  // the dW-accumulating backward and the max adjoint: 128 x 128 only (at
+  // 256 the dW accumulators do not fit beside the gather: Z^T dY instead)
+  return F_in == kXwF && F_out == kXwF && gemm_precision_is_x6();
+}
+
+extern "C" size_t mgcn_spmm_xw_fwd_workspace_bytes(int32_t F_in, int32_t F_out) {
+  return F_in == 256 && F_out == 256 ? xw_wide_workspace_bytes(false) : 0;
 }
 
 extern "C" int mgcn_spmm_xw_fwd(int64_t n_rows, int64_t n_cols, int32_t F_in, int32_t F_out,
                                 const int64_t *rowptr, const int32_t *col, const float *w,
                                 const float *X, int64_t ldx, const float *W, int64_t ldw,
                                 const float *bias, float *Y, int64_t ldy, int reduce, int relu,
-                                uint32_t *relu_mask, float *Z, int64_t ldz, void *stream) {
+                                uint32_t *relu_mask, float *Z, int64_t ldz, void *workspace,
+                                size_t workspace_bytes, void *stream) {
   clear_error();
   MGCN_REQUIRE(n_rows >= 0, "mgcn_spmm_xw_fwd: negative size");
   MGCN_REQUIRE(mgcn_spmm_xw_supported(F_in, F_out, reduce),
-               "mgcn_spmm_xw_fwd: unsupported F_in=%d F_out=%d reduce=%d (needs 128 x 128, sum/mean, "
-               "bf16x6)",
+               "mgcn_spmm_xw_fwd: unsupported F_in=%d F_out=%d reduce=%d (needs 128 x 128 or "
+               "256 x 256, sum/mean, bf16x6)",
                F_in, F_out, reduce);
   MGCN_REQUIRE(relu_mask == nullptr || relu, "mgcn_spmm_xw_fwd: relu_mask needs relu");
   if (n_rows == 0) return MGCN_OK;
@@ -843,6 +854,26 @@ extern "C" int mgcn_spmm_xw_fwd(int64_t n_rows, int64_t n_cols, int32_t F_in, in
   MGCN_REQUIRE(ldx >= F_in && ldx % 4 == 0 && reinterpret_cast<uintptr_t>(X) % 16 == 0,
                "mgcn_spmm_xw_fwd: X must have 16-byte aligned rows");
   MGCN_REQUIRE(ldw >= F_out && ldy >= F_out, "mgcn_spmm_xw_fwd: leading dimension too small");
+  if (F_in == 256) {
+    // the wide kernels address every gathered row through a 64-bit base:
+    // no table-size limit; 32-bit offsets only within a 16-row chunk
+    MGCN_REQUIRE(n_cols > 0 && (uint64_t)16 * (uint64_t)(ldy > ldz ? ldy : ldz) * 4u < (1ull << 31),
+                 "mgcn_spmm_xw_fwd: leading dimension too large");
+    MGCN_REQUIRE(relu_mask == nullptr || reinterpret_cast<uintptr_t>(relu_mask) % 16 == 0,
+                 "mgcn_spmm_xw_fwd: relu_mask not 16-byte aligned");
+    MGCN_REQUIRE(Z == nullptr || (ldz >= F_in && ldz % 4 == 0 && reinterpret_cast<uintptr_t>(Z) % 16 == 0),
+                 "mgcn_spmm_xw_fwd: Z must have 16-byte aligned rows (ldz >= F_in)");
+    MGCN_REQUIRE(ldy % 4 == 0 && reinterpret_cast<uintptr_t>(Y) % 16 == 0,
+                 "mgcn_spmm_xw_fwd: Y must have 16-byte aligned rows at F = 256");
+    const size_t need = mgcn_spmm_xw_fwd_workspace_bytes(F_in, F_out);
+    if (workspace == nullptr || workspace_bytes < need) {
+      set_error("mgcn_spmm_xw_fwd: workspace %zu < %zu", workspace_bytes, need);
+      return MGCN_EWORKSPACE;
+    }
+    return xw_wide_fwd(n_rows, rowptr, col, w, X, ldx, W, ldw, bias, Y, ldy,
+                       reduce == MGCN_REDUCE_MEAN, relu != 0, relu_mask, Z, ldz, workspace,
+                       g_xw_unroll, as_stream(stream));
+  }
   MGCN_REQUIRE(n_cols > 0 && (uint64_t)n_cols * (uint64_t)ldx * 4u <= 0xfffffff0ull,
                "mgcn_spmm_xw_fwd: X must hold 1 .. 4 GiB - 1 bytes (32-bit gather offsets)");
   MGCN_REQUIRE((uint64_t)kXwRows * (uint64_t)ldy * 4u < (1ull << 31),
@@ -876,8 +907,9 @@ extern "C" int mgcn_spmm_xw_fwd(int64_t n_rows, int64_t n_cols, int32_t F_in, in
   return g_xw_unroll == 4 ? launch_xw<4>(a, s) : launch_xw<8>(a, s);
 }
 
-extern "C" size_t mgcn_spmm_xw_bwd_workspace_bytes(int64_t n_rows) {
+extern "C" size_t mgcn_spmm_xw_bwd_workspace_bytes(int64_t n_rows, int32_t F_in, int32_t F_out) {
   (void)n_rows;
+  if (F_in == 256 && F_out == 256) return xw_wide_workspace_bytes(true);
   const size_t g = (size_t)xw_grid();
   return align_up(g * kXwF * kXwF * 4, 256) + align_up(g * kXwF * 4, 256);
 }
@@ -895,10 +927,12 @@ extern "C" int mgcn_spmm_xw_bwd(int64_t n_rows, int64_t n_cols, int32_t F_in, in
   MGCN_REQUIRE((win_mask == nullptr) == (slot_map == nullptr),
                "mgcn_spmm_xw_bwd: win_mask and slot_map go together (max adjoint)");
   MGCN_REQUIRE(mgcn_spmm_xw_supported(F_in, F_out, MGCN_REDUCE_SUM),
-               "mgcn_spmm_xw_bwd: unsupported F_in=%d F_out=%d (needs 128 x 128, bf16x6)", F_in,
-               F_out);
+               "mgcn_spmm_xw_bwd: unsupported F_in=%d F_out=%d (needs 128 x 128 or 256 x 256, "
+               "bf16x6)", F_in, F_out);
   // X == NULL and dW == NULL: dX only (dW formed by the caller from Z^T dY)
   const bool dx_only = X == nullptr && dW == nullptr;
+  MGCN_REQUIRE(dx_only || mgcn_spmm_xw_bwd_full_supported(F_in, F_out),
+               "mgcn_spmm_xw_bwd: at F=%d only the dX-only form (X = dW = NULL)", F_in);
   MGCN_REQUIRE(dx_only || (X != nullptr && dW != nullptr && lddw >= F_out),
                "mgcn_spmm_xw_bwd: bad dW (X and dW are given together, or both NULL for dX only)");
   MGCN_REQUIRE(!dx_only || (dX != nullptr && win_mask == nullptr),
@@ -919,6 +953,22 @@ extern "C" int mgcn_spmm_xw_bwd(int64_t n_rows, int64_t n_cols, int32_t F_in, in
   MGCN_REQUIRE(rowptr_t && dY, "mgcn_spmm_xw_bwd: null array");
   MGCN_REQUIRE(lddy >= F_out && lddy % 4 == 0 && reinterpret_cast<uintptr_t>(dY) % 16 == 0,
                "mgcn_spmm_xw_bwd: dY must have 16-byte aligned rows");
+  if (F_in == 256) {
+    MGCN_REQUIRE(dX != nullptr && win_mask == nullptr, "mgcn_spmm_xw_bwd: the dX-only form needs dX");
+    MGCN_REQUIRE(W != nullptr && ldw >= F_out && lddx >= F_in && lddx % 4 == 0 &&
+                     reinterpret_cast<uintptr_t>(dX) % 16 == 0 &&
+                     (uint64_t)16 * (uint64_t)lddx * 4u < (1ull << 31),
+                 "mgcn_spmm_xw_bwd: bad W/dX (16-byte aligned dX rows)");
+    MGCN_REQUIRE(relu_mask == nullptr || reinterpret_cast<uintptr_t>(relu_mask) % 16 == 0,
+                 "mgcn_spmm_xw_bwd: relu_mask not 16-byte aligned");
+    const size_t need = mgcn_spmm_xw_bwd_workspace_bytes(n_rows, F_in, F_out);
+    if (workspace == nullptr || workspace_bytes < need) {
+      set_error("mgcn_spmm_xw_bwd: workspace %zu < %zu", workspace_bytes, need);
+      return MGCN_EWORKSPACE;
+    }
+    return xw_wide_bwd_dx(n_rows, rowptr_t, col_t, w_t, row_scale, dY, lddy, W, ldw, dX, lddx,
+                          relu_mask, row_div, colsum, workspace, g_xw_unroll, s);
+  }
   MGCN_REQUIRE(dx_only || (ldx >= F_in && ldx % 4 == 0 && reinterpret_cast<uintptr_t>(X) % 16 == 0),
                "mgcn_spmm_xw_bwd: X must have 16-byte aligned rows");
   if (dx_only) ldx = 0;
@@ -930,7 +980,7 @@ extern "C" int mgcn_spmm_xw_bwd(int64_t n_rows, int64_t n_cols, int32_t F_in, in
                "mgcn_spmm_xw_bwd: bad W/dX");
   MGCN_REQUIRE(relu_mask == nullptr || reinterpret_cast<uintptr_t>(relu_mask) % 16 == 0,
                "mgcn_spmm_xw_bwd: relu_mask not 16-byte aligned");
-  const size_t need = mgcn_spmm_xw_bwd_workspace_bytes(n_rows);
+  const size_t need = mgcn_spmm_xw_bwd_workspace_bytes(n_rows, F_in, F_out);
   if (workspace == nullptr || workspace_bytes < need) {
     set_error("mgcn_spmm_xw_bwd: workspace %zu < %zu", workspace_bytes, need);
     return MGCN_EWORKSPACE;

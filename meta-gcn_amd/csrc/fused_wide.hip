@@ -1,0 +1,518 @@
+// Fused GCN layer kernels at F_in = F_out = 256 (config 5, BASELINE.json
+// configs[4]: 50M nodes, 500M edges, F = 256) on gfx950:
+//
+//   forward   Y = epi((A X) W + b)   (+ Z = A X, + ReLU mask words)
+//   backward  dX = relu'(lower) ((A^T dY) W^T) [/ row_div], colsum = sum_rows dX
+//             (the dX-only form: dW = Z^T dY is the caller's dense pass)
+//
+// The reference computes a layer as x @ W then gather -> * norm ->
+// scatter_add (src/gcn_meta/models/gcn_base_models.py:201, 223-237); the
+// association and the numerics follow fused.hip's F = 128 kernels (the
+// aggregation bit for bit the SpMM's, the dense product bf16x6), but the
+// shapes of a 256-wide layer change three things:
+//
+// * one WAVE per row: a gathered row is 1 KB = 64 lanes x 16 B, so the
+//   row's edges are wave-uniform.  Edge metadata is loaded 64 slots at a time
+//   lane-parallel and broadcast with v_readlane into SGPRs, and every gathered
+//   row gets its own buffer resource whose base is X + col * ldx computed in
+//   64-bit scalar arithmetic: no 32-bit offset limit on the table (config 5's
+//   [50M, 256] table is 51 GB), and a slot past the row's end gets a
+//   zero-byte resource (the load returns 0 without touching memory).
+// * W does not fit on chip: its three bf16 terms are 384 KB, the LDS holds
+//   160 KB and a wave's share of the fragments (32 columns x 256 k) would be
+//   192 VGPRs.  A prep launch splits W (W^T for the adjoint) once into a
+//   fragment-ordered image (ks, n-tile, term, lane; 16 B per lane), and each
+//   wave streams its two n-tiles' fragments from L2 every chunk (48 KB per
+//   wave per 16-row chunk), one k-step ahead of the MFMAs, the first k-step
+//   issued under the tail of the gathers.
+// * 16-row chunks: the three term images of a chunk are 24 KB (rows of
+//   512 B, 16-B chunk ch of row r at ch ^ (r & 15): conflict-free for the
+//   16x16x32 A-operand reads and the row writes), double-buffered, plus two
+//   fp32 staging tiles of 16 KB (column c of row r at c ^ (((r >> 2) & 3) << 4):
+//   conflict-free MFMA-layout writes and whole-row reads): 80 KB, two
+//   workgroups per CU, one barrier per chunk as in the F = 128 forward.
+//
+// Chunk loop (persistent 512-thread workgroups, chunk c to workgroup
+// c % grid): Phase A -- wave w aggregates rows 2w, 2w + 1 of the chunk (U
+// gathered rows in flight, folded in edge order with separately rounded
+// products and adds: mgcn_spmm_fwd / _bwd bit for bit) into the images;
+// barrier; the previous chunk's staged rows leave as whole 1-KB rows (the
+// ReLU mask words from four ballots; backward: the lower layer's mask,
+// column sums and divisor applied on the staged row); Phase B -- wave w
+// multiplies the chunk by its 32 output columns on v_mfma_f32_16x16x32_bf16
+// (bf16x6) and stages the result.
+//
+// ReLU mask words at F = 256: [rows][8] u32, feature f at word
+// 4 (f >> 7) + (f & 3), bit (f & 127) >> 2 (the F <= 128 layout, twice).
+//
+// Roofline: HBM-bound like the SpMM (B_spmm = 8 (N + 1) + nnz (8 + 4F) +
+// 4 N F; + 4 N F for Z, + 32 N for the masks); 2 N F^2 x 6 bf16 MFMA flops
+// and 24 KB of L2-resident W fragments per row ride under the gathers.
+
+#include "mgcn_internal.h"
+#include "x6.h"
+
+namespace mgcn {
+namespace {
+
+using namespace x6;
+
+constexpr int kWF = 256;
+constexpr int kWRows = 16;
+constexpr int kWWaves = 8;
+constexpr int kWThreads = 64 * kWWaves;
+constexpr int kWImg = kWRows * kWF * 2;           // one bf16 term image: 8 KB
+constexpr int kWBuf = 3 * kWImg;                  // a chunk's three images: 24 KB
+constexpr int kWStage = kWRows * kWF * 4;         // fp32 staging tile: 16 KB
+constexpr int kWStageOff = 2 * kWBuf;
+constexpr int kWLds = kWStageOff + 2 * kWStage;   // 80 KB
+static_assert(2 * kWLds <= 160 * 1024, "two wide workgroups per CU");
+constexpr int kWKs = kWF / 32;                    // k-steps of 16x16x32
+constexpr int kWNt = kWF / 16;                    // 16-column n-tiles
+constexpr int kWImgFrags = kWKs * kWNt * 3 * 64;  // 16-B fragments of the W image
+constexpr int kWMaskWords = 8;                    // mask words per row
+
+constexpr int WEPI_STORE = 0, WEPI_RELU = 1, WEPI_RELU_DIV = 2;
+
+__device__ __forceinline__ int wimg_off(int row, int ch) {
+  return 512 * row + 16 * (ch ^ (row & 15));
+}
+__device__ __forceinline__ int wstage(int row, int col) {
+  return row * kWF + (col ^ (((row >> 2) & 3) << 4));
+}
+
+// W (B[k][n] = W[k][n], the forward) or W^T (B[k][n] = W[n][k], the
+// adjoint's dX = dH W^T) split into bf16 terms in MFMA fragment order:
+// fragment ((ks * 16 + nt) * 3 + term) * 64 + lane holds, for lane
+// (g4 = lane >> 4, l16 = lane & 15), B[32 ks + 8 g4 + j][16 nt + l16], j < 8.
+__global__ __launch_bounds__(256) void wide_wimg_kernel(const float *__restrict__ W, int64_t ldw,
+                                                        int trans, u32x4 *__restrict__ img) {
+  const int idx = (int)(blockIdx.x * 256 + threadIdx.x);
+  if (idx >= kWKs * kWNt * 64) return;
+  const int lane = idx & 63, nt = (idx >> 6) & (kWNt - 1), ks = idx >> 10;
+  const int l16 = lane & 15, g4 = lane >> 4;
+  const int n = 16 * nt + l16;
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 32 * ks + 8 * g4 + j;
+    v[j] = trans ? W[(int64_t)n * ldw + k] : W[(int64_t)k * ldw + n];
+  }
+  bf16x8 h, m, l;
+  split3_bf16(v, h, m, l);
+  u32x4 *o = img + ((ks * kWNt + nt) * 3) * 64 + lane;
+  o[0] = __builtin_bit_cast(u32x4, h);
+  o[64] = __builtin_bit_cast(u32x4, m);
+  o[128] = __builtin_bit_cast(u32x4, l);
+}
+
+struct WideArgs {
+  int64_t n_rows;
+  const int64_t *rowptr;
+  const int32_t *col;
+  const float *w;         // per-slot weights, nullable
+  const float *X;         // gathered table (X forward, dY backward), rows of ldx floats
+  int64_t ldx;
+  const u32x4 *wimg;      // wide_wimg_kernel's image (W forward, W^T backward)
+  const float *bias;      // forward, nullable
+  float *Y;               // forward Y / backward dX
+  int64_t ldy;
+  uint32_t *mask_out;     // forward: [n_rows][8] ReLU mask words, nullable
+  float *Z;               // forward: the aggregate, nullable
+  int64_t ldz;
+  const float *row_scale;      // backward 'rw' post-scale, nullable
+  const uint32_t *mask_in;     // backward: the lower layer's [n_rows][8] mask words
+  const float *row_div;        // backward mean divisor
+  float *colsum_partial;       // backward: [grid][256]
+  int mean, relu;
+};
+
+// a row's edge slots: [beg, beg + deg) (wave-uniform), and lane l's slot
+// beg + l (col, weight) of the first 64
+struct WRow {
+  int64_t beg;
+  int64_t deg;
+  int mc;
+  float mw;
+};
+
+__device__ __forceinline__ void wrow_ptr(const int64_t *__restrict__ rowptr, int64_t row, bool ok,
+                                         WRow &m) {
+  m.beg = ok ? rowptr[row] : 0;
+  m.deg = ok ? rowptr[row + 1] - m.beg : 0;
+}
+
+__device__ __forceinline__ void wrow_first(const int32_t *__restrict__ col,
+                                           const float *__restrict__ w, int lane, WRow &m) {
+  m.mc = 0;
+  m.mw = 1.0f;
+  if (lane < m.deg) {
+    m.mc = col[m.beg + lane];
+    if (w != nullptr) m.mw = w[m.beg + lane];
+  }
+}
+
+// acc = sum_k X[col_k] * w_k over the row's slots in order (products and
+// sums rounded separately): lane l holds features 4 l .. 4 l + 3
+template <int U>
+__device__ __forceinline__ void wide_gather(const float *__restrict__ X, int64_t ldx,
+                                            const int32_t *__restrict__ col,
+                                            const float *__restrict__ w, const WRow &m, int lane,
+                                            float (&acc)[4]) {
+  acc[0] = acc[1] = acc[2] = acc[3] = 0.0f;
+  int mc = m.mc;
+  float mw = m.mw;
+  const int64_t deg = m.deg;
+  for (int64_t e0 = 0; e0 < deg; e0 += 64) {
+    if (e0 > 0) {  // rows longer than one metadata batch load the rest in place
+      mc = 0;
+      mw = 1.0f;
+      if (e0 + lane < deg) {
+        mc = col[m.beg + e0 + lane];
+        if (w != nullptr) mw = w[m.beg + e0 + lane];
+      }
+    }
+    const int nb = (int)(deg - e0 < 64 ? deg - e0 : 64);  // wave-uniform
+    for (int k0 = 0; k0 < nb; k0 += U) {
+      float4 xv[U];
+      float wk[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = (k0 + u) & 63;
+        const int ck = __builtin_amdgcn_readlane(mc, k);
+        wk[u] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mw), k));
+        // the row's own resource (64-bit base in SGPRs); slots past the row
+        // end get a zero-byte one: the load returns 0 and moves no bytes
+        const auto rs = buf_rsrc(X + (int64_t)ck * ldx, k0 + u < nb ? kWF * 4 : 0);
+        xv[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * lane, 0, 0));
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (k0 + u < nb) {  // wave-uniform: strictly ascending edge order
+          acc[0] = __fadd_rn(acc[0], __fmul_rn(xv[u].x, wk[u]));
+          acc[1] = __fadd_rn(acc[1], __fmul_rn(xv[u].y, wk[u]));
+          acc[2] = __fadd_rn(acc[2], __fmul_rn(xv[u].z, wk[u]));
+          acc[3] = __fadd_rn(acc[3], __fmul_rn(xv[u].w, wk[u]));
+        }
+      }
+    }
+  }
+}
+
+// one 16-row chunk's W fragments of k-step ks for this wave's two n-tiles
+struct WFrag {
+  u32x4 t[2][3];
+};
+
+__device__ __forceinline__ void load_wfrag(const __amdgpu_buffer_rsrc_t rw, int wave, int ks,
+                                           int lane, WFrag &f) {
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int term = 0; term < 3; ++term)
+      f.t[t][term] = __builtin_amdgcn_raw_buffer_load_b128(
+          rw, 16 * ((((ks * kWNt + 2 * wave + t) * 3) + term) * 64 + lane), 0, 0);
+}
+
+template <int U, bool BWD, int EPI>
+__global__ __launch_bounds__(kWThreads, 4) void spmm_xw_wide_kernel(const WideArgs a) {
+  __shared__ __attribute__((aligned(16))) char lds[kWLds];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l16 = lane & 15, g4 = lane >> 4;
+  const int64_t n_chunks = (a.n_rows + kWRows - 1) / kWRows;
+  const auto rw = buf_rsrc(a.wimg, (uint32_t)(kWImgFrags * 16));
+  const bool has_b = !BWD && a.bias != nullptr;
+  float bcol[2] = {0.0f, 0.0f};
+  if (has_b) {
+    bcol[0] = a.bias[32 * wave + l16];
+    bcol[1] = a.bias[32 * wave + 16 + l16];
+  }
+  auto rows_in = [&](int64_t c) -> uint32_t {
+    const int64_t r = a.n_rows - c * kWRows;
+    return (uint32_t)(r <= 0 ? 0 : r >= kWRows ? kWRows : r);
+  };
+
+  // backward epilogue state: the flushed rows' mask words / divisors are
+  // loaded at the start of the iteration (under the gathers), the column
+  // sums of this thread's four features (rows w and w + 8 of its chunks)
+  float cs[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  u32x4 mk[2] = {};
+  float dv[2] = {1.0f, 1.0f};
+  auto prefetch_epi = [&](int64_t c) {
+    if constexpr (BWD && EPI != WEPI_STORE) {
+      const int64_t r0 = c * kWRows;
+      const uint32_t rv = rows_in(c);
+      const auto rm = buf_rsrc(a.mask_in + r0 * kWMaskWords, rv * kWMaskWords * 4u);
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+        mk[m] = __builtin_amdgcn_raw_buffer_load_b128(
+            rm, 4 * ((wave + 8 * m) * kWMaskWords + 4 * (lane >> 5)), 0, 0);
+      if constexpr (EPI == WEPI_RELU_DIV) {
+        const auto rd = buf_rsrc(a.row_div + r0, rv * 4u);
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+          dv[m] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rd, 4 * (wave + 8 * m), 0, 0));
+      }
+    }
+  };
+
+  // staged rows of chunk c leave as whole 1-KB rows: wave w takes rows w, w + 8
+  auto flush = [&](int64_t c, const float *stage) {
+    const int64_t r0 = c * kWRows;
+    const uint32_t rv = rows_in(c);
+    const auto ry = buf_rsrc(a.Y + r0 * a.ldy, rv * (uint32_t)a.ldy * 4u);
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int lr = wave + 8 * m;
+      float v[4];
+      *reinterpret_cast<float4 *>(v) = *reinterpret_cast<const float4 *>(stage + wstage(lr, 4 * lane));
+      if constexpr (BWD && EPI != WEPI_STORE) {
+        // feature 4 lane + j: word 4 (lane >> 5) + j, bit lane & 31
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[j] = ((mk[m][j] >> (lane & 31)) & 1u) ? v[j] : 0.0f;
+          cs[j] = __fadd_rn(cs[j], v[j]);  // rows past the end staged zeros
+        }
+        if constexpr (EPI == WEPI_RELU_DIV) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = __fdiv_rn(v[j], dv[m]);
+        }
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, *reinterpret_cast<float4 *>(v)),
+                                             ry, 4 * (int)(lr * a.ldy + 4 * lane), 0, 0);
+      if constexpr (!BWD) {
+        if (a.mask_out != nullptr) {
+          const uint64_t b0 = __ballot(v[0] > 0.0f), b1 = __ballot(v[1] > 0.0f);
+          const uint64_t b2 = __ballot(v[2] > 0.0f), b3 = __ballot(v[3] > 0.0f);
+          if (lane == 0 && (uint32_t)lr < rv) {
+            uint4 *mo = reinterpret_cast<uint4 *>(a.mask_out + (r0 + lr) * kWMaskWords);
+            mo[0] = make_uint4((uint32_t)b0, (uint32_t)b1, (uint32_t)b2, (uint32_t)b3);
+            mo[1] = make_uint4((uint32_t)(b0 >> 32), (uint32_t)(b1 >> 32), (uint32_t)(b2 >> 32),
+                               (uint32_t)(b3 >> 32));
+          }
+        }
+      }
+    }
+  };
+
+  const int64_t n_my = blockIdx.x < n_chunks ? (n_chunks - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+  // the rows of this wave in order: row k = chunk (k >> 1) of this workgroup, row 2 wave + (k & 1)
+  auto row_of = [&](int64_t k) -> int64_t {
+    return ((int64_t)blockIdx.x + (k >> 1) * gridDim.x) * kWRows + 2 * wave + (k & 1);
+  };
+  WRow cur, nxt;
+  wrow_ptr(a.rowptr, row_of(0), row_of(0) < a.n_rows, cur);
+  wrow_first(a.col, a.w, lane, cur);
+  wrow_ptr(a.rowptr, row_of(1), row_of(1) < a.n_rows && 1 < 2 * n_my, nxt);
+  int it = 0;
+  for (int64_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x, ++it) {
+    char *buf = lds + (it & 1) * kWBuf;
+    const int64_t r0 = chunk * kWRows;
+    if (it > 0) prefetch_epi(chunk - gridDim.x);
+    // ---- Phase A: the chunk's rows -> bf16 term images ------------------
+#pragma unroll 1
+    for (int p = 0; p < 2; ++p) {
+      const int lr = 2 * wave + p;
+      const int64_t k = 2 * it + p;
+      wrow_first(a.col, a.w, lane, nxt);
+      WRow nn;
+      const int64_t rk2 = row_of(k + 2);
+      wrow_ptr(a.rowptr, rk2, rk2 < a.n_rows && k + 2 < 2 * n_my, nn);
+      float acc[4];
+      wide_gather<U>(a.X, a.ldx, a.col, a.w, cur, lane, acc);
+      const bool row_ok = r0 + lr < a.n_rows;
+      if constexpr (!BWD) {
+        if (a.Z != nullptr) {
+          const auto rz = buf_rsrc(a.Z + r0 * a.ldz, rows_in(chunk) * (uint32_t)a.ldz * 4u);
+          __builtin_amdgcn_raw_buffer_store_b128(
+              __builtin_bit_cast(u32x4, make_float4(acc[0], acc[1], acc[2], acc[3])), rz,
+              4 * (int)(lr * a.ldz + 4 * lane), 0, 0);
+        }
+        if (a.mean) {
+          const float c = (float)(cur.deg > 1 ? cur.deg : 1);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[j] = __fdiv_rn(acc[j], c);
+        }
+      } else {
+        if (a.row_scale != nullptr && row_ok) {
+          const float sc = a.row_scale[r0 + lr];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[j] = __fmul_rn(acc[j], sc);
+        }
+      }
+      uint32_t hi[2], mid[2], lo[2];
+      split3_pair(f32x2{acc[0], acc[1]}, hi[0], mid[0], lo[0]);
+      split3_pair(f32x2{acc[2], acc[3]}, hi[1], mid[1], lo[1]);
+      char *img = buf + wimg_off(lr, lane >> 1) + 8 * (lane & 1);
+      *reinterpret_cast<uint2 *>(img) = make_uint2(hi[0], hi[1]);
+      *reinterpret_cast<uint2 *>(img + kWImg) = make_uint2(mid[0], mid[1]);
+      *reinterpret_cast<uint2 *>(img + 2 * kWImg) = make_uint2(lo[0], lo[1]);
+      cur = nxt;
+      nxt = nn;
+    }
+    // the first k-step's W fragments, in flight across the barrier
+    WFrag fc, fn;
+    load_wfrag(rw, wave, 0, lane, fc);
+    __syncthreads();
+    // the previous chunk's staged rows go out
+    if (it > 0)
+      flush(chunk - gridDim.x,
+            reinterpret_cast<const float *>(lds + kWStageOff + ((it + 1) & 1) * kWStage));
+
+    // ---- Phase B: the chunk (16 x 256) times this wave's 32 columns ------
+    f32x4_t acc2[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc2[t][r] = 0.0f;
+#pragma unroll
+    for (int ks = 0; ks < kWKs; ++ks) {
+      if (ks + 1 < kWKs) load_wfrag(rw, wave, ks + 1, lane, fn);
+      const int off = wimg_off(l16, 4 * ks + g4);
+      const bf16x8 ah = *reinterpret_cast<const bf16x8 *>(buf + off);
+      const bf16x8 am = *reinterpret_cast<const bf16x8 *>(buf + kWImg + off);
+      const bf16x8 al = *reinterpret_cast<const bf16x8 *>(buf + 2 * kWImg + off);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        acc2[t] = mfma16_x6(ah, am, al, __builtin_bit_cast(bf16x8, fc.t[t][0]),
+                            __builtin_bit_cast(bf16x8, fc.t[t][1]),
+                            __builtin_bit_cast(bf16x8, fc.t[t][2]), acc2[t]);
+      if (ks + 1 < kWKs) fc = fn;
+    }
+    float *stage = reinterpret_cast<float *>(lds + kWStageOff + (it & 1) * kWStage);
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = acc2[t][r];
+        if constexpr (!BWD) {
+          if (has_b) v = __fadd_rn(v, bcol[t]);
+          if (a.relu) v = (v < 0.0f) ? 0.0f : v;
+        }
+        stage[wstage(4 * g4 + r, 32 * wave + 16 * t + l16)] = v;
+      }
+  }
+  if (it > 0) {
+    prefetch_epi(blockIdx.x + (int64_t)(it - 1) * gridDim.x);
+    __syncthreads();
+    flush(blockIdx.x + (int64_t)(it - 1) * gridDim.x,
+          reinterpret_cast<const float *>(lds + kWStageOff + ((it + 1) & 1) * kWStage));
+  }
+  if constexpr (BWD && EPI != WEPI_STORE) {
+    // column sums: fold the eight waves of each feature in wave order
+    __syncthreads();
+    float *red = reinterpret_cast<float *>(lds);  // [8 waves][256]
+    *reinterpret_cast<float4 *>(red + wave * kWF + 4 * lane) = make_float4(cs[0], cs[1], cs[2], cs[3]);
+    __syncthreads();
+    if (tid < kWF) {
+      float c = 0.0f;
+#pragma unroll
+      for (int w = 0; w < kWWaves; ++w) c = __fadd_rn(c, red[w * kWF + tid]);
+      a.colsum_partial[(int64_t)blockIdx.x * kWF + tid] = c;
+    }
+  }
+}
+
+int wide_grid() {
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 256;
+  return 2 * cus;
+}
+
+template <int U>
+int launch_wide(const WideArgs &a, bool bwd, int epi, int grid, hipStream_t s) {
+  if (!bwd)
+    hipLaunchKernelGGL((spmm_xw_wide_kernel<U, false, WEPI_STORE>), dim3(grid), dim3(kWThreads), 0,
+                       s, a);
+  else if (epi == WEPI_RELU_DIV)
+    hipLaunchKernelGGL((spmm_xw_wide_kernel<U, true, WEPI_RELU_DIV>), dim3(grid), dim3(kWThreads),
+                       0, s, a);
+  else if (epi == WEPI_RELU)
+    hipLaunchKernelGGL((spmm_xw_wide_kernel<U, true, WEPI_RELU>), dim3(grid), dim3(kWThreads), 0, s,
+                       a);
+  else
+    hipLaunchKernelGGL((spmm_xw_wide_kernel<U, true, WEPI_STORE>), dim3(grid), dim3(kWThreads), 0,
+                       s, a);
+  return check_launch("spmm_xw_wide_kernel");
+}
+
+int launch_wimg(const float *W, int64_t ldw, bool trans, u32x4 *img, hipStream_t s) {
+  hipLaunchKernelGGL(wide_wimg_kernel, dim3(kWKs * kWNt * 64 / 256), dim3(256), 0, s, W, ldw,
+                     trans ? 1 : 0, img);
+  return check_launch("wide_wimg_kernel");
+}
+
+}  // namespace
+
+size_t xw_wide_workspace_bytes(bool bwd) {
+  return align_up((size_t)kWImgFrags * 16, 256) +
+         (bwd ? align_up((size_t)wide_grid() * kWF * 4, 256) : 0);
+}
+
+int xw_wide_fwd(int64_t n_rows, const int64_t *rowptr, const int32_t *col, const float *w,
+                const float *X, int64_t ldx, const float *W, int64_t ldw, const float *bias,
+                float *Y, int64_t ldy, int mean, int relu, uint32_t *relu_mask, float *Z,
+                int64_t ldz, void *workspace, int unroll, hipStream_t s) {
+  u32x4 *img = static_cast<u32x4 *>(workspace);
+  if (int rc = launch_wimg(W, ldw, false, img, s)) return rc;
+  WideArgs a{};
+  a.n_rows = n_rows;
+  a.rowptr = rowptr;
+  a.col = col;
+  a.w = w;
+  a.X = X;
+  a.ldx = ldx;
+  a.wimg = img;
+  a.bias = bias;
+  a.Y = Y;
+  a.ldy = ldy;
+  a.mask_out = relu_mask;
+  a.Z = Z;
+  a.ldz = ldz;
+  a.mean = mean;
+  a.relu = relu;
+  const int64_t n_chunks = (n_rows + kWRows - 1) / kWRows;
+  int64_t grid = wide_grid();
+  if (grid > n_chunks) grid = n_chunks;
+  return unroll == 8 ? launch_wide<8>(a, false, WEPI_STORE, (int)grid, s)
+                     : launch_wide<4>(a, false, WEPI_STORE, (int)grid, s);
+}
+
+int xw_wide_bwd_dx(int64_t n_rows, const int64_t *rowptr_t, const int32_t *col_t,
+                   const float *w_t, const float *row_scale, const float *dY, int64_t lddy,
+                   const float *W, int64_t ldw, float *dX, int64_t lddx,
+                   const uint32_t *relu_mask, const float *row_div, float *colsum,
+                   void *workspace, int unroll, hipStream_t s) {
+  u32x4 *img = static_cast<u32x4 *>(workspace);
+  float *partial = reinterpret_cast<float *>(static_cast<char *>(workspace) +
+                                             align_up((size_t)kWImgFrags * 16, 256));
+  if (int rc = launch_wimg(W, ldw, true, img, s)) return rc;
+  const int epi = relu_mask == nullptr ? WEPI_STORE : row_div != nullptr ? WEPI_RELU_DIV : WEPI_RELU;
+  WideArgs a{};
+  a.n_rows = n_rows;
+  a.rowptr = rowptr_t;
+  a.col = col_t;
+  a.w = w_t;
+  a.X = dY;
+  a.ldx = lddy;
+  a.wimg = img;
+  a.Y = dX;
+  a.ldy = lddx;
+  a.row_scale = row_scale;
+  a.mask_in = relu_mask;
+  a.row_div = row_div;
+  a.colsum_partial = partial;
+  const int64_t n_chunks = (n_rows + kWRows - 1) / kWRows;
+  int64_t grid = wide_grid();
+  if (grid > n_chunks) grid = n_chunks;
+  int rc = unroll == 8 ? launch_wide<8>(a, true, epi, (int)grid, s)
+                       : launch_wide<4>(a, true, epi, (int)grid, s);
+  if (rc || epi == WEPI_STORE) return rc;
+  return launch_colsum_fold(partial, grid, kWF, colsum, s);
+}
+
+}  // namespace mgcn

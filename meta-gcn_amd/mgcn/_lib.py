@@ -71,9 +71,11 @@ SIGNATURES = {
     "mgcn_edge_merge_workspace_bytes": (_sz, [_i64, _i64]),
     "mgcn_edge_merge_greedy": (_int, [_i64, _i64, _vp, _vp, _vp, _vp, _sz, _vp, _vp, _vp, _vp]),
     "mgcn_spmm_xw_supported": (_int, [_i32, _i32, _int]),
+    "mgcn_spmm_xw_bwd_full_supported": (_int, [_i32, _i32]),
+    "mgcn_spmm_xw_fwd_workspace_bytes": (_sz, [_i32, _i32]),
     "mgcn_spmm_xw_fwd": (_int, [_i64, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp,
-                                _i64, _int, _int, _vp, _vp, _i64, _vp]),
-    "mgcn_spmm_xw_bwd_workspace_bytes": (_sz, [_i64]),
+                                _i64, _int, _int, _vp, _vp, _i64, _vp, _sz, _vp]),
+    "mgcn_spmm_xw_bwd_workspace_bytes": (_sz, [_i64, _i32, _i32]),
     "mgcn_spmm_xw_bwd": (_int, [_i64, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64,
                                 _vp, _i64, _vp, _i64, _int, _vp, _i64, _vp, _vp, _vp, _vp, _vp,
                                 _vp, _sz, _vp]),

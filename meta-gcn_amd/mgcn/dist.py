@@ -72,10 +72,10 @@ class HipBackend:
         return schedule_rows(view)
 
     def fused_ok(self, shard, F_in, F_out, reduce):
-        from .ops import gemm_bwd_supported, spmm_xw_supported
+        from .ops import dw_pass_supported, spmm_xw_supported
         return (spmm_xw_supported(shard.fwd, F_in, F_out, reduce) and
                 spmm_xw_supported(shard.bwd, F_out, F_in, L.REDUCE_SUM) and
-                gemm_bwd_supported(F_in, F_out))
+                dw_pass_supported(F_in, F_out))
 
     def spmm_xw_fwd(self, *a, **k):
         from .ops import spmm_xw_fwd
@@ -89,9 +89,12 @@ class HipBackend:
                            row_div=row_div, dx_out=out)[2]
 
     def gemm_bwd_dw(self, Z, dY, W, dh_colsum=False):
-        from .ops import gemm_bwd
-        dW, _, cs = gemm_bwd(Z, dY, W, want_dx=False, dh_colsum=dh_colsum)
-        return dW, cs
+        from .ops import dw_pass
+        return dw_pass(Z, dY, W, dh_colsum=dh_colsum)
+
+    def mask_words(self, F):
+        from .ops import mask_words
+        return mask_words(F)
 
     def spmm_fwd(self, *a, **k):
         from .ops import spmm_fwd
@@ -429,7 +432,8 @@ class _ShardedStack(torch.autograd.Function):
             z = torch.empty(sh.pad_rows, F_in, dtype=torch.float32, device=dev) if want_z else None
             rm = None
             if relus[i] and not last:
-                rm = torch.empty(sh.pad_rows, 4, dtype=torch.int32, device=dev)
+                rm = torch.empty(sh.pad_rows, 4 * ((F_out + 127) // 128), dtype=torch.int32,
+                                 device=dev)
             nxt = None if last else new_table(sh, F_out, torch.float32, dev, "f%d" % (i & 1))
             works = []
             for c in range(C):

@@ -130,12 +130,27 @@ def spmm_xw_supported(view: CSRView, F_in: int, F_out: int, reduce: int,
     """True when :func:`spmm_xw_fwd` (``view`` the fwd view, gathering [n_cols,
     F_in] rows of leading dimension ``ld``) or :func:`spmm_xw_bwd` (``view``
     the bwd view, gathering dY, F_in / F_out swapped) takes this layer:
-    128 -> 128, sum or mean, no heavy rows (skewed graphs keep the GEMM +
-    heavy-row SpMM path) and a gathered table within the kernels' 32-bit
-    offsets (:data:`XW_MAX_TABLE_BYTES`)."""
+    128 -> 128 or 256 -> 256, sum or mean, no heavy rows (skewed graphs keep
+    the GEMM + heavy-row SpMM path); at 128 a gathered table within the
+    kernels' 32-bit offsets (:data:`XW_MAX_TABLE_BYTES`; the 256-wide kernels
+    give every gathered row a 64-bit base).  At 256 the backward is the
+    dX-only form (:func:`xw_full_supported`)."""
     ld = int(F_in) if ld is None else max(int(ld), int(F_in))
-    return (view.n_heavy == 0 and 0 < view.n_cols * ld * 4 <= XW_MAX_TABLE_BYTES and
+    small = int(F_in) <= 128
+    return (view.n_heavy == 0 and view.n_cols > 0 and
+            (not small or view.n_cols * ld * 4 <= XW_MAX_TABLE_BYTES) and
             bool(L.load().mgcn_spmm_xw_supported(int(F_in), int(F_out), int(reduce))))
+
+
+def xw_full_supported(F_in: int, F_out: int) -> bool:
+    """mgcn_spmm_xw_bwd's dW-accumulating form (and its max adjoint): 128 x 128."""
+    return bool(L.load().mgcn_spmm_xw_bwd_full_supported(int(F_in), int(F_out)))
+
+
+def mask_words(F: int) -> int:
+    """int32 ReLU mask words per row: 4 per 128 features (bit b of word
+    4 (f >> 7) + v <-> feature f = 128 (f >> 7) + 4 b + v)."""
+    return 4 * ((int(F) + 127) // 128)
 
 
 def layer_fusable(plan: GraphPlan, x: torch.Tensor, W: torch.Tensor, reduce: int) -> bool:
@@ -179,10 +194,11 @@ def spmm_xw_fwd(view: CSRView, w: torch.Tensor | None, X: torch.Tensor, W: torch
         # the kernel writes n_rows x 16 B of mask words through this pointer
         if not relu:
             raise ValueError("spmm_xw_fwd: relu_mask needs relu")
-        if (relu_mask.shape != (view.n_rows, 4) or relu_mask.dtype != torch.int32 or
+        mw = mask_words(F_out)
+        if (relu_mask.shape != (view.n_rows, mw) or relu_mask.dtype != torch.int32 or
                 not relu_mask.is_contiguous() or relu_mask.data_ptr() % 16):
             raise ValueError(f"spmm_xw_fwd: relu_mask must be a contiguous, 16-byte aligned "
-                             f"int32 [{view.n_rows}, 4] tensor")
+                             f"int32 [{view.n_rows}, {mw}] tensor")
     Y = out if out is not None else torch.empty(view.n_rows, F_out, dtype=torch.float32,
                                                 device=dev)
     Z = None
@@ -195,6 +211,8 @@ def spmm_xw_fwd(view: CSRView, w: torch.Tensor | None, X: torch.Tensor, W: torch
                               or t.data_ptr() % 16):
             raise ValueError(f"spmm_xw_fwd: {name} must be float32 [{view.n_rows}, {f}] with "
                              f"16-byte aligned rows")
+    ws_bytes = int(lib.mgcn_spmm_xw_fwd_workspace_bytes(F_in, F_out))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev) if ws_bytes else None
     tname = "spmm_xw_fwd_z" if want_z else "spmm_xw_fwd"
     if _TIMER is not None:
         _TIMER(tname, True, view.n_rows, view.edges)
@@ -203,7 +221,8 @@ def spmm_xw_fwd(view: CSRView, w: torch.Tensor | None, X: torch.Tensor, W: torch
                                   L.ptr(view.col), L.ptr(w), L.ptr(X), X.stride(0), L.ptr(W),
                                   W.stride(0), L.ptr(bias), L.ptr(Y), Y.stride(0), reduce,
                                   int(bool(relu)), L.ptr(relu_mask), L.ptr(Z),
-                                  Z.stride(0) if Z is not None else 0, L.stream_of(dev))
+                                  Z.stride(0) if Z is not None else 0, L.ptr(ws), ws_bytes,
+                                  L.stream_of(dev))
     if _TIMER is not None:
         _TIMER(tname, False)
     L.check(rc, "mgcn_spmm_xw_fwd")
@@ -261,11 +280,12 @@ def spmm_xw_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tens
     if relu_mask is not None:
         if not want_dx:
             raise ValueError("spmm_xw_bwd: relu_mask needs want_dx")
-        if relu_mask.shape != (M, 4) or relu_mask.dtype != torch.int32:
-            raise ValueError(f"spmm_xw_bwd: relu_mask must be int32 [{M}, 4]")
+        mw = mask_words(F_in)
+        if relu_mask.shape != (M, mw) or relu_mask.dtype != torch.int32:
+            raise ValueError(f"spmm_xw_bwd: relu_mask must be int32 [{M}, {mw}]")
         relu_mask = relu_mask.contiguous()
         colsum = torch.empty(F_in, dtype=torch.float32, device=dev)
-    ws_bytes = int(lib.mgcn_spmm_xw_bwd_workspace_bytes(M))
+    ws_bytes = int(lib.mgcn_spmm_xw_bwd_workspace_bytes(M, F_in, F_out))
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
     tname = "spmm_xw_bwd_dx" if dx_only else "spmm_xw_bwd" if want_dx else "spmm_xw_bwd_dw"
     if _TIMER is not None:
@@ -522,6 +542,23 @@ def gemm_bwd(x: torch.Tensor, dH: torch.Tensor, W: torch.Tensor, want_dx: bool =
         _TIMER("gemm_bwd" if want_dx else "gemm_bwd_dw", False)
     L.check(rc, "mgcn_gemm_bwd")
     return dW, dX, colsum
+
+
+def dw_pass_supported(F_in: int, F_out: int) -> bool:
+    """The dense dW = Z^T dY pass of the reassociated backward: mgcn_gemm_bwd
+    (dW-only) at 128 x 128, mgcn_gemm_tn (bf16x6, 128 x 128 output tiles)
+    for other multiples of 128 (256 x 256: config 5)."""
+    return gemm_bwd_supported(F_in, F_out) or (int(F_in) % 128 == 0 and int(F_out) % 128 == 0)
+
+
+def dw_pass(Z: torch.Tensor, dY: torch.Tensor, W: torch.Tensor, dh_colsum: bool = False):
+    """(dW = Z^T dY, the column sums of dY or None) -- :func:`dw_pass_supported`."""
+    if gemm_bwd_supported(W.size(0), W.size(1)):
+        dW, _, cs = gemm_bwd(Z, dY, W, want_dx=False, dh_colsum=dh_colsum)
+        return dW, cs
+    dW = gemm_tn(Z, dY)
+    cs = relu_bwd_colsum(dY, None, False, True)[1] if dh_colsum else None
+    return dW, cs
 
 
 SMALL_K = 8  # mgcn_gemm_small_k: K <= 8, N <= 128
@@ -807,7 +844,7 @@ class _LayerXW(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, W, bias, plan: GraphPlan, norm: NormPlan, reduce: int, relu: bool):
         # Z = the aggregate before W: dW = Z^T dY needs no second gather
-        want_z = bool(ctx.needs_input_grad[1]) and gemm_bwd_supported(W.size(0), W.size(1))
+        want_z = bool(ctx.needs_input_grad[1]) and dw_pass_supported(W.size(0), W.size(1))
         Y = spmm_xw_fwd(plan.fwd, norm.w_fwd, x, W, reduce, bias, relu, want_z=want_z)
         Y, Z = Y if want_z else (Y, None)
         ctx.plan, ctx.norm, ctx.reduce, ctx.relu = plan, norm, reduce, relu
@@ -824,6 +861,11 @@ class _LayerXW(torch.autograd.Function):
         if Z is None:
             dY, db = relu_bwd_colsum(dZ.contiguous(), Y, ctx.relu, need_b,
                                      row_div=plan.in_cnt if mean else None)
+            if not xw_full_supported(W.size(0), W.size(1)):  # 256: W needs no grad here
+                dx = None
+                if ctx.needs_input_grad[0]:
+                    dx = spmm_xw_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, None, W)[1]
+                return dx, None, db, None, None, None, None
             dW, dx, _ = spmm_xw_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, x, W,
                                     want_dx=ctx.needs_input_grad[0])
             return dx, dW, db, None, None, None, None
@@ -835,7 +877,7 @@ class _LayerXW(torch.autograd.Function):
         else:
             dY, db = relu_bwd_colsum(dZ.contiguous(), Y, ctx.relu, need_b,
                                      row_div=plan.in_cnt if mean else None)
-        dW, _, cs = gemm_bwd(Z, dY, W, want_dx=False, dh_colsum=hcs)
+        dW, cs = dw_pass(Z, dY, W, dh_colsum=hcs)
         if hcs:
             db = cs
         dx = None
@@ -891,10 +933,17 @@ class _GCNStack(torch.autograd.Function):
             # the ReLU mask the next layer's dX GEMM reads (16 B per row)
             nxt = Ws[i + 1] if i + 1 < len(Ws) else None
             rm = None
-            if relu and nxt is not None and gemm_nn_epi_supported(nxt.size(1), nxt.size(0)):
-                rm = torch.empty(plan.fwd.n_rows, 4, dtype=torch.int32, device=h.device)
-            if _FUSE_XW and spmm_xw_supported(plan.fwd, W.size(0), W.size(1), reduce,
-                                              h.stride(0)):
+            xw = _FUSE_XW and spmm_xw_supported(plan.fwd, W.size(0), W.size(1), reduce,
+                                                h.stride(0))
+            if relu and nxt is not None and (
+                    gemm_nn_epi_supported(nxt.size(1), nxt.size(0)) or
+                    (xw and W.size(1) > 128 and
+                     spmm_xw_supported(plan.bwd, nxt.size(1), nxt.size(0), L.REDUCE_SUM))):
+                # (the 8-word masks of a 256-wide layer only from its fused
+                # forward, for the fused dX-only adjoint of the next layer)
+                rm = torch.empty(plan.fwd.n_rows, mask_words(W.size(1)), dtype=torch.int32,
+                                 device=h.device)
+            if xw:
                 # (A h) W in one launch: h @ W is never written (sum / mean);
                 # the aggregate A h is kept for dW = (A h)^T dY when the
                 # backward takes that form (same predicate as its z_path):
@@ -904,8 +953,8 @@ class _GCNStack(torch.autograd.Function):
                 below = i == 0 or (relus[i - 1] and rmasks[i - 1] is not None)
                 middle = 0 < i < len(Ws) - 1 and relus[i - 1]
                 want_z = (bool(ctx.needs_input_grad[5 + 2 * i]) and below and
-                          (_Z_MIDDLE or not middle) and
-                          gemm_bwd_supported(W.size(0), W.size(1)) and
+                          (_Z_MIDDLE or not middle or not xw_full_supported(*W.shape)) and
+                          dw_pass_supported(W.size(0), W.size(1)) and
                           spmm_xw_supported(plan.bwd, W.size(1), W.size(0), L.REDUCE_SUM))
                 h, am = spmm_xw_fwd(plan.fwd, norm.w_fwd, h, W, reduce, b, relu,
                                     relu_mask=rm, want_z=want_z), None
@@ -948,7 +997,7 @@ class _GCNStack(torch.autograd.Function):
         def z_path(l):  # dW = Z^T dY from the forward's aggregate (below)
             fused = l > 0 and relus[l - 1] and rmasks[l - 1].numel() > 0
             return bool(zs[l].numel() and (fused or l == 0) and
-                        gemm_bwd_supported(Ws[l].size(0), Ws[l].size(1)) and
+                        dw_pass_supported(Ws[l].size(0), Ws[l].size(1)) and
                         spmm_xw_supported(plan.bwd, Ws[l].size(1), Ws[l].size(0),
                                           L.REDUCE_SUM))
 
@@ -973,7 +1022,7 @@ class _GCNStack(torch.autograd.Function):
                 # product.  The gather runs only for dX (+ the lower layer's
                 # ReLU / bias gradient); the bottom layer needs no gather at all.
                 hcs = bool(top_z and l == top and ctx.has_bias[top])
-                gW[l], _, cs = gemm_bwd(zs[l], dY, W, want_dx=False, dh_colsum=hcs)
+                gW[l], cs = dw_pass(zs[l], dY, W, dh_colsum=hcs)
                 if hcs:
                     gb[top] = cs
                 if fused:
@@ -983,7 +1032,7 @@ class _GCNStack(torch.autograd.Function):
                 elif ctx.needs_input_grad[0]:
                     dx = spmm_xw_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, None, W)[1]
                 continue
-            if (_FUSE_XW and
+            if (_FUSE_XW and xw_full_supported(W.size(0), W.size(1)) and
                     spmm_xw_supported(plan.bwd, W.size(0), W.size(1), L.REDUCE_SUM)):
                 # adjoint SpMM + dW + dX (+ the lower layer's ReLU / bias
                 # gradient) in one pass: dH never leaves the chip (max: the

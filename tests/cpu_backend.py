@@ -168,7 +168,7 @@ class CpuBackend:
         if relu:
             y = torch.where(y < 0, torch.zeros_like(y), y)
         if relu_mask is not None:
-            relu_mask.copy_((y > 0).to(torch.int32)[:, :4])  # the double keeps a token mask
+            relu_mask.copy_((y > 0).to(torch.int32)[:, :relu_mask.size(1)])  # a token mask
             self._masks[relu_mask.data_ptr()] = (y > 0)
         if out is not None:
             out.copy_(y)
