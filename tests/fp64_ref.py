@@ -44,8 +44,11 @@ class A64:
 
 
 def within(err, bound, tol, atol=1e-6):
-    """(ok, worst err / bound) for |err| <= tol * bound + atol elementwise."""
+    """(ok, worst err / (tol bound + atol)) for |err| <= tol * bound + atol
+    elementwise; ``tol`` a number or a tensor broadcast against ``bound``
+    (e.g. a per-row rounding bound)."""
     err = err.abs()
-    ok = bool((err <= tol * bound + atol).all())
-    worst = float((err / (bound + atol / tol)).max()) if err.numel() else 0.0
+    lim = tol * bound + atol
+    ok = bool((err <= lim).all())
+    worst = float((err / lim).max()) if err.numel() else 0.0
     return ok, worst

@@ -17,7 +17,11 @@ botnet-shaped graphs batched (2 x 143,107 nodes), deg_K = out-degree:
       for bit the oracle chain, all 32 columns live in both directions;
   (c) bench_workloads' seeded model and inputs (x = [1, deg]): every layer's
       output against fp64 at its own input, and every parameter gradient
-      against the fp64 adjoint chain, within 1e-5 of the |.|-weighted chain.
+      against the fp64 adjoint chain, within the first-order rounding bound
+      of the |.|-weighted chain: gamma_n = n 2^-24 for a sum of n terms, so a
+      row of in-degree d is held to max(1e-5, (d + 2F) 2^-24) (the botnet
+      hubs sum ~6.5k same-signed terms at the input layer, x = 1), and the
+      adjoint chain to 1e-5 + (12 - l)(max out-degree + 2F) 2^-24 at layer l.
       The ReLU decisions are the kernels' own (the stack's saved masks), so
       a value that rounds across 0 does not fork the two chains.
 Config 4 (kernel/gin.py / graph_sage.py aggregators on the config-2 graph,
@@ -167,6 +171,10 @@ def test_config3_seeded_model_vs_fp64(cuda, oracle, config3_graph):
 
     wf, _, _ = oracle.edge_factors(ei.numpy(), N, "sm", deg=deg.numpy())
     A = A64(ei, wf, N, cuda)
+    u = 2.0 ** -24
+    deg_in = torch.bincount(eic[1], minlength=N).double()
+    tol_row = torch.clamp((deg_in + 64) * u, min=1e-5)[:, None]  # forward, per row
+    max_out = float(torch.bincount(eic[0], minlength=N).max())
     acts = [x[:, :1].double(), a1.double()] + [Zs[l].double() for l in range(L3 - 1)]
     m1 = [None] + [_bits(masks[l, :, 0]) for l in range(L3 - 1)]
     # layer 0 (1 -> 32 on the two-launch path): x = 1, so A (x W0) = W0 * (A 1)
@@ -183,7 +191,7 @@ def test_config3_seeded_model_vs_fp64(cuda, oracle, config3_graph):
         s = z1 + a @ Wr.t() + br
         sa = z1a + a.abs() @ Wr.abs().t() + br.abs()
         ref = s.clamp_min(0) if l < L3 - 1 else s
-        ok, worst = within(acts[l + 1] - ref, sa, 1e-5)
+        ok, worst = within(acts[l + 1] - ref, sa, tol_row)
         assert ok, ("forward", l, worst)
     a12 = acts[L3]
     yr = a12 @ d64(Wf).t() + d64(bf)
@@ -207,11 +215,12 @@ def test_config3_seeded_model_vs_fp64(cuda, oracle, config3_graph):
         dH = A.apply(dz1, transpose=True)
         dHa = A.apply(dz1a, transpose=True, absolute=True)
         gW, gWr, gbr = (d64(t.grad) for t in P[l])
+        tol = 1e-5 + (L3 - l) * (max_out + 64) * u
         for name, got, ref, bnd in [("dW", gW, a.t() @ dH, a.abs().t() @ dHa),
                                     ("dWr", gWr, ds.t() @ a, dsa.t() @ a.abs()),
                                     ("dbr", gbr, ds.sum(0), dsa.sum(0))]:
-            ok, worst = within(got - ref, bnd, 1e-5)
-            assert ok, (name, l, worst)
+            ok, worst = within(got - ref, bnd, tol)
+            assert ok, (name, l, worst, tol)
         d = dH @ W.t() + ds @ Wr
         da = dHa @ W.abs().t() + dsa @ Wr.abs()
 
