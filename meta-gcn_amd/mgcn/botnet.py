@@ -106,21 +106,31 @@ class GraphDataset:
 
 
 class GraphDataLoader:
-    """Batches of graphs collated PyG-style (data/dataloader.py)."""
+    """Batches of graphs collated PyG-style (data/dataloader.py).
+    ``share`` (data-parallel replicas, :class:`mgcn.dist.DataParallel`):
+    each global batch is cut down to this rank's share of its graphs (None
+    where the share is empty); ``generator``: the shuffle's RNG (every
+    replica must draw the same order)."""
 
-    def __init__(self, dataset, batch_size=1, shuffle=False):
+    def __init__(self, dataset, batch_size=1, shuffle=False, share=None, generator=None):
         self.dataset, self.batch_size, self.shuffle = dataset, int(batch_size), shuffle
+        self.share, self.generator = share, generator
 
     def __len__(self):
         return (len(self.dataset) + self.batch_size - 1) // self.batch_size
 
     def __iter__(self):
         n = len(self.dataset)
-        order = torch.randperm(n).tolist() if self.shuffle else list(range(n))
+        order = (torch.randperm(n, generator=self.generator).tolist() if self.shuffle
+                 else list(range(n)))
         for i in range(0, n, self.batch_size):
-            graphs = [self.dataset[j] for j in order[i:i + self.batch_size]]
-            b = Batch.from_data_list(graphs)
-            yield b
+            idx = order[i:i + self.batch_size]
+            if self.share is not None:
+                idx = self.share(idx)
+                if not idx:
+                    yield None
+                    continue
+            yield Batch.from_data_list([self.dataset[j] for j in idx])
 
 
 def save_npz(graphs, path: str) -> None:
@@ -276,13 +286,17 @@ def _forward(model, batch):
 
 
 @torch.no_grad()
-def evaluate(model, loader, criterion, device):
-    """train_botnet.py:249-283: loss and metrics per graph, averaged."""
+def evaluate(model, loader, criterion, device, dp=None):
+    """train_botnet.py:249-283: loss and metrics per graph, averaged.  With
+    ``dp`` (data-parallel replicas) every rank evaluates its share of the
+    graphs and the sums are combined (the same averages on every rank)."""
     model.eval()
     keys = ("loss", "acc", "fpr", "fnr", "rec", "prc", "f1")
     tot = dict.fromkeys(keys, 0.0)
     n = 0
     for batch in loader:
+        if batch is None:
+            continue
         batch.to(device)
         x = _forward(model, batch)
         y = batch.y.long()
@@ -293,6 +307,9 @@ def evaluate(model, loader, criterion, device):
         for k, v in zip(keys, vals):
             tot[k] += v
         n += 1
+    if dp is not None and dp.world > 1:
+        sums = dp.all_sum([tot[k] for k in keys] + [n])
+        tot, n = dict(zip(keys, sums[:-1])), int(sums[-1])
     return {k: v / max(n, 1) for k, v in tot.items()}
 
 
@@ -305,20 +322,43 @@ def _time_since(start):
 def train(train_ds, val_ds, test_ds, enc_sizes=(32,) * 8, residual_hop=0, deg_norm="sm",
           aggr="add", bias=False, dropout=0.0, final="proj", act="relu", layer_act="relu",
           lr=1e-3, weight_decay=5e-4, epochs=5, batch_size=1, shuffle=False, focal=False,
-          device="cuda:0", save_path=None, log=print):
+          device="cuda:0", save_path=None, log=print, dp=False, group=None, seed=None):
     """The train_botnet.py loop on mgcn.models.GCNModel; returns a history
-    dict (per-epoch train loss and validation metrics, final test metrics)."""
+    dict (per-epoch train loss and validation metrics, final test metrics).
+
+    ``dp=True`` (torch.distributed initialised, one process per GPU): the
+    same loop as data-parallel replicas (:class:`mgcn.dist.DataParallel`):
+    rank 0's initial parameters are broadcast, every global batch of
+    ``batch_size`` graphs is dealt out graph by graph, each rank's summed
+    loss is divided by the global node count (so the all-reduced gradient is
+    the single-process batch-mean one), every rank steps the same Adam;
+    validation / test graphs are split and their metric sums combined.
+    ``seed``: torch.manual_seed before the model is built (and the shuffle
+    order's generator)."""
     from .models import GCNModel
+    if seed is not None:
+        torch.manual_seed(seed)
     model = GCNModel(1, list(enc_sizes), 2, non_linear=act, non_linear_layer_wise=layer_act,
                      residual_hop=residual_hop, dropout=dropout, final_type=final,
                      pred_on="node", deg_norm=deg_norm, aggr=aggr, bias=bool(bias)).to(device)
-    criterion = FocalLoss(alpha=1, gamma=2) if focal else CrossEntropyLoss()
+    dpr = None
+    if dp:
+        from .dist import DataParallel
+        dpr = DataParallel(model.parameters(), group)
+        dpr.broadcast_params()
+    Crit = FocalLoss if focal else CrossEntropyLoss
+    kw = {"alpha": 1, "gamma": 2} if focal else {}
+    criterion = Crit(**kw)
+    crit_sum = Crit(reduction="sum", **kw)
     opt = torch.optim.Adam(model.parameters(), lr=lr, weight_decay=weight_decay)
     sched = torch.optim.lr_scheduler.ReduceLROnPlateau(opt, mode="min", factor=0.25, patience=1)
     stopper = EarlyStopping(patience=5, verbose=True)
-    train_loader = GraphDataLoader(train_ds, batch_size=batch_size, shuffle=shuffle)
-    val_loader = GraphDataLoader(val_ds, batch_size=1)
-    test_loader = GraphDataLoader(test_ds, batch_size=1)
+    gen = torch.Generator().manual_seed(seed if seed is not None else 0) if dpr else None
+    share = dpr.share if dpr is not None and dpr.world > 1 else None
+    train_loader = GraphDataLoader(train_ds, batch_size=batch_size, shuffle=shuffle, share=share,
+                                   generator=gen)
+    val_loader = GraphDataLoader(val_ds, batch_size=1, share=share)
+    test_loader = GraphDataLoader(test_ds, batch_size=1, share=share)
     hist = {"train_loss": [], "val": []}
     best_state, best_epoch = None, 0
     start = time.time()
@@ -326,16 +366,31 @@ def train(train_ds, val_ds, test_ds, enc_sizes=(32,) * 8, residual_hop=0, deg_no
         model.train()
         loss_sum, graphs = 0.0, 0
         for batch in train_loader:
-            batch.to(device)
             opt.zero_grad()
-            x = _forward(model, batch)
-            loss = criterion(x, batch.y.long())
-            loss.backward()
-            opt.step()
-            loss_sum += loss.item()
+            if share is None:
+                batch.to(device)
+                x = _forward(model, batch)
+                loss = criterion(x, batch.y.long())
+                loss.backward()
+                opt.step()
+                loss_sum += loss.item()
+            else:
+                # this rank's graphs: summed loss / the global batch's node count
+                n_loc = 0 if batch is None else int(batch.num_nodes)
+                (n_glob,) = dpr.all_sum([n_loc])
+                local = 0.0
+                if batch is not None:
+                    batch.to(device)
+                    x = _forward(model, batch)
+                    loss = crit_sum(x, batch.y.long()) / n_glob
+                    loss.backward()
+                    local = loss.item()
+                dpr.reduce_grads()
+                opt.step()
+                loss_sum += dpr.all_sum([local])[0]
             graphs += batch_size
         hist["train_loss"].append(loss_sum / max(graphs, 1))
-        m = evaluate(model, val_loader, criterion, device)
+        m = evaluate(model, val_loader, criterion, device, dpr)
         hist["val"].append(m)
         log(f"epoch {ep + 1}: train loss {hist['train_loss'][-1]:.5f}, val loss "
             f"{m['loss']:.5f}, acc {m['acc']:.5f}, f1 {m['f1']:.5f} ({_time_since(start)})")
@@ -352,7 +407,7 @@ def train(train_ds, val_ds, test_ds, enc_sizes=(32,) * 8, residual_hop=0, deg_no
     if best_state is not None:
         model.load_state_dict(best_state)
     hist["best_epoch"] = best_epoch
-    hist["test"] = evaluate(model, test_loader, criterion, device)
+    hist["test"] = evaluate(model, test_loader, criterion, device, dpr)
     log(f"test (best epoch {best_epoch + 1}): " +
         ", ".join(f"{k} {v:.5f}" for k, v in hist["test"].items()))
     return hist

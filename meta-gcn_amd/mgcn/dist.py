@@ -603,6 +603,131 @@ class ShardedGCN:
         return step
 
 
+class ShardedGCNStack(torch.nn.Module):
+    """The module surface of the sharded path: a :class:`mgcn.models.GCNStack`
+    (its GCNLayers and their reference-compatible parameters) run over a
+    destination-range sharded graph -- ``forward`` takes this rank's input
+    rows (or the replicated input in the exchange layout) and returns this
+    rank's output rows; gradients land on the wrapped stack's parameters,
+    partial per rank until :meth:`allreduce_grads` (one bucketed all_reduce)
+    makes them the single-device gradients.  Sum / mean stacks whose layers
+    below the top use ReLU run on :class:`_ShardedStack` (fused kernels,
+    chunked all-gathers overlapped with the compute); others layer by layer.
+
+    Equivalence with the single-device module (tests/test_dist_gloo.py,
+    tests/test_gpu_dist.py): forward rows and dX rows bit for bit, parameter
+    gradients within fp32 summation order.
+    """
+
+    def __init__(self, stack, edge_index, num_nodes, group=None, backend=None, chunks: int = 4,
+                 device=None, fused: bool = True, deg=None, emulate=None):
+        super().__init__()
+        self.stack = stack
+        layers = list(stack.layers)
+        nms = [layer.gcn.node_models[0] for layer in layers]
+        if any(len(layer.gcn.node_models) != 1 for layer in layers) or \
+                len({(nm.deg_norm, nm.aggr) for nm in nms}) != 1:
+            raise NotImplementedError("ShardedGCNStack: single-kernel layers with one deg_norm / "
+                                      "aggr")
+        acts = [layer.non_linear_name for layer in layers]
+        if any(a not in ("relu", "none") for a in acts):
+            raise NotImplementedError("ShardedGCNStack: 'relu' / 'none' layer activations")
+        self.group = group
+        self.backend = backend or HipBackend()
+        self.relus = tuple(a == "relu" for a in acts)
+        self.aggr = nms[0].aggr
+        self.reduce = L.REDUCE_CODES[self.aggr]
+        dev = device if device is not None else nms[0].weight_node.device
+        self.shard = build_shard(edge_index, num_nodes, nms[0].deg_norm, deg=deg, group=group,
+                                 backend=self.backend, device=dev, chunks=chunks, emulate=emulate)
+        self._nms = nms
+        self.fused = bool(fused) and self.reduce != L.REDUCE_MAX and all(self.relus[:-1]) and all(
+            self.backend.fused_ok(self.shard, nm.weight_node.size(0), nm.weight_node.size(1),
+                                  self.reduce) for nm in nms)
+
+    def local_rows(self, full: torch.Tensor) -> torch.Tensor:
+        return full[self.shard.lo:self.shard.hi]
+
+    def input_table(self, full: torch.Tensor) -> torch.Tensor:
+        return self.shard.to_table(full)
+
+    def forward(self, x_local=None, x_table=None):
+        if (x_local is None) == (x_table is None):
+            raise ValueError("ShardedGCNStack: give x_local (this rank's rows) or x_table")
+        if self.fused:
+            params = []
+            for nm in self._nms:
+                params += [nm.weight_node, nm.bias]
+            x, is_tab = (x_table, True) if x_table is not None else (x_local, False)
+            return _ShardedStack.apply(x, self.shard, self.reduce, self.relus, self.backend,
+                                       self.group, is_tab, *params)
+        h = x_local if x_local is not None else x_table[
+            table_positions(torch.arange(self.shard.lo, self.shard.hi, device=x_table.device),
+                            self.shard.bounds, self.shard.chunk_rows)]
+        for nm, relu in zip(self._nms, self.relus):
+            H = self.backend.linear(h, nm.weight_node)
+            h = sharded_aggregate(H, self.shard, self.aggr, nm.bias, relu=relu,
+                                  backend=self.backend, group=self.group)
+        return h
+
+    def allreduce_grads(self) -> None:
+        allreduce_grads(list(self.parameters()), self.group)
+
+
+class DataParallel:
+    """Data-parallel replicas over torch.distributed (one process per GPU,
+    the whole model on every rank): the north star's "natural DP cases"
+     -- the config-3 botnet loop and the config-1 CV loop,
+    whose graphs are independent.  A step's global batch (the items one
+    process would take) is dealt out item by item (rank r takes items r, r +
+    P, ...); each rank sums its items' losses and divides by the GLOBAL
+    count, so after :meth:`reduce_grads` (one bucketed all_reduce SUM) every
+    rank holds the gradient of the single-process mean loss and takes the
+    same optimizer step.  Equal to one process within fp32 summation order
+    (tests/test_dist_gloo.py).  World 1 (or torch.distributed not
+    initialised): a pass-through."""
+
+    def __init__(self, params, group=None):
+        self.params = [p for p in params]
+        self.group = group
+        on = dist.is_available() and dist.is_initialized()
+        self.rank = dist.get_rank(group) if on else 0
+        self.world = dist.get_world_size(group) if on else 1
+
+    def share(self, items):
+        return list(items)[self.rank::self.world]
+
+    def broadcast_params(self) -> None:
+        """Rank 0's parameters to every rank (identical replicas)."""
+        if self.world == 1:
+            return
+        with torch.no_grad():
+            for p in self.params:
+                dist.broadcast(p.data, src=dist.get_global_rank(self.group, 0)
+                               if self.group is not None else 0, group=self.group)
+
+    def all_sum(self, values, device=None):
+        """Sum a few numbers over the ranks (one all_reduce); returns floats."""
+        if self.world == 1:
+            return [float(v) for v in values]
+        dev = device if device is not None else (self.params[0].device if self.params else "cpu")
+        if dist.get_backend(self.group) == "nccl" and torch.device(dev).type != "cuda":
+            dev = torch.device("cuda", torch.cuda.current_device())
+        t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, group=self.group)
+        return [float(v) for v in t.tolist()]
+
+    def reduce_grads(self) -> None:
+        """All-reduce (sum) every parameter's gradient; a rank whose share
+        was empty (or whose parameters took no gradient) contributes zeros."""
+        if self.world == 1:
+            return
+        for p in self.params:
+            if p.requires_grad and p.grad is None:
+                p.grad = torch.zeros_like(p)
+        allreduce_grads([p for p in self.params if p.requires_grad], self.group)
+
+
 def allreduce_grads(params, group=None) -> None:
     """One bucketed all_reduce (sum) of the replicated parameters' gradients."""
     grads = [p.grad for p in params if p.grad is not None]

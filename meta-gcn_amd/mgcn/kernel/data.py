@@ -109,19 +109,28 @@ class DataLoader:
     permutation from torch's global generator every epoch (as torch's
     RandomSampler under PyG's DataLoader does)."""
 
-    def __init__(self, dataset, batch_size=1, shuffle=False):
+    def __init__(self, dataset, batch_size=1, shuffle=False, share=None, generator=None):
         self.dataset = dataset
         self.batch_size = int(batch_size)
         self.shuffle = shuffle
+        self.share, self.generator = share, generator  # data-parallel replicas
 
     def __len__(self):
         return (len(self.dataset) + self.batch_size - 1) // self.batch_size
 
-    def __iter__(self):
+    def _batches(self):
+        """Index lists of the global batches, cut to this rank's share (an
+        empty share stays in the sequence: every replica steps together)."""
         n = len(self.dataset)
-        order = torch.randperm(n).tolist() if self.shuffle else list(range(n))
+        order = (torch.randperm(n, generator=self.generator).tolist() if self.shuffle
+                 else list(range(n)))
         for i in range(0, n, self.batch_size):
-            yield Batch.from_data_list([self.dataset[j] for j in order[i:i + self.batch_size]])
+            idx = order[i:i + self.batch_size]
+            yield self.share(idx) if self.share is not None else idx
+
+    def __iter__(self):
+        for idx in self._batches():
+            yield Batch.from_data_list([self.dataset[j] for j in idx]) if idx else None
 
 
 class DenseData:
@@ -184,19 +193,23 @@ class ToDense:
 class DenseDataLoader:
     """torch_geometric.data.DenseDataLoader: stacks every attribute."""
 
-    def __init__(self, dataset, batch_size=1, shuffle=False):
+    def __init__(self, dataset, batch_size=1, shuffle=False, share=None, generator=None):
         self.dataset = dataset
         self.batch_size = int(batch_size)
         self.shuffle = shuffle
+        self.share, self.generator = share, generator
 
     def __len__(self):
         return (len(self.dataset) + self.batch_size - 1) // self.batch_size
 
+    _batches = DataLoader._batches
+
     def __iter__(self):
-        n = len(self.dataset)
-        order = torch.randperm(n).tolist() if self.shuffle else list(range(n))
-        for i in range(0, n, self.batch_size):
-            items = [self.dataset[j] for j in order[i:i + self.batch_size]]
+        for idx in self._batches():
+            if not idx:
+                yield None
+                continue
+            items = [self.dataset[j] for j in idx]
             yield DenseData(**{k: torch.stack([getattr(d, k) for d in items])
                                for k in ("x", "adj", "mask", "y")})
 

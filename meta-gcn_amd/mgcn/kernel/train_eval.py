@@ -79,9 +79,29 @@ def num_graphs(data):
     return data.num_graphs if data.batch is not None else data.x.size(0)
 
 
-def train(model, optimizer, loader, device):
+def train(model, optimizer, loader, device, dp=None):
+    """One epoch (train_eval.py:134-148).  ``dp`` (:class:`mgcn.dist.
+    DataParallel`, the loader built with its ``share``): each rank sums the
+    nll of its share of a batch over the batch's GLOBAL graph count, the
+    gradients are all-reduced, every rank steps the same optimizer -- the
+    single-process step within fp32 summation order."""
     model.train()
     total = 0.0
+    if dp is not None and dp.world > 1:
+        for data in loader:
+            optimizer.zero_grad()
+            n_loc = 0 if data is None else num_graphs(data)
+            (n_glob,) = dp.all_sum([n_loc])
+            local = 0.0
+            if data is not None:
+                data = data.to(device)
+                loss = F.nll_loss(model(data), data.y.view(-1), reduction="sum") / n_glob
+                loss.backward()
+                local = loss.item() * n_glob
+            dp.reduce_grads()
+            total += dp.all_sum([local])[0]
+            optimizer.step()
+        return total / len(loader.dataset)
     for data in loader:
         optimizer.zero_grad()
         data = data.to(device)
@@ -93,65 +113,95 @@ def train(model, optimizer, loader, device):
     return total / len(loader.dataset)
 
 
+def _combine(dp, *vals):
+    return tuple(dp.all_sum(vals)) if dp is not None and dp.world > 1 else vals
+
+
 @torch.no_grad()
-def eval_acc(model, loader, device):
+def eval_acc(model, loader, device, dp=None):
     model.eval()
     correct = 0
     for data in loader:
+        if data is None:
+            continue
         data = data.to(device)
         pred = model(data).max(1)[1]
         correct += pred.eq(data.y.view(-1)).sum().item()
+    (correct,) = _combine(dp, correct)
     return correct / len(loader.dataset)
 
 
 @torch.no_grad()
-def eval_loss(model, loader, device):
+def eval_loss(model, loader, device, dp=None):
     model.eval()
     loss = 0.0
     for data in loader:
+        if data is None:
+            continue
         data = data.to(device)
         loss += F.nll_loss(model(data), data.y.view(-1), reduction="sum").item()
+    (loss,) = _combine(dp, loss)
     return loss / len(loader.dataset)
 
 
 @torch.no_grad()
-def eval_loss_acc(model, loader, device):
+def eval_loss_acc(model, loader, device, dp=None):
     model.eval()
     loss, correct = 0.0, 0
     for data in loader:
+        if data is None:
+            continue
         data = data.to(device)
         out = model(data)
         loss += F.nll_loss(out, data.y.view(-1), reduction="sum").item()
         correct += out.max(1)[1].eq(data.y.view(-1)).sum().item()
+    loss, correct = _combine(dp, loss, correct)
     return loss / len(loader.dataset), correct / len(loader.dataset)
 
 
 def cross_validation_with_val_set(dataset, model, folds, epochs, batch_size, lr,
                                   lr_decay_factor, lr_decay_step_size, weight_decay,
                                   random_state=12345, es_patience=-1, logger=None,
-                                  log_details=False, device=None):
+                                  log_details=False, device=None, dp=False, group=None,
+                                  seed=0):
     """Returns (val_loss_mean, val_acc_mean, val_acc_std, test_loss_mean,
-    test_acc_mean, test_acc_std) -- train_eval.py:17-117."""
+    test_acc_mean, test_acc_std) -- train_eval.py:17-117.
+
+    ``dp=True`` (torch.distributed initialised, one process per GPU): every
+    fold trains as data-parallel replicas (:class:`mgcn.dist.DataParallel`:
+    rank 0's reset parameters broadcast, each batch dealt out graph by
+    graph, gradients all-reduced, the shuffle drawn from a generator seeded
+    with ``seed`` on every rank), evaluation split and combined."""
     logging = logger.info if logger is not None else print
     device = device or torch.device("cuda")
     val_losses, val_accs, test_losses, test_accs, durations = [], [], [], [], []
     for fold, (train_idx, test_idx, val_idx) in enumerate(
             zip(*k_fold(dataset, folds, random_state))):
         Loader = DenseDataLoader if 'adj' in dataset[0] else DataLoader  # train_eval.py:32-39
-        train_loader = Loader(dataset[train_idx], batch_size, shuffle=True)
-        val_loader = Loader(dataset[val_idx], batch_size, shuffle=False)
-        test_loader = Loader(dataset[test_idx], batch_size, shuffle=False)
         model.to(device).reset_parameters()
+        dpr = share = gen = None
+        if dp:
+            from ..dist import DataParallel
+            dpr = DataParallel(model.parameters(), group)
+            dpr.broadcast_params()
+            gen = torch.Generator().manual_seed(seed + fold)  # the same order on every rank
+            if dpr.world > 1:
+                share = dpr.share
+        train_loader = Loader(dataset[train_idx], batch_size, shuffle=True, share=share,
+                              generator=gen)
+        val_loader = Loader(dataset[val_idx], batch_size, shuffle=False, share=share)
+        test_loader = Loader(dataset[test_idx], batch_size, shuffle=False, share=share)
         optimizer = torch.optim.Adam(model.parameters(), lr=lr, weight_decay=weight_decay)
         stopper = EarlyStopping(patience=es_patience, mode="min", verbose=True)
-        torch.cuda.synchronize(device)
+        if torch.device(device).type == "cuda":
+            torch.cuda.synchronize(device)
         t0 = time.perf_counter()
         for epoch in range(1, epochs + 1):
-            train_loss = train(model, optimizer, train_loader, device)
-            val_loss, val_acc = eval_loss_acc(model, val_loader, device)
+            train_loss = train(model, optimizer, train_loader, device, dpr)
+            val_loss, val_acc = eval_loss_acc(model, val_loader, device, dpr)
             val_losses.append(val_loss)
             val_accs.append(val_acc)
-            test_loss, test_acc = eval_loss_acc(model, test_loader, device)
+            test_loss, test_acc = eval_loss_acc(model, test_loader, device, dpr)
             test_losses.append(test_loss)
             test_accs.append(test_acc)
             if log_details:
@@ -159,12 +209,13 @@ def cross_validation_with_val_set(dataset, model, folds, epochs, batch_size, lr,
                         f"{train_loss:.4f}, Val loss: {val_loss:.4f}, Val acc: {val_acc:.3f}, "
                         f"Test loss: {test_loss:.4f}, Test acc: {test_acc:.3f}")
             if epoch % lr_decay_step_size == 0:
-                for group in optimizer.param_groups:
-                    group["lr"] = lr_decay_factor * group["lr"]
+                for pg in optimizer.param_groups:
+                    pg["lr"] = lr_decay_factor * pg["lr"]
             stopper(val_loss)
             if stopper.early_stop:
                 break
-        torch.cuda.synchronize(device)
+        if torch.device(device).type == "cuda":
+            torch.cuda.synchronize(device)
         durations.append(time.perf_counter() - t0)
     # (the reference views the per-epoch lists as [folds, epochs]: early
     # stopping would break that reshape; here the runs must be complete too)
