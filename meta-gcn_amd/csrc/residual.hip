@@ -107,10 +107,11 @@ constexpr int kTileLd = 2 * kRF + 4;
 template <int U, bool BWD>
 __global__ __launch_bounds__(kRBlock) void residual_layer_kernel(const RlArgs a) {
   __shared__ __attribute__((aligned(16))) float tile[kRWaves][kTileRows][kTileLd];
+  // the rows' workgroups come first; their grid stride excludes the extra ones
+  const unsigned n_extra = (unsigned)(a.gemm.blocks + a.side[0].blocks + a.side[1].blocks);
+  const unsigned row_blocks = gridDim.x - n_extra;
   {
-    const unsigned n_extra =
-        (unsigned)(a.gemm.blocks + a.side[0].blocks + a.side[1].blocks);
-    if (blockIdx.x >= gridDim.x - n_extra) {
+    if (blockIdx.x >= row_blocks) {
       int b = (int)(blockIdx.x - (gridDim.x - n_extra));
       float *lds = &tile[0][0][0];  // 4352 floats >= the GEMM's 4096 / the fold's 256
       if (b < a.gemm.blocks) {
@@ -160,7 +161,7 @@ __global__ __launch_bounds__(kRBlock) void residual_layer_kernel(const RlArgs a)
   float msa[4] = {0.f, 0.f, 0.f, 0.f}, mss[4] = {0.f, 0.f, 0.f, 0.f};  // fmask column sums
   const int64_t n_tiles = (a.n_items + kTileRows - 1) / kTileRows;
   for (int64_t wv = (int64_t)blockIdx.x * kRWaves + wib; wv < n_tiles;
-       wv += (int64_t)gridDim.x * kRWaves) {
+       wv += (int64_t)row_blocks * kRWaves) {
     // ---- two row steps of 8 rows: aggregate, stage with the own rows ----
 #pragma unroll 1
     for (int st = 0; st < 2; ++st) {

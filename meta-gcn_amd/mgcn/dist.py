@@ -232,7 +232,9 @@ def new_table(shard: Shard, F: int, dtype, device, slot: str) -> torch.Tensor:
     """An exchange table [C*P*cr, F]: a fresh buffer, or (emulated rank) the
     shard's persistent one for ``slot`` -- a rank-local timing of the
     sharded step must not allocate 51 GB per layer where the real step
-    receives it from its peers."""
+    receives it from its peers.  The stack's forward and backward share the
+    two slots "t0" / "t1" (a forward table is dead once the next layer has
+    read it), so an emulated config-5 rank holds the input and two tables."""
     if not shard.emulated:
         return torch.empty(shard.table_rows, F, dtype=dtype, device=device)
     if shard._tables is None:
@@ -421,7 +423,7 @@ class _ShardedStack(torch.autograd.Function):
         sh, be = shard, backend
         rows, C = sh.rows, sh.chunks
         dev = x.device
-        tab = x if x_is_table else gather_table(sh, x, group, slot="f1")
+        tab = x if x_is_table else gather_table(sh, x, group, slot="t1")
         zs, rms, outs = [], [], []
         n = len(Ws)
         for i, (W, b) in enumerate(zip(Ws, bs)):
@@ -434,7 +436,7 @@ class _ShardedStack(torch.autograd.Function):
             if relus[i] and not last:
                 rm = torch.empty(sh.pad_rows, 4 * ((F_out + 127) // 128), dtype=torch.int32,
                                  device=dev)
-            nxt = None if last else new_table(sh, F_out, torch.float32, dev, "f%d" % (i & 1))
+            nxt = None if last else new_table(sh, F_out, torch.float32, dev, "t%d" % (i & 1))
             works = []
             for c in range(C):
                 a, e = sh.chunk(c)
@@ -488,7 +490,7 @@ class _ShardedStack(torch.autograd.Function):
         # top layer's dY: all of it is local already; gather it in chunks
         tab = works = None
         if wants_dx(top):
-            tab = new_table(sh, dY.size(1), torch.float32, dev, "b%d" % (top & 1))
+            tab = new_table(sh, dY.size(1), torch.float32, dev, "t%d" % (top & 1))
             works = [_gather_chunk(sh, c, dY, tab, group) for c in range(C)]
         dx = None
         for l in range(top, -1, -1):
@@ -505,7 +507,7 @@ class _ShardedStack(torch.autograd.Function):
             dX = torch.empty(sh.pad_rows, W.size(0), dtype=torch.float32, device=dev)
             ntab = None
             if l > 0 and wants_dx(l - 1):
-                ntab = new_table(sh, W.size(0), torch.float32, dev, "b%d" % ((l - 1) & 1))
+                ntab = new_table(sh, W.size(0), torch.float32, dev, "t%d" % ((l - 1) & 1))
             works, sums = [], []
             for c in range(C):
                 a, e = sh.chunk(c)
