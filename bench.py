@@ -306,6 +306,8 @@ def main():
     ap.add_argument("--layers", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timers", action="store_true")
+    ap.add_argument("--dense-exchange", action="store_true",
+                    help="N > 1 sharded: send every exchanged table dense (no zero-skipping)")
     ap.add_argument("--mode", choices=["auto", "replica", "shard"], default="auto",
                     help="N > 1: 'auto' measures the dst-range sharded graph (value, strong "
                          "scaling) and data-parallel replicas (the 'replicas' field, weak "
@@ -349,12 +351,16 @@ def main():
     N = args.nodes
     ei_cpu = None
     if do_shard:
+        from mgcn import dist as mdist
         from mgcn.dist import ShardedGCN
+        mdist.set_pack_exchange(not args.dense_exchange)
         ei_cpu, N = make_er_graph(args.nodes, args.pairs)
         model = ShardedGCN(ei_cpu, N, Ws, bs, device=dev, chunks=args.chunks)
         nnz = ei_cpu.shape[1]
+        mdist.STATS.update(dense_words=0, sent_words=0)
         t_sh, prep_sh = timed(model.step_fn(X, dY), args.steps, args.warmup, world, dev,
                               timer if mode == "shard" else None)
+        st = dict(mdist.STATS)
         sharded = {"value": n_edges * L / (t_sh / args.steps), "unit": "edges/s",
                    "ms_per_step": t_sh / args.steps * 1e3, "scaling": "strong",
                    "parallelism": f"dst-range x{world}",
@@ -363,7 +369,10 @@ def main():
                             if model.fused else "per-layer GEMM + SpMM, RCCL all-gathers"),
                    "workload": "config 2 (one 10M-edge graph) sharded by destination range",
                    "graph_prep_plus_first_step_ms": prep_sh,
-                   "rows_per_rank": model.shard.rows}
+                   "rows_per_rank": model.shard.rows,
+                   # ReLU'd tables sent packed (zero-skipping): words sent / dense words
+                   "packed_exchange_ratio": (st["sent_words"] / st["dense_words"]
+                                             if st["dense_words"] else None)}
         del model
         torch.cuda.empty_cache()
     if do_replica:

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define MGCN_ABI_VERSION 15
+#define MGCN_ABI_VERSION 16
 
 /* return codes */
 #define MGCN_OK 0
@@ -577,6 +577,30 @@ int mgcn_residual_stack_bwd(int64_t n_rows, int32_t F, int32_t n_layers, const i
 int mgcn_segment_mean(int64_t n_seg, int32_t F, const int64_t *ptr,
                       const float *x, int64_t ldx, float *out, int64_t ldo,
                       void *stream);
+
+/*
+ * Zero-skipping row packing for the sharded path's table exchange
+ * (mgcn.dist: the all-gathered tables between layers are ReLU outputs or
+ * ReLU-masked gradients, about half +0.0 words; the reference is
+ * single-device, so this replaces nothing of it -- it shrinks the exchange of
+ * SURVEY.md §8(e)'s destination-range sharding).  A chunk of n rows of F
+ * floats (F % 32 == 0) travels as one int32 buffer
+ *   [offs: n][masks: n * F/32][vals: the rows' words that are not +0.0]
+ * bit b of mask word w of a row <=> word 32 w + b is not +0.0 (bit-pattern
+ * test: -0.0 / NaN travel as values); offs[i] = index in vals of row i's
+ * first value.  mgcn_pack_rows_count writes the masks and per-row counts;
+ * the caller forms offs (exclusive prefix sum of counts);
+ * mgcn_pack_rows_values writes vals.  mgcn_unpack_rows expands n_seg such
+ * segments (segment p at buf + p seg_words) into rows p n + i of T, bit for
+ * bit the packed rows.
+ */
+int mgcn_pack_rows_count(int64_t n, int32_t F, const float *X, int64_t ldx, uint32_t *masks,
+                         int32_t *counts, void *stream);
+int mgcn_pack_rows_values(int64_t n, int32_t F, const float *X, int64_t ldx,
+                          const uint32_t *masks, const int32_t *offs, uint32_t *vals,
+                          void *stream);
+int mgcn_unpack_rows(int64_t n_seg, int64_t n, int32_t F, const uint32_t *buf, int64_t seg_words,
+                     float *T, int64_t ldt, void *stream);
 
 #ifdef __cplusplus
 }

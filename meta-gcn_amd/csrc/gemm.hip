@@ -165,8 +165,18 @@ __global__ __launch_bounds__(256, 3) void gemm_tn_x6_kernel(
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wi = wave >> 1, wj = wave & 1;
-  const int tile_m = blockIdx.x / tiles_n, tile_n = blockIdx.x % tiles_n;
-  const int64_t kb = (int64_t)blockIdx.y * k_per_split;
+  // XCD-aware order (1-D grid of tiles x splits): workgroup L runs on XCD
+  // L % 8; consecutive logical ids -- the C tiles of one split, which read
+  // the same K rows of A and B -- go to one XCD, so the second read of each
+  // row is an L2 hit instead of a second HBM read
+  const int tiles = (M / kTile) * tiles_n;
+  const int64_t G = gridDim.x, G8 = G - G % 8;
+  const int64_t L = blockIdx.x;
+  const int64_t lj = L < G8 ? (L % 8) * (G8 / 8) + L / 8 : L;
+  const int tile = (int)(lj % tiles);
+  const int tile_m = tile / tiles_n, tile_n = tile % tiles_n;
+  const int64_t split = lj / tiles;
+  const int64_t kb = split * k_per_split;
   const int64_t ke = (kb + k_per_split < K) ? kb + k_per_split : K;
   const int h = lane >> 5, lc = lane & 31;
 
@@ -263,7 +273,7 @@ __global__ __launch_bounds__(256, 3) void gemm_tn_x6_kernel(
                              acc[t][s2]);
   }
 
-  float *slab = partial + (int64_t)blockIdx.y * M * N;
+  float *slab = partial + split * M * N;
   const int i0 = tile_m * kTile + wi * 64, j0 = tile_n * kTile + wj * 64;
 #pragma unroll
   for (int t = 0; t < 2; ++t)
@@ -288,8 +298,18 @@ __global__ __launch_bounds__(256, WPS) void gemm_tn_lds_kernel(
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wi = wave >> 1, wj = wave & 1;
-  const int tile_m = blockIdx.x / tiles_n, tile_n = blockIdx.x % tiles_n;
-  const int64_t kb = (int64_t)blockIdx.y * k_per_split;
+  // XCD-aware order (1-D grid of tiles x splits): workgroup L runs on XCD
+  // L % 8; consecutive logical ids -- the C tiles of one split, which read
+  // the same K rows of A and B -- go to one XCD, so the second read of each
+  // row is an L2 hit instead of a second HBM read
+  const int tiles = (M / kTile) * tiles_n;
+  const int64_t G = gridDim.x, G8 = G - G % 8;
+  const int64_t L = blockIdx.x;
+  const int64_t lj = L < G8 ? (L % 8) * (G8 / 8) + L / 8 : L;
+  const int tile = (int)(lj % tiles);
+  const int tile_m = tile / tiles_n, tile_n = tile % tiles_n;
+  const int64_t split = lj / tiles;
+  const int64_t kb = split * k_per_split;
   const int64_t ke = (kb + k_per_split < K) ? kb + k_per_split : K;
   const int h = lane >> 5, lc = lane & 31;
   // glds source: lane -> row pair half (lane >> 5), 4 floats at column 4 (lane & 31)
@@ -363,7 +383,7 @@ __global__ __launch_bounds__(256, WPS) void gemm_tn_lds_kernel(
       compute((int)(c & 1), (int)left);
   }
 
-  float *slab = partial + (int64_t)blockIdx.y * M * N;
+  float *slab = partial + split * M * N;
   const int i0 = tile_m * kTile + wi * 64, j0 = tile_n * kTile + wj * 64;
 #pragma unroll
   for (int t = 0; t < 2; ++t)
@@ -571,8 +591,8 @@ int gemm_tn_core(int64_t K, int32_t M, int32_t N, const float *A, int64_t lda, c
              reinterpret_cast<uintptr_t>(B) % 16 == 0 && lda % 4 == 0 && ldb % 4 == 0) {
     const dim3 grid(tiles_m * tiles_n, used);
     if (g_gemm_precision == PREC_BF16X6)
-      hipLaunchKernelGGL(gemm_tn_x6_kernel, grid, dim3(256), 0, s, A, lda, B, ldb, K, M, N, kps,
-                         tiles_n, partial);
+      hipLaunchKernelGGL(gemm_tn_x6_kernel, dim3(tiles_m * tiles_n * used), dim3(256), 0, s, A,
+                         lda, B, ldb, K, M, N, kps, tiles_n, partial);
     else if (g_tn_lds_variant == 1)
       hipLaunchKernelGGL((gemm_tn_lds_kernel<32, 2>), grid, dim3(256), 0, s, A, lda, B, ldb, K, M,
                          N, kps, tiles_n, partial);

@@ -29,10 +29,18 @@ DESIGN.md §7):
   kernel (mgcn_spmm_xw_bwd, X = NULL) over the rank's sources, with the lower
   layer's ReLU mask / mean divisor / bias column sums in its epilogue;
 * replicated parameters: one bucketed all_reduce of every weight / bias
-  gradient per step.
+  gradient per step;
+* zero-skipping exchange: the tables exchanged between layers are ReLU
+  outputs (forward) or gradients masked by the same ReLU (backward), about
+  half +0.0 words.  Such a chunk travels packed (libmgcn mgcn_pack_rows_*:
+  per-row offsets, nonzero bit masks, the nonzero words) and is expanded in
+  place on arrival (mgcn_unpack_rows), bit for bit; the ranks first
+  all-gather their packed sizes so every rank sends the same buffer length,
+  and a chunk whose largest packed form is no smaller than the dense one goes
+  dense (:class:`_ChunkExchange`).
 
-Layers the fused kernels do not take (max, F != 128, heavy rows, tables past
-4 GiB) run per layer: H_k = X_k W, all-gather H, the aggregation SpMM over the
+Layers the fused kernels do not take (max, F not 128 / 256, heavy rows,
+128-wide tables past 4 GiB) run per layer: H_k = X_k W, all-gather H, the aggregation SpMM over the
 rank's destinations; adjoint: all-gather dY (and argmax for max), the adjoint
 SpMM over the rank's sources.
 
@@ -95,6 +103,18 @@ class HipBackend:
     def mask_words(self, F):
         from .ops import mask_words
         return mask_words(F)
+
+    def pack_count(self, rows, masks, counts):
+        from .ops import pack_rows_count
+        pack_rows_count(rows, masks, counts)
+
+    def pack_values(self, rows, masks, offs, vals):
+        from .ops import pack_rows_values
+        pack_rows_values(rows, masks, offs, vals)
+
+    def unpack(self, buf, n_seg, n, seg_words, out):
+        from .ops import unpack_rows
+        unpack_rows(buf, n_seg, n, seg_words, out)
 
     def spmm_fwd(self, *a, **k):
         from .ops import spmm_fwd
@@ -251,6 +271,103 @@ def _wait(works):
     for w in works:
         if w is not None:
             w.wait()
+
+
+PACK_EXCHANGE = True  # mgcn.dist.set_pack_exchange
+# words a dense exchange would have received vs words sent, over every packed
+# exchange of this process (bench / scripts/config5_rank.py report the ratio)
+STATS = {"dense_words": 0, "sent_words": 0}
+
+
+def set_pack_exchange(enabled: bool) -> None:
+    """Zero-skipping (packed) exchange of the ReLU'd tables of the sharded
+    stack (default on); off: every chunk travels dense."""
+    global PACK_EXCHANGE
+    PACK_EXCHANGE = bool(enabled)
+
+
+class _ChunkExchange:
+    """All-gathers the row chunks of one [rows, F] fp32 tensor into an
+    exchange table, chunk by chunk as the caller produces them.  ``packed``:
+    each chunk is packed (offsets, nonzero masks, nonzero words; libmgcn
+    mgcn_pack_rows_*), the ranks all-gather their packed sizes, send buffers
+    of the largest size and unpack every rank's segment into the table --
+    bit for bit the dense exchange; a chunk whose largest packed form is not
+    smaller than the dense chunk goes dense.  The packed path needs each
+    chunk's sizes on the host: :meth:`start` issues a chunk's pack and size
+    exchange, :meth:`finish` (called one chunk later, so the GPU has the next
+    chunk's compute queued while the host waits) its payload.  Emulated rank:
+    the rank's own segment is copied (dense) or packed and unpacked at all P
+    positions (the receive-side work of a real rank, with its own data)."""
+
+    def __init__(self, shard: Shard, local_pad: torch.Tensor, table: torch.Tensor, group,
+                 backend, packed: bool):
+        self.sh, self.local, self.table, self.group, self.be = shard, local_pad, table, group, backend
+        F = local_pad.size(1)
+        self.packed = bool(packed) and local_pad.dtype == torch.float32 and F % 32 == 0 and \
+            hasattr(backend, "pack_count") and (shard.world > 1 or shard.emulated)
+        self.words = F // 32
+        self.pending = []
+        self.works = []
+        self.stats = STATS
+
+    def start(self, c: int) -> None:
+        sh = self.sh
+        if not self.packed:
+            self.works.append(_gather_chunk(sh, c, self.local, self.table, self.group))
+            return
+        cr = sh.chunk_rows
+        rows = self.local[c * cr:(c + 1) * cr]
+        dev = rows.device
+        head = cr * (1 + self.words)
+        send = torch.empty(head + cr * rows.size(1), dtype=torch.int32, device=dev)
+        counts = torch.empty(cr, dtype=torch.int32, device=dev)
+        self.be.pack_count(rows, send[cr:head].view(cr, self.words), counts)
+        total = counts.sum(dtype=torch.int64).view(1)
+        P = sh.world
+        if sh.emulated or P == 1:
+            totals, work = total, None
+        else:
+            totals = torch.empty(P, dtype=torch.int64, device=dev)
+            work = _gather_into(totals, total, P, self.group, True)
+        self.pending.append((c, rows, send, counts, totals, work))
+
+    def finish(self, keep: int = 0) -> None:
+        """Issue the payloads of all started chunks but the last ``keep``."""
+        while len(self.pending) > keep:
+            self._finish_one(*self.pending.pop(0))
+
+    def _finish_one(self, c, rows, send, counts, totals, work):
+        sh = self.sh
+        cr, P, F = sh.chunk_rows, sh.world, rows.size(1)
+        if work is not None:
+            work.wait()
+        cap = int(totals.max())  # the host waits for this chunk's pack
+        head = cr * (1 + self.words)
+        seg = head + cap
+        self.stats["dense_words"] += cr * F * P
+        if seg >= cr * F:  # nothing to gain: dense
+            self.stats["sent_words"] += cr * F * P
+            self.works.append(_gather_chunk(sh, c, self.local, self.table, self.group))
+            return
+        self.stats["sent_words"] += seg * P
+        offs = send[:cr]
+        torch.cumsum(counts, 0, dtype=torch.int32, out=offs)
+        offs.sub_(counts)
+        self.be.pack_values(rows, send[cr:head].view(cr, self.words), offs, send[head:head + cap])
+        blk = self.table[c * P * cr:(c + 1) * P * cr]
+        if sh.emulated:
+            recv = send[:seg].repeat(P)
+            self.be.unpack(recv, P, cr, seg, blk)
+            return
+        recv = torch.empty(P * seg, dtype=torch.int32, device=rows.device)
+        _gather_into(recv, send[:seg], P, self.group, False)
+        self.be.unpack(recv, P, cr, seg, blk)
+
+    def wait(self) -> None:
+        self.finish()
+        _wait(self.works)
+        self.works = []
 
 
 def gather_table(shard: Shard, local: torch.Tensor, group=None, slot: str = "g") -> torch.Tensor:
@@ -430,6 +547,8 @@ class _ShardedStack(torch.autograd.Function):
             F_in, F_out = W.shape
             last = i == n - 1
             out = torch.empty(sh.pad_rows, F_out, dtype=torch.float32, device=dev)
+            if sh.pad_rows > rows:
+                out[rows:].zero_()  # padding rows travel too (packed: as zeros)
             want_z = bool(ctx.needs_input_grad[7 + 2 * i])
             z = torch.empty(sh.pad_rows, F_in, dtype=torch.float32, device=dev) if want_z else None
             rm = None
@@ -437,7 +556,9 @@ class _ShardedStack(torch.autograd.Function):
                 rm = torch.empty(sh.pad_rows, 4 * ((F_out + 127) // 128), dtype=torch.int32,
                                  device=dev)
             nxt = None if last else new_table(sh, F_out, torch.float32, dev, "t%d" % (i & 1))
-            works = []
+            # the layer's output rows (ReLU'd below the top) travel packed
+            xch = None if nxt is None else _ChunkExchange(sh, out, nxt, group, be,
+                                                          PACK_EXCHANGE and relus[i])
             for c in range(C):
                 a, e = sh.chunk(c)
                 if e > a:
@@ -445,9 +566,11 @@ class _ShardedStack(torch.autograd.Function):
                                    reduce, b, relus[i], relu_mask=None if rm is None else rm[a:e],
                                    want_z=want_z, out=out[a:e],
                                    z_out=None if z is None else z[a:e])
-                if nxt is not None:
-                    works.append(_gather_chunk(sh, c, out, nxt, group))
-            _wait(works)
+                if xch is not None:
+                    xch.start(c)
+                    xch.finish(keep=1)
+            if xch is not None:
+                xch.wait()
             outs.append(out)
             zs.append(z)
             rms.append(rm)
@@ -505,9 +628,13 @@ class _ShardedStack(torch.autograd.Function):
                 break
             _wait(works)
             dX = torch.empty(sh.pad_rows, W.size(0), dtype=torch.float32, device=dev)
-            ntab = None
+            ntab = xch = None
             if l > 0 and wants_dx(l - 1):
                 ntab = new_table(sh, W.size(0), torch.float32, dev, "t%d" % ((l - 1) & 1))
+                if sh.pad_rows > rows:
+                    dX[rows:].zero_()  # padding rows travel too (packed: as zeros)
+                # masked by the lower layer's ReLU: travels packed
+                xch = _ChunkExchange(sh, dX, ntab, group, be, PACK_EXCHANGE and relus[l - 1])
             works, sums = [], []
             for c in range(C):
                 a, e = sh.chunk(c)
@@ -519,8 +646,11 @@ class _ShardedStack(torch.autograd.Function):
                         row_div=rd[a:e] if (l > 0 and rd is not None) else None, out=dX[a:e])
                     if cs is not None:
                         sums.append(cs)
-                if ntab is not None:
-                    works.append(_gather_chunk(sh, c, dX, ntab, group))
+                if xch is not None:
+                    xch.start(c)
+                    xch.finish(keep=1)
+            if xch is not None:
+                works = [xch]  # its last chunk is finished at the wait, after the next dW
             if l > 0:
                 if ctx.has_bias[l - 1]:
                     gb[l - 1] = (torch.stack(sums).sum(0) if sums else

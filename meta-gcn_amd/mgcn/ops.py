@@ -1488,3 +1488,50 @@ class _SegmentMean(torch.autograd.Function):
                                       output_size=ctx.n)
         scale = counts.clamp(min=1).to(dout.dtype)
         return (dout / scale.unsqueeze(1))[seg], None
+
+
+# ------------------------------------------------- packed table exchange
+def pack_rows_count(rows: torch.Tensor, masks: torch.Tensor, counts: torch.Tensor) -> None:
+    """masks[i] = the not-+0.0 bits of rows[i] (F / 32 words), counts[i] =
+    their number (``mgcn_pack_rows_count``; mgcn.dist's packed exchange)."""
+    lib = L.load()
+    rows = _contig_f32(rows, "rows")
+    n, F = rows.shape
+    dev = L.require_device(rows, masks, counts)
+    if masks.shape != (n, F // 32) or masks.dtype != torch.int32 or not masks.is_contiguous() \
+            or counts.shape != (n,) or counts.dtype != torch.int32:
+        raise ValueError("pack_rows_count: masks int32 [n, F/32], counts int32 [n]")
+    with L.device_guard(dev):
+        rc = lib.mgcn_pack_rows_count(n, F, L.ptr(rows), rows.stride(0), L.ptr(masks),
+                                      L.ptr(counts), L.stream_of(dev))
+    L.check(rc, "mgcn_pack_rows_count")
+
+
+def pack_rows_values(rows: torch.Tensor, masks: torch.Tensor, offs: torch.Tensor,
+                     vals: torch.Tensor) -> None:
+    """vals[offs[i] ...] = the not-+0.0 words of rows[i] in order
+    (``mgcn_pack_rows_values``)."""
+    lib = L.load()
+    rows = _contig_f32(rows, "rows")
+    n, F = rows.shape
+    dev = L.require_device(rows, masks, offs, vals)
+    if offs.shape != (n,) or offs.dtype != torch.int32 or vals.dtype != torch.int32:
+        raise ValueError("pack_rows_values: offs int32 [n], vals int32")
+    with L.device_guard(dev):
+        rc = lib.mgcn_pack_rows_values(n, F, L.ptr(rows), rows.stride(0), L.ptr(masks),
+                                       L.ptr(offs), L.ptr(vals), L.stream_of(dev))
+    L.check(rc, "mgcn_pack_rows_values")
+
+
+def unpack_rows(buf: torch.Tensor, n_seg: int, n: int, seg_words: int, out: torch.Tensor) -> None:
+    """out[p n + i] = row i of packed segment p of ``buf`` (``mgcn_unpack_rows``)."""
+    lib = L.load()
+    dev = L.require_device(buf, out)
+    F = out.size(1)
+    if buf.dtype != torch.int32 or not buf.is_contiguous() or buf.numel() < n_seg * seg_words or \
+            out.dtype != torch.float32 or out.size(0) < n_seg * n or out.stride(1) != 1:
+        raise ValueError("unpack_rows: buf int32 [n_seg * seg_words], out float32 [n_seg * n, F]")
+    with L.device_guard(dev):
+        rc = lib.mgcn_unpack_rows(n_seg, n, F, L.ptr(buf), seg_words, L.ptr(out), out.stride(0),
+                                  L.stream_of(dev))
+    L.check(rc, "mgcn_unpack_rows")

@@ -46,11 +46,15 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-fused", action="store_true")
+    ap.add_argument("--dense-exchange", action="store_true",
+                    help="no zero-skipping: the ReLU'd tables travel dense")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
     from mgcn import ops
+    from mgcn import dist as mdist
     from mgcn.dist import ShardedGCN
+    mdist.set_pack_exchange(not args.dense_exchange)
     N, P, F, L = args.nodes, args.pairs, args.feat, args.layers
     t0 = time.perf_counter()
     g = torch.Generator(device=dev).manual_seed(0)
@@ -79,11 +83,14 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    mdist.STATS.update(dense_words=0, sent_words=0)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / args.steps * 1e3
+    st = dict(mdist.STATS)
+    ratio = st["sent_words"] / st["dense_words"] if st["dense_words"] else 1.0
     timer = KernelTimer()
     ops.set_kernel_timer(timer)
     step()
@@ -102,11 +109,15 @@ def main():
     # exchanged table is an all-gather of [N, F] fp32, a rank receiving
     # (P - 1) / P of it over P - 1 links
     tables = (2 * (L - 1)) if model.fused else (2 * L)
+    # the fused stack packs the ReLU'd forward tables (L - 1) and the
+    # ReLU-masked backward ones (L - 2); the top layer's dY travels dense
+    packed_tables = (2 * L - 3) if (model.fused and not args.dense_exchange) else 0
+    eff_tables = tables - packed_tables + packed_tables * ratio
     per_rank_rows = sh.rows
     curve = {}
     for p in (1, 2, 4, 8):
         compute = ms * (per_rank_rows * args.world / p) / per_rank_rows
-        xch = 0.0 if p == 1 else tables * (4.0 * N * F * (p - 1) / p) / (
+        xch = 0.0 if p == 1 else eff_tables * (4.0 * N * F * (p - 1) / p) / (
             (p - 1) * XGMI_LINK_GBS * 1e9) * 1e3
         curve[str(p)] = {"compute_ms": compute, "exchange_ms": xch,
                          "step_ms_overlapped": max(compute, xch),
@@ -123,6 +134,9 @@ def main():
            "ms_per_step": ms, "kernel_ms_per_step": kernel_ms,
            "rank_edges_per_s": (sh.fwd.nnz - sh.rows) * L / (ms * 1e-3),
            "kernels": kern, "exchanged_tables_per_step": tables,
+           "packed_tables_per_step": packed_tables,
+           "packed_exchange_ratio": ratio if packed_tables else None,
+           "dense_equivalent_tables_per_step": eff_tables,
            "xgmi_link_gbs": XGMI_LINK_GBS, "predicted_curve": curve,
            "peak_mem_gb": torch.cuda.max_memory_allocated() / 1e9}
     print(json.dumps(out), flush=True)

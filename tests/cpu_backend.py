@@ -143,6 +143,43 @@ class CpuBackend:
             out = out * row_scale.view(-1, 1)
         return out
 
+    # ------------------------------------------------ packed table exchange
+    # (libmgcn mgcn_pack_rows_count / _values, mgcn_unpack_rows: the same
+    # buffer layout [offs: n][masks: n x F/32][vals], bit-pattern test)
+    @staticmethod
+    def _bits_to_words(bits):
+        n, F = bits.shape
+        w = bits.view(n, F // 32, 32).to(torch.int64) << torch.arange(32, dtype=torch.int64)
+        w = w.sum(-1)
+        return torch.where(w >= 2 ** 31, w - 2 ** 32, w).to(torch.int32)
+
+    @staticmethod
+    def _words_to_bits(words, F):
+        w = words.to(torch.int64) & 0xFFFFFFFF
+        return ((w.unsqueeze(-1) >> torch.arange(32, dtype=torch.int64)) & 1).bool().view(-1, F)
+
+    def pack_count(self, rows, masks, counts):
+        bits = rows.contiguous().view(torch.int32) != 0
+        masks.copy_(self._bits_to_words(bits))
+        counts.copy_(bits.sum(1).to(torch.int32))
+
+    def pack_values(self, rows, masks, offs, vals):
+        v = rows.contiguous().view(torch.int32)
+        bits = self._words_to_bits(masks, rows.size(1))
+        nz = v[bits]
+        vals[:nz.numel()] = nz
+
+    def unpack(self, buf, n_seg, n, seg_words, out):
+        F = out.size(1)
+        words = F // 32
+        for p in range(n_seg):
+            seg = buf[p * seg_words:(p + 1) * seg_words]
+            bits = self._words_to_bits(seg[n:n + n * words].view(n, words), F)
+            o = torch.zeros(n, F, dtype=torch.int32)
+            k = int(bits.sum())
+            o[bits] = seg[n + n * words:n + n * words + k]
+            out[p * n:(p + 1) * n] = o.view(torch.float32)
+
     def relu_bwd_colsum(self, dZ, Z, relu, want_db, row_div=None):
         dY = torch.where(Z > 0, dZ, torch.zeros_like(dZ)) if relu else dZ
         db = dY.sum(0) if want_db else None

@@ -36,7 +36,7 @@ def _problem(N=300, pairs=1500, F=16, L=3, seed=0):
     return ei, N, X, Ws, bs, dY
 
 
-def _run(rank, world, port, aggr, out_q, F=16, fused=True, chunks=4):
+def _run(rank, world, port, aggr, out_q, F=16, fused=True, chunks=4, pack=True):
     sys.path[:0] = [os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "meta-gcn_amd"),
                     HERE]
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -45,7 +45,9 @@ def _run(rank, world, port, aggr, out_q, F=16, fused=True, chunks=4):
     try:
         torch.set_num_threads(1)
         from cpu_backend import CpuBackend
+        from mgcn import dist as mdist
         from mgcn.dist import ShardedGCN
+        mdist.set_pack_exchange(pack)
         ei, N, X, Ws, bs, dY = _problem(F=F)
         m = ShardedGCN(ei, N, Ws, bs, device=torch.device("cpu"), aggr=aggr,
                        backend=CpuBackend(), fused=fused, chunks=chunks)
@@ -65,16 +67,17 @@ def _run(rank, world, port, aggr, out_q, F=16, fused=True, chunks=4):
         allreduce_grads(m.params())
         res["out_table"] = out2.detach().numpy()
         res["grads_table"] = [p.grad.numpy() for p in m.params()]
+        res["stats"] = dict(mdist.STATS)
         out_q.put(res)
     finally:
         dist.destroy_process_group()
 
 
-def _launch(world, aggr, F=16, fused=True, chunks=4):
+def _launch(world, aggr, F=16, fused=True, chunks=4, pack=True):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_run, args=(r, world, port, aggr, q, F, fused, chunks))
+    procs = [ctx.Process(target=_run, args=(r, world, port, aggr, q, F, fused, chunks, pack))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -106,6 +109,24 @@ def test_sharded_matches_single_process(world, aggr, F, fused, chunks):
         for key in ("grads", "grads_table"):                            # all-reduced partials
             for g, g1 in zip(r[key], single[key]):
                 np.testing.assert_allclose(g, g1, rtol=1e-5, atol=1e-5 * max(1, np.abs(g1).max()))
+
+
+@pytest.mark.parametrize("world,aggr,F,chunks", [(2, "add", 32, 4), (4, "mean", 64, 3)])
+def test_packed_exchange_is_bitwise_the_dense_one(world, aggr, F, chunks):
+    """The zero-skipping exchange (ReLU'd forward tables, ReLU-masked
+    backward tables) against the dense exchange of the same sharded stack:
+    every output, dX row and gradient bit for bit, with fewer words sent."""
+    packed = _launch(world, aggr, F, True, chunks, pack=True)
+    dense = _launch(world, aggr, F, True, chunks, pack=False)
+    for rp, rd in zip(packed, dense):
+        for key in ("out", "dX", "out_table"):
+            np.testing.assert_array_equal(rp[key], rd[key])
+        for key in ("grads", "grads_table"):
+            for g, g1 in zip(rp[key], rd[key]):
+                np.testing.assert_array_equal(g, g1)
+        st = rp["stats"]
+        assert 0 < st["sent_words"] < 0.8 * st["dense_words"], st
+        assert rd["stats"]["dense_words"] == 0
 
 
 def test_fused_and_per_layer_paths_agree():
