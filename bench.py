@@ -205,6 +205,15 @@ def launch_bytes(name: str, rows: int, edges: int, F: int):
         Fr = 32
         return (8 * (rows + 1) + edges * (8 + 4 * Fr) + 8 * rows * Fr + 8 * rows,
                 4.0 * rows * Fr * Fr)
+    if name.startswith("pack_rows") or name == "unpack_rows":
+        # zero-skipping exchange (mgcn.dist): a dense [rows, F] side plus the
+        # packed side at the ~half density of a ReLU'd table (4 B offset +
+        # F / 8 B of mask + ~2F B of values per row)
+        packed = 4 + F / 8 + 2 * F
+        dense = 4 * F
+        if name == "pack_rows_count":
+            return rows * (dense + 4 + F / 8), 0.0
+        return rows * (dense + packed), 0.0
     if name.startswith("residual_stack"):
         return None, None  # one launch runs a whole run of layers: no per-launch count
     if name == "gemm_bwd":        # dW and dX: X, dH read, dX + mask

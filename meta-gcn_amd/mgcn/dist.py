@@ -298,7 +298,8 @@ class _ChunkExchange:
     exchange, :meth:`finish` (called one chunk later, so the GPU has the next
     chunk's compute queued while the host waits) its payload.  Emulated rank:
     the rank's own segment is copied (dense) or packed and unpacked at all P
-    positions (the receive-side work of a real rank, with its own data)."""
+    positions (the receive-side work of a real rank, with its own data; no
+    collective runs)."""
 
     def __init__(self, shard: Shard, local_pad: torch.Tensor, table: torch.Tensor, group,
                  backend, packed: bool):
@@ -356,9 +357,9 @@ class _ChunkExchange:
         offs.sub_(counts)
         self.be.pack_values(rows, send[cr:head].view(cr, self.words), offs, send[head:head + cap])
         blk = self.table[c * P * cr:(c + 1) * P * cr]
-        if sh.emulated:
-            recv = send[:seg].repeat(P)
-            self.be.unpack(recv, P, cr, seg, blk)
+        if sh.emulated:  # a real rank's receive-side work: P segments unpacked
+            for p in range(P):
+                self.be.unpack(send[:seg], 1, cr, seg, blk[p * cr:(p + 1) * cr])
             return
         recv = torch.empty(P * seg, dtype=torch.int32, device=rows.device)
         _gather_into(recv, send[:seg], P, self.group, False)

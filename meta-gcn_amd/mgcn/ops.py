@@ -1501,9 +1501,13 @@ def pack_rows_count(rows: torch.Tensor, masks: torch.Tensor, counts: torch.Tenso
     if masks.shape != (n, F // 32) or masks.dtype != torch.int32 or not masks.is_contiguous() \
             or counts.shape != (n,) or counts.dtype != torch.int32:
         raise ValueError("pack_rows_count: masks int32 [n, F/32], counts int32 [n]")
+    if _TIMER is not None:
+        _TIMER("pack_rows_count", True, n)
     with L.device_guard(dev):
         rc = lib.mgcn_pack_rows_count(n, F, L.ptr(rows), rows.stride(0), L.ptr(masks),
                                       L.ptr(counts), L.stream_of(dev))
+    if _TIMER is not None:
+        _TIMER("pack_rows_count", False)
     L.check(rc, "mgcn_pack_rows_count")
 
 
@@ -1517,9 +1521,13 @@ def pack_rows_values(rows: torch.Tensor, masks: torch.Tensor, offs: torch.Tensor
     dev = L.require_device(rows, masks, offs, vals)
     if offs.shape != (n,) or offs.dtype != torch.int32 or vals.dtype != torch.int32:
         raise ValueError("pack_rows_values: offs int32 [n], vals int32")
+    if _TIMER is not None:
+        _TIMER("pack_rows_values", True, n)
     with L.device_guard(dev):
         rc = lib.mgcn_pack_rows_values(n, F, L.ptr(rows), rows.stride(0), L.ptr(masks),
                                        L.ptr(offs), L.ptr(vals), L.stream_of(dev))
+    if _TIMER is not None:
+        _TIMER("pack_rows_values", False)
     L.check(rc, "mgcn_pack_rows_values")
 
 
@@ -1531,7 +1539,11 @@ def unpack_rows(buf: torch.Tensor, n_seg: int, n: int, seg_words: int, out: torc
     if buf.dtype != torch.int32 or not buf.is_contiguous() or buf.numel() < n_seg * seg_words or \
             out.dtype != torch.float32 or out.size(0) < n_seg * n or out.stride(1) != 1:
         raise ValueError("unpack_rows: buf int32 [n_seg * seg_words], out float32 [n_seg * n, F]")
+    if _TIMER is not None:
+        _TIMER("unpack_rows", True, n_seg * n)
     with L.device_guard(dev):
         rc = lib.mgcn_unpack_rows(n_seg, n, F, L.ptr(buf), seg_words, L.ptr(out), out.stride(0),
                                   L.stream_of(dev))
+    if _TIMER is not None:
+        _TIMER("unpack_rows", False)
     L.check(rc, "mgcn_unpack_rows")

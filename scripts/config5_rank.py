@@ -54,7 +54,6 @@ def main():
     from mgcn import ops
     from mgcn import dist as mdist
     from mgcn.dist import ShardedGCN
-    mdist.set_pack_exchange(not args.dense_exchange)
     N, P, F, L = args.nodes, args.pairs, args.feat, args.layers
     t0 = time.perf_counter()
     g = torch.Generator(device=dev).manual_seed(0)
@@ -80,17 +79,27 @@ def main():
     Xt = torch.randn(sh.table_rows, F, device=dev, generator=g)
     dYl = torch.randn(sh.rows, F, device=dev, generator=g)
     step = model.step_fn(None, None, X_table=Xt, dY_local=dYl)
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    mdist.STATS.update(dense_words=0, sent_words=0)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    ms = (time.perf_counter() - t0) / args.steps * 1e3
-    st = dict(mdist.STATS)
-    ratio = st["sent_words"] / st["dense_words"] if st["dense_words"] else 1.0
+
+    def run(packed):
+        mdist.set_pack_exchange(packed)
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        mdist.STATS.update(dense_words=0, sent_words=0)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / args.steps * 1e3
+        st = dict(mdist.STATS)
+        return ms, (st["sent_words"] / st["dense_words"] if st["dense_words"] else 1.0)
+
+    # the step with every table kept dense (the rank-local compute alone), then
+    # with the zero-skipping exchange (adds the pack and, for every table, the
+    # unpack of all P segments: a real rank's receive-side work)
+    ms_dense, _ = run(False)
+    packed = model.fused and not args.dense_exchange
+    ms, ratio = run(True) if packed else (ms_dense, 1.0)
     timer = KernelTimer()
     ops.set_kernel_timer(timer)
     step()
@@ -105,34 +114,45 @@ def main():
         t = k["total_ms"] * 1e-3
         kern[name] = dict(k, bytes=byts / k["launches"], gbs=byts / t / 1e9 if t else None)
     kernel_ms = sum(k["total_ms"] for k in kern.values())
-    # predicted curve: rank-local compute scales with the rank's rows; each
+    # predicted curve.  Local work of a rank at P: the compute scales with its
+    # rows (8 / P of rank 0's here); the pack / unpack work with the share of
+    # each table received, (P - 1) / P (measured here at P = 8: 7/8).  Each
     # exchanged table is an all-gather of [N, F] fp32, a rank receiving
-    # (P - 1) / P of it over P - 1 links
+    # (P - 1) / P of it over P - 1 xGMI links; packed tables at `ratio` of
+    # their words.
     tables = (2 * (L - 1)) if model.fused else (2 * L)
     # the fused stack packs the ReLU'd forward tables (L - 1) and the
     # ReLU-masked backward ones (L - 2); the top layer's dY travels dense
-    packed_tables = (2 * L - 3) if (model.fused and not args.dense_exchange) else 0
+    packed_tables = (2 * L - 3) if packed else 0
     eff_tables = tables - packed_tables + packed_tables * ratio
-    per_rank_rows = sh.rows
+    xwork = max(ms - ms_dense, 0.0)
     curve = {}
     for p in (1, 2, 4, 8):
-        compute = ms * (per_rank_rows * args.world / p) / per_rank_rows
+        compute = ms_dense * args.world / p
+        local = compute + (xwork * ((p - 1) / p) / ((args.world - 1) / args.world) if p > 1 else 0.0)
         xch = 0.0 if p == 1 else eff_tables * (4.0 * N * F * (p - 1) / p) / (
             (p - 1) * XGMI_LINK_GBS * 1e9) * 1e3
-        curve[str(p)] = {"compute_ms": compute, "exchange_ms": xch,
-                         "step_ms_overlapped": max(compute, xch),
-                         "step_ms_serial": compute + xch,
-                         "edges_per_s_overlapped": 2 * P * L / (max(compute, xch) * 1e-3)}
+        xch_dense = 0.0 if p == 1 else tables * (4.0 * N * F * (p - 1) / p) / (
+            (p - 1) * XGMI_LINK_GBS * 1e9) * 1e3
+        step_ms = max(local, xch)
+        curve[str(p)] = {"compute_ms": compute, "local_ms": local, "exchange_ms": xch,
+                         "exchange_ms_dense": xch_dense,
+                         "step_ms_overlapped": step_ms,
+                         "step_ms_overlapped_dense": max(compute, xch_dense),
+                         "step_ms_serial": local + xch,
+                         "edges_per_s_overlapped": 2 * P * L / (step_ms * 1e-3)}
     out = {"workload": f"config5 rank {args.rank} of {args.world}: N={N}, E={2 * P} (+{N} loops), "
                        f"F={F}, {L}-layer GCN (sm, add, bias, ReLU) fwd+bwd, exchange tables "
-                       "resident (no RCCL)",
+                       "resident (no RCCL; ms_per_step includes the zero-skipping exchange's "
+                       "pack and the unpack of all P segments of every packed table)",
            "path": ("fused layer kernels (_ShardedStack)" if model.fused else
                     "per layer: x @ W (mgcn_gemm_nn) + SpMM; adjoint SpMM + dW (mgcn_gemm_tn) + "
                     "dX (mgcn_gemm_nn)"),
            "rows": sh.rows, "fwd_slots": int(sh.fwd.nnz), "bwd_slots": int(sh.bwd.nnz),
            "nnz_global": nnz, "table_rows": sh.table_rows, "prep_s": prep_s,
-           "ms_per_step": ms, "kernel_ms_per_step": kernel_ms,
-           "rank_edges_per_s": (sh.fwd.nnz - sh.rows) * L / (ms * 1e-3),
+           "ms_per_step": ms, "ms_per_step_dense_exchange": ms_dense,
+           "kernel_ms_per_step": kernel_ms,
+           "rank_edges_per_s": (sh.fwd.nnz - sh.rows) * L / (ms_dense * 1e-3),
            "kernels": kern, "exchanged_tables_per_step": tables,
            "packed_tables_per_step": packed_tables,
            "packed_exchange_ratio": ratio if packed_tables else None,
