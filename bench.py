@@ -317,6 +317,9 @@ def main():
     ap.add_argument("--no-kernel-timers", action="store_true")
     ap.add_argument("--dense-exchange", action="store_true",
                     help="N > 1 sharded: send every exchanged table dense (no zero-skipping)")
+    ap.add_argument("--packed-exchange", action="store_true",
+                    help="N > 1 sharded: pack the ReLU'd tables at every N (default: up to 4 "
+                         "ranks, mgcn.dist.set_pack_exchange('auto'))")
     ap.add_argument("--mode", choices=["auto", "replica", "shard"], default="auto",
                     help="N > 1: 'auto' measures the dst-range sharded graph (value, strong "
                          "scaling) and data-parallel replicas (the 'replicas' field, weak "
@@ -362,7 +365,8 @@ def main():
     if do_shard:
         from mgcn import dist as mdist
         from mgcn.dist import ShardedGCN
-        mdist.set_pack_exchange(not args.dense_exchange)
+        mdist.set_pack_exchange(False if args.dense_exchange else
+                                True if args.packed_exchange else "auto")
         ei_cpu, N = make_er_graph(args.nodes, args.pairs)
         model = ShardedGCN(ei_cpu, N, Ws, bs, device=dev, chunks=args.chunks)
         nnz = ei_cpu.shape[1]

@@ -199,67 +199,6 @@ __device__ __forceinline__ void wide_gather(const float *__restrict__ X, int64_t
   }
 }
 
-// The wave's two rows of a chunk gathered as ONE slot sequence: row a's
-// slots, then row b's (each row still folded in its own edge order), so the
-// pair's d_a + d_b gathers fill U-wide rounds together -- at the config-5
-// degree (11) three rounds of 8 instead of two rounds of 8 + 3 per row.
-// Lane l's metadata is pair slot e0 + l of the current 64-slot batch.
-__device__ __forceinline__ void pair_meta(const int32_t *__restrict__ col,
-                                          const float *__restrict__ w, int64_t sl,
-                                          const WRow &a, const WRow &b, int &mc, float &mw) {
-  mc = 0;
-  mw = 1.0f;
-  const int64_t nb = a.deg + b.deg;
-  if (sl < nb) {
-    const int64_t s = sl < a.deg ? a.beg + sl : b.beg + (sl - a.deg);
-    mc = col[s];
-    if (w != nullptr) mw = w[s];
-  }
-}
-
-template <int U>
-__device__ __forceinline__ void pair_gather(const float *__restrict__ X, int64_t ldx,
-                                            const int32_t *__restrict__ col,
-                                            const float *__restrict__ w, const WRow &a,
-                                            const WRow &b, int mc, float mw, int lane,
-                                            float (&acc0)[4], float (&acc1)[4]) {
-  acc0[0] = acc0[1] = acc0[2] = acc0[3] = 0.0f;
-  acc1[0] = acc1[1] = acc1[2] = acc1[3] = 0.0f;
-  const int64_t d0 = a.deg, nb = d0 + b.deg;  // wave-uniform
-  for (int64_t e0 = 0; e0 < nb; e0 += 64) {
-    if (e0 > 0) pair_meta(col, w, e0 + lane, a, b, mc, mw);  // pairs past 64 slots
-    const int n = (int)(nb - e0 < 64 ? nb - e0 : 64);
-    for (int k0 = 0; k0 < n; k0 += U) {
-      float4 xv[U];
-      float wk[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int k = (k0 + u) & 63;
-        const int ck = __builtin_amdgcn_readlane(mc, k);
-        wk[u] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mw), k));
-        const auto rs = buf_rsrc(X + (int64_t)ck * ldx, k0 + u < n ? kWF * 4 : 0);
-        xv[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * lane, 0, 0));
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int64_t sl = e0 + k0 + u;  // wave-uniform: row a's slots in order, then row b's
-        if (k0 + u >= n) continue;
-        if (sl < d0) {
-          acc0[0] = __fadd_rn(acc0[0], __fmul_rn(xv[u].x, wk[u]));
-          acc0[1] = __fadd_rn(acc0[1], __fmul_rn(xv[u].y, wk[u]));
-          acc0[2] = __fadd_rn(acc0[2], __fmul_rn(xv[u].z, wk[u]));
-          acc0[3] = __fadd_rn(acc0[3], __fmul_rn(xv[u].w, wk[u]));
-        } else {
-          acc1[0] = __fadd_rn(acc1[0], __fmul_rn(xv[u].x, wk[u]));
-          acc1[1] = __fadd_rn(acc1[1], __fmul_rn(xv[u].y, wk[u]));
-          acc1[2] = __fadd_rn(acc1[2], __fmul_rn(xv[u].z, wk[u]));
-          acc1[3] = __fadd_rn(acc1[3], __fmul_rn(xv[u].w, wk[u]));
-        }
-      }
-    }
-  }
-}
-
 // one 16-row chunk's W fragments of k-step ks for this wave's two n-tiles
 struct WFrag {
   u32x4 t[2][3];
@@ -363,95 +302,55 @@ __global__ __launch_bounds__(kWThreads, 4) void spmm_xw_wide_kernel(const WideAr
   auto row_of = [&](int64_t k) -> int64_t {
     return ((int64_t)blockIdx.x + (k >> 1) * gridDim.x) * kWRows + 2 * wave + (k & 1);
   };
-  // a finished row of the chunk -> Z (forward), mean / row scale, its bf16
-  // term images
-  auto stage_row = [&](char *buf, int64_t chunk, int lr, int64_t deg, float (&acc)[4]) {
-    const int64_t r0 = chunk * kWRows;
-    const bool row_ok = r0 + lr < a.n_rows;
-    if constexpr (!BWD) {
-      if (a.Z != nullptr) {
-        const auto rz = buf_rsrc(a.Z + r0 * a.ldz, rows_in(chunk) * (uint32_t)a.ldz * 4u);
-        __builtin_amdgcn_raw_buffer_store_b128(
-            __builtin_bit_cast(u32x4, make_float4(acc[0], acc[1], acc[2], acc[3])), rz,
-            4 * (int)(lr * a.ldz + 4 * lane), 0, 0);
-      }
-      if (a.mean) {
-        const float c = (float)(deg > 1 ? deg : 1);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[j] = __fdiv_rn(acc[j], c);
-      }
-    } else {
-      if (a.row_scale != nullptr && row_ok) {
-        const float sc = a.row_scale[r0 + lr];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[j] = __fmul_rn(acc[j], sc);
-      }
-    }
-    uint32_t hi[2], mid[2], lo[2];
-    split3_pair(f32x2{acc[0], acc[1]}, hi[0], mid[0], lo[0]);
-    split3_pair(f32x2{acc[2], acc[3]}, hi[1], mid[1], lo[1]);
-    char *img = buf + wimg_off(lr, lane >> 1) + 8 * (lane & 1);
-    *reinterpret_cast<uint2 *>(img) = make_uint2(hi[0], hi[1]);
-    *reinterpret_cast<uint2 *>(img + kWImg) = make_uint2(mid[0], mid[1]);
-    *reinterpret_cast<uint2 *>(img + 2 * kWImg) = make_uint2(lo[0], lo[1]);
-  };
-  // forward: the wave's row pair of a chunk gathered as one slot sequence
-  // (pair_gather; this pair's ptr + metadata and the next pair's ptr held);
-  // backward: row by row, one row ahead (its epilogue state leaves no
-  // registers for the pair's)
-  auto pair_ptr = [&](int64_t k, WRow &m0, WRow &m1) {
-    const int64_t q0 = row_of(k), q1 = row_of(k + 1);
-    wrow_ptr(a.rowptr, q0, q0 < a.n_rows && k < 2 * n_my, m0);
-    wrow_ptr(a.rowptr, q1, q1 < a.n_rows && k + 1 < 2 * n_my, m1);
-  };
-  WRow c0, c1, n0, n1;
-  int pmc = 0;
-  float pmw = 1.0f;
-  pair_ptr(0, c0, c1);
-  if constexpr (!BWD) {
-    pair_meta(a.col, a.w, lane, c0, c1, pmc, pmw);
-    pair_ptr(2, n0, n1);
-  } else {
-    wrow_first(a.col, a.w, lane, c0);
-    n0 = c1;  // the row after c0
-  }
+  WRow cur, nxt;
+  wrow_ptr(a.rowptr, row_of(0), row_of(0) < a.n_rows, cur);
+  wrow_first(a.col, a.w, lane, cur);
+  wrow_ptr(a.rowptr, row_of(1), row_of(1) < a.n_rows && 1 < 2 * n_my, nxt);
   int it = 0;
   for (int64_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x, ++it) {
     char *buf = lds + (it & 1) * kWBuf;
+    const int64_t r0 = chunk * kWRows;
     if (it > 0) prefetch_epi(chunk - gridDim.x);
     // ---- Phase A: the chunk's rows -> bf16 term images ------------------
-    if constexpr (!BWD) {
-      // the next pair's metadata and the one after's row pointers load
-      // under this pair's gathers
-      int qmc;
-      float qmw;
-      pair_meta(a.col, a.w, lane, n0, n1, qmc, qmw);
-      WRow m0, m1;
-      pair_ptr(2 * it + 4, m0, m1);
-      float acc0[4], acc1[4];
-      pair_gather<U>(a.X, a.ldx, a.col, a.w, c0, c1, pmc, pmw, lane, acc0, acc1);
-      stage_row(buf, chunk, 2 * wave, c0.deg, acc0);
-      stage_row(buf, chunk, 2 * wave + 1, c1.deg, acc1);
-      c0 = n0;
-      c1 = n1;
-      n0 = m0;
-      n1 = m1;
-      pmc = qmc;
-      pmw = qmw;
-    } else {
 #pragma unroll 1
-      for (int p = 0; p < 2; ++p) {
-        const int64_t k = 2 * it + p;
-        wrow_first(a.col, a.w, lane, n0);
-        WRow nn;
-        const int64_t rk2 = row_of(k + 2);
-        wrow_ptr(a.rowptr, rk2, rk2 < a.n_rows && k + 2 < 2 * n_my, nn);
-        float acc[4];
-        wide_gather<U>(a.X, a.ldx, a.col, a.w, c0, lane, acc);
-        stage_row(buf, chunk, 2 * wave + p, c0.deg, acc);
-        c0 = n0;
-        n0 = nn;
+    for (int p = 0; p < 2; ++p) {
+      const int lr = 2 * wave + p;
+      const int64_t k = 2 * it + p;
+      wrow_first(a.col, a.w, lane, nxt);
+      WRow nn;
+      const int64_t rk2 = row_of(k + 2);
+      wrow_ptr(a.rowptr, rk2, rk2 < a.n_rows && k + 2 < 2 * n_my, nn);
+      float acc[4];
+      wide_gather<U>(a.X, a.ldx, a.col, a.w, cur, lane, acc);
+      const bool row_ok = r0 + lr < a.n_rows;
+      if constexpr (!BWD) {
+        if (a.Z != nullptr) {
+          const auto rz = buf_rsrc(a.Z + r0 * a.ldz, rows_in(chunk) * (uint32_t)a.ldz * 4u);
+          __builtin_amdgcn_raw_buffer_store_b128(
+              __builtin_bit_cast(u32x4, make_float4(acc[0], acc[1], acc[2], acc[3])), rz,
+              4 * (int)(lr * a.ldz + 4 * lane), 0, 0);
+        }
+        if (a.mean) {
+          const float c = (float)(cur.deg > 1 ? cur.deg : 1);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[j] = __fdiv_rn(acc[j], c);
+        }
+      } else {
+        if (a.row_scale != nullptr && row_ok) {
+          const float sc = a.row_scale[r0 + lr];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[j] = __fmul_rn(acc[j], sc);
+        }
       }
+      uint32_t hi[2], mid[2], lo[2];
+      split3_pair(f32x2{acc[0], acc[1]}, hi[0], mid[0], lo[0]);
+      split3_pair(f32x2{acc[2], acc[3]}, hi[1], mid[1], lo[1]);
+      char *img = buf + wimg_off(lr, lane >> 1) + 8 * (lane & 1);
+      *reinterpret_cast<uint2 *>(img) = make_uint2(hi[0], hi[1]);
+      *reinterpret_cast<uint2 *>(img + kWImg) = make_uint2(mid[0], mid[1]);
+      *reinterpret_cast<uint2 *>(img + 2 * kWImg) = make_uint2(lo[0], lo[1]);
+      cur = nxt;
+      nxt = nn;
     }
     // the first k-step's W fragments, in flight across the barrier
     WFrag fc, fn;

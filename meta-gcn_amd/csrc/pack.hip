@@ -10,13 +10,16 @@
 // restores every row bit for bit); offs[i] = the index in vals of row i's
 // first value (exclusive prefix sum of the rows' popcounts).
 //
-// Kernels (one wave per row, 64 words per step; F % 32 == 0):
-//   pack_count   row -> mask words (into the send buffer) + popcount
-//   pack_values  row + mask + offs -> its nonzero words at vals + offs[i]
-//   unpack       for every received segment p and row i: mask + offs + vals
-//                -> the dense row at T[(p n + i) ldt]
+// Layout of the work: a row is cut into segments of 256 words; a group of
+// G = min(64, F/4) lanes (a power of two) takes one segment, lane gl words
+// 4 gl .. 4 gl + 3 as one 16-B access, so a wave moves 1 KB per instruction
+// (G = 32 at F = 128: two rows per wave).  Four ballots give the group's
+// nonzero bits by word position j; a value's place in the packed row is the
+// values of the lanes below it (popcounts of the ballots under a lane mask)
+// plus those of its own lane's lower words.  Mask word w of a segment is
+// lanes 8 w .. 8 w + 7's nibbles, interleaved out of the four ballots.
 // HBM-bound: pack reads the chunk once per kernel (4 F bytes per row) and
-// writes 4 (1 + F/32) + 4 nnz; unpack reads the segment and writes 4 F.
+// writes 4 + F/8 (+ 4 nnz); unpack reads 4 + F/8 + 4 nnz and writes 4 F.
 
 #include "mgcn_internal.h"
 
@@ -25,91 +28,181 @@ namespace {
 
 constexpr int kPkWaves = 4;
 
+// word w (w < G / 8) of a segment from the group's four ballots (bit gl of
+// b[j] <=> word 4 gl + j is nonzero): bit 4 i + j <- bit 8 w + i of b[j]
+__device__ __forceinline__ uint32_t seg_word(const uint64_t (&b)[4], int w) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    uint32_t byte = (uint32_t)(b[j] >> (8 * w)) & 0xffu;
+    // spread the 8 bits of `byte` to positions 0, 4, 8, ..., 28
+    uint32_t x = byte;
+    x = (x | (x << 12)) & 0x000f000fu;
+    x = (x | (x << 6)) & 0x03030303u;
+    x = (x | (x << 3)) & 0x11111111u;
+    r |= x << j;
+  }
+  return r;
+}
+
+template <int G>
+struct PkLane {
+  int gl, grp;
+  uint64_t gmask;  // the group's lanes
+  uint64_t below;  // the group's lanes below this one
+};
+
+template <int G>
+__device__ __forceinline__ PkLane<G> pk_lane() {
+  PkLane<G> p;
+  const int lane = threadIdx.x & 63;
+  p.gl = lane & (G - 1);
+  p.grp = lane / G;
+  const uint64_t g = G == 64 ? ~0ull : ((1ull << G) - 1ull);
+  p.gmask = g << (p.grp * G);
+  p.below = ((1ull << lane) - 1ull) & p.gmask;
+  return p;
+}
+
+// one 256-word segment of a row: nonzero bits of this lane's four words and
+// the group's ballots
+template <int G>
+__device__ __forceinline__ void seg_bits(const PkLane<G> &p, bool ok, const uint4 &v, bool (&nz)[4],
+                                         uint64_t (&b)[4]) {
+  nz[0] = ok && v.x != 0u;
+  nz[1] = ok && v.y != 0u;
+  nz[2] = ok && v.z != 0u;
+  nz[3] = ok && v.w != 0u;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) b[j] = (__ballot(nz[j]) & p.gmask) >> (p.grp * G);
+}
+
+template <int G>
 __global__ __launch_bounds__(64 * kPkWaves) void pack_count_kernel(int64_t n, int F,
                                                                    const float *__restrict__ X,
                                                                    int64_t ldx,
                                                                    uint32_t *__restrict__ masks,
                                                                    int32_t *__restrict__ counts) {
-  const int lane = threadIdx.x & 63;
-  const int64_t stride = (int64_t)gridDim.x * kPkWaves;
+  const PkLane<G> p = pk_lane<G>();
+  constexpr int RPW = 64 / G;  // rows per wave
+  const int64_t stride = (int64_t)gridDim.x * kPkWaves * RPW;
   const int words = F >> 5;
-  for (int64_t r = (int64_t)blockIdx.x * kPkWaves + (threadIdx.x >> 6); r < n; r += stride) {
-    const uint32_t *x = reinterpret_cast<const uint32_t *>(X + r * ldx);
+  for (int64_t r = ((int64_t)blockIdx.x * kPkWaves + (threadIdx.x >> 6)) * RPW + p.grp; r < n + p.grp;
+       r += stride) {
+    // (r < n) is not group-uniform across the wave: every lane runs the loop
+    // the same number of times and masks its loads
+    const bool rok = r < n;
+    const uint32_t *x = reinterpret_cast<const uint32_t *>(X + (rok ? r : 0) * ldx);
     int cnt = 0;
-    for (int f0 = 0; f0 < F; f0 += 64) {
-      const int f = f0 + lane;
-      const bool nz = f < F && x[f] != 0u;
-      const uint64_t b = __ballot(nz);
-      cnt += __popcll(b);
-      const int w = f0 >> 5;
-      if (lane == 0) masks[r * words + w] = (uint32_t)b;
-      if (lane == 1 && w + 1 < words) masks[r * words + w + 1] = (uint32_t)(b >> 32);
+    for (int f0 = 0; f0 < F; f0 += 4 * G) {
+      const int f = f0 + 4 * p.gl;
+      const bool ok = rok && f < F;
+      const uint4 v = ok ? *reinterpret_cast<const uint4 *>(x + f) : make_uint4(0u, 0u, 0u, 0u);
+      bool nz[4];
+      uint64_t b[4];
+      seg_bits<G>(p, ok, v, nz, b);
+      cnt += __popcll(b[0]) + __popcll(b[1]) + __popcll(b[2]) + __popcll(b[3]);
+      const int w0 = f0 >> 5;
+      if (rok && p.gl < G / 8 && w0 + p.gl < words) masks[r * words + w0 + p.gl] = seg_word(b, p.gl);
     }
-    if (lane == 0) counts[r] = cnt;
+    if (rok && p.gl == 0) counts[r] = cnt;
   }
 }
 
+template <int G>
 __global__ __launch_bounds__(64 * kPkWaves) void pack_values_kernel(
-    int64_t n, int F, const float *__restrict__ X, int64_t ldx,
-    const uint32_t *__restrict__ masks, const int32_t *__restrict__ offs,
+    int64_t n, int F, const float *__restrict__ X, int64_t ldx, const int32_t *__restrict__ offs,
     uint32_t *__restrict__ vals) {
-  const int lane = threadIdx.x & 63;
-  const int64_t stride = (int64_t)gridDim.x * kPkWaves;
-  const int words = F >> 5;
-  for (int64_t r = (int64_t)blockIdx.x * kPkWaves + (threadIdx.x >> 6); r < n; r += stride) {
-    const uint32_t *x = reinterpret_cast<const uint32_t *>(X + r * ldx);
-    int64_t pos = offs[r];
-    for (int f0 = 0; f0 < F; f0 += 64) {
-      const int f = f0 + lane;
-      const uint32_t v = f < F ? x[f] : 0u;
-      const int w = f0 >> 5;
-      const uint64_t m = (uint64_t)masks[r * words + w] |
-                         (w + 1 < words ? (uint64_t)masks[r * words + w + 1] << 32 : 0ull);
-      const bool nz = (m >> lane) & 1ull;
-      // lanes below this one holding a value
-      const int below = __popcll(m & ((1ull << lane) - 1ull));
-      if (nz) vals[pos + below] = v;
-      pos += __popcll(m);
+  const PkLane<G> p = pk_lane<G>();
+  constexpr int RPW = 64 / G;
+  const int64_t stride = (int64_t)gridDim.x * kPkWaves * RPW;
+  for (int64_t r = ((int64_t)blockIdx.x * kPkWaves + (threadIdx.x >> 6)) * RPW + p.grp; r < n + p.grp;
+       r += stride) {
+    const bool rok = r < n;
+    const uint32_t *x = reinterpret_cast<const uint32_t *>(X + (rok ? r : 0) * ldx);
+    int64_t pos = rok ? offs[r] : 0;
+    for (int f0 = 0; f0 < F; f0 += 4 * G) {
+      const int f = f0 + 4 * p.gl;
+      const bool ok = rok && f < F;
+      const uint4 v = ok ? *reinterpret_cast<const uint4 *>(x + f) : make_uint4(0u, 0u, 0u, 0u);
+      bool nz[4];
+      uint64_t b[4];
+      seg_bits<G>(p, ok, v, nz, b);
+      const uint64_t lo = p.below >> (p.grp * G);
+      int64_t q = pos + __popcll(b[0] & lo) + __popcll(b[1] & lo) + __popcll(b[2] & lo) +
+                  __popcll(b[3] & lo);
+      if (nz[0]) vals[q++] = v.x;
+      if (nz[1]) vals[q++] = v.y;
+      if (nz[2]) vals[q++] = v.z;
+      if (nz[3]) vals[q++] = v.w;
+      pos += __popcll(b[0]) + __popcll(b[1]) + __popcll(b[2]) + __popcll(b[3]);
     }
   }
 }
 
+template <int G>
 __global__ __launch_bounds__(64 * kPkWaves) void unpack_kernel(int64_t n_seg, int64_t n, int F,
                                                                const uint32_t *__restrict__ buf,
                                                                int64_t seg_words,
                                                                float *__restrict__ T,
                                                                int64_t ldt) {
-  const int lane = threadIdx.x & 63;
+  const PkLane<G> p = pk_lane<G>();
+  constexpr int RPW = 64 / G;
   const int64_t total = n_seg * n;
-  const int64_t stride = (int64_t)gridDim.x * kPkWaves;
+  const int64_t stride = (int64_t)gridDim.x * kPkWaves * RPW;
   const int words = F >> 5;
-  for (int64_t k = (int64_t)blockIdx.x * kPkWaves + (threadIdx.x >> 6); k < total; k += stride) {
-    const int64_t p = k / n, i = k - p * n;
-    const uint32_t *seg = buf + p * seg_words;
-    const int32_t *offs = reinterpret_cast<const int32_t *>(seg);
+  for (int64_t k = ((int64_t)blockIdx.x * kPkWaves + (threadIdx.x >> 6)) * RPW + p.grp;
+       k < total + p.grp; k += stride) {
+    const bool rok = k < total;
+    const int64_t sg = rok ? k / n : 0, i = rok ? k - sg * n : 0;
+    const uint32_t *seg = buf + sg * seg_words;
     const uint32_t *mk = seg + n + i * words;
     const uint32_t *vals = seg + n + n * words;
-    int64_t pos = offs[i];
-    uint32_t *t = reinterpret_cast<uint32_t *>(T + k * ldt);
-    for (int f0 = 0; f0 < F; f0 += 64) {
-      const int f = f0 + lane;
-      const int w = f0 >> 5;
-      const uint64_t m = (uint64_t)mk[w] | (w + 1 < words ? (uint64_t)mk[w + 1] << 32 : 0ull);
-      const bool nz = (m >> lane) & 1ull;
-      const int below = __popcll(m & ((1ull << lane) - 1ull));
-      const uint32_t v = nz ? vals[pos + below] : 0u;
-      if (f < F) t[f] = v;
-      pos += __popcll(m);
+    int64_t pos = rok ? reinterpret_cast<const int32_t *>(seg)[i] : 0;
+    uint32_t *t = reinterpret_cast<uint32_t *>(T + (rok ? k : 0) * ldt);
+    for (int f0 = 0; f0 < F; f0 += 4 * G) {
+      const int f = f0 + 4 * p.gl;
+      const bool ok = rok && f < F;
+      // this lane's nibble of its mask word: word f >> 5, bits (f & 31) .. + 3
+      const uint32_t nib = ok ? (mk[f >> 5] >> (f & 31)) & 0xfu : 0u;
+      bool nz[4] = {(nib & 1u) != 0, (nib & 2u) != 0, (nib & 4u) != 0, (nib & 8u) != 0};
+      uint64_t b[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = (__ballot(nz[j]) & p.gmask) >> (p.grp * G);
+      const uint64_t lo = p.below >> (p.grp * G);
+      int64_t q = pos + __popcll(b[0] & lo) + __popcll(b[1] & lo) + __popcll(b[2] & lo) +
+                  __popcll(b[3] & lo);
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (nz[0]) v.x = vals[q++];
+      if (nz[1]) v.y = vals[q++];
+      if (nz[2]) v.z = vals[q++];
+      if (nz[3]) v.w = vals[q++];
+      if (ok) *reinterpret_cast<uint4 *>(t + f) = v;
+      pos += __popcll(b[0]) + __popcll(b[1]) + __popcll(b[2]) + __popcll(b[3]);
     }
   }
 }
 
-unsigned pk_grid(int64_t rows) { return grid_for((rows + kPkWaves - 1) / kPkWaves, 1); }
+int pk_group(int F) { return F >= 256 ? 64 : F >= 128 ? 32 : F >= 64 ? 16 : 8; }
+
+unsigned pk_grid(int64_t rows, int G) {
+  return grid_for((rows * G / 64 + kPkWaves - 1) / kPkWaves, 1);
+}
+
+bool pk_aligned(const void *p, int64_t ld) { return (uintptr_t)p % 16 == 0 && ld % 4 == 0; }
 
 }  // namespace
 }  // namespace mgcn
 
 using namespace mgcn;
+
+#define PK_DISPATCH(G, KERNEL, ...)                                                          \
+  switch (G) {                                                                               \
+    case 64: hipLaunchKernelGGL(KERNEL<64>, __VA_ARGS__); break;                             \
+    case 32: hipLaunchKernelGGL(KERNEL<32>, __VA_ARGS__); break;                             \
+    case 16: hipLaunchKernelGGL(KERNEL<16>, __VA_ARGS__); break;                             \
+    default: hipLaunchKernelGGL(KERNEL<8>, __VA_ARGS__); break;                              \
+  }
 
 extern "C" int mgcn_pack_rows_count(int64_t n, int32_t F, const float *X, int64_t ldx,
                                     uint32_t *masks, int32_t *counts, void *stream) {
@@ -118,8 +211,10 @@ extern "C" int mgcn_pack_rows_count(int64_t n, int32_t F, const float *X, int64_
                "mgcn_pack_rows_count: need n >= 0, F a multiple of 32, ldx >= F");
   if (n == 0) return MGCN_OK;
   MGCN_REQUIRE(X && masks && counts, "mgcn_pack_rows_count: null array");
-  hipLaunchKernelGGL(pack_count_kernel, dim3(pk_grid(n)), dim3(64 * kPkWaves), 0,
-                     as_stream(stream), n, (int)F, X, ldx, masks, counts);
+  MGCN_REQUIRE(pk_aligned(X, ldx), "mgcn_pack_rows_count: rows must be 16-byte aligned");
+  const int G = pk_group(F);
+  PK_DISPATCH(G, pack_count_kernel, dim3(pk_grid(n, G)), dim3(64 * kPkWaves), 0,
+              as_stream(stream), n, (int)F, X, ldx, masks, counts);
   return check_launch("pack_count_kernel");
 }
 
@@ -131,8 +226,11 @@ extern "C" int mgcn_pack_rows_values(int64_t n, int32_t F, const float *X, int64
                "mgcn_pack_rows_values: need n >= 0, F a multiple of 32, ldx >= F");
   if (n == 0) return MGCN_OK;
   MGCN_REQUIRE(X && masks && offs && vals, "mgcn_pack_rows_values: null array");
-  hipLaunchKernelGGL(pack_values_kernel, dim3(pk_grid(n)), dim3(64 * kPkWaves), 0,
-                     as_stream(stream), n, (int)F, X, ldx, masks, offs, vals);
+  MGCN_REQUIRE(pk_aligned(X, ldx), "mgcn_pack_rows_values: rows must be 16-byte aligned");
+  // the masks are recomputed from the rows (the same bits pack_count wrote)
+  const int G = pk_group(F);
+  PK_DISPATCH(G, pack_values_kernel, dim3(pk_grid(n, G)), dim3(64 * kPkWaves), 0,
+              as_stream(stream), n, (int)F, X, ldx, offs, vals);
   return check_launch("pack_values_kernel");
 }
 
@@ -143,9 +241,11 @@ extern "C" int mgcn_unpack_rows(int64_t n_seg, int64_t n, int32_t F, const uint3
                "mgcn_unpack_rows: need n_seg, n >= 0, F a multiple of 32, ldt >= F");
   if (n_seg == 0 || n == 0) return MGCN_OK;
   MGCN_REQUIRE(buf && T, "mgcn_unpack_rows: null array");
+  MGCN_REQUIRE(pk_aligned(T, ldt), "mgcn_unpack_rows: T rows must be 16-byte aligned");
   MGCN_REQUIRE(seg_words >= n * (1 + F / 32), "mgcn_unpack_rows: segment of %lld words < header",
                (long long)seg_words);
-  hipLaunchKernelGGL(unpack_kernel, dim3(pk_grid(n_seg * n)), dim3(64 * kPkWaves), 0,
-                     as_stream(stream), n_seg, n, (int)F, buf, seg_words, T, ldt);
+  const int G = pk_group(F);
+  PK_DISPATCH(G, unpack_kernel, dim3(pk_grid(n_seg * n, G)), dim3(64 * kPkWaves), 0,
+              as_stream(stream), n_seg, n, (int)F, buf, seg_words, T, ldt);
   return check_launch("unpack_kernel");
 }

@@ -273,17 +273,30 @@ def _wait(works):
             w.wait()
 
 
-PACK_EXCHANGE = True  # mgcn.dist.set_pack_exchange
+PACK_EXCHANGE = "auto"  # mgcn.dist.set_pack_exchange
+PACK_AUTO_MAX_WORLD = 4
 # words a dense exchange would have received vs words sent, over every packed
 # exchange of this process (bench / scripts/config5_rank.py report the ratio)
 STATS = {"dense_words": 0, "sent_words": 0}
 
 
-def set_pack_exchange(enabled: bool) -> None:
+def set_pack_exchange(enabled) -> None:
     """Zero-skipping (packed) exchange of the ReLU'd tables of the sharded
-    stack (default on); off: every chunk travels dense."""
+    stack: True / False, or "auto" (the default): packed up to
+    PACK_AUTO_MAX_WORLD ranks.  Packing halves the words on xGMI but adds an
+    unpack pass that writes the received (P - 1)/P of every table locally;
+    the link time a table saves shrinks as 1/P while that pass grows, and on
+    the measured config-5 rank the two cross between P = 4
+    (packed 315 vs dense 335 ms predicted) and P = 8 (193 vs 167 ms) at the
+    ideal 153 GB/s per link."""
     global PACK_EXCHANGE
-    PACK_EXCHANGE = bool(enabled)
+    PACK_EXCHANGE = enabled if enabled == "auto" else bool(enabled)
+
+
+def _pack_on(shard: Shard) -> bool:
+    if PACK_EXCHANGE == "auto":
+        return shard.world <= PACK_AUTO_MAX_WORLD
+    return bool(PACK_EXCHANGE)
 
 
 class _ChunkExchange:
@@ -559,7 +572,7 @@ class _ShardedStack(torch.autograd.Function):
             nxt = None if last else new_table(sh, F_out, torch.float32, dev, "t%d" % (i & 1))
             # the layer's output rows (ReLU'd below the top) travel packed
             xch = None if nxt is None else _ChunkExchange(sh, out, nxt, group, be,
-                                                          PACK_EXCHANGE and relus[i])
+                                                          _pack_on(sh) and relus[i])
             for c in range(C):
                 a, e = sh.chunk(c)
                 if e > a:
@@ -635,7 +648,7 @@ class _ShardedStack(torch.autograd.Function):
                 if sh.pad_rows > rows:
                     dX[rows:].zero_()  # padding rows travel too (packed: as zeros)
                 # masked by the lower layer's ReLU: travels packed
-                xch = _ChunkExchange(sh, dX, ntab, group, be, PACK_EXCHANGE and relus[l - 1])
+                xch = _ChunkExchange(sh, dX, ntab, group, be, _pack_on(sh) and relus[l - 1])
             works, sums = [], []
             for c in range(C):
                 a, e = sh.chunk(c)
