@@ -484,6 +484,154 @@ __global__ __launch_bounds__(256) void gemm_tn_staged_kernel(
   tn_staged_block<NT, CK>(A, lda, B, ldb, K, k_per_split, partial, (int)blockIdx.x, stage);
 }
 
+// dW at M = N = 256 (config 5's F = 256 layers: C = Z^T dY over K = the
+// rank's rows).  gemm_tn_x6_kernel's 128 x 128 tiles would split (and read)
+// every element of A and B twice -- once per C tile sharing its K rows; here
+// one 512-thread workgroup per split owns the whole 256 x 256 C: wave w the
+// 64 x 128 block (rows 64 (w >> 1), columns 128 (w & 1)) = 2 x 4 tiles of
+// v_mfma_f32_32x32x16_bf16 (bf16x6), 128 accumulators.  Per 16-row chunk the
+// rows of A and B (16 KB each) are split once into twelve 4-KB term images
+// ([operand][128-column half][term], gemm_tn_x6's swizzle), double-buffered
+// (96 KB: one workgroup per CU, one barrier per chunk); the next chunk's
+// loads (buffer loads: the split's tail reads zeros) are in flight in
+// registers under the current chunk's 48 MFMAs per wave.  K = 6.2M: 4.66 ms
+// (6.18 for the 128 x 128 tiles; 5.49 here with the loads' zero select,
+// which made every load wait at once).  Same products as gemm_tn_x6 (each C element a sum over its split's
+// rows in k-step order), partial slabs folded in split order.
+constexpr int kTnWideChunk = 12 * kTnX6Img;  // one chunk's images: 48 KB
+
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void
+gemm_tn_x6_wide_kernel(const float *__restrict__ A, int64_t lda, const float *__restrict__ B,
+                       int64_t ldb, int64_t K, int64_t k_per_split, float *__restrict__ partial) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * kTnWideChunk];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t kb = (int64_t)blockIdx.x * k_per_split;
+  const int64_t ke = (kb + k_per_split < K) ? kb + k_per_split : K;
+  const int h = lane >> 5, lc = lane & 31;
+
+  // staging: thread -> float4 items tid, tid + 512 of a [16][64] float4
+  // chunk, per operand (one chunk in flight in registers)
+  struct Regs {
+    float4 a[2], b[2];
+  };
+  // buffer loads over the split's rows: a row past its end reads zeros with
+  // no select on the loaded value (a select would make the load synchronous)
+  const auto rsa = buf_rsrc(A + kb * lda, (uint32_t)((ke - kb) * lda * 4));
+  const auto rsb = buf_rsrc(B + kb * ldb, (uint32_t)((ke - kb) * ldb * 4));
+  auto load_chunk = [&](int64_t k0, Regs &R) {
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int f = tid + 512 * m;
+      const int64_t row = k0 - kb + (f >> 6);  // split-relative
+      R.a[m] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                              rsa, (int)((row * lda + 4 * (f & 63)) * 4), 0, 0));
+      R.b[m] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                              rsb, (int)((row * ldb + 4 * (f & 63)) * 4), 0, 0));
+    }
+  };
+  auto store_chunk = [&](char *img0, const Regs &R) {
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int f = tid + 512 * m;
+      const int row = f >> 6, c4 = f & 63;
+      const int half = c4 >> 5, c = c4 & 31;
+      const int off = tn_x6_off(row, c >> 1) + 8 * (c & 1);
+#pragma unroll
+      for (int op = 0; op < 2; ++op) {
+        const float4 v = op ? R.b[m] : R.a[m];
+        uint32_t hi[2], mid[2], lo[2];
+        split3_pair(f32x2{v.x, v.y}, hi[0], mid[0], lo[0]);
+        split3_pair(f32x2{v.z, v.w}, hi[1], mid[1], lo[1]);
+        char *img = img0 + (op * 2 + half) * 3 * kTnX6Img + off;
+        *reinterpret_cast<uint2 *>(img) = make_uint2(hi[0], hi[1]);
+        *reinterpret_cast<uint2 *>(img + kTnX6Img) = make_uint2(mid[0], mid[1]);
+        *reinterpret_cast<uint2 *>(img + 2 * kTnX6Img) = make_uint2(lo[0], lo[1]);
+      }
+    }
+  };
+  // fragment addresses (gemm_tn_x6_kernel's): lane = 16 g + 4 q + p reads
+  // rows 8 h + q (+ 4) and chunk (col0 >> 3) + 2 (g & 1) + (p >> 1), half p & 1
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  auto frag_off = [&](int op, int gcol0, int second) {
+    const int half = gcol0 >> 7, col0 = gcol0 & 127;
+    const int row = 8 * h + q + 4 * second;
+    return (op * 2 + half) * 3 * kTnX6Img +
+           tn_x6_off(row, (col0 >> 3) + 2 * (g & 1) + (p >> 1)) + 8 * (p & 1);
+  };
+  int offa[2][2], offb[4][2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) offa[t][r] = frag_off(0, wm * 64 + 32 * t, r);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) offb[u][r] = frag_off(1, wn * 128 + 32 * u, r);
+  }
+  auto read8 = [&](const char *img0, const int (&o)[2], int term) {
+    const v4i16 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_v4i16_t *)(img0 + o[0] + term * kTnX6Img));
+    const v4i16 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_v4i16_t *)(img0 + o[1] + term * kTnX6Img));
+    const short y[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+    return __builtin_bit_cast(bf16x8, y);
+  };
+
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][u][r] = 0.0f;
+
+  // (tried: chunk c's MFMAs in one basic block with the split and store of
+  // chunk c + 1 -- 4.84 vs 4.66 ms at K = 6.2M; two chunks of register
+  // prefetch -- slower again)
+  const int64_t nchunks = (ke - kb + kTnX6Rows - 1) / kTnX6Rows;
+  Regs R;
+  if (nchunks > 0) load_chunk(kb, R);
+  for (int64_t c = 0; c < nchunks; ++c) {
+    char *img0 = lds + (c & 1) * kTnWideChunk;
+    // this buffer was last read two chunks ago, before the previous barrier
+    store_chunk(img0, R);
+    if (c + 1 < nchunks) load_chunk(kb + (c + 1) * kTnX6Rows, R);
+    __syncthreads();
+    bf16x8 fa[2][3];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int term = 0; term < 3; ++term) fa[t][term] = read8(img0, offa[t], term);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      bf16x8 fb[3];
+#pragma unroll
+      for (int term = 0; term < 3; ++term) fb[term] = read8(img0, offb[u], term);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        acc[t][u] = mfma_x6(fa[t][0], fa[t][1], fa[t][2], fb[0], fb[1], fb[2], acc[t][u]);
+    }
+  }
+
+  float *slab = partial + (int64_t)blockIdx.x * 256 * 256;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = wm * 64 + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        slab[(int64_t)row * 256 + wn * 128 + u * 32 + lc] = acc[t][u][r];
+      }
+}
+
+bool tn_wide(int M, int N) { return M == 256 && N == 256; }
+// gemm_tn_x6_wide_kernel addresses a split's rows with 32-bit buffer offsets
+bool tn_wide_fits(int64_t kps, int64_t lda, int64_t ldb) {
+  return (kps + 16) * (lda > ldb ? lda : ldb) * 4 < (int64_t(1) << 31);
+}
+
 bool tn_lds(int M, int N) { return M % kTile == 0 && N % kTile == 0; }
 
 // LDS-staged dW variants (mgcn_set_option "gemm_tn_variant"; measured at
@@ -496,7 +644,13 @@ int tn_lds_wgs() { return g_tn_lds_variant == 1 ? 2 : g_tn_lds_variant == 2 ? 3 
 int gemm_splits(int64_t K, int M, int N) {
   // one resident round: 256 CUs x 3 workgroups (3 waves/SIMD at 134 VGPRs),
   // or x 2 for the LDS-staged kernel (64 KB of LDS each); at least 64 rows of
-  // K per split (partials: splits x 64 KB per tile)
+  // K per split (partials: splits x 64 KB per tile).  256 x 256 bf16x6
+  // (gemm_tn_x6_wide_kernel): one workgroup per CU
+  if (tn_wide(M, N) && g_gemm_precision == PREC_BF16X6) {
+    int64_t s = 256, max_s = (K + 63) / 64;
+    if (s > max_s) s = max_s;
+    return (int)(s < 1 ? 1 : s);
+  }
   const int tiles = ((M + kTile - 1) / kTile) * ((N + kTile - 1) / kTile);
   const int per_cu = !tn_lds(M, N) ? 3 : g_gemm_precision == PREC_BF16X6 ? 3 : tn_lds_wgs();
   int64_t s = 256 * per_cu / (tiles > 0 ? tiles : 1);
@@ -589,10 +743,14 @@ int gemm_tn_core(int64_t K, int32_t M, int32_t N, const float *A, int64_t lda, c
     if (int rc = check_launch("gemm_tn_small_kernel")) return rc;
   } else if (tn_lds(M, N) && reinterpret_cast<uintptr_t>(A) % 16 == 0 &&
              reinterpret_cast<uintptr_t>(B) % 16 == 0 && lda % 4 == 0 && ldb % 4 == 0) {
-    const dim3 grid(tiles_m * tiles_n, used);
-    if (g_gemm_precision == PREC_BF16X6)
-      hipLaunchKernelGGL(gemm_tn_x6_kernel, dim3(tiles_m * tiles_n * used), dim3(256), 0, s, A,
-                         lda, B, ldb, K, M, N, kps, tiles_n, partial);
+    // 1-D grids of tiles x splits in the kernels' XCD-aware order
+    const dim3 grid(tiles_m * tiles_n * used);
+    if (g_gemm_precision == PREC_BF16X6 && tn_wide(M, N) && tn_wide_fits(kps, lda, ldb))
+      hipLaunchKernelGGL(gemm_tn_x6_wide_kernel, dim3(used), dim3(512), 0, s, A, lda, B, ldb, K,
+                         kps, partial);
+    else if (g_gemm_precision == PREC_BF16X6)
+      hipLaunchKernelGGL(gemm_tn_x6_kernel, grid, dim3(256), 0, s, A, lda, B, ldb, K, M, N, kps,
+                         tiles_n, partial);
     else if (g_tn_lds_variant == 1)
       hipLaunchKernelGGL((gemm_tn_lds_kernel<32, 2>), grid, dim3(256), 0, s, A, lda, B, ldb, K, M,
                          N, kps, tiles_n, partial);

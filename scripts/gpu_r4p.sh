@@ -1,0 +1,8 @@
+set -e -o pipefail
+R=$PWD
+O=$R/gpurun_out/r4p
+mkdir -p $O
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests/test_gpu_parity.py -k "gemm_tn" > $O/t.log 2>&1 || { tail -40 $O/t.log; exit 1; }
+tail -1 $O/t.log
+timeout -k 10 200 python -u scripts/bench_wide_gemm.py > $O/wgemm.json 2> $O/wgemm.err
+head -1 $O/wgemm.json

@@ -255,7 +255,11 @@ def gemm_precision(request):
                                    (1001, 17, 5), (77, 128, 256), (1_000_003, 128, 128),
                                    # M = 32, N = 32 / 64: the staged kernel (config 3's
                                    # [dW | dWr^T]), whole and ragged 64-row chunks
-                                   (286_214, 32, 64), (100, 32, 64), (64, 32, 32), (65, 32, 64)])
+                                   (286_214, 32, 64), (100, 32, 64), (64, 32, 32), (65, 32, 64),
+                                   # 256 x 256 (config 5's dW): one workgroup per split
+                                   # owns the whole C; whole, ragged and tiny splits
+                                   (2_000_003, 256, 256), (4097, 256, 256), (17, 256, 256),
+                                   (1, 256, 256)])
 def test_gemm_tn_matches_fp64(cuda, K, M, N, gemm_precision):
     """dW = A^T B (f32 MFMA: exact f32 products; bf16x6: the exact three-term
     bf16 split, six products on bf16 MFMA; f32 accumulation in a different
@@ -273,6 +277,7 @@ def test_gemm_tn_matches_fp64(cuda, K, M, N, gemm_precision):
 
 
 @pytest.mark.parametrize("K,M,N,n1", [(286_214, 32, 64, 32), (4097, 128, 256, 128),
+                                      (4097, 256, 256, 128),
                                       (3000, 7, 130, 5), (1001, 17, 5, 0), (1001, 17, 5, 5),
                                       (0, 4, 6, 2)])
 def test_gemm_tn_split_equals_gemm_tn(cuda, K, M, N, n1):
