@@ -195,7 +195,7 @@ def test_fused_backward_accumulate_and_empty(cuda):
     dY = torch.randn(N, F, device=cuda)
     dW = ops.spmm_xw_bwd(plan.bwd, norm.w_bwd, None, dY, X, W, want_dx=False)[0]
     acc = torch.ones(F, F, device=cuda)
-    ws_bytes = int(lib.mgcn_spmm_xw_bwd_workspace_bytes(N))
+    ws_bytes = int(lib.mgcn_spmm_xw_bwd_workspace_bytes(N, F, F))
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=cuda)
     v = plan.bwd
     rc = lib.mgcn_spmm_xw_bwd(N, N, F, F, L.ptr(v.rowptr), L.ptr(v.col), L.ptr(norm.w_bwd), None,
