@@ -51,6 +51,13 @@
 #include "mgcn_internal.h"
 #include "x6.h"
 
+// cache policy of the streamed (read-once / written-once) rows -- Z written
+// by the forward, the own X rows of the backward: 0 default, 2 nt (the
+// experiment build `make nt`)
+#ifndef MGCN_NT_AUX
+#define MGCN_NT_AUX 0
+#endif
+
 namespace mgcn {
 namespace {
 
@@ -389,7 +396,7 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_fwd_kernel(c
         const auto rz = buf_rsrc(a.Z + r0 * a.ldz, rows_in * (uint32_t)a.ldz * 4u);
         __builtin_amdgcn_raw_buffer_store_b128(
             __builtin_bit_cast(u32x4, make_float4(acc[0], acc[1], acc[2], acc[3])), rz,
-            4 * (int)(lr * a.ldz + 4 * gl), 0, 0);
+            4 * (int)(lr * a.ldz + 4 * gl), 0, MGCN_NT_AUX);
       }
       if (a.mean) {
         const float c = (float)(cur.deg > 1 ? cur.deg : 1);
@@ -608,8 +615,8 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
     u32x4 xa{}, xb{};
     if constexpr (DW) {
       const auto rxx = buf_rsrc(a.X + r0 * a.ldx, rows_in * (uint32_t)a.ldx * 4u);
-      xa = __builtin_amdgcn_raw_buffer_load_b128(rxx, xoff, 0, 0);
-      xb = __builtin_amdgcn_raw_buffer_load_b128(rxx, xoff + 64 * (int)a.ldx, 0, 0);
+      xa = __builtin_amdgcn_raw_buffer_load_b128(rxx, xoff, 0, MGCN_NT_AUX);
+      xb = __builtin_amdgcn_raw_buffer_load_b128(rxx, xoff + 64 * (int)a.ldx, 0, MGCN_NT_AUX);
     }
     // the chunk's mask / divisor words straight into LDS (LDS-DMA: no registers
     // held across the gathers); rows past the end read row r0 and are never used

@@ -22,6 +22,12 @@
 #include "x6.h"
 #include "tn_staged.h"
 
+// cache policy of gemm_bwd's X / Z rows (streamed once): 0 default, 2 nt
+// (the experiment build `make nt`)
+#ifndef MGCN_NT_AUX
+#define MGCN_NT_AUX 0
+#endif
+
 namespace mgcn {
 namespace {
 
@@ -1654,7 +1660,8 @@ __global__ __launch_bounds__(kBwThreads, 1) void gemm_bwd_kernel(
     const auto rh = buf_rsrc(dH + r0 * lddh, rv * (uint32_t)lddh * 4u);
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
-      b.v[m] = __builtin_amdgcn_raw_buffer_load_b128(rx, ld_off_x + m * 64 * (int)ldx, 0, 0);
+      b.v[m] = __builtin_amdgcn_raw_buffer_load_b128(rx, ld_off_x + m * 64 * (int)ldx, 0,
+                                                     MGCN_NT_AUX);
       b.v[2 + m] = __builtin_amdgcn_raw_buffer_load_b128(rh, ld_off_h + m * 64 * (int)lddh, 0, 0);
     }
     if constexpr (DX && EPI != EPI_STORE) {

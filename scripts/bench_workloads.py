@@ -45,6 +45,23 @@ def timed(step, steps, warmup):
     return t
 
 
+def kernel_times(step):
+    """{kernel: launches, avg_ms, total_ms} of one step (HIP events on the
+    launch stream around every libmgcn call)."""
+    from bench import KernelTimer
+    from mgcn import ops
+    timer = KernelTimer()
+    ops.set_kernel_timer(timer)
+    step()
+    torch.cuda.synchronize()
+    ops.set_kernel_timer(None)
+    out = {}
+    for name, k in timer.summary().items():
+        k.pop("sizes")
+        out[name] = {kk: round(v, 4) if isinstance(v, float) else v for kk, v in k.items()}
+    return out
+
+
 def config3(args, dev):
     from mgcn.models import GCNModel
     g1, n1, m1 = make_botnet_graph(seed=0)
@@ -102,6 +119,8 @@ def config4(args, dev):
             stack(X, ei).backward(dY)
         t = timed(step, args.steps, args.warmup)
         res[aggr] = {"ms_per_step": t * 1e3, "edges_per_s": n_edges * 3 / t}
+        if args.timers:
+            res[aggr]["kernels"] = kernel_times(step)
     return res
 
 
@@ -113,6 +132,9 @@ def main():
     ap.add_argument("--aggr", default="add,mean,max", help="config4: aggregators to run")
     ap.add_argument("--adam", choices=["default", "fused"], default="default",
                     help="config3: torch Adam implementation (default = foreach)")
+    ap.add_argument("--timers", action="store_true",
+                    help="also time one more step with HIP events around every libmgcn launch "
+                         "(bench.KernelTimer) and report them per kernel")
     ap.add_argument("--opt", action="append", default=[],
                     help="libmgcn option name=value (mgcn_set_option), repeatable")
     args = ap.parse_args()
