@@ -52,10 +52,19 @@
 #include "x6.h"
 
 // cache policy of the streamed (read-once / written-once) rows -- Z written
-// by the forward, the own X rows of the backward: 0 default, 2 nt (the
-// experiment build `make nt`)
+// by the forward, the own X rows of the backward: 2 = nt (config 2: 5.16 ->
+// 5.11-5.12 ms/step, A/B on one box: the fwd-with-Z launch 0.933 -> 0.917 ms,
+// the full backward 1.14 -> 1.13 ms)
 #ifndef MGCN_NT_AUX
-#define MGCN_NT_AUX 0
+#define MGCN_NT_AUX 2
+#endif
+// and for the layer outputs (Y forward, dX backward), although they are the
+// next kernel's gathered table: the config-2 tables are twice the 256-MB
+// Infinity Cache, and allocating the written lines there costs more than it
+// saves the next gather (5.14 -> 5.07-5.08 ms/step, three A/B pairs on one
+// box: forward 0.864 -> 0.852 ms, dX-only 0.883 -> 0.868, full 1.134 -> 1.119)
+#ifndef MGCN_NT_OUT
+#define MGCN_NT_OUT 2
 #endif
 
 namespace mgcn {
@@ -351,7 +360,7 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_fwd_kernel(c
       const int lr = 16 * m + (tid >> 5);
       const float4 v = *reinterpret_cast<const float4 *>(stage + lr * kXwF + 4 * gl);
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ry,
-                                             4 * (int)(lr * a.ldy + 4 * gl), 0, 0);
+                                             4 * (int)(lr * a.ldy + 4 * gl), 0, MGCN_NT_OUT);
       if (a.relu_mask != nullptr) {
         // word j of the row: bit gl <=> feature 4 gl + j > 0 (the SpMM's layout)
         const uint32_t m0 = (uint32_t)(__ballot(v.x > 0.0f) >> (32 * grp));
@@ -585,7 +594,7 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
         }
       }
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, *reinterpret_cast<float4 *>(v)),
-                                             rx, 4 * (int)(lr * a.lddx + 4 * lc), 0, 0);
+                                             rx, 4 * (int)(lr * a.lddx + 4 * lc), 0, MGCN_NT_OUT);
     }
   };
 

@@ -73,6 +73,9 @@ constexpr int kWImgFrags = kWKs * kWNt * 3 * 64;  // 16-B fragments of the W ima
 constexpr int kWMaskWords = 8;                    // mask words per row
 
 constexpr int WEPI_STORE = 0, WEPI_RELU = 1, WEPI_RELU_DIV = 2;
+// Y / Z rows leave with the nt cache policy, as in fused.hip (a 51-GB table
+// never stays in the Infinity Cache anyway)
+constexpr int kWideNt = 2;
 
 __device__ __forceinline__ int wimg_off(int row, int ch) {
   return 512 * row + 16 * (ch ^ (row & 15));
@@ -281,7 +284,7 @@ __global__ __launch_bounds__(kWThreads, 4) void spmm_xw_wide_kernel(const WideAr
         }
       }
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, *reinterpret_cast<float4 *>(v)),
-                                             ry, 4 * (int)(lr * a.ldy + 4 * lane), 0, 0);
+                                             ry, 4 * (int)(lr * a.ldy + 4 * lane), 0, kWideNt);
       if constexpr (!BWD) {
         if (a.mask_out != nullptr) {
           const uint64_t b0 = __ballot(v[0] > 0.0f), b1 = __ballot(v[1] > 0.0f);
@@ -328,7 +331,7 @@ __global__ __launch_bounds__(kWThreads, 4) void spmm_xw_wide_kernel(const WideAr
           const auto rz = buf_rsrc(a.Z + r0 * a.ldz, rows_in(chunk) * (uint32_t)a.ldz * 4u);
           __builtin_amdgcn_raw_buffer_store_b128(
               __builtin_bit_cast(u32x4, make_float4(acc[0], acc[1], acc[2], acc[3])), rz,
-              4 * (int)(lr * a.ldz + 4 * lane), 0, 0);
+              4 * (int)(lr * a.ldz + 4 * lane), 0, kWideNt);
         }
         if (a.mean) {
           const float c = (float)(cur.deg > 1 ? cur.deg : 1);

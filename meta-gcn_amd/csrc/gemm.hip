@@ -22,10 +22,9 @@
 #include "x6.h"
 #include "tn_staged.h"
 
-// cache policy of gemm_bwd's X / Z rows (streamed once): 0 default, 2 nt
-// (the experiment build `make nt`)
+// cache policy of gemm_bwd's X / Z rows (streamed once): 2 = nt (fused.hip)
 #ifndef MGCN_NT_AUX
-#define MGCN_NT_AUX 0
+#define MGCN_NT_AUX 2
 #endif
 
 namespace mgcn {
@@ -857,6 +856,18 @@ namespace mgcn {
 namespace {
 using namespace x6;
 
+// the product's rows leave with the nt cache policy (MGCN_NT_EXTRA: an
+// experiment build, `make nt3`)
+#ifndef MGCN_NT_EXTRA
+#define MGCN_NT_EXTRA 0
+#endif
+__device__ __forceinline__ void nn_store(float *p, float v) {
+  if constexpr (MGCN_NT_EXTRA != 0)
+    __builtin_nontemporal_store(v, p);
+  else
+    *p = v;
+}
+
 constexpr int kNNWaves = 8;  // waves per workgroup
 constexpr int kNNThreads = 64 * kNNWaves;
 constexpr int kNNMaxGrid = 1024;  // colsum partial slots
@@ -1090,15 +1101,15 @@ __global__ __launch_bounds__(kNNThreads, P == PREC_BF16X6 ? 1 : 2) void gemm_nn_
                 csum[j] = __fadd_rn(csum[j], v);  // bias gradient: undivided
                 const int rr = (r & 3) + 8 * (r >> 2);
                 if constexpr (EPI == EPI_RELU_DIV)
-                  cp[rr * ldc] = __fdiv_rn(v, row_div[r0 + 4 * h + rr]);
+                  nn_store(cp + rr * ldc, __fdiv_rn(v, row_div[r0 + 4 * h + rr]));
                 else
-                  cp[rr * ldc] = v;
+                  nn_store(cp + rr * ldc, v);
               }
             }
           } else {
             if (n_ok) {
 #pragma unroll
-              for (int r = 0; r < 16; ++r) cp[((r & 3) + 8 * (r >> 2)) * ldc] = acc[g][j][r];
+              for (int r = 0; r < 16; ++r) nn_store(cp + ((r & 3) + 8 * (r >> 2)) * ldc, acc[g][j][r]);
             }
           }
         } else {
@@ -1798,7 +1809,8 @@ __global__ __launch_bounds__(kBwThreads, 1) void gemm_bwd_kernel(
               v = __fdiv_rn(v, *reinterpret_cast<const float *>(buf + kBwDivOff + 4 * lr));
           }
           __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rx,
-                                                4 * (int)(lr * lddx + ncol), 0, 0);
+                                                4 * (int)(lr * lddx + ncol), 0,
+                                                MGCN_NT_EXTRA ? 2 : 0);
         }
     }
   };

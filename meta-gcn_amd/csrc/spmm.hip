@@ -123,6 +123,24 @@ __device__ __forceinline__ I32v<V> load_i(const int32_t *p) {
   return r;
 }
 
+// rows of a wide SpMM output (G >= 32 lanes: F >= 128) leave with the nt
+// cache policy (MGCN_NT_EXTRA: an experiment build, `make nt3`)
+#ifndef MGCN_NT_EXTRA
+#define MGCN_NT_EXTRA 0
+#endif
+typedef float nt_f4 __attribute__((ext_vector_type(4)));
+typedef float nt_f2 __attribute__((ext_vector_type(2)));
+template <int V>
+__device__ __forceinline__ void store_f_nt(float *p, const F32v<V> &r) {
+  if constexpr (V == 4) {
+    __builtin_nontemporal_store(nt_f4{r.v[0], r.v[1], r.v[2], r.v[3]}, reinterpret_cast<nt_f4 *>(p));
+  } else if constexpr (V == 2) {
+    __builtin_nontemporal_store(nt_f2{r.v[0], r.v[1]}, reinterpret_cast<nt_f2 *>(p));
+  } else {
+    __builtin_nontemporal_store(r.v[0], p);
+  }
+}
+
 template <int V>
 __device__ __forceinline__ void store_f(float *p, const F32v<V> &r) {
   if constexpr (V == 4) {
@@ -408,7 +426,8 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(const SpmmArgs a) {
           if (a.relu) y = (y < 0.0f) ? 0.0f : y;
           acc.v[j] = y;
         }
-        store_f<VEC>(dst, acc);
+        if constexpr (MGCN_NT_EXTRA != 0 && G >= 32) store_f_nt<VEC>(dst, acc);
+        else store_f<VEC>(dst, acc);
         if constexpr (VEC == 4 && G == 32) {
           // ReLU mask for the dX GEMM epilogue: lane gl holds features 4 gl + j,
           // so word j of the row is the group's 32 bits of one ballot
@@ -439,7 +458,8 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(const SpmmArgs a) {
 #pragma unroll
           for (int j = 0; j < VEC; ++j) acc.v[j] = __fadd_rn(old.v[j], acc.v[j]);
         }
-        store_f<VEC>(dst, acc);
+        if constexpr (MGCN_NT_EXTRA != 0 && G >= 32) store_f_nt<VEC>(dst, acc);
+        else store_f<VEC>(dst, acc);
       }
     }
   }
