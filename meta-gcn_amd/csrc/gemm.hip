@@ -856,10 +856,10 @@ namespace mgcn {
 namespace {
 using namespace x6;
 
-// the product's rows leave with the nt cache policy (MGCN_NT_EXTRA: an
-// experiment build, `make nt3`)
+// the product's rows leave with the nt cache policy (with the SpMM outputs',
+// spmm.hip: measured together); MGCN_NT_EXTRA=0 builds the default-policy form
 #ifndef MGCN_NT_EXTRA
-#define MGCN_NT_EXTRA 0
+#define MGCN_NT_EXTRA 1
 #endif
 __device__ __forceinline__ void nn_store(float *p, float v) {
   if constexpr (MGCN_NT_EXTRA != 0)

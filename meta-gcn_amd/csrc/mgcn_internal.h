@@ -135,11 +135,23 @@ int gemm_tn_split_fold(int64_t K, int32_t M, int32_t N, int32_t N1, const float 
                        const float *B, int64_t ldb, float *C1, int64_t ldc1, float *C2t,
                        int64_t ldc2t, void *workspace, size_t workspace_bytes,
                        const SideFold &side, hipStream_t s, SideFold *defer = nullptr);
+// The residual layer's forward transform (residual.hip, F = 32) applied by
+// the heavy-row kernels to their rows' aggregates: Z = relu2(relu1(agg W + b)
+// + x Wr^T + br) and the rows' two mask words.  W == NULL: plain aggregate.
+struct ResEpi {
+  const float *W, *Wr, *b, *br;
+  int64_t ldw, ldwr;
+  const float *X;  // the rows' own inputs
+  int64_t ldx;
+  uint32_t *masks;
+  int relu1, relu2;
+};
 // heavy rows of a view alone (spmm.hip), for the fused layer kernels of residual.hip
 int heavy_rows(int bwd, int64_t n_rows, int32_t F, const int64_t *rowptr, const int32_t *col,
                const int32_t *eid, const float *w, const float *X, int64_t ldx, float *Y,
                int64_t ldy, const float *row_scale, int mean, const int32_t *order,
-               int64_t n_heavy, int64_t n_giant, hipStream_t stream, bool *side_used);
+               int64_t n_heavy, int64_t n_giant, hipStream_t stream, bool *side_used,
+               const ResEpi *rs = nullptr);
 int heavy_rows_join(hipStream_t stream);
 // fused layer kernels at F = 256 (fused_wide.hip)
 size_t xw_wide_workspace_bytes(bool bwd);

@@ -481,12 +481,15 @@ extern "C" int mgcn_residual_layer_fwd(int64_t n_rows, int32_t F, const int64_t 
   hipStream_t s = as_stream(stream);
   const bool mean = reduce == MGCN_REDUCE_MEAN;
   if (order == nullptr) n_heavy = n_giant = 0;
-  // heavy rows: their aggregate (A X, mean-divided) into Z, giant ones on the side stream
+  // heavy rows: the workgroup-per-row kernels aggregate them and apply the
+  // layer's transform in their epilogue (giant ones on the side stream)
   bool side = false;
-  if (n_heavy > 0)
+  if (n_heavy > 0) {
+    ResEpi rs{W, Wr, bias, rbias, ldw, ldwr, X, ldx, masks, relu1 != 0, relu2 != 0};
     if (int rc = heavy_rows(0, n_rows, F, rowptr, col, eid, w, X, ldx, Z, ldz, nullptr, mean, order,
-                            n_heavy, n_giant, s, &side))
+                            n_heavy, n_giant, s, &side, &rs))
       return rc;
+  }
   RlArgs a{};
   a.rowptr = rowptr;
   a.col = col;
@@ -514,13 +517,10 @@ extern "C" int mgcn_residual_layer_fwd(int64_t n_rows, int32_t F, const int64_t 
   a.items = order != nullptr ? order + n_heavy : nullptr;
   a.n_items = n_rows - n_heavy;
   if (int rc = launch_rl<false>(a, s)) return rc;
-  if (n_heavy == 0) return MGCN_OK;
+  // the next reader of Z needs the giant rows too
   if (side)
     if (int rc = heavy_rows_join(s)) return rc;
-  a.gather = 0;  // heavy rows: the transform of their aggregate
-  a.items = order;
-  a.n_items = n_heavy;
-  return launch_rl<false>(a, s);
+  return MGCN_OK;
 }
 
 namespace mgcn {

@@ -82,6 +82,10 @@ struct SpmmArgs {
   int64_t n_heavy;
   int64_t n_giant;
   const int32_t *heavy_rows;  // per heavy launch: its slice of order
+  // FWD_SUM at F = 32 with rs.W set: the heavy row's aggregate goes through
+  // the residual layer's transform in the epilogue (residual.hip) instead of
+  // a second launch
+  ResEpi rs;
 };
 
 template <int V>
@@ -124,9 +128,11 @@ __device__ __forceinline__ I32v<V> load_i(const int32_t *p) {
 }
 
 // rows of a wide SpMM output (G >= 32 lanes: F >= 128) leave with the nt
-// cache policy (MGCN_NT_EXTRA: an experiment build, `make nt3`)
+// cache policy: at config 4 (tables twice the Infinity Cache) max forward
+// 0.997 -> 0.970 ms, max adjoint 1.055 -> 1.027, 7.67 -> 7.54 ms/step (two
+// A/B pairs); MGCN_NT_EXTRA=0 builds the default-policy form
 #ifndef MGCN_NT_EXTRA
-#define MGCN_NT_EXTRA 0
+#define MGCN_NT_EXTRA 1
 #endif
 typedef float nt_f4 __attribute__((ext_vector_type(4)));
 typedef float nt_f2 __attribute__((ext_vector_type(2)));
@@ -717,6 +723,36 @@ __global__ __launch_bounds__(HB) void spmm_heavy_kernel(const SpmmArgs a, int FC
 #endif
       __syncthreads();
     }
+    if constexpr (MODE == FWD_SUM) {
+      if (a.rs.W != nullptr) {
+        // the residual layer's transform of this row (F = 32: one chunk, one
+        // fold lane per feature): Z = relu2(relu1(agg W + b) + x Wr^T + br)
+        // and its two mask words, the light rows' epilogue with the two
+        // 32-term products summed in k order
+        float *ep = smem;  // the product buffers are free after the last barrier
+        if (t < 32) {
+          ep[t] = a.mean ? __fdiv_rn(acc, (float)(deg > 1 ? deg : 1)) : acc;
+          ep[32 + t] = a.rs.X[row * a.rs.ldx + t];
+        }
+        __syncthreads();
+        if (t < 32) {
+          float hv = 0.0f, rv = 0.0f;
+#pragma unroll 8
+          for (int k = 0; k < 32; ++k) {
+            hv = __fadd_rn(hv, __fmul_rn(ep[k], a.rs.W[k * a.rs.ldw + t]));
+            rv = __fadd_rn(rv, __fmul_rn(ep[32 + k], a.rs.Wr[t * a.rs.ldwr + k]));
+          }
+          float v = __fadd_rn(hv, a.rs.b != nullptr ? a.rs.b[t] : 0.0f);
+          if (a.rs.relu1 && v < 0.0f) v = 0.0f;
+          float z = __fadd_rn(v, __fadd_rn(rv, a.rs.br != nullptr ? a.rs.br[t] : 0.0f));
+          if (a.rs.relu2 && z < 0.0f) z = 0.0f;
+          const uint32_t m1 = (uint32_t)__ballot(v > 0.0f), m2 = (uint32_t)__ballot(z > 0.0f);
+          a.Y[row * a.ldy + t] = z;
+          if (t == 0) *reinterpret_cast<uint2 *>(a.rs.masks + 2 * row) = make_uint2(m1, m2);
+        }
+        continue;  // F = 32: the only feature chunk
+      }
+    }
     if (t < fc) {
       const int f = f0 + t;
       float *dst = a.Y + row * a.ldy + f;
@@ -1081,7 +1117,8 @@ int launch_mode(SpmmArgs a, int vec, hipStream_t stream) {
 int heavy_rows(int bwd, int64_t n_rows, int32_t F, const int64_t *rowptr, const int32_t *col,
                const int32_t *eid, const float *w, const float *X, int64_t ldx, float *Y,
                int64_t ldy, const float *row_scale, int mean, const int32_t *order,
-               int64_t n_heavy, int64_t n_giant, hipStream_t stream, bool *side_used) {
+               int64_t n_heavy, int64_t n_giant, hipStream_t stream, bool *side_used,
+               const ResEpi *rs) {
   *side_used = false;
   if (order == nullptr || n_heavy <= 0) return MGCN_OK;
   SpmmArgs a{};
@@ -1101,6 +1138,7 @@ int heavy_rows(int bwd, int64_t n_rows, int32_t F, const int64_t *rowptr, const 
   a.order = order;
   a.n_heavy = n_heavy;
   a.n_giant = n_giant;
+  if (rs != nullptr) a.rs = *rs;
   const int vec = pick_vec(F, X, ldx, Y, ldy);
   if (n_giant > 0) {
     SideStream *side = nullptr;
