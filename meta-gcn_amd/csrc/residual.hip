@@ -33,8 +33,10 @@
 // heavy rows (degree > the schedule's threshold: the botnet graphs have
 //           ~1k rows holding a third of the edges) are aggregated by the
 //           SpMM's workgroup-per-row kernels (giant rows on the side stream,
-//           overlapping the light rows) into the output rows, then a second
-//           launch of the fused kernel without the gather finishes them.
+//           overlapping the light rows); forward, those kernels apply the
+//           layer's transform in their epilogue (spmm.hip, ResEpi); backward,
+//           a second launch of the fused kernel without the gather finishes
+//           them, with the layer's weight GEMM riding beside.
 //
 // Roofline: HBM-bound like the SpMM; bytes per forward launch
 //   8 (N + 1) + nnz (4 col + 4 w + 4 F) + 4 N F (own X rows) + 4 N F (Z) + 8 N
