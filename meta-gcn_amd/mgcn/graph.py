@@ -83,7 +83,7 @@ class CSRView:
         return None if self.order is None or self.n_heavy == 0 else self.order[:self.n_heavy]
 
 
-def schedule_rows(view: CSRView, thr: int = HEAVY_THRESHOLD) -> CSRView:
+def schedule_rows(view: CSRView, thr: int | None = None) -> CSRView:
     """Fill ``view.order`` / ``n_heavy`` / ``n_giant`` (mgcn_row_schedule).
 
     The degree order pays on skewed graphs (waves of similar-degree rows,
@@ -91,6 +91,8 @@ def schedule_rows(view: CSRView, thr: int = HEAVY_THRESHOLD) -> CSRView:
     scatters the row-pointer and edge-slot reads, so there the natural order
     is kept (``order`` None): no heavy rows and max degree <= 4x mean + 8."""
     import ctypes
+    if thr is None:
+        thr = HEAVY_THRESHOLD  # read at call time (a tuning run may set it)
     lib = L.load()
     dev = view.rowptr.device
     if view.n_rows == 0:

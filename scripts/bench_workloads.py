@@ -135,10 +135,15 @@ def main():
     ap.add_argument("--timers", action="store_true",
                     help="also time one more step with HIP events around every libmgcn launch "
                          "(bench.KernelTimer) and report them per kernel")
+    ap.add_argument("--heavy-thr", type=int, default=None,
+                    help="rows above this degree take the heavy-row kernels (mgcn.graph.HEAVY_THRESHOLD)")
     ap.add_argument("--opt", action="append", default=[],
                     help="libmgcn option name=value (mgcn_set_option), repeatable")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
+    if args.heavy_thr is not None:
+        import mgcn.graph
+        mgcn.graph.HEAVY_THRESHOLD = args.heavy_thr
     if args.opt:
         import mgcn
         lib = mgcn.load()
