@@ -1,6 +1,6 @@
-// The heavy-row SpMM body shared by spmm.hip (spmm_heavy_kernel) and
-// residual.hip (extra workgroups of the fused layer's light-row launch), with
-// the argument block and the vector helpers it uses.  Internal header.
+// The SpMM argument block, its vector helpers and the heavy-row body
+// (spmm.hip's spmm_heavy_kernel) as a device function that other launches can
+// run per workgroup.  Internal header.
 #pragma once
 
 #include "mgcn_internal.h"
@@ -170,8 +170,9 @@ __device__ unsigned long long g_hprof[3][256][2];
 // kernel (launch_mode).
 // One heavy row (schedule slot `hidx` of a.heavy_rows) by the calling
 // workgroup of HB threads, with `smem` >= 2 FC (BE + 4) + 12 BE floats of LDS:
-// the body of spmm_heavy_kernel, also run by extra workgroups of residual.hip's
-// light-row launches.
+// the body of spmm_heavy_kernel.  Taking the LDS block as a restrict pointer
+// made the heavy kernels 3-4 us faster per launch than the same code over the
+// kernel's extern array (config 3).
 // (Q: edge quads in flight per producer thread, 0 = the kernel's choice; a
 // caller with fewer registers to spare passes a smaller one)
 template <int VEC, int MODE, int HB, int Q = 0>

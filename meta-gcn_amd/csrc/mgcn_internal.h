@@ -63,7 +63,6 @@ int gemm_set_precision(int value);
 int gemm_precision_is_x6();  // 1 under bf16x6 (the fused kernels need it)
 int xw_set_unroll(int value);  // fused.hip
 extern int g_fused_mask;       // residual.hip: the stack's fused lower-layer mask pass
-extern int g_mid_in_light;     // residual.hip: non-giant heavy rows inside the light-row launch
 // deterministic folds of per-workgroup partials (gemm.hip)
 // deterministic fold of split partials: C[e] (+)= sum_sp partial[sp * MN + e]
 int launch_fold(const float *partial, int64_t splits, int64_t MN, int N, float *C, int64_t ldc,
@@ -147,16 +146,12 @@ struct ResEpi {
   uint32_t *masks;
   int relu1, relu2;
 };
-// heavy rows of a view alone (spmm.hip), for the fused layer kernels of
-// residual.hip; with `mid` given, the non-giant heavy rows are not launched:
-// *mid receives their arguments (heavy.h: heavy_row_block per row) for the
-// caller to run in its own launch
-struct SpmmArgs;
+// heavy rows of a view alone (spmm.hip), for the fused layer kernels of residual.hip
 int heavy_rows(int bwd, int64_t n_rows, int32_t F, const int64_t *rowptr, const int32_t *col,
                const int32_t *eid, const float *w, const float *X, int64_t ldx, float *Y,
                int64_t ldy, const float *row_scale, int mean, const int32_t *order,
                int64_t n_heavy, int64_t n_giant, hipStream_t stream, bool *side_used,
-               const ResEpi *rs = nullptr, SpmmArgs *mid = nullptr);
+               const ResEpi *rs = nullptr);
 int heavy_rows_join(hipStream_t stream);
 // fused layer kernels at F = 256 (fused_wide.hip)
 size_t xw_wide_workspace_bytes(bool bwd);

@@ -42,7 +42,6 @@
 //   8 (N + 1) + nnz (4 col + 4 w + 4 F) + 4 N F (own X rows) + 4 N F (Z) + 8 N
 // and the 2 x 2 N F^2 FMA flops ride under the gathers.
 
-#include "heavy.h"
 #include "mgcn_internal.h"
 #include "tn_staged.h"
 
@@ -95,12 +94,6 @@ struct RlArgs {
   // GEMM's split-K partials, the lower layer's bias-gradient column sums)
   TnJob gemm;
   SideFold side[2];
-  // the non-giant heavy rows (heavy_rows' arguments), one row per extra
-  // workgroup at the front of the grid: they run beside the light rows
-  // instead of in a launch before them
-  SpmmArgs hv;
-  int64_t hv_blocks;
-  int hv_BE;
 };
 
 __device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
@@ -117,28 +110,19 @@ constexpr int kTileLd = 2 * kRF + 4;
 constexpr int kTileFloats = kRWaves * kTileRows * kTileLd;
 constexpr int kBFloats = 2 * 64 * 8;
 constexpr int kLdsFloats = kTileFloats + 2 * kBFloats + 2 * kRWaves * kTileRows;
-// heavy-row batches in that block (heavy.h, FC = 32: 2 FC (BE + 4) + 12 BE floats)
-constexpr int kHvBE = ((kLdsFloats - 8 * kRF) / (2 * kRF + 12)) & ~15;
-constexpr int kHvQ = 1;  // edge quads in flight per producer: the light rows' registers
 
-// occupancy: the forward light rows fit 96 VGPRs (5 waves per SIMD); the
-// heavy-row path of the same kernel is held to that
+// occupancy: the forward light rows fit 96 VGPRs (5 waves per SIMD), the
+// backward ones 107 (4 waves; held to 96 they spill 10 VGPRs)
 template <int U, bool BWD>
 __global__ __launch_bounds__(kRBlock) __attribute__((amdgpu_waves_per_eu(BWD ? 4 : 5)))
 void residual_layer_kernel(const RlArgs a) {
   __shared__ __attribute__((aligned(16))) float lds_all[kLdsFloats];
   float(*tile)[kTileRows][kTileLd] = reinterpret_cast<float(*)[kTileRows][kTileLd]>(lds_all);
-  // grid: [heavy rows][the rows' workgroups][GEMM, folds]; the rows' grid
-  // stride excludes the others
-  const unsigned n_hv = (unsigned)a.hv_blocks;
-  if (blockIdx.x < n_hv) {
-    heavy_row_block<4, BWD ? BWD_SUM : FWD_SUM, kRBlock, kHvQ>(a.hv, kRF, a.hv_BE, blockIdx.x,
-                                                               lds_all);
-    return;
-  }
+  // grid: [the rows' workgroups][GEMM, folds]; the rows' grid stride
+  // excludes the others
   const unsigned n_extra = (unsigned)(a.gemm.blocks + a.side[0].blocks + a.side[1].blocks);
-  const unsigned row_blocks = gridDim.x - n_hv - n_extra;
-  const unsigned rblk = blockIdx.x - n_hv;  // this workgroup's index among the rows'
+  const unsigned row_blocks = gridDim.x - n_extra;
+  const unsigned rblk = blockIdx.x;  // this workgroup's index among the rows'
   {
     if (rblk >= row_blocks) {
       int b = (int)(rblk - row_blocks);
@@ -466,30 +450,18 @@ int64_t rl_blocks(int64_t n_items, bool fused_mask) {
 
 template <bool BWD>
 int launch_rl(const RlArgs &a, hipStream_t s) {
-  if (a.n_items <= 0 && a.hv_blocks == 0) {  // nothing to ride in (callers attach the GEMM
-                                              // only to a launch with rows)
+  if (a.n_items <= 0) {  // nothing to ride in (callers attach the GEMM only to a launch with rows)
     if (int rc = launch_side_fold(a.side[0], s)) return rc;
     return launch_side_fold(a.side[1], s);
   }
-  const int64_t blocks = a.hv_blocks + rl_blocks(a.n_items, BWD && a.mmask != nullptr) +
-                         a.gemm.blocks + a.side[0].blocks + a.side[1].blocks;
+  const int64_t blocks = rl_blocks(a.n_items, BWD && a.mmask != nullptr) + a.gemm.blocks +
+                         a.side[0].blocks + a.side[1].blocks;
   hipLaunchKernelGGL((residual_layer_kernel<8, BWD>), dim3((unsigned)blocks), dim3(kRBlock), 0, s, a);
   return check_launch("residual_layer_kernel");
 }
 
 bool al16(const void *p, int64_t ld) { return p == nullptr || ((uintptr_t)p % 16 == 0 && ld % 4 == 0); }
 
-// the non-giant heavy rows in the light-row launch (heavy.h at VEC = 4: the
-// gathered table and the output need 16-byte aligned rows, as here anyway)
-bool mid_in_light(int64_t n_heavy, int64_t n_giant, const float *T, int64_t ldt, const float *Y,
-                  int64_t ldy) {
-  return g_mid_in_light && n_heavy > n_giant && al16(T, ldt) && al16(Y, ldy);
-}
-void set_mid(RlArgs &a, const SpmmArgs &mid) {
-  a.hv = mid;
-  a.hv_blocks = mid.heavy_rows != nullptr ? mid.n_heavy - mid.n_giant : 0;
-  a.hv_BE = kHvBE;
-}
 
 }  // namespace
 }  // namespace mgcn
@@ -527,11 +499,10 @@ extern "C" int mgcn_residual_layer_fwd(int64_t n_rows, int32_t F, const int64_t 
   // heavy rows: the workgroup-per-row kernels aggregate them and apply the
   // layer's transform in their epilogue (giant ones on the side stream)
   bool side = false;
-  SpmmArgs mid{};
   if (n_heavy > 0) {
     ResEpi rs{W, Wr, bias, rbias, ldw, ldwr, X, ldx, masks, relu1 != 0, relu2 != 0};
     if (int rc = heavy_rows(0, n_rows, F, rowptr, col, eid, w, X, ldx, Z, ldz, nullptr, mean, order,
-                            n_heavy, n_giant, s, &side, &rs, mid_in_light(n_heavy, n_giant, X, ldx, Z, ldz) ? &mid : nullptr))
+                            n_heavy, n_giant, s, &side, &rs))
       return rc;
   }
   RlArgs a{};
@@ -556,12 +527,10 @@ extern "C" int mgcn_residual_layer_fwd(int64_t n_rows, int32_t F, const int64_t 
   a.mean = mean;
   a.relu1 = relu1 != 0;
   a.relu2 = relu2 != 0;
-  // light rows: the whole layer in one pass (the non-giant heavy rows in
-  // workgroups of the same launch)
+  // light rows: the whole layer in one pass
   a.gather = 1;
   a.items = order != nullptr ? order + n_heavy : nullptr;
   a.n_items = n_rows - n_heavy;
-  set_mid(a, mid);
   if (int rc = launch_rl<false>(a, s)) return rc;
   // the next reader of Z needs the giant rows too
   if (side)
@@ -571,7 +540,6 @@ extern "C" int mgcn_residual_layer_fwd(int64_t n_rows, int32_t F, const int64_t 
 
 namespace mgcn {
 int g_fused_mask = 1;  // mgcn_set_option("residual_fused_mask")
-int g_mid_in_light = 0;  // mgcn_set_option("residual_mid_in_light"): 1 measured slower
 namespace {
 // The mask pass of the layer below, fused into this layer's dX store (stack
 // backward): its masks / flags / mean divisor, where dS and dA go, the block
@@ -602,11 +570,9 @@ int residual_bwd_core(int64_t n_rows, const int64_t *rowptr_t, const int32_t *co
   const int F = kRF;
   if (order == nullptr) n_heavy = n_giant = 0;
   bool side = false;
-  SpmmArgs mid{};
   if (n_heavy > 0)
     if (int rc = heavy_rows(1, n_rows, F, rowptr_t, col_t, eid_t, w_t, dA, F, DH, lddh, row_scale,
-                            0, order, n_heavy, n_giant, s, &side, nullptr,
-                            mid_in_light(n_heavy, n_giant, dA, F, DH, lddh) ? &mid : nullptr))
+                            0, order, n_heavy, n_giant, s, &side))
       return rc;
   RlArgs a{};
   a.rowptr = rowptr_t;
@@ -640,10 +606,8 @@ int residual_bwd_core(int64_t n_rows, const int64_t *rowptr_t, const int32_t *co
   a.items = order != nullptr ? order + n_heavy : nullptr;
   a.n_items = n_rows - n_heavy;
   if (ride != nullptr) a.side[0] = ride[0], a.side[1] = ride[1];
-  set_mid(a, mid);
   if (int rc = launch_rl<true>(a, s)) return rc;
   a.side[0] = a.side[1] = SideFold{};
-  a.hv_blocks = 0;
   int64_t parts = rl_blocks(a.n_items, lm != nullptr);
   if (n_heavy > 0) {
     if (side)

@@ -659,7 +659,7 @@ int heavy_rows(int bwd, int64_t n_rows, int32_t F, const int64_t *rowptr, const 
                const int32_t *eid, const float *w, const float *X, int64_t ldx, float *Y,
                int64_t ldy, const float *row_scale, int mean, const int32_t *order,
                int64_t n_heavy, int64_t n_giant, hipStream_t stream, bool *side_used,
-               const ResEpi *rs, SpmmArgs *mid) {
+               const ResEpi *rs) {
   *side_used = false;
   if (order == nullptr || n_heavy <= 0) return MGCN_OK;
   SpmmArgs a{};
@@ -698,15 +698,9 @@ int heavy_rows(int bwd, int64_t n_rows, int32_t F, const int64_t *rowptr, const 
       if (rc) return rc;
     }
   }
-  if (n_heavy > n_giant) {
-    if (mid != nullptr) {
-      a.heavy_rows = order + n_giant;
-      *mid = a;
-      return MGCN_OK;
-    }
+  if (n_heavy > n_giant)
     return bwd ? launch_heavy_v<BWD_SUM>(a, vec, false, stream)
                : launch_heavy_v<FWD_SUM>(a, vec, false, stream);
-  }
   return MGCN_OK;
 }
 
@@ -778,11 +772,6 @@ extern "C" int mgcn_set_option(const char *name, int value) {
     return gemm_set_precision(value);
   }
   if (n == "spmm_xw_unroll") return xw_set_unroll(value);
-  if (n == "residual_mid_in_light") {
-    MGCN_REQUIRE(value == 0 || value == 1, "residual_mid_in_light must be 0 or 1");
-    g_mid_in_light = value;
-    return MGCN_OK;
-  }
   if (n == "residual_fused_mask") {
     MGCN_REQUIRE(value == 0 || value == 1, "residual_fused_mask must be 0 or 1");
     g_fused_mask = value;

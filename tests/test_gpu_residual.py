@@ -182,3 +182,4 @@ def test_residual_stack_matches_layer_by_layer(cuda, aggr, deg_norm, bias):
             torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6 * max(1.0, b.abs().max().item()))
         else:
             assert torch.equal(a, b)
+
