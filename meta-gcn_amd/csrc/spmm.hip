@@ -343,10 +343,10 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(const SpmmArgs a) {
   }
 }
 
-template <int VEC, int MODE, int HB>
+template <int VEC, int MODE, int HB, int Q>
 __global__ __launch_bounds__(HB) void spmm_heavy_kernel(const SpmmArgs a, int FC, int BE) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  heavy_row_block<VEC, MODE, HB>(a, FC, BE, blockIdx.x, smem);
+  heavy_row_block<VEC, MODE, HB, Q>(a, FC, BE, blockIdx.x, smem);
 }
 
 __global__ __launch_bounds__(kBlock) void row_degree_kernel(int64_t n_rows,
@@ -517,8 +517,27 @@ int launch_g(const SpmmArgs &a, hipStream_t stream) {
 // heavy rows (a few hundred edges) take little, so several share a CU.
 int g_heavy_lds = 160 * 1024;     // giant rows
 int g_heavy_mid_lds = 40 * 1024;  // other heavy rows
+int g_heavy_mid_q1 = 1;           // narrow rows: one edge quad in flight (heavy_mid_q1)
 int g_heavy_block = 1024;         // threads per giant-row workgroup
 int64_t g_giant_thr = 512;        // degree above which a heavy row is giant
+
+template <int VEC, int MODE, int HB, int Q>
+int launch_heavy_q(const SpmmArgs &a, int64_t n, int FC, int BE, size_t lds, hipStream_t stream) {
+  // the 160 KB dynamic-LDS attribute is per device: one bit per device id,
+  // per instantiation (VEC, MODE, HB, Q); racing threads at worst both set it
+  static std::atomic<uint64_t> attr_set{0};
+  int dev = 0;
+  MGCN_HIP_TRY(hipGetDevice(&dev));
+  const uint64_t bit = uint64_t(1) << (dev & 63);
+  if (!(attr_set.load(std::memory_order_acquire) & bit)) {
+    MGCN_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(&spmm_heavy_kernel<VEC, MODE, HB, Q>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr_set.fetch_or(bit, std::memory_order_release);
+  }
+  hipLaunchKernelGGL((spmm_heavy_kernel<VEC, MODE, HB, Q>), dim3((unsigned)n), dim3(HB), lds, stream,
+                     a, FC, BE);
+  return check_launch("spmm_heavy_kernel");
+}
 
 template <int VEC, int MODE, int HB>
 int launch_heavy_hb(SpmmArgs a, const int32_t *rows, int64_t n, int lds_budget,
@@ -534,20 +553,12 @@ int launch_heavy_hb(SpmmArgs a, const int32_t *rows, int64_t n, int lds_budget,
   BE &= ~15;
   if (BE < 16) BE = 16;  // a small budget still gets one 16-edge batch (<= 21 KB)
   const size_t lds = sizeof(float) * ((size_t)2 * FC * (BE + 4) + (size_t)12 * BE);
-  // the 160 KB dynamic-LDS attribute is per device: one bit per device id,
-  // per instantiation (VEC, MODE, HB); racing threads at worst both set it
-  static std::atomic<uint64_t> attr_set{0};
-  int dev = 0;
-  MGCN_HIP_TRY(hipGetDevice(&dev));
-  const uint64_t bit = uint64_t(1) << (dev & 63);
-  if (!(attr_set.load(std::memory_order_acquire) & bit)) {
-    MGCN_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(&spmm_heavy_kernel<VEC, MODE, HB>),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    attr_set.fetch_or(bit, std::memory_order_release);
-  }
-  hipLaunchKernelGGL((spmm_heavy_kernel<VEC, MODE, HB>), dim3((unsigned)n), dim3(HB), lds, stream,
-                     a, FC, BE);
-  return check_launch("spmm_heavy_kernel");
+  // narrow rows (FC <= 32, config 3's F = 32) in the 256-thread workgroups:
+  // one edge quad in flight per producer (84 VGPRs instead of 172-188, so
+  // LDS, not registers, sets the workgroups per CU): 2.77 -> 2.67 ms/step
+  if constexpr (HB == 256)
+    if (FC <= 32 && g_heavy_mid_q1) return launch_heavy_q<VEC, MODE, HB, 1>(a, n, FC, BE, lds, stream);
+  return launch_heavy_q<VEC, MODE, HB, 0>(a, n, FC, BE, lds, stream);
 }
 
 template <int VEC, int MODE>
@@ -747,6 +758,11 @@ extern "C" int mgcn_set_option(const char *name, int value) {
   if (n == "heavy_block") {
     MGCN_REQUIRE(value == 256 || value == 512 || value == 1024, "heavy_block must be 256, 512 or 1024");
     g_heavy_block = value;
+    return MGCN_OK;
+  }
+  if (n == "heavy_mid_q1") {
+    MGCN_REQUIRE(value == 0 || value == 1, "heavy_mid_q1 must be 0 or 1");
+    g_heavy_mid_q1 = value;
     return MGCN_OK;
   }
   if (n == "heavy_mid_lds_kb") {
