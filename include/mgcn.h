@@ -70,6 +70,9 @@ const char *mgcn_last_error(void);
  *   "heavy_lds_kb": LDS per giant-row workgroup, 16..160 (default 160)
  *   "heavy_block" : threads per giant-row workgroup, 256/512/1024 (1024)
  *   "heavy_mid_lds_kb": LDS per (non-giant) heavy-row workgroup (default 40)
+ *   "heavy_mid_q1": 1 (default) = one edge quad in flight per producer in the
+ *                   non-giant heavy-row workgroups when a row is <= 32 floats
+ *                   wide (fewer registers, more workgroups per CU); 0 = four
  *   "heavy_giant_thr" : degree above which a heavy row is giant, read by
  *                   mgcn_row_schedule (default 512)
  *   "gemm_tn_variant": LDS-staged dW kernel chunk depth (M, N multiples of
