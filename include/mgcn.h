@@ -70,6 +70,8 @@ const char *mgcn_last_error(void);
  *   "heavy_lds_kb": LDS per giant-row workgroup, 16..160 (default 160)
  *   "heavy_block" : threads per giant-row workgroup, 256/512/1024 (1024)
  *   "heavy_mid_lds_kb": LDS per (non-giant) heavy-row workgroup (default 40)
+ *   "residual_blocks": workgroup cap of the fused residual layer's launches
+ *                   (default 8192; the backward's is also capped at 4096)
  *   "heavy_mid_q1": 1 (default) = one edge quad in flight per producer in the
  *                   non-giant heavy-row workgroups when a row is <= 32 floats
  *                   wide (fewer registers, more workgroups per CU); 0 = four

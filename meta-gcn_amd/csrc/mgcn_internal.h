@@ -63,6 +63,7 @@ int gemm_set_precision(int value);
 int gemm_precision_is_x6();  // 1 under bf16x6 (the fused kernels need it)
 int xw_set_unroll(int value);  // fused.hip
 extern int g_fused_mask;       // residual.hip: the stack's fused lower-layer mask pass
+extern int g_rl_cap;           // residual.hip: workgroups per light-row launch (grid-stride beyond)
 // deterministic folds of per-workgroup partials (gemm.hip)
 // deterministic fold of split partials: C[e] (+)= sum_sp partial[sp * MN + e]
 int launch_fold(const float *partial, int64_t splits, int64_t MN, int N, float *C, int64_t ldc,

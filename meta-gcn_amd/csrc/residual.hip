@@ -382,7 +382,11 @@ void residual_layer_kernel(const RlArgs a) {
 // partials [block][2F] in a fixed row order (launch_colsum_fold folds them).
 // Thread (t_row, q): features 4 q .. 4 q + 3 of rows t_row, t_row + R, ...
 constexpr int kMaxParts = 1024;
-constexpr int kMaxRlParts = 2048;  // fused mask pass: partials per residual_layer_kernel launch
+// fused mask pass: partials per residual_layer_kernel launch, i.e. its
+// workgroup cap (grid-stride beyond): 2048 -> 4096 took config 3 2.67 -> 2.63
+// ms/step (the backward light pass had fewer workgroups than row tiles);
+// 8192 no better
+constexpr int kMaxRlParts = 4096;
 
 __global__ __launch_bounds__(256) void residual_mask_bwd_kernel(
     int64_t n, const float *__restrict__ dZ, int64_t lddz, const uint32_t *__restrict__ masks,
@@ -440,11 +444,15 @@ int mask_parts(int64_t n) {
 
 // blocks of one launch: grid-stride beyond (W / Wr^T staged once per block);
 // with the fused mask pass, each block also writes one partial of the sums
+}  // namespace
+int g_rl_cap = 8192;  // mgcn_set_option("residual_blocks"): workgroups per light-row launch
+namespace {
 int64_t rl_blocks(int64_t n_items, bool fused_mask) {
   if (n_items <= 0) return 0;
   const int64_t waves = (n_items + kTileRows - 1) / kTileRows;
   int64_t blocks = (waves + kRWaves - 1) / kRWaves;
-  const int64_t cap = fused_mask ? kMaxRlParts : 8192;
+  int64_t cap = g_rl_cap;
+  if (fused_mask && cap > kMaxRlParts) cap = kMaxRlParts;
   return blocks > cap ? cap : blocks;
 }
 

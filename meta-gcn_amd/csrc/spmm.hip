@@ -788,6 +788,11 @@ extern "C" int mgcn_set_option(const char *name, int value) {
     return gemm_set_precision(value);
   }
   if (n == "spmm_xw_unroll") return xw_set_unroll(value);
+  if (n == "residual_blocks") {
+    MGCN_REQUIRE(value >= 64 && value <= 65536, "residual_blocks must be in [64, 65536]");
+    g_rl_cap = value;
+    return MGCN_OK;
+  }
   if (n == "residual_fused_mask") {
     MGCN_REQUIRE(value == 0 || value == 1, "residual_fused_mask must be 0 or 1");
     g_fused_mask = value;
