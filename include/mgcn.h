@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define MGCN_ABI_VERSION 16
+#define MGCN_ABI_VERSION 17
 
 /* return codes */
 #define MGCN_OK 0
@@ -399,6 +399,9 @@ size_t mgcn_spmm_xw_bwd_workspace_bytes(int64_t n_rows, int32_t F_in, int32_t F_
  * dX only: X == NULL and dW == NULL (dX required, no win_mask) -- the
  * gather, dX = dH W^T and its epilogue, nothing else; dX bit for bit the
  * full form's.  Pair with mgcn_spmm_xw_fwd's Z and mgcn_gemm_bwd (dW-only).
+ * In the dX-only form `accumulate` != 0 ADDS the column sums into colsum
+ * (colsum += ...; ABI v17), so the row chunks of one adjoint fold their bias
+ * gradient on the device, in chunk order.
  * F = 256: the dX-only form only (dY any size: 64-bit row bases; relu_mask
  * in the 8-word layout of mgcn_spmm_xw_fwd at 256; dX 16-byte aligned rows).
  */

@@ -963,7 +963,8 @@ extern "C" int mgcn_spmm_xw_bwd(int64_t n_rows, int64_t n_cols, int32_t F_in, in
     if (!accumulate && dW != nullptr)
       for (int32_t r = 0; r < F_in; ++r)
         MGCN_HIP_TRY(hipMemsetAsync(dW + r * lddw, 0, sizeof(float) * F_out, s));
-    if (colsum) MGCN_HIP_TRY(hipMemsetAsync(colsum, 0, sizeof(float) * F_in, s));
+    if (colsum && !(dx_only && accumulate))
+      MGCN_HIP_TRY(hipMemsetAsync(colsum, 0, sizeof(float) * F_in, s));
     return MGCN_OK;
   }
   MGCN_REQUIRE(rowptr_t && dY, "mgcn_spmm_xw_bwd: null array");
@@ -983,7 +984,7 @@ extern "C" int mgcn_spmm_xw_bwd(int64_t n_rows, int64_t n_cols, int32_t F_in, in
       return MGCN_EWORKSPACE;
     }
     return xw_wide_bwd_dx(n_rows, rowptr_t, col_t, w_t, row_scale, dY, lddy, W, ldw, dX, lddx,
-                          relu_mask, row_div, colsum, workspace, g_xw_unroll, s);
+                          relu_mask, row_div, colsum, accumulate, workspace, g_xw_unroll, s);
   }
   MGCN_REQUIRE(dx_only || (ldx >= F_in && ldx % 4 == 0 && reinterpret_cast<uintptr_t>(X) % 16 == 0),
                "mgcn_spmm_xw_bwd: X must have 16-byte aligned rows");
@@ -1030,7 +1031,9 @@ extern "C" int mgcn_spmm_xw_bwd(int64_t n_rows, int64_t n_cols, int32_t F_in, in
   if (dx_only) {
     rc = g_xw_unroll == 4 ? launch_xb_dx<4>(a, epi, grid, s) : launch_xb_dx<8>(a, epi, grid, s);
     if (rc || epi == EPI_STORE) return rc;
-    return launch_colsum_fold(a.colsum_partial, grid, kXwF, colsum, s);
+    // dX only: accumulate != 0 adds the column sums into colsum (row chunks
+    // of one adjoint fold their bias gradient on the device)
+    return launch_fold(a.colsum_partial, grid, kXwF, kXwF, colsum, kXwF, accumulate, s);
   }
   rc = g_xw_unroll == 4 ? launch_xb_u<4>(a, epi, grid, s) : launch_xb_u<8>(a, epi, grid, s);
   if (rc) return rc;

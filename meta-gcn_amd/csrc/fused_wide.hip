@@ -489,7 +489,7 @@ int xw_wide_bwd_dx(int64_t n_rows, const int64_t *rowptr_t, const int32_t *col_t
                    const float *w_t, const float *row_scale, const float *dY, int64_t lddy,
                    const float *W, int64_t ldw, float *dX, int64_t lddx,
                    const uint32_t *relu_mask, const float *row_div, float *colsum,
-                   void *workspace, int unroll, hipStream_t s) {
+                   int accumulate, void *workspace, int unroll, hipStream_t s) {
   u32x4 *img = static_cast<u32x4 *>(workspace);
   float *partial = reinterpret_cast<float *>(static_cast<char *>(workspace) +
                                              align_up((size_t)kWImgFrags * 16, 256));
@@ -515,7 +515,7 @@ int xw_wide_bwd_dx(int64_t n_rows, const int64_t *rowptr_t, const int32_t *col_t
   int rc = unroll == 8 ? launch_wide<8>(a, true, epi, (int)grid, s)
                        : launch_wide<4>(a, true, epi, (int)grid, s);
   if (rc || epi == WEPI_STORE) return rc;
-  return launch_colsum_fold(partial, grid, kWF, colsum, s);
+  return launch_fold(partial, (int)grid, kWF, kWF, colsum, kWF, accumulate, s);
 }
 
 }  // namespace mgcn

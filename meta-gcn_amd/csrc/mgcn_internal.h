@@ -164,6 +164,6 @@ int xw_wide_bwd_dx(int64_t n_rows, const int64_t *rowptr_t, const int32_t *col_t
                    const float *w_t, const float *row_scale, const float *dY, int64_t lddy,
                    const float *W, int64_t ldw, float *dX, int64_t lddx,
                    const uint32_t *relu_mask, const float *row_div, float *colsum,
-                   void *workspace, int unroll, hipStream_t s);
+                   int accumulate, void *workspace, int unroll, hipStream_t s);
 
 }  // namespace mgcn

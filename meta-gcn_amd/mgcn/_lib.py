@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmgcn.so")
 
 # constants mirrored from include/mgcn.h
-ABI_VERSION = 16
+ABI_VERSION = 17
 OK, EINVAL, EINDEX, EHIP, EWORKSPACE = 0, 1, 2, 3, 4
 REDUCE_SUM, REDUCE_MEAN, REDUCE_MAX = 0, 1, 2
 NORM_NONE, NORM_SM, NORM_RW = 0, 1, 2

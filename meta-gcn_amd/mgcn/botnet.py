@@ -399,7 +399,9 @@ def train(train_ds, val_ds, test_ds, enc_sizes=(32,) * 8, residual_hop=0, deg_no
         if stopper.improved:
             best_state = {k: v.detach().clone() for k, v in model.state_dict().items()}
             best_epoch = ep
-            if save_path:
+            # the replicas hold identical states: one writer (rank 0), so
+            # ranks on a shared filesystem never write the file concurrently
+            if save_path and (dpr is None or dpr.rank == 0):
                 torch.save(best_state, save_path)
         elif stopper.early_stop:
             log("Early stopping here.")

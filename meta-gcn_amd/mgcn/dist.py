@@ -51,6 +51,7 @@ substitute a CPU double (tests/cpu_backend.py) under gloo.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import torch
@@ -90,11 +91,13 @@ class HipBackend:
         return spmm_xw_fwd(*a, **k)
 
     def spmm_xw_bwd_dx(self, view_t, w_t, row_scale, dY, W, relu_mask=None, row_div=None,
-                       out=None):
-        """dX only (X = NULL): returns the lower layer's bias column sums or None."""
+                       out=None, colsum=None):
+        """dX only (X = NULL): returns the lower layer's bias column sums or
+        None; with ``colsum`` (and relu_mask) they are added into it on the
+        device instead."""
         from .ops import spmm_xw_bwd
         return spmm_xw_bwd(view_t, w_t, row_scale, dY, None, W, relu_mask=relu_mask,
-                           row_div=row_div, dx_out=out)[2]
+                           row_div=row_div, dx_out=out, colsum_acc=colsum)[2]
 
     def gemm_bwd_dw(self, Z, dY, W, dh_colsum=False):
         from .ops import dw_pass
@@ -215,11 +218,30 @@ class Shard:
         return full[self.lo:self.hi]
 
 
+# Run every collective of the sharded path even in a one-rank group
+# (set_force_collectives / env MGCN_FORCE_COLLECTIVES=1): the RCCL calls --
+# the chunked all_gather_into_tensor(async_op=True), the packed exchange's
+# size gather and payload, the bucketed all_reduce -- then execute on one GPU
+# exactly as a rank of a multi-GPU group issues them
+# (tests/test_gpu_rccl.py); by default world 1 copies instead.
+FORCE_COLLECTIVES = os.environ.get("MGCN_FORCE_COLLECTIVES", "0") != "0"
+
+
+def set_force_collectives(enabled: bool) -> None:
+    global FORCE_COLLECTIVES
+    FORCE_COLLECTIVES = bool(enabled)
+
+
+def _collective(world: int) -> bool:
+    """True when a group of ``world`` ranks exchanges through torch.distributed."""
+    return world > 1 or (FORCE_COLLECTIVES and dist.is_available() and dist.is_initialized())
+
+
 def _all_gather_flat(local: torch.Tensor, n_pad: int, world: int, group=None) -> torch.Tensor:
     """[n, ...] per rank (n <= n_pad) -> [world * n_pad, ...] rank-major."""
     buf = torch.zeros((n_pad,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
     buf[:local.size(0)] = local
-    if world == 1:
+    if not _collective(world):
         return buf
     out = torch.empty((world * n_pad,) + tuple(local.shape[1:]), dtype=local.dtype,
                       device=local.device)
@@ -228,7 +250,7 @@ def _all_gather_flat(local: torch.Tensor, n_pad: int, world: int, group=None) ->
 
 
 def _gather_into(out, inp, world, group, async_op):
-    if world == 1:
+    if not _collective(world):
         out.copy_(inp)
         return None
     if dist.get_backend(group) == "nccl":
@@ -318,8 +340,11 @@ class _ChunkExchange:
                  backend, packed: bool):
         self.sh, self.local, self.table, self.group, self.be = shard, local_pad, table, group, backend
         F = local_pad.size(1)
+        # (the packed form's row offsets are int32, pack.hip: a chunk of 2^31
+        # words or more goes dense)
         self.packed = bool(packed) and local_pad.dtype == torch.float32 and F % 32 == 0 and \
-            hasattr(backend, "pack_count") and (shard.world > 1 or shard.emulated)
+            hasattr(backend, "pack_count") and (_collective(shard.world) or shard.emulated) and \
+            shard.chunk_rows * F < 2 ** 31
         self.words = F // 32
         self.pending = []
         self.works = []
@@ -339,7 +364,7 @@ class _ChunkExchange:
         self.be.pack_count(rows, send[cr:head].view(cr, self.words), counts)
         total = counts.sum(dtype=torch.int64).view(1)
         P = sh.world
-        if sh.emulated or P == 1:
+        if sh.emulated or not _collective(P):
             totals, work = total, None
         else:
             totals = torch.empty(P, dtype=torch.int64, device=dev)
@@ -649,17 +674,22 @@ class _ShardedStack(torch.autograd.Function):
                     dX[rows:].zero_()  # padding rows travel too (packed: as zeros)
                 # masked by the lower layer's ReLU: travels packed
                 xch = _ChunkExchange(sh, dX, ntab, group, be, _pack_on(sh) and relus[l - 1])
-            works, sums = [], []
+            works = []
+            # the lower layer's bias gradient: every chunk's column sums are
+            # added into one device vector by the adjoint launches themselves
+            # (mgcn_spmm_xw_bwd accumulate, in chunk order; no host reduction)
+            csum = None
+            if l > 0 and ctx.has_bias[l - 1]:
+                csum = torch.zeros(W.size(0), dtype=torch.float32, device=dev)
             for c in range(C):
                 a, e = sh.chunk(c)
                 if e > a:
-                    cs = be.spmm_xw_bwd_dx(
+                    be.spmm_xw_bwd_dx(
                         sh.bwd.rows(a, e, sh.chunk_edges_bwd[c]), sh.w_bwd,
                         None if sh.row_scale is None else sh.row_scale[a:e], tab, W,
                         relu_mask=rms[l - 1][a:e] if l > 0 else None,
-                        row_div=rd[a:e] if (l > 0 and rd is not None) else None, out=dX[a:e])
-                    if cs is not None:
-                        sums.append(cs)
+                        row_div=rd[a:e] if (l > 0 and rd is not None) else None, out=dX[a:e],
+                        colsum=csum)
                 if xch is not None:
                     xch.start(c)
                     xch.finish(keep=1)
@@ -667,8 +697,7 @@ class _ShardedStack(torch.autograd.Function):
                 works = [xch]  # its last chunk is finished at the wait, after the next dW
             if l > 0:
                 if ctx.has_bias[l - 1]:
-                    gb[l - 1] = (torch.stack(sums).sum(0) if sums else
-                                 torch.zeros(W.size(0), dtype=torch.float32, device=dev))
+                    gb[l - 1] = csum
                 dY, tab = dX, ntab
             else:
                 dx = dX[:rows]
@@ -845,7 +874,7 @@ class DataParallel:
 
     def broadcast_params(self) -> None:
         """Rank 0's parameters to every rank (identical replicas)."""
-        if self.world == 1:
+        if not _collective(self.world):
             return
         with torch.no_grad():
             for p in self.params:
@@ -854,7 +883,7 @@ class DataParallel:
 
     def all_sum(self, values, device=None):
         """Sum a few numbers over the ranks (one all_reduce); returns floats."""
-        if self.world == 1:
+        if not _collective(self.world):
             return [float(v) for v in values]
         dev = device if device is not None else (self.params[0].device if self.params else "cpu")
         if dist.get_backend(self.group) == "nccl" and torch.device(dev).type != "cuda":
@@ -865,24 +894,43 @@ class DataParallel:
 
     def reduce_grads(self) -> None:
         """All-reduce (sum) every parameter's gradient; a rank whose share
-        was empty (or whose parameters took no gradient) contributes zeros."""
-        if self.world == 1:
+        was empty (or whose parameters took no gradient) contributes zeros.
+        A parameter that NO rank gave a gradient keeps ``grad = None`` -- as
+        in one process, where the optimizer then skips it (no weight decay,
+        no moment decay): a per-parameter "has grad" flag travels in the same
+        bucketed all_reduce."""
+        if not _collective(self.world):
             return
-        for p in self.params:
-            if p.requires_grad and p.grad is None:
+        params = [p for p in self.params if p.requires_grad]
+        if not params:
+            return
+        dev = params[0].device
+        has = torch.tensor([float(p.grad is not None) for p in params], dtype=torch.float32,
+                           device=dev)
+        for p in params:
+            if p.grad is None:
                 p.grad = torch.zeros_like(p)
-        allreduce_grads([p for p in self.params if p.requires_grad], self.group)
+        _allreduce_flat([p.grad for p in params] + [has], self.group)
+        for p, h in zip(params, has.tolist()):
+            if h == 0.0:
+                p.grad = None
+
+
+def _allreduce_flat(tensors, group=None) -> None:
+    """Sum the tensors over the ranks in place with ONE all_reduce of their
+    concatenation (a bucket: one RCCL call per step, not one per tensor)."""
+    flat = torch.cat([t.reshape(-1) for t in tensors])
+    dist.all_reduce(flat, group=group)
+    off = 0
+    for t in tensors:
+        n = t.numel()
+        t.copy_(flat[off:off + n].view_as(t))
+        off += n
 
 
 def allreduce_grads(params, group=None) -> None:
     """One bucketed all_reduce (sum) of the replicated parameters' gradients."""
     grads = [p.grad for p in params if p.grad is not None]
-    if not grads or not dist.is_initialized() or dist.get_world_size(group) == 1:
+    if not grads or not dist.is_initialized() or not _collective(dist.get_world_size(group)):
         return
-    flat = torch.cat([g.reshape(-1) for g in grads])
-    dist.all_reduce(flat, group=group)
-    off = 0
-    for g in grads:
-        n = g.numel()
-        g.copy_(flat[off:off + n].view_as(g))
-        off += n
+    _allreduce_flat(grads, group)

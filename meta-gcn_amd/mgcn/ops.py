@@ -233,7 +233,7 @@ def spmm_xw_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tens
                 dY: torch.Tensor, X: torch.Tensor, W: torch.Tensor, want_dx: bool = True,
                 relu_mask: torch.Tensor | None = None, row_div: torch.Tensor | None = None,
                 win_mask: torch.Tensor | None = None, slot_map: torch.Tensor | None = None,
-                dx_out: torch.Tensor | None = None):
+                dx_out: torch.Tensor | None = None, colsum_acc: torch.Tensor | None = None):
     """Both adjoints of a 128 -> 128 layer from one pass (``mgcn_spmm_xw_bwd``):
     dH = A^T dY [* row_scale] stays on chip, and dW = X^T dH, dX = dH W^T
     (with the lower layer's ReLU mask / row divisor / bias column sums, as
@@ -284,7 +284,18 @@ def spmm_xw_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tens
         if relu_mask.shape != (M, mw) or relu_mask.dtype != torch.int32:
             raise ValueError(f"spmm_xw_bwd: relu_mask must be int32 [{M}, {mw}]")
         relu_mask = relu_mask.contiguous()
-        colsum = torch.empty(F_in, dtype=torch.float32, device=dev)
+        if colsum_acc is not None:
+            if not dx_only or colsum_acc.dtype != torch.float32 or \
+                    tuple(colsum_acc.shape) != (F_in,) or not colsum_acc.is_contiguous():
+                raise ValueError(f"spmm_xw_bwd: colsum_acc must be a contiguous float32 [{F_in}] "
+                                 f"tensor (dX-only form)")
+            L.require_device(colsum_acc)
+            colsum = colsum_acc
+        else:
+            colsum = torch.empty(F_in, dtype=torch.float32, device=dev)
+    elif colsum_acc is not None:
+        raise ValueError("spmm_xw_bwd: colsum_acc needs relu_mask")
+    acc_flag = 1 if colsum_acc is not None else 0
     ws_bytes = int(lib.mgcn_spmm_xw_bwd_workspace_bytes(M, F_in, F_out))
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
     tname = "spmm_xw_bwd_dx" if dx_only else "spmm_xw_bwd" if want_dx else "spmm_xw_bwd_dw"
@@ -295,7 +306,7 @@ def spmm_xw_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tens
                                   L.ptr(view_t.col), L.ptr(w_t), L.ptr(row_scale), L.ptr(dY),
                                   dY.stride(0), L.ptr(X), 0 if dx_only else X.stride(0),
                                   L.ptr(W), W.stride(0), L.ptr(dW),
-                                  0 if dx_only else dW.stride(0), 0, L.ptr(dX),
+                                  0 if dx_only else dW.stride(0), acc_flag, L.ptr(dX),
                                   dX.stride(0) if dX is not None else 0, L.ptr(relu_mask),
                                   L.ptr(row_div), L.ptr(colsum), L.ptr(win_mask),
                                   L.ptr(slot_map), L.ptr(ws), ws_bytes, L.stream_of(dev))
@@ -1015,6 +1026,21 @@ class _GCNStack(torch.autograd.Function):
             am = args[l] if args[l].numel() else None
             W = Ws[l]
             fused = l > 0 and relus[l - 1] and rmasks[l - 1].numel() > 0
+            if not ctx.needs_input_grad[5 + 2 * l]:
+                # a frozen weight: no dW; only dX (with the lower layer's ReLU
+                # / bias gradient) is wanted -- the dX-only adjoint, which
+                # also takes the 8-word masks of a 256-wide layer
+                if l == 0 and not ctx.needs_input_grad[0]:
+                    continue
+                if am is None and (fused or l == 0) and _FUSE_XW and \
+                        spmm_xw_supported(plan.bwd, W.size(1), W.size(0), L.REDUCE_SUM):
+                    if fused:
+                        _, dY, db = spmm_xw_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY,
+                                                None, W, relu_mask=rmasks[l - 1], row_div=rd)
+                        gb[l - 1] = db if ctx.has_bias[l - 1] else None
+                    else:
+                        dx = spmm_xw_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, None, W)[1]
+                    continue
             if z_path(l):
                 # dW = Z^T dY from the forward's aggregate Z = A h (a dense
                 # pass over Z and dY, no gather); mean: Z is the undivided sum
@@ -1060,7 +1086,8 @@ class _GCNStack(torch.autograd.Function):
             if l == 0 and not ctx.needs_input_grad[0] and gemm_bwd_supported(W.size(0), W.size(1)):
                 gW[l] = gemm_bwd(inputs[l], dH, W, want_dx=False)[0]  # dW alone, same pass shape
                 continue
-            gW[l] = gemm_tn(inputs[l], dH)
+            if ctx.needs_input_grad[5 + 2 * l]:
+                gW[l] = gemm_tn(inputs[l], dH)
             if l > 0:
                 if fused:
                     dY, db = gemm_nn(dH, W, transpose_w=True, relu_mask=rmasks[l - 1],

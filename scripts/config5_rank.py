@@ -34,6 +34,68 @@ from bench import KernelTimer, launch_bytes  # noqa: E402
 XGMI_LINK_GBS = 153.0  # per link and direction
 
 
+def _global_ids(t, sh):
+    """exchange-table positions -> global node ids (mgcn.dist.table_positions
+    inverted): t = c P cr + k cr + (i - c cr)."""
+    P, cr = sh.world, sh.chunk_rows
+    c = torch.div(t, P * cr, rounding_mode="floor")
+    k = torch.div(t - c * P * cr, cr, rounding_mode="floor")
+    i = c * cr + (t - c * P * cr - k * cr)
+    b = torch.tensor(sh.bounds, dtype=torch.int64, device=t.device)
+    return b[k] + i
+
+
+def sample_check(model, Xt, odeg, n_rows, F, tol=1e-5):
+    """Config-5 parity at its own size (gcn_base_models.py:201, 223-241):
+    windows of ``n_rows`` destination rows of the rank's forward layer
+    (mgcn_spmm_xw_fwd on the fused wide kernel: Y = relu((A X) W + b)) and of
+    its dX-only adjoint (dX = (A^T dY) W^T) against a host-independent fp64
+    restatement -- the symmetric norm rebuilt from the global out-degrees in
+    fp64, the table positions mapped back to global ids, the sums in fp64 --
+    within tol x the |.| bound (|A| |X| |W| + |b|)."""
+    from mgcn import _lib as L
+    from mgcn import ops
+    sh = model.shard
+    W0, b0, W1 = model.W[0].detach(), model.b[0].detach(), model.W[1].detach()
+    dinv = odeg.to(torch.float64).pow(-0.5)
+    dinv[torch.isinf(dinv)] = 0.0
+    res = {"rows_per_window": n_rows, "windows": [], "tol": tol}
+    worst = 0.0
+    for a in (0, sh.rows // 2, max(sh.rows - n_rows, 0)):
+        e = min(a + n_rows, sh.rows)
+        for kind, view, w in (("fwd", sh.fwd, sh.w_fwd), ("dx", sh.bwd, sh.w_bwd)):
+            v = view.rows(a, e)
+            rp = v.rowptr.to(torch.int64)
+            s0, s1 = int(rp[0]), int(rp[-1])
+            cols = v.col[s0:s1].to(torch.int64)
+            deg = (rp[1:] - rp[:-1])
+            row_of = torch.repeat_interleave(torch.arange(e - a, device=cols.device), deg)
+            me = sh.lo + a + row_of            # this rank's node of each slot
+            other = _global_ids(cols, sh)      # the gathered node
+            w64 = dinv[me] * dinv[other]
+            g = Xt[cols].to(torch.float64)
+            agg = torch.zeros(e - a, F, dtype=torch.float64, device=g.device)
+            agg.index_add_(0, row_of, g * w64[:, None])
+            absg = torch.zeros_like(agg).index_add_(0, row_of, g.abs() * w64.abs()[:, None])
+            if kind == "fwd":
+                y = ops.spmm_xw_fwd(v, w, Xt, W0, L.REDUCE_SUM, b0, True)
+                ref = torch.relu(agg @ W0.double() + b0.double())
+                bound = absg @ W0.double().abs() + b0.double().abs()
+            else:
+                y = ops.spmm_xw_bwd(v, w, None, Xt, None, W1)[1]
+                ref = agg @ W1.double().t()
+                bound = absg @ W1.double().abs().t()
+            err = (y.double() - ref).abs()
+            ratio = float((err / (tol * bound + 1e-30)).max())
+            worst = max(worst, ratio)
+            res["windows"].append({"kind": kind, "rows": [sh.lo + a, sh.lo + e],
+                                   "slots": s1 - s0, "max_err_over_bound": ratio,
+                                   "max_abs_err": float(err.max())})
+    res["worst"] = worst
+    res["ok"] = worst <= 1.0
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--nodes", type=int, default=50_000_000)
@@ -48,6 +110,8 @@ def main():
     ap.add_argument("--no-fused", action="store_true")
     ap.add_argument("--dense-exchange", action="store_true",
                     help="no zero-skipping: the ReLU'd tables travel dense")
+    ap.add_argument("--check-rows", type=int, default=1024,
+                    help="rows per window of the sampled fp64 check (0: no check)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
@@ -71,6 +135,8 @@ def main():
                        emulate=(args.rank, args.world))
     sh = model.shard
     nnz = int(ei.size(1))
+    # out-degrees for the fp64 restatement of the norms (sampled check)
+    odeg = torch.bincount(ei[0], minlength=N) if args.check_rows else None
     del ei
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
@@ -114,6 +180,8 @@ def main():
         t = k["total_ms"] * 1e-3
         kern[name] = dict(k, bytes=byts / k["launches"], gbs=byts / t / 1e9 if t else None)
     kernel_ms = sum(k["total_ms"] for k in kern.values())
+    check = sample_check(model, Xt, odeg, args.check_rows, F) if args.check_rows else None
+    del odeg
     # predicted curve.  Local work of a rank at P: the compute scales with its
     # rows (8 / P of rank 0's here); the pack / unpack work with the share of
     # each table received, (P - 1) / P (measured here at P = 8: 7/8).  Each
@@ -158,8 +226,11 @@ def main():
            "packed_exchange_ratio": ratio if packed_tables else None,
            "dense_equivalent_tables_per_step": eff_tables,
            "xgmi_link_gbs": XGMI_LINK_GBS, "predicted_curve": curve,
-           "peak_mem_gb": torch.cuda.max_memory_allocated() / 1e9}
+           "peak_mem_gb": torch.cuda.max_memory_allocated() / 1e9,
+           "sampled_check": check}
     print(json.dumps(out), flush=True)
+    if check is not None and not check["ok"]:
+        sys.exit("config5_rank: sampled rows outside the fp64 bound")
 
 
 if __name__ == "__main__":

@@ -214,7 +214,7 @@ class CpuBackend:
         return (y, Z) if want_z else y
 
     def spmm_xw_bwd_dx(self, view_t, w_t, row_scale, dY, W, relu_mask=None, row_div=None,
-                       out=None):
+                       out=None, colsum=None):
         dH = self.spmm_bwd(view_t, w_t, row_scale, dY, L.REDUCE_SUM)
         dX = _mm(dH, W.detach().t())
         cs = None
@@ -224,6 +224,9 @@ class CpuBackend:
             if row_div is not None:
                 dX = dX / row_div.view(-1, 1)
         out.copy_(dX)
+        if colsum is not None and cs is not None:
+            colsum.add_(cs)
+            return None
         return cs
 
     def gemm_bwd_dw(self, Z, dY, W, dh_colsum=False):

@@ -36,7 +36,7 @@ def _problem(N=300, pairs=1500, F=16, L=3, seed=0):
     return ei, N, X, Ws, bs, dY
 
 
-def _run(rank, world, port, aggr, out_q, F=16, fused=True, chunks=4, pack=True):
+def _run(rank, world, port, aggr, out_q, F=16, fused=True, chunks=4, pack=True, force=False):
     sys.path[:0] = [os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "meta-gcn_amd"),
                     HERE]
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -48,6 +48,7 @@ def _run(rank, world, port, aggr, out_q, F=16, fused=True, chunks=4, pack=True):
         from mgcn import dist as mdist
         from mgcn.dist import ShardedGCN
         mdist.set_pack_exchange(pack)
+        mdist.set_force_collectives(force)
         ei, N, X, Ws, bs, dY = _problem(F=F)
         m = ShardedGCN(ei, N, Ws, bs, device=torch.device("cpu"), aggr=aggr,
                        backend=CpuBackend(), fused=fused, chunks=chunks)
@@ -73,11 +74,12 @@ def _run(rank, world, port, aggr, out_q, F=16, fused=True, chunks=4, pack=True):
         dist.destroy_process_group()
 
 
-def _launch(world, aggr, F=16, fused=True, chunks=4, pack=True):
+def _launch(world, aggr, F=16, fused=True, chunks=4, pack=True, force=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_run, args=(r, world, port, aggr, q, F, fused, chunks, pack))
+    procs = [ctx.Process(target=_run, args=(r, world, port, aggr, q, F, fused, chunks, pack,
+                                            force))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -127,6 +129,25 @@ def test_packed_exchange_is_bitwise_the_dense_one(world, aggr, F, chunks):
         st = rp["stats"]
         assert 0 < st["sent_words"] < 0.8 * st["dense_words"], st
         assert rd["stats"]["dense_words"] == 0
+
+
+@pytest.mark.parametrize("aggr", ["add", "mean"])
+def test_forced_collectives_at_world_one(aggr):
+    """set_force_collectives(True) in a one-rank group: every exchange
+    (chunked all-gathers, the packed exchange's size gather and payload, the
+    gradient all-reduce) goes through torch.distributed -- the path
+    tests/test_gpu_rccl.py runs on RCCL -- and the results are bit for bit
+    the world-1 copies'."""
+    forced = _launch(1, aggr, 32, True, 3, pack=True, force=True)[0]
+    plain = _launch(1, aggr, 32, True, 3, pack=True, force=False)[0]
+    for key in ("out", "dX", "out_table"):
+        np.testing.assert_array_equal(forced[key], plain[key])
+    for key in ("grads", "grads_table"):
+        for g, g1 in zip(forced[key], plain[key]):
+            np.testing.assert_array_equal(g, g1)
+    st = forced["stats"]
+    assert 0 < st["sent_words"] < st["dense_words"], st
+    assert plain["stats"]["dense_words"] == 0
 
 
 def test_fused_and_per_layer_paths_agree():

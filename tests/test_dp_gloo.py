@@ -159,3 +159,34 @@ def test_sharded_gcn_stack_module_matches_one_process(world, aggr):
         np.testing.assert_array_equal(r["dx"], one["dx"][lo:hi])
         for a, b in zip(r["grads"], one["grads"]):
             np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-5 * max(1, np.abs(b).max()))
+
+
+def _grad_flag_worker(rank, world, port, q):
+    sys.path[:0] = [os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "meta-gcn_amd")]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mgcn.dist import DataParallel
+        a = torch.nn.Parameter(torch.ones(3))      # every rank takes a gradient
+        b = torch.nn.Parameter(torch.ones(2))      # only rank 0 does
+        c = torch.nn.Parameter(torch.ones(4))      # no rank does
+        dp = DataParallel([a, b, c])
+        loss = (a * (rank + 1)).sum() + ((b * 2).sum() if rank == 0 else 0.0)
+        loss.backward()
+        dp.reduce_grads()
+        q.put({"rank": rank, "a": a.grad.numpy().copy(), "b": b.grad.numpy().copy(),
+               "c": c.grad is None})
+    finally:
+        dist.destroy_process_group()
+
+
+def test_data_parallel_keeps_untouched_grads_none():
+    """A parameter no rank gave a gradient keeps grad None after reduce_grads
+    (as in one process, so Adam skips it); one that only some ranks touched
+    gets the sum (no zero grads for untouched parameters)."""
+    res = _spawn(_grad_flag_worker, 2)
+    for r in res:
+        np.testing.assert_array_equal(r["a"], np.full(3, 3.0))
+        np.testing.assert_array_equal(r["b"], np.full(2, 2.0))
+        assert r["c"]
