@@ -290,3 +290,38 @@ def test_wide_stack_random_weights_vs_fp64(cuda, oracle):
         else:
             mask = (acts[l] > 0).double()
             g, gm = dX * mask, dXm * mask
+
+
+def test_wide_stack_frozen_middle_weight(cuda, oracle):
+    """a 256-wide stack whose middle weight needs no gradient (and
+    a frozen bottom one).  The middle layer keeps no Z, so its backward runs
+    the dX-only adjoint with the 8-word ReLU mask of the layer below (no dW
+    product, no 4-word-mask GEMM epilogue); the other gradients equal the
+    unfrozen stack's bit for bit, the frozen weights get none."""
+    rng = np.random.default_rng(31)
+    N = 20000
+    ei = _graph(rng, N, 200000)
+    a = (6.0 / (2 * F)) ** 0.5
+    Ws = [torch.from_numpy(rng.uniform(-a, a, (F, F)).astype(np.float32)) for _ in range(3)]
+    bs = [torch.from_numpy(rng.uniform(-0.1, 0.1, F).astype(np.float32)) for _ in range(3)]
+    X = _t(rng.standard_normal((N, F)).astype(np.float32), cuda)
+    dY = _t(rng.standard_normal((N, F)).astype(np.float32), cuda)
+    eic = _t(ei, cuda)
+    res = []
+    for frozen in ((), (1,), (0, 1)):
+        stack = _stack(cuda, Ws, bs)
+        params = list(stack.parameters())
+        for l in frozen:
+            params[2 * l].requires_grad_(False)
+        x = X.clone().requires_grad_(True)
+        y = stack(x, eic)
+        y.backward(dY)
+        for l in frozen:
+            assert params[2 * l].grad is None
+        res.append((y.detach(), x.grad, [p.grad for p in params]))
+    base = res[0]
+    for y, gx, grads in res[1:]:
+        assert torch.equal(y, base[0]) and torch.equal(gx, base[1])
+        for g, g0 in zip(grads, base[2]):
+            if g is not None:
+                assert torch.equal(g, g0)
