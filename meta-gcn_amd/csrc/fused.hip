@@ -951,15 +951,10 @@ extern "C" int mgcn_spmm_xw_bwd(int64_t n_rows, int64_t n_cols, int32_t F_in, in
                "mgcn_spmm_xw_bwd: at F=%d only the dX-only form (X = dW = NULL)", F_in);
   MGCN_REQUIRE(dx_only || (X != nullptr && dW != nullptr && lddw >= F_out),
                "mgcn_spmm_xw_bwd: bad dW (X and dW are given together, or both NULL for dX only)");
-  MGCN_REQUIRE(!dx_only || (dX != nullptr && win_mask == nullptr),
-               "mgcn_spmm_xw_bwd: the dX-only form needs dX and takes no win_mask");
-  const int epi = relu_mask == nullptr ? EPI_STORE : row_div != nullptr ? EPI_RELU_DIV : EPI_RELU;
-  MGCN_REQUIRE(epi == EPI_STORE || (dX != nullptr && colsum != nullptr),
-               "mgcn_spmm_xw_bwd: relu_mask needs dX and colsum");
   MGCN_REQUIRE(row_div == nullptr || relu_mask != nullptr,
                "mgcn_spmm_xw_bwd: row_div needs relu_mask");
   hipStream_t s = as_stream(stream);
-  if (n_rows == 0) {
+  if (n_rows == 0) {  // an empty row range (a sharded chunk): no dX rows to write
     if (!accumulate && dW != nullptr)
       for (int32_t r = 0; r < F_in; ++r)
         MGCN_HIP_TRY(hipMemsetAsync(dW + r * lddw, 0, sizeof(float) * F_out, s));
@@ -967,6 +962,11 @@ extern "C" int mgcn_spmm_xw_bwd(int64_t n_rows, int64_t n_cols, int32_t F_in, in
       MGCN_HIP_TRY(hipMemsetAsync(colsum, 0, sizeof(float) * F_in, s));
     return MGCN_OK;
   }
+  MGCN_REQUIRE(!dx_only || (dX != nullptr && win_mask == nullptr),
+               "mgcn_spmm_xw_bwd: the dX-only form needs dX and takes no win_mask");
+  const int epi = relu_mask == nullptr ? EPI_STORE : row_div != nullptr ? EPI_RELU_DIV : EPI_RELU;
+  MGCN_REQUIRE(epi == EPI_STORE || (dX != nullptr && colsum != nullptr),
+               "mgcn_spmm_xw_bwd: relu_mask needs dX and colsum");
   MGCN_REQUIRE(rowptr_t && dY, "mgcn_spmm_xw_bwd: null array");
   MGCN_REQUIRE(lddy >= F_out && lddy % 4 == 0 && reinterpret_cast<uintptr_t>(dY) % 16 == 0,
                "mgcn_spmm_xw_bwd: dY must have 16-byte aligned rows");
