@@ -888,7 +888,7 @@ extern "C" int mgcn_spmm_xw_fwd(int64_t n_rows, int64_t n_cols, int32_t F_in, in
     }
     return xw_wide_fwd(n_rows, rowptr, col, w, X, ldx, W, ldw, bias, Y, ldy,
                        reduce == MGCN_REDUCE_MEAN, relu != 0, relu_mask, Z, ldz, workspace,
-                       g_xw_unroll, as_stream(stream));
+                       as_stream(stream));
   }
   MGCN_REQUIRE(n_cols > 0 && (uint64_t)n_cols * (uint64_t)ldx * 4u <= 0xfffffff0ull,
                "mgcn_spmm_xw_fwd: X must hold 1 .. 4 GiB - 1 bytes (32-bit gather offsets)");
@@ -984,7 +984,7 @@ extern "C" int mgcn_spmm_xw_bwd(int64_t n_rows, int64_t n_cols, int32_t F_in, in
       return MGCN_EWORKSPACE;
     }
     return xw_wide_bwd_dx(n_rows, rowptr_t, col_t, w_t, row_scale, dY, lddy, W, ldw, dX, lddx,
-                          relu_mask, row_div, colsum, accumulate, workspace, g_xw_unroll, s);
+                          relu_mask, row_div, colsum, accumulate, workspace, s);
   }
   MGCN_REQUIRE(dx_only || (ldx >= F_in && ldx % 4 == 0 && reinterpret_cast<uintptr_t>(X) % 16 == 0),
                "mgcn_spmm_xw_bwd: X must have 16-byte aligned rows");

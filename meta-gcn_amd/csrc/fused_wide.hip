@@ -53,6 +53,24 @@
 #include "x6.h"
 
 namespace mgcn {
+
+// mgcn_set_option("wide_pair") / ("wide_unroll"): both rows of a wave's pair
+// gathered together or one after the other -- bit 0 the forward, bit 1 the
+// adjoint (default 3: both paired); gathered rows in flight per row and
+// round (4 or 8)
+int g_wide_pair = 3;
+int g_wide_unroll = 4;
+
+int wide_set_option(const char *name, int value) {
+  const bool pair = name[5] == 'p';
+  if (pair ? (value < 0 || value > 3) : (value != 4 && value != 8)) {
+    set_error(pair ? "wide_pair must be 0 .. 3" : "wide_unroll must be 4 or 8");
+    return MGCN_EINVAL;
+  }
+  (pair ? g_wide_pair : g_wide_unroll) = value;
+  return MGCN_OK;
+}
+
 namespace {
 
 using namespace x6;
@@ -202,6 +220,77 @@ __device__ __forceinline__ void wide_gather(const float *__restrict__ X, int64_t
   }
 }
 
+// Both rows of a wave's pair gathered together (PAIR kernels): U slots of
+// EACH row in flight per round, so a wave keeps 2 U gathered 1-KB rows in
+// flight instead of U -- one wave's rows are the chunk's rows 2 w and 2 w + 1,
+// and alone each pays its dependent round trips (deg 11 at U = 4: three)
+// while the other waits.  Each row is still folded in its own edge order
+// with separately rounded products and adds (bit for bit wide_gather).
+template <int U>
+__device__ __forceinline__ void wide_gather2(const float *__restrict__ X, int64_t ldx,
+                                             const int32_t *__restrict__ col,
+                                             const float *__restrict__ w, const WRow &ma,
+                                             const WRow &mb, int lane, float (&aa)[4],
+                                             float (&ab)[4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) aa[j] = ab[j] = 0.0f;
+  int mca = ma.mc, mcb = mb.mc;
+  float mwa = ma.mw, mwb = mb.mw;
+  const int64_t da = ma.deg, db = mb.deg;
+  const int64_t dm = da > db ? da : db;
+  for (int64_t e0 = 0; e0 < dm; e0 += 64) {
+    if (e0 > 0) {  // rows longer than one metadata batch load the rest in place
+      mca = mcb = 0;
+      mwa = mwb = 1.0f;
+      if (e0 + lane < da) {
+        mca = col[ma.beg + e0 + lane];
+        if (w != nullptr) mwa = w[ma.beg + e0 + lane];
+      }
+      if (e0 + lane < db) {
+        mcb = col[mb.beg + e0 + lane];
+        if (w != nullptr) mwb = w[mb.beg + e0 + lane];
+      }
+    }
+    const int na = (int)(da - e0 <= 0 ? 0 : da - e0 < 64 ? da - e0 : 64);  // wave-uniform
+    const int nb = (int)(db - e0 <= 0 ? 0 : db - e0 < 64 ? db - e0 : 64);
+    const int nm = na > nb ? na : nb;
+    for (int k0 = 0; k0 < nm; k0 += U) {
+      float4 xa[U], xb[U];
+      float wa[U], wb[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = (k0 + u) & 63;
+        const int ca = __builtin_amdgcn_readlane(mca, k);
+        const int cb = __builtin_amdgcn_readlane(mcb, k);
+        wa[u] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mwa), k));
+        wb[u] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mwb), k));
+        // a 64-bit scalar row base + the lane's 16-B offset (global_load
+        // saddr form: 2 SGPRs per load, no buffer resource); a slot past a
+        // row's end reads row col = 0 of its batch (loaded, never folded)
+        const float4 *pa = reinterpret_cast<const float4 *>(X + (int64_t)ca * ldx) + lane;
+        const float4 *pb = reinterpret_cast<const float4 *>(X + (int64_t)cb * ldx) + lane;
+        xa[u] = *pa;
+        xb[u] = *pb;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (k0 + u < na) {  // wave-uniform: strictly ascending edge order per row
+          aa[0] = __fadd_rn(aa[0], __fmul_rn(xa[u].x, wa[u]));
+          aa[1] = __fadd_rn(aa[1], __fmul_rn(xa[u].y, wa[u]));
+          aa[2] = __fadd_rn(aa[2], __fmul_rn(xa[u].z, wa[u]));
+          aa[3] = __fadd_rn(aa[3], __fmul_rn(xa[u].w, wa[u]));
+        }
+        if (k0 + u < nb) {
+          ab[0] = __fadd_rn(ab[0], __fmul_rn(xb[u].x, wb[u]));
+          ab[1] = __fadd_rn(ab[1], __fmul_rn(xb[u].y, wb[u]));
+          ab[2] = __fadd_rn(ab[2], __fmul_rn(xb[u].z, wb[u]));
+          ab[3] = __fadd_rn(ab[3], __fmul_rn(xb[u].w, wb[u]));
+        }
+      }
+    }
+  }
+}
+
 // one 16-row chunk's W fragments of k-step ks for this wave's two n-tiles
 struct WFrag {
   u32x4 t[2][3];
@@ -217,7 +306,7 @@ __device__ __forceinline__ void load_wfrag(const __amdgpu_buffer_rsrc_t rw, int 
           rw, 16 * ((((ks * kWNt + 2 * wave + t) * 3) + term) * 64 + lane), 0, 0);
 }
 
-template <int U, bool BWD, int EPI>
+template <int U, bool BWD, int EPI, bool PAIR>
 __global__ __launch_bounds__(kWThreads, 4) void spmm_xw_wide_kernel(const WideArgs a) {
   __shared__ __attribute__((aligned(16))) char lds[kWLds];
   const int tid = threadIdx.x;
@@ -305,26 +394,29 @@ __global__ __launch_bounds__(kWThreads, 4) void spmm_xw_wide_kernel(const WideAr
   auto row_of = [&](int64_t k) -> int64_t {
     return ((int64_t)blockIdx.x + (k >> 1) * gridDim.x) * kWRows + 2 * wave + (k & 1);
   };
-  WRow cur, nxt;
-  wrow_ptr(a.rowptr, row_of(0), row_of(0) < a.n_rows, cur);
-  wrow_first(a.col, a.w, lane, cur);
-  wrow_ptr(a.rowptr, row_of(1), row_of(1) < a.n_rows && 1 < 2 * n_my, nxt);
+  // row pipeline: one row (PAIR = false) or the wave's pair (PAIR) ahead --
+  // the next rows' first edge slots and the pointers of the rows after them
+  // load under the current gathers
+  WRow cur, nxt, cur2, nxt2;
+  if constexpr (PAIR) {
+    wrow_ptr(a.rowptr, row_of(0), row_of(0) < a.n_rows, cur);
+    wrow_ptr(a.rowptr, row_of(1), row_of(1) < a.n_rows, cur2);
+    wrow_first(a.col, a.w, lane, cur);
+    wrow_first(a.col, a.w, lane, cur2);
+    wrow_ptr(a.rowptr, row_of(2), row_of(2) < a.n_rows && 1 < n_my, nxt);
+    wrow_ptr(a.rowptr, row_of(3), row_of(3) < a.n_rows && 1 < n_my, nxt2);
+  } else {
+    wrow_ptr(a.rowptr, row_of(0), row_of(0) < a.n_rows, cur);
+    wrow_first(a.col, a.w, lane, cur);
+    wrow_ptr(a.rowptr, row_of(1), row_of(1) < a.n_rows && 1 < 2 * n_my, nxt);
+  }
   int it = 0;
   for (int64_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x, ++it) {
     char *buf = lds + (it & 1) * kWBuf;
     const int64_t r0 = chunk * kWRows;
     if (it > 0) prefetch_epi(chunk - gridDim.x);
-    // ---- Phase A: the chunk's rows -> bf16 term images ------------------
-#pragma unroll 1
-    for (int p = 0; p < 2; ++p) {
-      const int lr = 2 * wave + p;
-      const int64_t k = 2 * it + p;
-      wrow_first(a.col, a.w, lane, nxt);
-      WRow nn;
-      const int64_t rk2 = row_of(k + 2);
-      wrow_ptr(a.rowptr, rk2, rk2 < a.n_rows && k + 2 < 2 * n_my, nn);
-      float acc[4];
-      wide_gather<U>(a.X, a.ldx, a.col, a.w, cur, lane, acc);
+    // a finished row (lane: features 4 lane .. + 3) -> Z / scaling -> images
+    auto finish_row = [&](int lr, float (&acc)[4], int64_t deg) {
       const bool row_ok = r0 + lr < a.n_rows;
       if constexpr (!BWD) {
         if (a.Z != nullptr) {
@@ -334,7 +426,7 @@ __global__ __launch_bounds__(kWThreads, 4) void spmm_xw_wide_kernel(const WideAr
               4 * (int)(lr * a.ldz + 4 * lane), 0, kWideNt);
         }
         if (a.mean) {
-          const float c = (float)(cur.deg > 1 ? cur.deg : 1);
+          const float c = (float)(deg > 1 ? deg : 1);
 #pragma unroll
           for (int j = 0; j < 4; ++j) acc[j] = __fdiv_rn(acc[j], c);
         }
@@ -352,8 +444,38 @@ __global__ __launch_bounds__(kWThreads, 4) void spmm_xw_wide_kernel(const WideAr
       *reinterpret_cast<uint2 *>(img) = make_uint2(hi[0], hi[1]);
       *reinterpret_cast<uint2 *>(img + kWImg) = make_uint2(mid[0], mid[1]);
       *reinterpret_cast<uint2 *>(img + 2 * kWImg) = make_uint2(lo[0], lo[1]);
+    };
+    // ---- Phase A: the chunk's rows -> bf16 term images ------------------
+    if constexpr (PAIR) {
+      wrow_first(a.col, a.w, lane, nxt);
+      wrow_first(a.col, a.w, lane, nxt2);
+      WRow nn, nn2;
+      const int64_t ra = row_of(2 * (int64_t)it + 4), rb = row_of(2 * (int64_t)it + 5);
+      wrow_ptr(a.rowptr, ra, ra < a.n_rows && it + 2 < n_my, nn);
+      wrow_ptr(a.rowptr, rb, rb < a.n_rows && it + 2 < n_my, nn2);
+      float acc[4], acc2r[4];
+      wide_gather2<U>(a.X, a.ldx, a.col, a.w, cur, cur2, lane, acc, acc2r);
+      finish_row(2 * wave, acc, cur.deg);
+      finish_row(2 * wave + 1, acc2r, cur2.deg);
       cur = nxt;
+      cur2 = nxt2;
       nxt = nn;
+      nxt2 = nn2;
+    } else {
+#pragma unroll 1
+      for (int p = 0; p < 2; ++p) {
+        const int lr = 2 * wave + p;
+        const int64_t k = 2 * it + p;
+        wrow_first(a.col, a.w, lane, nxt);
+        WRow nn;
+        const int64_t rk2 = row_of(k + 2);
+        wrow_ptr(a.rowptr, rk2, rk2 < a.n_rows && k + 2 < 2 * n_my, nn);
+        float acc[4];
+        wide_gather<U>(a.X, a.ldx, a.col, a.w, cur, lane, acc);
+        finish_row(lr, acc, cur.deg);
+        cur = nxt;
+        nxt = nn;
+      }
     }
     // the first k-step's W fragments, in flight across the barrier
     WFrag fc, fn;
@@ -426,21 +548,29 @@ int wide_grid() {
   return 2 * cus;
 }
 
-template <int U>
-int launch_wide(const WideArgs &a, bool bwd, int epi, int grid, hipStream_t s) {
+template <int U, bool PAIR>
+int launch_wide_p(const WideArgs &a, bool bwd, int epi, int grid, hipStream_t s) {
   if (!bwd)
-    hipLaunchKernelGGL((spmm_xw_wide_kernel<U, false, WEPI_STORE>), dim3(grid), dim3(kWThreads), 0,
-                       s, a);
+    hipLaunchKernelGGL((spmm_xw_wide_kernel<U, false, WEPI_STORE, PAIR>), dim3(grid),
+                       dim3(kWThreads), 0, s, a);
   else if (epi == WEPI_RELU_DIV)
-    hipLaunchKernelGGL((spmm_xw_wide_kernel<U, true, WEPI_RELU_DIV>), dim3(grid), dim3(kWThreads),
-                       0, s, a);
+    hipLaunchKernelGGL((spmm_xw_wide_kernel<U, true, WEPI_RELU_DIV, PAIR>), dim3(grid),
+                       dim3(kWThreads), 0, s, a);
   else if (epi == WEPI_RELU)
-    hipLaunchKernelGGL((spmm_xw_wide_kernel<U, true, WEPI_RELU>), dim3(grid), dim3(kWThreads), 0, s,
-                       a);
+    hipLaunchKernelGGL((spmm_xw_wide_kernel<U, true, WEPI_RELU, PAIR>), dim3(grid),
+                       dim3(kWThreads), 0, s, a);
   else
-    hipLaunchKernelGGL((spmm_xw_wide_kernel<U, true, WEPI_STORE>), dim3(grid), dim3(kWThreads), 0,
-                       s, a);
+    hipLaunchKernelGGL((spmm_xw_wide_kernel<U, true, WEPI_STORE, PAIR>), dim3(grid),
+                       dim3(kWThreads), 0, s, a);
   return check_launch("spmm_xw_wide_kernel");
+}
+
+int launch_wide(const WideArgs &a, bool bwd, int epi, int grid, hipStream_t s) {
+  if (g_wide_pair & (bwd ? 2 : 1))
+    return g_wide_unroll == 8 ? launch_wide_p<8, true>(a, bwd, epi, grid, s)
+                              : launch_wide_p<4, true>(a, bwd, epi, grid, s);
+  return g_wide_unroll == 8 ? launch_wide_p<8, false>(a, bwd, epi, grid, s)
+                            : launch_wide_p<4, false>(a, bwd, epi, grid, s);
 }
 
 int launch_wimg(const float *W, int64_t ldw, bool trans, u32x4 *img, hipStream_t s) {
@@ -459,7 +589,7 @@ size_t xw_wide_workspace_bytes(bool bwd) {
 int xw_wide_fwd(int64_t n_rows, const int64_t *rowptr, const int32_t *col, const float *w,
                 const float *X, int64_t ldx, const float *W, int64_t ldw, const float *bias,
                 float *Y, int64_t ldy, int mean, int relu, uint32_t *relu_mask, float *Z,
-                int64_t ldz, void *workspace, int unroll, hipStream_t s) {
+                int64_t ldz, void *workspace, hipStream_t s) {
   u32x4 *img = static_cast<u32x4 *>(workspace);
   if (int rc = launch_wimg(W, ldw, false, img, s)) return rc;
   WideArgs a{};
@@ -481,15 +611,14 @@ int xw_wide_fwd(int64_t n_rows, const int64_t *rowptr, const int32_t *col, const
   const int64_t n_chunks = (n_rows + kWRows - 1) / kWRows;
   int64_t grid = wide_grid();
   if (grid > n_chunks) grid = n_chunks;
-  return unroll == 8 ? launch_wide<8>(a, false, WEPI_STORE, (int)grid, s)
-                     : launch_wide<4>(a, false, WEPI_STORE, (int)grid, s);
+  return launch_wide(a, false, WEPI_STORE, (int)grid, s);
 }
 
 int xw_wide_bwd_dx(int64_t n_rows, const int64_t *rowptr_t, const int32_t *col_t,
                    const float *w_t, const float *row_scale, const float *dY, int64_t lddy,
                    const float *W, int64_t ldw, float *dX, int64_t lddx,
                    const uint32_t *relu_mask, const float *row_div, float *colsum,
-                   int accumulate, void *workspace, int unroll, hipStream_t s) {
+                   int accumulate, void *workspace, hipStream_t s) {
   u32x4 *img = static_cast<u32x4 *>(workspace);
   float *partial = reinterpret_cast<float *>(static_cast<char *>(workspace) +
                                              align_up((size_t)kWImgFrags * 16, 256));
@@ -512,8 +641,7 @@ int xw_wide_bwd_dx(int64_t n_rows, const int64_t *rowptr_t, const int32_t *col_t
   const int64_t n_chunks = (n_rows + kWRows - 1) / kWRows;
   int64_t grid = wide_grid();
   if (grid > n_chunks) grid = n_chunks;
-  int rc = unroll == 8 ? launch_wide<8>(a, true, epi, (int)grid, s)
-                       : launch_wide<4>(a, true, epi, (int)grid, s);
+  int rc = launch_wide(a, true, epi, (int)grid, s);
   if (rc || epi == WEPI_STORE) return rc;
   return launch_fold(partial, (int)grid, kWF, kWF, colsum, kWF, accumulate, s);
 }
