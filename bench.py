@@ -214,6 +214,10 @@ def launch_bytes(name: str, rows: int, edges: int, F: int):
         if name == "pack_rows_count":
             return rows * (dense + 4 + F / 8), 0.0
         return rows * (dense + packed), 0.0
+    if name == "input_layer_fwd":  # a, x read; Z written (the 1-wide SpMM is its own launch)
+        return 8 * rows + 4 * F * rows, 0.0
+    if name == "input_layer_bwd":  # dZ, Z, a, x read
+        return 8 * F * rows + 8 * rows, 0.0
     if name.startswith("residual_stack"):
         return None, None  # one launch runs a whole run of layers: no per-launch count
     if name == "gemm_bwd":        # dW and dX: X, dH read, dX + mask

@@ -504,6 +504,38 @@ int mgcn_residual_act_bwd(int64_t n_rows, int32_t F, const float *dZ, int64_t ld
                           void *workspace, size_t workspace_bytes, void *stream);
 
 /*
+ * GCNModel's INPUT layer with its residual Linear when in_channels = 1 (the
+ * botnet node feature; GCNLayer(1, F) + residuals[0] + the join,
+ * gcn_model.py:89-105 with residual_hop = 1) associated as (A x) W (ABI
+ * v17): with a = A x (mgcn_spmm_fwd at F = 1; for MEAN already divided)
+ *   Z[i][j] = relu2( relu1(a[i] W[j] + b[j]) + (x[i] Wr[j] + br[j]) )
+ * W = weight_node [1][F], Wr = the Linear weight [F][1] (contiguous: F
+ * floats each), b / br nullable; Z [n_rows][F] (ldz, 16-byte aligned rows).
+ * The reference's A (x W) to fp32 rounding, without an F-wide gather.
+ * Supported: F_in = 1, F / 4 a power of two, 4 <= F <= 256.
+ */
+int mgcn_input_layer_supported(int32_t F_in, int32_t F);
+int mgcn_input_layer_fwd(int64_t n_rows, int32_t F, const float *a, const float *x,
+                         const float *W, const float *b, const float *Wr, const float *br,
+                         int relu1, int relu2, float *Z, int64_t ldz, void *stream);
+/* Bytes of scratch mgcn_input_layer_bwd needs (block partials of 4 F sums). */
+size_t mgcn_input_layer_bwd_workspace_bytes(int64_t n_rows, int32_t F);
+/*
+ * Its adjoint in one pass over dZ (and Z when relu2): dS = relu2' dZ, dA =
+ * relu1' dS (relu1's decision recomputed bit for bit), and
+ *   grads[0:F] = dW = sum_i a[i] dA[i]    grads[F:2F]  = db  = sum_i dA[i]
+ *   grads[2F:3F] = dWr = sum_i x[i] dS[i] grads[3F:4F] = dbr = sum_i dS[i]
+ * (deterministic fixed-order sums).  da / dxr (nullable, together): da[i] =
+ * sum_j dA[i][j] W[j] [/ row_div[i]] -- the input of the 1-wide adjoint
+ * SpMM (dx = A^T da + dxr) -- and dxr[i] = sum_j dS[i][j] Wr[j].
+ */
+int mgcn_input_layer_bwd(int64_t n_rows, int32_t F, const float *dZ, int64_t lddz,
+                         const float *Z, int64_t ldz, const float *a, const float *x,
+                         const float *W, const float *b, const float *Wr, int relu1, int relu2,
+                         const float *row_div, float *da, float *dxr, float *grads,
+                         void *workspace, size_t workspace_bytes, void *stream);
+
+/*
  * One GCNModel layer with its residual Linear, F = 32 (the botnet stack of
  * config 3: GCNLayer + residuals[n] + the join, gcn_model.py:89-105 with
  * residual_hop = 1; NodeModelAdditive.forward gcn_base_models.py:199-243):

@@ -211,6 +211,122 @@ __global__ __launch_bounds__(kBlock) void residual_act_bwd_kernel(
   }
 }
 
+
+// GCNModel's input layer (in_channels = 1, the botnet node feature; gcn_model.py
+// :89-105 with residual_hop = 1) associated as (A x) W: with a = A x (the
+// 1-wide aggregation, mgcn_spmm_fwd) every output is elementwise,
+//   Z[i, j] = relu2( relu1(a_i W_j + b_j) + (x_i Wr_j + br_j) )
+// -- the reference's A (x W) to fp32 rounding, without the 32-wide gather.
+// Thread t of a row group owns columns 4 t .. 4 t + 3.
+__global__ __launch_bounds__(kBlock) void input_layer_fwd_kernel(
+    int64_t n, int F, const float *__restrict__ a, const float *__restrict__ x,
+    const float *__restrict__ W, const float *__restrict__ b, const float *__restrict__ Wr,
+    const float *__restrict__ br, int relu1, int relu2, float *__restrict__ Z, int64_t ldz) {
+  const int fv = F / 4;
+  const int64_t total = n * fv;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * kBlock) {
+    const int64_t r = i / fv;
+    const int f0 = (int)(i % fv) * 4;
+    const float ar = a[r], xr = x[r];
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float z1 = __fmul_rn(ar, W[f0 + j]);
+      if (b != nullptr) z1 = __fadd_rn(z1, b[f0 + j]);
+      if (relu1 && z1 < 0.0f) z1 = 0.0f;
+      float rv = __fmul_rn(xr, Wr[f0 + j]);
+      if (br != nullptr) rv = __fadd_rn(rv, br[f0 + j]);
+      v[j] = __fadd_rn(z1, rv);
+      if (relu2 && v[j] < 0.0f) v[j] = 0.0f;
+    }
+    *reinterpret_cast<float4 *>(Z + r * ldz + f0) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+// Its adjoint: dS = relu2' dZ, dA = relu1' dS (relu1's decision recomputed
+// with the forward's arithmetic, bit for bit), and the four parameter
+// gradients as column sums in a fixed row order (block partials [block][4F]:
+// dW_j = sum a_i dA_ij | db_j = sum dA_ij | dWr_j = sum x_i dS_ij | dbr_j =
+// sum dS_ij); with da (nullable): da_i = sum_j dA_ij W_j [/ row_div_i] (the
+// 1-wide adjoint SpMM's input) and dxr_i = sum_j dS_ij Wr_j, the row sums in
+// a fixed xor-butterfly over the row's T threads.
+__global__ __launch_bounds__(kBlock) void input_layer_bwd_kernel(
+    int64_t n, int F, const float *__restrict__ dZ, int64_t lddz, const float *__restrict__ Z,
+    int64_t ldz, const float *__restrict__ a, const float *__restrict__ x,
+    const float *__restrict__ W, const float *__restrict__ b, const float *__restrict__ Wr,
+    int relu1, int relu2, const float *__restrict__ row_div, float *__restrict__ da,
+    float *__restrict__ dxr, float *__restrict__ partial, int T) {
+  __shared__ float red[kBlock * 16];
+  const int R = kBlock / T;
+  const int t_col = threadIdx.x % T, t_row = threadIdx.x / T;
+  const int f0 = t_col * 4;
+  float sw[4] = {0, 0, 0, 0}, sb[4] = {0, 0, 0, 0}, swr[4] = {0, 0, 0, 0}, sbr[4] = {0, 0, 0, 0};
+  float w[4], bb[4], wr[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    w[j] = W[f0 + j];
+    bb[j] = b != nullptr ? b[f0 + j] : 0.0f;
+    wr[j] = Wr[f0 + j];
+  }
+  const int64_t stride = (int64_t)gridDim.x * R;
+  // every thread of a row group runs the same rows (the butterfly below)
+  for (int64_t r = (int64_t)blockIdx.x * R + t_row; r - t_row < n; r += stride) {
+    const bool ok = r < n;
+    const int64_t rr = ok ? r : 0;
+    const float4 g4 = *reinterpret_cast<const float4 *>(dZ + rr * lddz + f0);
+    float4 z4 = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+    if (relu2) z4 = *reinterpret_cast<const float4 *>(Z + rr * ldz + f0);
+    const float ar = a[rr], xr = x[rr];
+    const float g[4] = {g4.x, g4.y, g4.z, g4.w}, zz[4] = {z4.x, z4.y, z4.z, z4.w};
+    float pa = 0.0f, ps = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float ds = (!ok || (relu2 && !(zz[j] > 0.0f))) ? 0.0f : g[j];
+      float z1 = __fmul_rn(ar, w[j]);
+      if (b != nullptr) z1 = __fadd_rn(z1, bb[j]);
+      const float dA = (relu1 && !(z1 > 0.0f)) ? 0.0f : ds;
+      sw[j] = __fadd_rn(sw[j], __fmul_rn(ar, dA));
+      sb[j] = __fadd_rn(sb[j], dA);
+      swr[j] = __fadd_rn(swr[j], __fmul_rn(xr, ds));
+      sbr[j] = __fadd_rn(sbr[j], ds);
+      if (da != nullptr) {
+        pa = __fadd_rn(pa, __fmul_rn(dA, w[j]));
+        ps = __fadd_rn(ps, __fmul_rn(ds, wr[j]));
+      }
+    }
+    if (da != nullptr) {
+      for (int m = 1; m < T; m <<= 1) {
+        pa = __fadd_rn(pa, __shfl_xor(pa, m, 64));
+        ps = __fadd_rn(ps, __shfl_xor(ps, m, 64));
+      }
+      if (ok && t_col == 0) {
+        da[r] = row_div != nullptr ? __fdiv_rn(pa, row_div[r]) : pa;
+        dxr[r] = ps;
+      }
+    }
+  }
+  if (partial == nullptr) return;
+  float *my = red + threadIdx.x * 16;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    my[j] = sw[j];
+    my[4 + j] = sb[j];
+    my[8 + j] = swr[j];
+    my[12 + j] = sbr[j];
+  }
+  __syncthreads();
+  if (t_row == 0) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      float acc = red[t_col * 16 + q];
+      for (int k = 1; k < R; ++k) acc = __fadd_rn(acc, red[(k * T + t_col) * 16 + q]);
+      // [dW | db | dWr | dbr], 4 columns per quantity
+      partial[(int64_t)blockIdx.x * 4 * F + (q >> 2) * F + f0 + (q & 3)] = acc;
+    }
+  }
+}
+
 // one wave per segment; lanes stride the features
 __global__ __launch_bounds__(kBlock) void segment_mean_kernel(int64_t n_seg, int F,
                                                               const int64_t *__restrict__ ptr,
@@ -444,4 +560,61 @@ extern "C" int mgcn_residual_act_bwd(int64_t n_rows, int32_t F, const float *dZ,
   if (int rc = check_launch("residual_act_bwd_kernel")) return rc;
   if (colsums == nullptr) return MGCN_OK;
   return launch_colsum_fold(partial, nblk, 2 * F, colsums, s);
+}
+
+extern "C" int mgcn_input_layer_supported(int32_t F_in, int32_t F) {
+  return F_in == 1 && F >= 4 && F <= 256 && F % 4 == 0 && ((F / 4) & (F / 4 - 1)) == 0;
+}
+
+extern "C" int mgcn_input_layer_fwd(int64_t n_rows, int32_t F, const float *a, const float *x,
+                                    const float *W, const float *b, const float *Wr,
+                                    const float *br, int relu1, int relu2, float *Z, int64_t ldz,
+                                    void *stream) {
+  clear_error();
+  MGCN_REQUIRE(n_rows >= 0 && mgcn_input_layer_supported(1, F),
+               "mgcn_input_layer_fwd: F = %d (needs F / 4 a power of two, 4 <= F <= 256)", F);
+  if (n_rows == 0) return MGCN_OK;
+  MGCN_REQUIRE(a && x && W && Wr && Z && ldz >= F && ldz % 4 == 0 && (uintptr_t)Z % 16 == 0,
+               "mgcn_input_layer_fwd: bad arguments (Z needs 16-byte aligned rows)");
+  const unsigned g = grid_for(n_rows * (F / 4), kBlock);
+  hipLaunchKernelGGL(input_layer_fwd_kernel, dim3(g), dim3(kBlock), 0, as_stream(stream), n_rows,
+                     (int)F, a, x, W, b, Wr, br, relu1, relu2, Z, ldz);
+  return check_launch("input_layer_fwd_kernel");
+}
+
+extern "C" size_t mgcn_input_layer_bwd_workspace_bytes(int64_t n_rows, int32_t F) {
+  return mgcn_colsum_workspace_bytes(n_rows, 4 * (F > 0 ? F : 1));
+}
+
+extern "C" int mgcn_input_layer_bwd(int64_t n_rows, int32_t F, const float *dZ, int64_t lddz,
+                                    const float *Z, int64_t ldz, const float *a, const float *x,
+                                    const float *W, const float *b, const float *Wr, int relu1,
+                                    int relu2, const float *row_div, float *da, float *dxr,
+                                    float *grads, void *workspace, size_t workspace_bytes,
+                                    void *stream) {
+  clear_error();
+  MGCN_REQUIRE(n_rows >= 0 && mgcn_input_layer_supported(1, F),
+               "mgcn_input_layer_bwd: F = %d (needs F / 4 a power of two, 4 <= F <= 256)", F);
+  MGCN_REQUIRE(grads != nullptr && (da == nullptr) == (dxr == nullptr),
+               "mgcn_input_layer_bwd: grads required; da and dxr go together");
+  hipStream_t s = as_stream(stream);
+  if (n_rows == 0) {
+    MGCN_HIP_TRY(hipMemsetAsync(grads, 0, sizeof(float) * 4 * F, s));
+    return MGCN_OK;
+  }
+  MGCN_REQUIRE(dZ && a && x && W && Wr && lddz >= F && lddz % 4 == 0 && (uintptr_t)dZ % 16 == 0 &&
+                   (!relu2 || (Z && ldz >= F && ldz % 4 == 0 && (uintptr_t)Z % 16 == 0)),
+               "mgcn_input_layer_bwd: bad arguments (dZ / Z need 16-byte aligned rows)");
+  const size_t need = mgcn_input_layer_bwd_workspace_bytes(n_rows, F);
+  if (workspace == nullptr || workspace_bytes < need) {
+    set_error("mgcn_input_layer_bwd: workspace %zu < %zu", workspace_bytes, need);
+    return MGCN_EWORKSPACE;
+  }
+  const int nblk = colsum_blocks(n_rows);
+  float *partial = static_cast<float *>(workspace);
+  hipLaunchKernelGGL(input_layer_bwd_kernel, dim3(nblk), dim3(kBlock), 0, s, n_rows, (int)F, dZ,
+                     lddz, Z, ldz, a, x, W, b, Wr, relu1, relu2, row_div, da, dxr, partial,
+                     (int)(F / 4));
+  if (int rc = check_launch("input_layer_bwd_kernel")) return rc;
+  return launch_colsum_fold(partial, nblk, 4 * F, grads, s);
 }

@@ -83,6 +83,12 @@ SIGNATURES = {
     "mgcn_relu_bwd_colsum": (_int, [_i64, _i32, _vp, _vp, _int, _vp, _vp, _vp, _vp, _sz, _vp]),
     "mgcn_residual_act": (_int, [_i64, _i32, _vp, _i64, _vp, _i64, _vp, _int, _vp, _i64, _vp]),
     "mgcn_residual_act_bwd_workspace_bytes": (_sz, [_i64, _i32]),
+    "mgcn_input_layer_supported": (_int, [_i32, _i32]),
+    "mgcn_input_layer_fwd": (_int, [_i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _int, _int, _vp,
+                                    _i64, _vp]),
+    "mgcn_input_layer_bwd_workspace_bytes": (_sz, [_i64, _i32]),
+    "mgcn_input_layer_bwd": (_int, [_i64, _i32, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp,
+                                    _int, _int, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "mgcn_residual_act_bwd": (_int, [_i64, _i32, _vp, _i64, _vp, _i64, _int, _vp, _i64, _int, _vp,
                                      _vp, _i64, _vp, _i64, _vp, _vp, _sz, _vp]),
     "mgcn_segment_mean": (_int, [_i64, _i32, _vp, _vp, _i64, _vp, _i64, _vp]),

@@ -1423,11 +1423,102 @@ def residual_stack(x, plan: GraphPlan, norm: NormPlan, aggr: str, relu1s, relu2s
                                 *flat)
 
 
+def input_layer_supported(plan: GraphPlan, x: torch.Tensor, W: torch.Tensor, Wr: torch.Tensor,
+                          reduce: int) -> bool:
+    """True when :class:`_InputLayer` takes this layer: in_channels = 1 with a
+    1 -> F residual Linear, sum or mean, fp32, on a square graph plan."""
+    return (_FUSE_XW and x.dim() == 2 and x.size(1) == 1 and x.dtype == torch.float32 and
+            x.is_cuda and W.dtype == torch.float32 and Wr.dtype == torch.float32 and
+            W.dim() == 2 and W.size(0) == 1 and tuple(Wr.shape) == (W.size(1), 1) and
+            reduce in (L.REDUCE_SUM, L.REDUCE_MEAN) and
+            x.size(0) == plan.fwd.n_rows == plan.fwd.n_cols and
+            bool(L.load().mgcn_input_layer_supported(1, W.size(1))))
+
+
+class _InputLayer(torch.autograd.Function):
+    """GCNModel's input layer with its residual Linear when in_channels = 1
+    (config 3's botnet node feature; gcn_model.py:89-105, residual_hop = 1),
+    associated as (A x) W: a = A x is a 1-wide aggregation (mgcn_spmm_fwd,
+    4 gathered bytes per edge instead of 4 F) and everything after it is
+    elementwise (mgcn_input_layer_fwd):
+
+        Z = relu2( relu1(a W + b) + (x Wr^T + br) )
+
+    backward: one pass over dZ (mgcn_input_layer_bwd) gives dW, db, dWr, dbr
+    as fixed-order column sums -- no adjoint gather at all unless x itself
+    needs a gradient (then dx = A^T (dA W^T) + dS Wr, a 1-wide adjoint SpMM).
+    The reference's A (x W) to fp32 rounding (a different association)."""
+
+    @staticmethod
+    def forward(ctx, x, plan, norm, reduce, relu1, relu2, W, b, Wr, br):
+        lib = L.load()
+        dev = L.require_device(x, W, b, Wr, br)
+        x = x.contiguous()
+        n, F = x.size(0), W.size(1)
+        a, _ = spmm_fwd(plan.fwd, norm.w_fwd, x, reduce)
+        Wd, Wrd = W.detach().contiguous(), Wr.detach().contiguous()
+        bd = b.detach().contiguous() if b is not None else None
+        brd = br.detach().contiguous() if br is not None else None
+        Z = torch.empty(n, F, dtype=torch.float32, device=dev)
+        if _TIMER is not None:
+            _TIMER("input_layer_fwd", True, n)
+        with L.device_guard(dev):
+            rc = lib.mgcn_input_layer_fwd(n, F, L.ptr(a), L.ptr(x), L.ptr(Wd), L.ptr(bd),
+                                          L.ptr(Wrd), L.ptr(brd), int(relu1), int(relu2),
+                                          L.ptr(Z), Z.stride(0), L.stream_of(dev))
+        if _TIMER is not None:
+            _TIMER("input_layer_fwd", False)
+        L.check(rc, "mgcn_input_layer_fwd")
+        ctx.plan, ctx.norm, ctx.reduce, ctx.relu1, ctx.relu2 = plan, norm, reduce, relu1, relu2
+        ctx.has_b, ctx.has_br = b is not None, br is not None
+        ctx.save_for_backward(x, a, Z, Wd, bd if bd is not None else torch.empty(0), Wrd)
+        return Z
+
+    @staticmethod
+    def backward(ctx, dZ):
+        lib = L.load()
+        x, a, Z, W, b, Wr = ctx.saved_tensors
+        plan, norm = ctx.plan, ctx.norm
+        n, F = Z.shape
+        dev = Z.device
+        dZ = _aligned_rows(dZ)
+        need_x = bool(ctx.needs_input_grad[0])
+        da = torch.empty(n, dtype=torch.float32, device=dev) if need_x else None
+        dxr = torch.empty(n, dtype=torch.float32, device=dev) if need_x else None
+        grads = torch.empty(4 * F, dtype=torch.float32, device=dev)
+        mean = ctx.reduce == L.REDUCE_MEAN
+        ws_bytes = int(lib.mgcn_input_layer_bwd_workspace_bytes(n, F))
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+        if _TIMER is not None:
+            _TIMER("input_layer_bwd", True, n)
+        with L.device_guard(dev):
+            rc = lib.mgcn_input_layer_bwd(
+                n, F, L.ptr(dZ), dZ.stride(0), L.ptr(Z), Z.stride(0), L.ptr(a), L.ptr(x),
+                L.ptr(W), L.ptr(b if b.numel() else None), L.ptr(Wr), int(ctx.relu1),
+                int(ctx.relu2), L.ptr(plan.in_cnt if (mean and need_x) else None), L.ptr(da),
+                L.ptr(dxr), L.ptr(grads), L.ptr(ws), ws_bytes, L.stream_of(dev))
+        if _TIMER is not None:
+            _TIMER("input_layer_bwd", False)
+        L.check(rc, "mgcn_input_layer_bwd")
+        dx = None
+        if need_x:
+            dx = spmm_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, da.view(n, 1), L.REDUCE_SUM)
+            dx.add_(dxr.view(n, 1))
+        dW = grads[:F].view(1, F)
+        db = grads[F:2 * F] if ctx.has_b else None
+        dWr = grads[2 * F:3 * F].view(F, 1)
+        dbr = grads[3 * F:] if ctx.has_br else None
+        return (dx, None, None, None, None, None, dW, db, dWr, dbr)
+
+
 def residual_gcn_layer(x, plan: GraphPlan, norm: NormPlan, aggr: str, relu1: bool, relu2: bool,
                        W, b, Wr, br):
     """One GCNModel layer + residual join: :class:`_ResidualLayerFused` where
-    it applies (32 -> 32, sum / mean), else :class:`_ResidualGCNLayer`."""
+    it applies (32 -> 32, sum / mean), :class:`_InputLayer` for an
+    in_channels = 1 input layer, else :class:`_ResidualGCNLayer`."""
     reduce = L.REDUCE_CODES[aggr]
+    if input_layer_supported(plan, x, W, Wr, reduce):
+        return _InputLayer.apply(x, plan, norm, reduce, bool(relu1), bool(relu2), W, b, Wr, br)
     if residual_layer_supported(plan, x, W, Wr, reduce):
         return _ResidualLayerFused.apply(x, plan, norm, reduce, bool(relu1), bool(relu2), W, b,
                                          Wr, br)

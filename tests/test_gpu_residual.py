@@ -183,3 +183,65 @@ def test_residual_stack_matches_layer_by_layer(cuda, aggr, deg_norm, bias):
         else:
             assert torch.equal(a, b)
 
+
+
+@pytest.mark.parametrize("deg_norm,aggr,bias", [("sm", "add", False), ("sm", "add", True),
+                                                ("rw", "mean", True)])
+@pytest.mark.parametrize("relu1,relu2", [(True, True), (True, False)])
+@pytest.mark.parametrize("need_x", [False, True])
+def test_input_layer_vs_two_launch_and_fp64(cuda, deg_norm, aggr, bias, relu1, relu2, need_x):
+    """The in_channels = 1 input layer as (A x) W (ops._InputLayer: a 1-wide
+    SpMM + mgcn_input_layer_fwd / _bwd) against the two-launch layer
+    (_ResidualGCNLayer: x @ [W | Wr^T], 32-wide SpMM, join -- the reference's
+    A (x W)) on a skewed graph with heavy and giant rows: Z, the four
+    parameter gradients and dx within fp32 tolerance, and Z within 1e-5 of an
+    fp64 restatement relative to its |.| bound."""
+    from fp64_ref import A64, within
+    from mgcn import _lib as L
+    from mgcn import ops
+    rng = np.random.default_rng(41 + bias + 2 * relu2 + 4 * need_x)
+    N, F = 7000, 32
+    ei = _skewed(rng, N, 50000)
+    plan, norm = _plan(cuda, ei, N, deg_norm)
+    assert plan.fwd.n_giant > 0
+    reduce = L.REDUCE_CODES[aggr]
+    g = torch.Generator(device=cuda).manual_seed(13)
+    x = torch.randn(N, 1, device=cuda, generator=g)
+    dZ = torch.randn(N, F, device=cuda, generator=g)
+    params = [torch.randn(1, F, device=cuda, generator=g),
+              torch.randn(F, device=cuda, generator=g) * 0.3 if bias else None,
+              torch.randn(F, 1, device=cuda, generator=g),
+              torch.randn(F, device=cuda, generator=g) * 0.3]
+    assert ops.input_layer_supported(plan, x, params[0], params[2], reduce)
+    outs = []
+    for fn in (ops._InputLayer, ops._ResidualGCNLayer):
+        xi = x.clone().requires_grad_(need_x)
+        ps = [None if p is None else p.clone().requires_grad_(True) for p in params]
+        Z = fn.apply(xi, plan, norm, reduce, relu1, relu2, *ps)
+        Z.backward(dZ)
+        outs.append([Z.detach(), xi.grad] + [None if p is None else p.grad for p in ps])
+    for a, b in zip(*outs):
+        if b is None:
+            assert a is None
+            continue
+        scale = float(b.abs().max())
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=2e-5 * max(1.0, scale))
+    # Z against fp64 (the relu decisions from the fp32 result where it is not
+    # within rounding of zero)
+    from oracle import oracle as orc
+    wf, _, _ = orc.edge_factors(ei, N, deg_norm)
+    A = A64(torch.from_numpy(ei), wf, N, cuda, mean=aggr == "mean")
+    a64 = A.apply(x.double())
+    am = A.apply(x.double().abs(), absolute=True)
+    W64, Wr64 = params[0].double(), params[2].double()
+    b64 = params[1].double() if bias else torch.zeros(F, dtype=torch.float64, device=cuda)
+    br64 = params[3].double()
+    z1 = a64 @ W64 + b64
+    if relu1:
+        z1 = z1.clamp_min(0)
+    z = z1 + x.double() @ Wr64.t() + br64
+    if relu2:
+        z = z.clamp_min(0)
+    bound = am @ W64.abs() + b64.abs() + x.double().abs() @ Wr64.abs().t() + br64.abs()
+    ok, worst = within(outs[0][0].double() - z, bound, 1e-5)
+    assert ok, worst
