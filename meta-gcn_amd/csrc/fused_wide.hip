@@ -60,8 +60,27 @@ namespace mgcn {
 // round (4 or 8)
 int g_wide_pair = 3;
 int g_wide_unroll = 4;
+// mgcn_set_option("wide_ws"): the warp-specialised kernels (below) -- bit 0
+// the forward, bit 1 the adjoint
+int g_wide_ws = 0;
+// mgcn_set_option("wide_dbg"): timing experiments on the warp-specialised
+// kernels (results are WRONG when set): bit 0 the MFMA waves skip their W
+// loads, bit 1 they skip the products, bit 2 the gather waves skip the gathers
+int g_wide_dbg = 0;
 
 int wide_set_option(const char *name, int value) {
+  if (name[5] == 'd') {
+    g_wide_dbg = value;
+    return MGCN_OK;
+  }
+  if (name[5] == 'w') {
+    if (value < 0 || value > 3) {
+      set_error("wide_ws must be 0 .. 3");
+      return MGCN_EINVAL;
+    }
+    g_wide_ws = value;
+    return MGCN_OK;
+  }
   const bool pair = name[5] == 'p';
   if (pair ? (value < 0 || value > 3) : (value != 4 && value != 8)) {
     set_error(pair ? "wide_pair must be 0 .. 3" : "wide_unroll must be 4 or 8");
@@ -146,6 +165,7 @@ struct WideArgs {
   const float *row_div;        // backward mean divisor
   float *colsum_partial;       // backward: [grid][256]
   int mean, relu;
+  int dbg;                     // wide_dbg (timing experiments only; 0 in production)
 };
 
 // a row's edge slots: [beg, beg + deg) (wave-uniform), and lane l's slot
@@ -540,6 +560,377 @@ __global__ __launch_bounds__(kWThreads, 4) void spmm_xw_wide_kernel(const WideAr
   }
 }
 
+// ===================== warp-specialised form (round 5) =====================
+//
+// The kernel above pays for its 16-row chunks twice: every chunk streams the
+// whole W image from L2 (384 KB per 16 rows = 24 KB per row, twice the
+// gathered bytes), and every wave stops gathering for the chunk's barrier and
+// Phase B.  Here one 1024-thread workgroup per CU splits the work by role:
+//
+// * 12 GATHER waves take the workgroup's row pairs in turn (pair p = rows
+//   2 (p & 15), + 1 of its chunk p >> 4; wave g: p = g, g + 12, ...), each
+//   pair's U slots per row in flight (wide_gather2, bit for bit the SpMM's
+//   fold), write Z and the rows' bf16 term images into a ring of three
+//   32-row chunk buffers (48 KB each), and count the rows in (filled[b]).
+//   They never wait for the MFMAs except when the ring is full.
+// * 4 MFMA waves (one per SIMD) take the chunks in order: wave m computes the
+//   32 rows x its 64 output columns as D = W^T-image x rows (the rows are the
+//   B operand, so a lane's D fragment is 4 CONSECUTIVE columns of one row and
+//   leaves as one 16-B store -- no staging tile), each W fragment serving both
+//   16-row tiles: 384 KB of W per 32 rows, half the L2 stream.  The epilogue
+//   (bias, ReLU, mask ballots -- combined across the two waves of a 128-column
+//   half by ds_or in LDS; backward: the lower layer's mask, column sums,
+//   divisor) runs on the fragments; the last wave out of a chunk writes its
+//   mask words and frees the buffer (freed[b]).
+//
+// Hand-offs are LDS counters inside the workgroup (monotonic per buffer; a
+// wave's LDS operations complete in order, so its image writes land before
+// its counter add), polled with s_sleep and bounded: a spin that exceeds
+// kSpinLimit sets the abort word and every wave leaves its loop.  The MFMA
+// term order is the 16-row kernel's with the operands swapped (the same six
+// products per k-step in the same order), so Y / dX equal its results.
+constexpr int kSRows = 32;
+constexpr int kSBufs = 3;
+constexpr int kSImg = kSRows * kWF * 2;     // one term image of a chunk: 16 KB
+constexpr int kSBuf = 3 * kSImg;            // 48 KB
+constexpr int kSGather = 12;
+constexpr int kSMfma = 4;
+constexpr int kSThreads = 64 * (kSGather + kSMfma);
+constexpr int kSMaskOff = kSBufs * kSBuf;                                 // [3][32][8] u32
+constexpr int kSCtrOff = kSMaskOff + kSBufs * kSRows * kWMaskWords * 4;  // counters
+constexpr int kSLds = kSCtrOff + 64;
+static_assert(kSLds <= 160 * 1024, "one warp-specialised workgroup per CU");
+static_assert(16 * kWF * 4 <= kSMaskOff, "column-sum fold fits in the image ring");
+constexpr uint32_t kSpinLimit = 1u << 25;
+
+// the 16-row kernel's six products (rows_l W_h, rows_h W_l, rows_m W_m,
+// rows_m W_h, rows_h W_m, rows_h W_h) with W as the A operand
+__device__ __forceinline__ f32x4_t mfma16_x6_wt(const u32x4 (&w)[3], const bf16x8 &xh,
+                                               const bf16x8 &xm, const bf16x8 &xl, f32x4_t c) {
+  const bf16x8 wh = __builtin_bit_cast(bf16x8, w[0]);
+  const bf16x8 wm = __builtin_bit_cast(bf16x8, w[1]);
+  const bf16x8 wl = __builtin_bit_cast(bf16x8, w[2]);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, xl, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl, xh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm, xm, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, xm, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm, xh, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, xh, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ int lds_load(const int *p) {
+  return __builtin_amdgcn_readfirstlane(
+      __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+
+// wait until *p >= target (false: the abort word is set, leave)
+__device__ __forceinline__ bool lds_wait_ge(const int *p, int target, int *abort_word) {
+  for (uint32_t n = 0;; ++n) {
+    if (lds_load(p) >= target) break;
+    if (lds_load(abort_word) != 0) return false;
+    if (n >= kSpinLimit) {
+      __hip_atomic_store(abort_word, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  asm volatile("" ::: "memory");
+  return true;
+}
+
+// this wave's LDS writes complete, then lane 0 adds v to *p; returns the old value
+__device__ __forceinline__ int lds_signal(int *p, int v, int lane) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  int old = 0;
+  if (lane == 0) old = __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  return __builtin_amdgcn_readfirstlane(old);
+}
+
+template <int U, bool BWD, int EPI>
+__global__ __launch_bounds__(kSThreads) void spmm_xw_wide_ws_kernel(const WideArgs a) {
+  __shared__ __attribute__((aligned(16))) char lds[kSLds];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l16 = lane & 15, g4 = lane >> 4;
+  int *ctr = reinterpret_cast<int *>(lds + kSCtrOff);
+  int *filled = ctr, *mdone = ctr + 3, *freed = ctr + 6, *abort_word = ctr + 9;
+  uint32_t *maskbuf = reinterpret_cast<uint32_t *>(lds + kSMaskOff);
+  if (tid < 16) ctr[tid] = 0;
+  __syncthreads();
+
+  const int64_t n_chunks = (a.n_rows + kSRows - 1) / kSRows;
+  const int64_t n_my = blockIdx.x < n_chunks ? (n_chunks - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+  auto chunk_of = [&](int64_t i) { return (int64_t)blockIdx.x + i * gridDim.x; };
+  auto rows_in = [&](int64_t c) -> uint32_t {
+    const int64_t r = a.n_rows - c * kSRows;
+    return (uint32_t)(r <= 0 ? 0 : r >= kSRows ? kSRows : r);
+  };
+
+  float cs[4][4];  // backward column sums (MFMA waves)
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) cs[t][r] = 0.0f;
+
+  if (wave < kSGather) {
+    // ------------------------------- gather waves ---------------------------
+    const int64_t n_pairs = 16 * n_my;
+    auto pair_row = [&](int64_t p) { return chunk_of(p >> 4) * kSRows + 2 * (p & 15); };
+    WRow cur, cur2, nxt, nxt2;
+    {
+      const int64_t p = wave, ra = pair_row(p);
+      const bool ok = p < n_pairs;
+      wrow_ptr(a.rowptr, ra, ok && ra < a.n_rows, cur);
+      wrow_ptr(a.rowptr, ra + 1, ok && ra + 1 < a.n_rows, cur2);
+      wrow_first(a.col, a.w, lane, cur);
+      wrow_first(a.col, a.w, lane, cur2);
+      const int64_t q = p + kSGather, rq = pair_row(q);
+      wrow_ptr(a.rowptr, rq, q < n_pairs && rq < a.n_rows, nxt);
+      wrow_ptr(a.rowptr, rq + 1, q < n_pairs && rq + 1 < a.n_rows, nxt2);
+    }
+    for (int64_t p = wave; p < n_pairs; p += kSGather) {
+      wrow_first(a.col, a.w, lane, nxt);
+      wrow_first(a.col, a.w, lane, nxt2);
+      WRow nn, nn2;
+      const int64_t q = p + 2 * kSGather, rq = pair_row(q);
+      wrow_ptr(a.rowptr, rq, q < n_pairs && rq < a.n_rows, nn);
+      wrow_ptr(a.rowptr, rq + 1, q < n_pairs && rq + 1 < a.n_rows, nn2);
+      float acc[2][4];
+      if (a.dbg & 4) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[0][j] = acc[1][j] = 0.0f;
+      } else {
+        wide_gather2<U>(a.X, a.ldx, a.col, a.w, cur, cur2, lane, acc[0], acc[1]);
+      }
+      const int64_t i = p >> 4;
+      const int b = (int)(i % kSBufs);
+      const int gen = (int)(i / kSBufs);
+      const int64_t c = chunk_of(i);
+      const int64_t r0 = c * kSRows;
+      const int lr0 = 2 * (int)(p & 15);
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int lr = lr0 + k;
+        const int64_t deg = k == 0 ? cur.deg : cur2.deg;
+        if constexpr (!BWD) {
+          if (a.Z != nullptr) {
+            const auto rz = buf_rsrc(a.Z + r0 * a.ldz, rows_in(c) * (uint32_t)a.ldz * 4u);
+            __builtin_amdgcn_raw_buffer_store_b128(
+                __builtin_bit_cast(u32x4, make_float4(acc[k][0], acc[k][1], acc[k][2], acc[k][3])),
+                rz, 4 * (int)(lr * a.ldz + 4 * lane), 0, kWideNt);
+          }
+          if (a.mean) {
+            const float dc = (float)(deg > 1 ? deg : 1);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[k][j] = __fdiv_rn(acc[k][j], dc);
+          }
+        } else {
+          if (a.row_scale != nullptr && r0 + lr < a.n_rows) {
+            const float sc = a.row_scale[r0 + lr];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[k][j] = __fmul_rn(acc[k][j], sc);
+          }
+        }
+      }
+      uint32_t hi[2][2], mid[2][2], lo[2][2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        split3_pair(f32x2{acc[k][0], acc[k][1]}, hi[k][0], mid[k][0], lo[k][0]);
+        split3_pair(f32x2{acc[k][2], acc[k][3]}, hi[k][1], mid[k][1], lo[k][1]);
+      }
+      // the buffer's previous chunk has left the MFMA waves
+      if (!lds_wait_ge(freed + b, gen, abort_word)) break;
+      char *buf = lds + b * kSBuf;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        char *img = buf + wimg_off(lr0 + k, lane >> 1) + 8 * (lane & 1);
+        *reinterpret_cast<uint2 *>(img) = make_uint2(hi[k][0], hi[k][1]);
+        *reinterpret_cast<uint2 *>(img + kSImg) = make_uint2(mid[k][0], mid[k][1]);
+        *reinterpret_cast<uint2 *>(img + 2 * kSImg) = make_uint2(lo[k][0], lo[k][1]);
+      }
+      if constexpr (!BWD) {  // the rows' mask words start empty (the MFMA waves OR into them)
+        if (lane < 2 * kWMaskWords) maskbuf[(b * kSRows + lr0) * kWMaskWords + lane] = 0u;
+      }
+      lds_signal(filled + b, 2, lane);
+      cur = nxt;
+      cur2 = nxt2;
+      nxt = nn;
+      nxt2 = nn2;
+    }
+  } else {
+    // -------------------------------- MFMA waves ----------------------------
+    const int m = wave - kSGather;  // output columns 64 m .. 64 m + 63 (n-tiles 4 m .. 4 m + 3)
+    const int h = m >> 1;           // 128-column half: mask words 4 h .. 4 h + 3
+    const auto rw = buf_rsrc(a.wimg, (uint32_t)(kWImgFrags * 16));
+    auto load_step = [&](int s, u32x4 (&f)[3]) {  // step s = 4 ks + t
+      const int ks = s >> 2, nt = 4 * m + (s & 3);
+#pragma unroll
+      for (int term = 0; term < 3; ++term)
+        f[term] = __builtin_amdgcn_raw_buffer_load_b128(
+            rw, 16 * (((ks * kWNt + nt) * 3 + term) * 64 + lane), 0, 0);
+    };
+    u32x4 wf[2][3];
+    load_step(0, wf[0]);
+    for (int64_t i = 0; i < n_my; ++i) {
+      const int b = (int)(i % kSBufs);
+      const int gen = (int)(i / kSBufs);
+      const int64_t c = chunk_of(i);
+      const int64_t r0 = c * kSRows;
+      const uint32_t rv = rows_in(c);
+      u32x4 mk[2] = {};
+      float dv[2] = {1.0f, 1.0f};
+      if constexpr (BWD && EPI != WEPI_STORE) {
+        const auto rm = buf_rsrc(a.mask_in + r0 * kWMaskWords, rv * kWMaskWords * 4u);
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+          mk[rt] = __builtin_amdgcn_raw_buffer_load_b128(
+              rm, 4 * ((16 * rt + l16) * kWMaskWords + 4 * h), 0, 0);
+        if constexpr (EPI == WEPI_RELU_DIV) {
+          const auto rd = buf_rsrc(a.row_div + r0, rv * 4u);
+#pragma unroll
+          for (int rt = 0; rt < 2; ++rt)
+            dv[rt] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rd, 4 * (16 * rt + l16), 0, 0));
+        }
+      }
+      if (!lds_wait_ge(filled + b, kSRows * (gen + 1), abort_word)) break;
+      if (a.dbg & 2) {
+        const int old = lds_signal(mdone + b, 1, lane);
+        if (old == kSMfma * gen + kSMfma - 1) lds_signal(freed + b, 1, lane);
+        continue;
+      }
+      const char *buf = lds + b * kSBuf;
+      f32x4_t acc[4][2];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[t][rt][r] = 0.0f;
+      // steps s = 4 ks + t, each W fragment one step ahead (a two-deep ring:
+      // the MFMA waves have slack -- a chunk's products are ~6 k cycles per
+      // SIMD against ~50 k of gathering); past the last step, the next
+      // chunk's first
+#pragma unroll 1
+      for (int ks = 0; ks < kWKs; ++ks) {
+        bf16x8 xf[2][3];
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) {
+          const int off = wimg_off(16 * rt + l16, 4 * ks + g4);
+#pragma unroll
+          for (int term = 0; term < 3; ++term)
+            xf[rt][term] = *reinterpret_cast<const bf16x8 *>(buf + term * kSImg + off);
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          if (!(a.dbg & 1)) load_step((4 * ks + t + 1) & 31, wf[(t + 1) & 1]);
+#pragma unroll
+          for (int rt = 0; rt < 2; ++rt)
+            acc[t][rt] = mfma16_x6_wt(wf[t & 1], xf[rt][0], xf[rt][1], xf[rt][2], acc[t][rt]);
+        }
+      }
+      const auto ry = buf_rsrc(a.Y + r0 * a.ldy, rv * (uint32_t)a.ldy * 4u);
+      uint32_t mw[2][4] = {};
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          float v[4];
+          float bb[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+          if (!BWD && a.bias != nullptr)
+            *reinterpret_cast<float4 *>(bb) =
+                *reinterpret_cast<const float4 *>(a.bias + 16 * (4 * m + t) + 4 * g4);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            v[r] = acc[t][rt][r];
+            if constexpr (!BWD) {
+              if (a.bias != nullptr) v[r] = __fadd_rn(v[r], bb[r]);
+              if (a.relu) v[r] = (v[r] < 0.0f) ? 0.0f : v[r];
+              mw[rt][r] |= (v[r] > 0.0f ? 1u : 0u) << (16 * (m & 1) + 4 * t + g4);
+            } else if constexpr (EPI != WEPI_STORE) {
+              v[r] = ((mk[rt][r] >> (16 * (m & 1) + 4 * t + g4)) & 1u) ? v[r] : 0.0f;
+              cs[t][r] = __fadd_rn(cs[t][r], v[r]);  // rows past the end: zero mask words
+              if constexpr (EPI == WEPI_RELU_DIV) v[r] = __fdiv_rn(v[r], dv[rt]);
+            }
+          }
+          __builtin_amdgcn_raw_buffer_store_b128(
+              __builtin_bit_cast(u32x4, make_float4(v[0], v[1], v[2], v[3])), ry,
+              4 * (int)((16 * rt + l16) * a.ldy + 16 * (4 * m + t) + 4 * g4), 0, kWideNt);
+        }
+      if constexpr (!BWD) {
+        if (a.mask_out != nullptr) {
+          // the four lanes of a row (g4) hold its bits of this wave's 16;
+          // lane g4 adds word 4 h + g4 into the chunk's mask row
+#pragma unroll
+          for (int rt = 0; rt < 2; ++rt) {
+            uint32_t mine = 0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              uint32_t x = mw[rt][r];
+              x |= (uint32_t)__shfl_xor((int)x, 16);
+              x |= (uint32_t)__shfl_xor((int)x, 32);
+              mine = (r == g4) ? x : mine;
+            }
+            __hip_atomic_fetch_or(maskbuf + (b * kSRows + 16 * rt + l16) * kWMaskWords + 4 * h + g4,
+                                  mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+        }
+      }
+      const int old = lds_signal(mdone + b, 1, lane);
+      if (old == kSMfma * gen + kSMfma - 1) {
+        // the last MFMA wave out: the chunk's mask words leave, the buffer is free
+        if constexpr (!BWD) {
+          if (a.mask_out != nullptr) {
+            const int row = lane >> 1;
+            const u32x4 wv = *reinterpret_cast<const u32x4 *>(
+                maskbuf + (b * kSRows + row) * kWMaskWords + 4 * (lane & 1));
+            const auto rmo = buf_rsrc(a.mask_out + r0 * kWMaskWords, rv * kWMaskWords * 4u);
+            __builtin_amdgcn_raw_buffer_store_b128(wv, rmo, 4 * (row * kWMaskWords + 4 * (lane & 1)),
+                                                   0, 0);
+          }
+        }
+        lds_signal(freed + b, 1, lane);
+      }
+    }
+  }
+  if constexpr (BWD && EPI != WEPI_STORE) {
+    // column sums: each column's 16 row lanes (one MFMA wave) folded in lane order
+    __syncthreads();
+    float *red = reinterpret_cast<float *>(lds);  // [16 row lanes][256]
+    if (wave >= kSGather) {
+      const int m = wave - kSGather;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        *reinterpret_cast<float4 *>(red + l16 * kWF + 16 * (4 * m + t) + 4 * g4) =
+            make_float4(cs[t][0], cs[t][1], cs[t][2], cs[t][3]);
+    }
+    __syncthreads();
+    if (tid < kWF) {
+      float s = 0.0f;
+#pragma unroll
+      for (int l = 0; l < 16; ++l) s = __fadd_rn(s, red[l * kWF + tid]);
+      a.colsum_partial[(int64_t)blockIdx.x * kWF + tid] = s;
+    }
+  }
+}
+
+template <int U>
+int launch_wide_ws_u(const WideArgs &a, bool bwd, int epi, int grid, hipStream_t s) {
+  if (!bwd)
+    hipLaunchKernelGGL((spmm_xw_wide_ws_kernel<U, false, WEPI_STORE>), dim3(grid), dim3(kSThreads),
+                       0, s, a);
+  else if (epi == WEPI_RELU_DIV)
+    hipLaunchKernelGGL((spmm_xw_wide_ws_kernel<U, true, WEPI_RELU_DIV>), dim3(grid),
+                       dim3(kSThreads), 0, s, a);
+  else if (epi == WEPI_RELU)
+    hipLaunchKernelGGL((spmm_xw_wide_ws_kernel<U, true, WEPI_RELU>), dim3(grid), dim3(kSThreads),
+                       0, s, a);
+  else
+    hipLaunchKernelGGL((spmm_xw_wide_ws_kernel<U, true, WEPI_STORE>), dim3(grid), dim3(kSThreads),
+                       0, s, a);
+  return check_launch("spmm_xw_wide_ws_kernel");
+}
+
 int wide_grid() {
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) != hipSuccess ||
@@ -565,7 +956,24 @@ int launch_wide_p(const WideArgs &a, bool bwd, int epi, int grid, hipStream_t s)
   return check_launch("spmm_xw_wide_kernel");
 }
 
-int launch_wide(const WideArgs &a, bool bwd, int epi, int grid, hipStream_t s) {
+int launch_wide_legacy(const WideArgs &a, bool bwd, int epi, int grid, hipStream_t s);
+
+// *grid: the workgroups launched (= the column-sum partials written)
+int launch_wide(const WideArgs &a, bool bwd, int epi, int *grid, hipStream_t s) {
+  if (g_wide_ws & (bwd ? 2 : 1)) {
+    const int64_t n_chunks = (a.n_rows + kSRows - 1) / kSRows;
+    const int64_t cus = wide_grid() / 2;  // one workgroup per CU
+    *grid = (int)(cus < n_chunks ? cus : n_chunks);
+    return g_wide_unroll == 8 ? launch_wide_ws_u<8>(a, bwd, epi, *grid, s)
+                              : launch_wide_ws_u<4>(a, bwd, epi, *grid, s);
+  }
+  const int64_t n_chunks = (a.n_rows + kWRows - 1) / kWRows;
+  const int64_t g = wide_grid();
+  *grid = (int)(g < n_chunks ? g : n_chunks);
+  return launch_wide_legacy(a, bwd, epi, *grid, s);
+}
+
+int launch_wide_legacy(const WideArgs &a, bool bwd, int epi, int grid, hipStream_t s) {
   if (g_wide_pair & (bwd ? 2 : 1))
     return g_wide_unroll == 8 ? launch_wide_p<8, true>(a, bwd, epi, grid, s)
                               : launch_wide_p<4, true>(a, bwd, epi, grid, s);
@@ -608,10 +1016,9 @@ int xw_wide_fwd(int64_t n_rows, const int64_t *rowptr, const int32_t *col, const
   a.ldz = ldz;
   a.mean = mean;
   a.relu = relu;
-  const int64_t n_chunks = (n_rows + kWRows - 1) / kWRows;
-  int64_t grid = wide_grid();
-  if (grid > n_chunks) grid = n_chunks;
-  return launch_wide(a, false, WEPI_STORE, (int)grid, s);
+  a.dbg = g_wide_dbg;
+  int grid = 0;
+  return launch_wide(a, false, WEPI_STORE, &grid, s);
 }
 
 int xw_wide_bwd_dx(int64_t n_rows, const int64_t *rowptr_t, const int32_t *col_t,
@@ -638,12 +1045,11 @@ int xw_wide_bwd_dx(int64_t n_rows, const int64_t *rowptr_t, const int32_t *col_t
   a.mask_in = relu_mask;
   a.row_div = row_div;
   a.colsum_partial = partial;
-  const int64_t n_chunks = (n_rows + kWRows - 1) / kWRows;
-  int64_t grid = wide_grid();
-  if (grid > n_chunks) grid = n_chunks;
-  int rc = launch_wide(a, true, epi, (int)grid, s);
+  a.dbg = g_wide_dbg;
+  int grid = 0;
+  int rc = launch_wide(a, true, epi, &grid, s);
   if (rc || epi == WEPI_STORE) return rc;
-  return launch_fold(partial, (int)grid, kWF, kWF, colsum, kWF, accumulate, s);
+  return launch_fold(partial, grid, kWF, kWF, colsum, kWF, accumulate, s);
 }
 
 }  // namespace mgcn

@@ -165,6 +165,6 @@ int xw_wide_bwd_dx(int64_t n_rows, const int64_t *rowptr_t, const int32_t *col_t
                    const float *W, int64_t ldw, float *dX, int64_t lddx,
                    const uint32_t *relu_mask, const float *row_div, float *colsum,
                    int accumulate, void *workspace, hipStream_t s);
-int wide_set_option(const char *name, int value);  // "wide_pair" / "wide_unroll"
+int wide_set_option(const char *name, int value);  // "wide_pair" / "wide_unroll" / "wide_ws"
 
 }  // namespace mgcn

@@ -41,6 +41,16 @@ def _graph(rng, N, E, hub=0):
 GRAPHS = [(20000, 200000, 0), (4097, 40000, 0), (33, 100, 0), (1, 0, 0), (3000, 20000, 700)]
 
 
+@pytest.fixture(autouse=True, params=[3, 0], ids=["ws", "legacy"])
+def wide_form(request):
+    """Every test runs on the warp-specialised kernels (wide_ws = 3) and on
+    the 16-row two-workgroup form (wide_ws = 0, the default)."""
+    from mgcn import _lib as L
+    L.set_option("wide_ws", request.param)
+    yield request.param
+    L.set_option("wide_ws", 0)
+
+
 def _plan(cuda, ei, N, deg_norm):
     from mgcn.graph import plan_for
     plan = plan_for(_t(ei, cuda), N)
@@ -325,3 +335,37 @@ def test_wide_stack_frozen_middle_weight(cuda, oracle):
         for g, g0 in zip(grads, base[2]):
             if g is not None:
                 assert torch.equal(g, g0)
+
+
+@pytest.mark.parametrize("N,E,hub", GRAPHS)
+@pytest.mark.parametrize("aggr", ["add", "mean"])
+def test_wide_forms_agree_bitwise(cuda, wide_form, N, E, hub, aggr):
+    """Random W, bias, ReLU: the warp-specialised kernels (W^T image as the A
+    operand, the same six products per k-step in the same order) give the
+    16-row kernels' Y, Z, mask words and dX bit for bit; column sums agree
+    within fp32 reordering."""
+    from mgcn import _lib as L
+    from mgcn import ops
+    if wide_form != 3:
+        pytest.skip("one comparison per graph")
+    rng = np.random.default_rng(5 * N + E + hub)
+    ei = _graph(rng, N, E, hub)
+    plan, norm = _plan(cuda, ei, N, "sm")
+    X = _t(rng.standard_normal((N, F)).astype(np.float32), cuda)
+    W = _t((rng.standard_normal((F, F)) * 0.1).astype(np.float32), cuda)
+    b = _t(rng.uniform(-0.5, 0.5, F).astype(np.float32), cuda)
+    lower = _t(_mask_words(rng.standard_normal((N, F)).astype(np.float32)), cuda)
+    rd = plan.in_cnt if aggr == "mean" else None
+    out = {}
+    for form in (3, 0):
+        L.set_option("wide_ws", form)
+        rm = torch.empty(N, 8, dtype=torch.int32, device=cuda)
+        Y, Z = ops.spmm_xw_fwd(plan.fwd, norm.w_fwd, X, W, L.REDUCE_CODES[aggr], b, True,
+                               relu_mask=rm, want_z=True)
+        _, dX, cs = ops.spmm_xw_bwd(plan.bwd, norm.w_bwd, None, X, None, W, relu_mask=lower,
+                                    row_div=rd)
+        out[form] = (Y, Z, rm, dX, cs)
+    L.set_option("wide_ws", 0)
+    for a, c in zip(out[3][:4], out[0][:4]):
+        assert torch.equal(a, c)
+    torch.testing.assert_close(out[3][4], out[0][4], rtol=1e-5, atol=1e-4)
