@@ -62,13 +62,24 @@ int g_wide_pair = 3;
 int g_wide_unroll = 4;
 // mgcn_set_option("wide_ws"): the warp-specialised kernels (below) -- bit 0
 // the forward, bit 1 the adjoint
-int g_wide_ws = 0;
+int g_wide_ws = 3;
 // mgcn_set_option("wide_dbg"): timing experiments on the warp-specialised
 // kernels (results are WRONG when set): bit 0 the MFMA waves skip their W
-// loads, bit 1 they skip the products, bit 2 the gather waves skip the gathers
+// loads, bit 1 they skip the products, bit 2 the gather waves skip the gathers;
+// bits 3 / 4: s_setprio 2 on the gather / MFMA waves (results stay exact)
 int g_wide_dbg = 0;
+// mgcn_set_option("wide_mfma"): MFMA waves of the warp-specialised kernels (4 or 8)
+int g_wide_mfma = 8;
 
 int wide_set_option(const char *name, int value) {
+  if (name[5] == 'm') {
+    if (value != 4 && value != 8) {
+      set_error("wide_mfma must be 4 or 8");
+      return MGCN_EINVAL;
+    }
+    g_wide_mfma = value;
+    return MGCN_OK;
+  }
   if (name[5] == 'd') {
     g_wide_dbg = value;
     return MGCN_OK;
@@ -593,9 +604,7 @@ constexpr int kSRows = 32;
 constexpr int kSBufs = 3;
 constexpr int kSImg = kSRows * kWF * 2;     // one term image of a chunk: 16 KB
 constexpr int kSBuf = 3 * kSImg;            // 48 KB
-constexpr int kSGather = 12;
-constexpr int kSMfma = 4;
-constexpr int kSThreads = 64 * (kSGather + kSMfma);
+constexpr int kSThreads = 1024;  // 16 waves: 16 - NM gather, NM MFMA
 constexpr int kSMaskOff = kSBufs * kSBuf;                                 // [3][32][8] u32
 constexpr int kSCtrOff = kSMaskOff + kSBufs * kSRows * kWMaskWords * 4;  // counters
 constexpr int kSLds = kSCtrOff + 64;
@@ -646,8 +655,13 @@ __device__ __forceinline__ int lds_signal(int *p, int v, int lane) {
   return __builtin_amdgcn_readfirstlane(old);
 }
 
-template <int U, bool BWD, int EPI>
+template <int U, bool BWD, int EPI, int NM>
 __global__ __launch_bounds__(kSThreads) void spmm_xw_wide_ws_kernel(const WideArgs a) {
+  // NM MFMA waves (4 or 8), 16 - NM gather waves; MFMA wave m owns the NT
+  // n-tiles NT m .. NT m + NT - 1 (16 NT output columns)
+  constexpr int NG = 16 - NM;
+  constexpr int NT = kWNt / NM;
+  constexpr int KSI = 4 / NT;  // k-steps per ring turn (4 W steps)
   __shared__ __attribute__((aligned(16))) char lds[kSLds];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -667,14 +681,15 @@ __global__ __launch_bounds__(kSThreads) void spmm_xw_wide_ws_kernel(const WideAr
     return (uint32_t)(r <= 0 ? 0 : r >= kSRows ? kSRows : r);
   };
 
-  float cs[4][4];  // backward column sums (MFMA waves)
+  float cs[NT][4];  // backward column sums (MFMA waves)
 #pragma unroll
-  for (int t = 0; t < 4; ++t)
+  for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) cs[t][r] = 0.0f;
 
-  if (wave < kSGather) {
+  if (wave < NG) {
     // ------------------------------- gather waves ---------------------------
+    if (a.dbg & 8) __builtin_amdgcn_s_setprio(2);
     const int64_t n_pairs = 16 * n_my;
     auto pair_row = [&](int64_t p) { return chunk_of(p >> 4) * kSRows + 2 * (p & 15); };
     WRow cur, cur2, nxt, nxt2;
@@ -685,15 +700,15 @@ __global__ __launch_bounds__(kSThreads) void spmm_xw_wide_ws_kernel(const WideAr
       wrow_ptr(a.rowptr, ra + 1, ok && ra + 1 < a.n_rows, cur2);
       wrow_first(a.col, a.w, lane, cur);
       wrow_first(a.col, a.w, lane, cur2);
-      const int64_t q = p + kSGather, rq = pair_row(q);
+      const int64_t q = p + NG, rq = pair_row(q);
       wrow_ptr(a.rowptr, rq, q < n_pairs && rq < a.n_rows, nxt);
       wrow_ptr(a.rowptr, rq + 1, q < n_pairs && rq + 1 < a.n_rows, nxt2);
     }
-    for (int64_t p = wave; p < n_pairs; p += kSGather) {
+    for (int64_t p = wave; p < n_pairs; p += NG) {
       wrow_first(a.col, a.w, lane, nxt);
       wrow_first(a.col, a.w, lane, nxt2);
       WRow nn, nn2;
-      const int64_t q = p + 2 * kSGather, rq = pair_row(q);
+      const int64_t q = p + 2 * NG, rq = pair_row(q);
       wrow_ptr(a.rowptr, rq, q < n_pairs && rq < a.n_rows, nn);
       wrow_ptr(a.rowptr, rq + 1, q < n_pairs && rq + 1 < a.n_rows, nn2);
       float acc[2][4];
@@ -760,18 +775,24 @@ __global__ __launch_bounds__(kSThreads) void spmm_xw_wide_ws_kernel(const WideAr
     }
   } else {
     // -------------------------------- MFMA waves ----------------------------
-    const int m = wave - kSGather;  // output columns 64 m .. 64 m + 63 (n-tiles 4 m .. 4 m + 3)
-    const int h = m >> 1;           // 128-column half: mask words 4 h .. 4 h + 3
+    if (a.dbg & 16) __builtin_amdgcn_s_setprio(2);
+    const int m = wave - NG;
+    const int nt0 = NT * m;
+    const int h = nt0 >> 3;  // 128-column half: mask words 4 h .. 4 h + 3
     const auto rw = buf_rsrc(a.wimg, (uint32_t)(kWImgFrags * 16));
-    auto load_step = [&](int s, u32x4 (&f)[3]) {  // step s = 4 ks + t
-      const int ks = s >> 2, nt = 4 * m + (s & 3);
+    // W step s = NT ks + t (t < NT), 8 NT steps per chunk; a four-deep ring
+    // two steps ahead (the step after a chunk's last is the next chunk's first)
+    constexpr int kSteps = kWKs * NT;
+    auto load_step = [&](int s, u32x4 (&f)[3]) {
+      const int ks = s / NT, nt = nt0 + s % NT;
 #pragma unroll
       for (int term = 0; term < 3; ++term)
         f[term] = __builtin_amdgcn_raw_buffer_load_b128(
             rw, 16 * (((ks * kWNt + nt) * 3 + term) * 64 + lane), 0, 0);
     };
-    u32x4 wf[2][3];
+    u32x4 wf[4][3];
     load_step(0, wf[0]);
+    load_step(1, wf[1]);
     for (int64_t i = 0; i < n_my; ++i) {
       const int b = (int)(i % kSBufs);
       const int gen = (int)(i / kSBufs);
@@ -796,37 +817,38 @@ __global__ __launch_bounds__(kSThreads) void spmm_xw_wide_ws_kernel(const WideAr
       if (!lds_wait_ge(filled + b, kSRows * (gen + 1), abort_word)) break;
       if (a.dbg & 2) {
         const int old = lds_signal(mdone + b, 1, lane);
-        if (old == kSMfma * gen + kSMfma - 1) lds_signal(freed + b, 1, lane);
+        if (old == NM * gen + NM - 1) lds_signal(freed + b, 1, lane);
         continue;
       }
       const char *buf = lds + b * kSBuf;
-      f32x4_t acc[4][2];
+      f32x4_t acc[NT][2];
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
+      for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc[t][rt][r] = 0.0f;
-      // steps s = 4 ks + t, each W fragment one step ahead (a two-deep ring:
-      // the MFMA waves have slack -- a chunk's products are ~6 k cycles per
-      // SIMD against ~50 k of gathering); past the last step, the next
-      // chunk's first
 #pragma unroll 1
-      for (int ks = 0; ks < kWKs; ++ks) {
-        bf16x8 xf[2][3];
+      for (int k0 = 0; k0 < kWKs; k0 += KSI) {
 #pragma unroll
-        for (int rt = 0; rt < 2; ++rt) {
-          const int off = wimg_off(16 * rt + l16, 4 * ks + g4);
+        for (int kk = 0; kk < KSI; ++kk) {
+          const int ks = k0 + kk;
+          bf16x8 xf[2][3];
 #pragma unroll
-          for (int term = 0; term < 3; ++term)
-            xf[rt][term] = *reinterpret_cast<const bf16x8 *>(buf + term * kSImg + off);
-        }
+          for (int rt = 0; rt < 2; ++rt) {
+            const int off = wimg_off(16 * rt + l16, 4 * ks + g4);
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          if (!(a.dbg & 1)) load_step((4 * ks + t + 1) & 31, wf[(t + 1) & 1]);
+            for (int term = 0; term < 3; ++term)
+              xf[rt][term] = *reinterpret_cast<const bf16x8 *>(buf + term * kSImg + off);
+          }
 #pragma unroll
-          for (int rt = 0; rt < 2; ++rt)
-            acc[t][rt] = mfma16_x6_wt(wf[t & 1], xf[rt][0], xf[rt][1], xf[rt][2], acc[t][rt]);
+          for (int t = 0; t < NT; ++t) {
+            const int q = kk * NT + t;  // step within the ring turn: ring slot q
+            if (!(a.dbg & 1)) load_step((NT * ks + t + 2) % kSteps, wf[(q + 2) & 3]);
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt)
+              acc[t][rt] = mfma16_x6_wt(wf[q], xf[rt][0], xf[rt][1], xf[rt][2], acc[t][rt]);
+          }
         }
       }
       const auto ry = buf_rsrc(a.Y + r0 * a.ldy, rv * (uint32_t)a.ldy * 4u);
@@ -834,33 +856,35 @@ __global__ __launch_bounds__(kSThreads) void spmm_xw_wide_ws_kernel(const WideAr
 #pragma unroll
       for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
+        for (int t = 0; t < NT; ++t) {
+          const int nt = nt0 + t;
+          const int bit = 4 * (nt & 7) + g4;
           float v[4];
           float bb[4] = {0.0f, 0.0f, 0.0f, 0.0f};
           if (!BWD && a.bias != nullptr)
             *reinterpret_cast<float4 *>(bb) =
-                *reinterpret_cast<const float4 *>(a.bias + 16 * (4 * m + t) + 4 * g4);
+                *reinterpret_cast<const float4 *>(a.bias + 16 * nt + 4 * g4);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             v[r] = acc[t][rt][r];
             if constexpr (!BWD) {
               if (a.bias != nullptr) v[r] = __fadd_rn(v[r], bb[r]);
               if (a.relu) v[r] = (v[r] < 0.0f) ? 0.0f : v[r];
-              mw[rt][r] |= (v[r] > 0.0f ? 1u : 0u) << (16 * (m & 1) + 4 * t + g4);
+              mw[rt][r] |= (v[r] > 0.0f ? 1u : 0u) << bit;
             } else if constexpr (EPI != WEPI_STORE) {
-              v[r] = ((mk[rt][r] >> (16 * (m & 1) + 4 * t + g4)) & 1u) ? v[r] : 0.0f;
+              v[r] = ((mk[rt][r] >> bit) & 1u) ? v[r] : 0.0f;
               cs[t][r] = __fadd_rn(cs[t][r], v[r]);  // rows past the end: zero mask words
               if constexpr (EPI == WEPI_RELU_DIV) v[r] = __fdiv_rn(v[r], dv[rt]);
             }
           }
           __builtin_amdgcn_raw_buffer_store_b128(
               __builtin_bit_cast(u32x4, make_float4(v[0], v[1], v[2], v[3])), ry,
-              4 * (int)((16 * rt + l16) * a.ldy + 16 * (4 * m + t) + 4 * g4), 0, kWideNt);
+              4 * (int)((16 * rt + l16) * a.ldy + 16 * nt + 4 * g4), 0, kWideNt);
         }
       if constexpr (!BWD) {
         if (a.mask_out != nullptr) {
-          // the four lanes of a row (g4) hold its bits of this wave's 16;
-          // lane g4 adds word 4 h + g4 into the chunk's mask row
+          // the four lanes of a row (g4) hold its bits of this wave's n-tiles;
+          // lane g4 ORs word 4 h + g4 into the chunk's mask row
 #pragma unroll
           for (int rt = 0; rt < 2; ++rt) {
             uint32_t mine = 0;
@@ -877,7 +901,7 @@ __global__ __launch_bounds__(kSThreads) void spmm_xw_wide_ws_kernel(const WideAr
         }
       }
       const int old = lds_signal(mdone + b, 1, lane);
-      if (old == kSMfma * gen + kSMfma - 1) {
+      if (old == NM * gen + NM - 1) {
         // the last MFMA wave out: the chunk's mask words leave, the buffer is free
         if constexpr (!BWD) {
           if (a.mask_out != nullptr) {
@@ -897,11 +921,11 @@ __global__ __launch_bounds__(kSThreads) void spmm_xw_wide_ws_kernel(const WideAr
     // column sums: each column's 16 row lanes (one MFMA wave) folded in lane order
     __syncthreads();
     float *red = reinterpret_cast<float *>(lds);  // [16 row lanes][256]
-    if (wave >= kSGather) {
-      const int m = wave - kSGather;
+    if (wave >= NG) {
+      const int m = wave - NG;
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
-        *reinterpret_cast<float4 *>(red + l16 * kWF + 16 * (4 * m + t) + 4 * g4) =
+      for (int t = 0; t < NT; ++t)
+        *reinterpret_cast<float4 *>(red + l16 * kWF + 16 * (NT * m + t) + 4 * g4) =
             make_float4(cs[t][0], cs[t][1], cs[t][2], cs[t][3]);
     }
     __syncthreads();
@@ -914,21 +938,27 @@ __global__ __launch_bounds__(kSThreads) void spmm_xw_wide_ws_kernel(const WideAr
   }
 }
 
-template <int U>
-int launch_wide_ws_u(const WideArgs &a, bool bwd, int epi, int grid, hipStream_t s) {
+template <int U, int NM>
+int launch_wide_ws_un(const WideArgs &a, bool bwd, int epi, int grid, hipStream_t s) {
   if (!bwd)
-    hipLaunchKernelGGL((spmm_xw_wide_ws_kernel<U, false, WEPI_STORE>), dim3(grid), dim3(kSThreads),
-                       0, s, a);
+    hipLaunchKernelGGL((spmm_xw_wide_ws_kernel<U, false, WEPI_STORE, NM>), dim3(grid),
+                       dim3(kSThreads), 0, s, a);
   else if (epi == WEPI_RELU_DIV)
-    hipLaunchKernelGGL((spmm_xw_wide_ws_kernel<U, true, WEPI_RELU_DIV>), dim3(grid),
+    hipLaunchKernelGGL((spmm_xw_wide_ws_kernel<U, true, WEPI_RELU_DIV, NM>), dim3(grid),
                        dim3(kSThreads), 0, s, a);
   else if (epi == WEPI_RELU)
-    hipLaunchKernelGGL((spmm_xw_wide_ws_kernel<U, true, WEPI_RELU>), dim3(grid), dim3(kSThreads),
-                       0, s, a);
+    hipLaunchKernelGGL((spmm_xw_wide_ws_kernel<U, true, WEPI_RELU, NM>), dim3(grid),
+                       dim3(kSThreads), 0, s, a);
   else
-    hipLaunchKernelGGL((spmm_xw_wide_ws_kernel<U, true, WEPI_STORE>), dim3(grid), dim3(kSThreads),
-                       0, s, a);
+    hipLaunchKernelGGL((spmm_xw_wide_ws_kernel<U, true, WEPI_STORE, NM>), dim3(grid),
+                       dim3(kSThreads), 0, s, a);
   return check_launch("spmm_xw_wide_ws_kernel");
+}
+
+template <int U>
+int launch_wide_ws_u(const WideArgs &a, bool bwd, int epi, int grid, hipStream_t s) {
+  return g_wide_mfma == 8 ? launch_wide_ws_un<U, 8>(a, bwd, epi, grid, s)
+                          : launch_wide_ws_un<U, 4>(a, bwd, epi, grid, s);
 }
 
 int wide_grid() {

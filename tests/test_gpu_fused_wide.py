@@ -43,12 +43,12 @@ GRAPHS = [(20000, 200000, 0), (4097, 40000, 0), (33, 100, 0), (1, 0, 0), (3000, 
 
 @pytest.fixture(autouse=True, params=[3, 0], ids=["ws", "legacy"])
 def wide_form(request):
-    """Every test runs on the warp-specialised kernels (wide_ws = 3) and on
-    the 16-row two-workgroup form (wide_ws = 0, the default)."""
+    """Every test runs on the warp-specialised kernels (wide_ws = 3, the
+    default) and on the 16-row two-workgroup form (wide_ws = 0)."""
     from mgcn import _lib as L
     L.set_option("wide_ws", request.param)
     yield request.param
-    L.set_option("wide_ws", 0)
+    L.set_option("wide_ws", 3)
 
 
 def _plan(cuda, ei, N, deg_norm):
@@ -365,7 +365,7 @@ def test_wide_forms_agree_bitwise(cuda, wide_form, N, E, hub, aggr):
         _, dX, cs = ops.spmm_xw_bwd(plan.bwd, norm.w_bwd, None, X, None, W, relu_mask=lower,
                                     row_div=rd)
         out[form] = (Y, Z, rm, dX, cs)
-    L.set_option("wide_ws", 0)
+    L.set_option("wide_ws", 3)
     for a, c in zip(out[3][:4], out[0][:4]):
         assert torch.equal(a, c)
     torch.testing.assert_close(out[3][4], out[0][4], rtol=1e-5, atol=1e-4)
