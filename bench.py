@@ -196,6 +196,9 @@ def launch_bytes(name: str, rows: int, edges: int, F: int):
             b += 4 * rows * F     # the aggregate Z written beside Y
         elif name == "spmm_xw_bwd_dx":
             b += 16 * rows        # the lower layer's ReLU mask words
+        elif name == "spmm_xw_bwd_dwl":
+            b += 16 * rows + 4 * rows * F   # masks + the lower layer's Z rows read
+            fl *= 2                         # + dWl = Z^T dX
         return b, fl
     if name.startswith("spmm"):
         return spmm_bytes(rows, edges, F), 0.0
@@ -331,6 +334,8 @@ def main():
     ap.add_argument("--chunks", type=int, default=4,
                     help="N > 1 sharded path: row chunks per layer output (all-gathers "
                          "pipelined behind the compute)")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="mgcn_set_option before the run (A/B experiments; repeatable)")
     ap.add_argument("--dist-backend", default="nccl", help=argparse.SUPPRESS)  # gloo: tests
     ap.add_argument("--one-device", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
@@ -353,6 +358,9 @@ def main():
             dist.init_process_group(args.dist_backend)
 
     import mgcn  # noqa: F401
+    for kv in args.opt:
+        k, v = kv.split("=")
+        mgcn.set_option(k, int(v))
 
     F, L = args.feat, args.layers
     n_edges = 2 * args.pairs          # graph edges, self-loops not counted
@@ -426,9 +434,11 @@ def main():
                        "bf16x6 (exact 3-term bf16 split of each fp32 operand, 6 MFMA products, "
                        "fp32 accumulate; error at fp32 level, tests/test_gpu_parity.py); "
                        "forward fused as (A x) W in one launch per layer, keeping Z = A x; "
-                       "backward dW = Z^T dY in one dense pass (mgcn_gemm_bwd) and dX from a "
-                       "gather of A^T dY (mgcn_spmm_xw_bwd, dX only); the bottom layer runs "
-                       "no gather (tests/test_gpu_fused.py, tests/test_gpu_headline.py)"),
+                       "backward: the top layer's dW = Z^T dY in one dense pass "
+                       "(mgcn_gemm_bwd), every other layer's dW = Z^T dY fused into the "
+                       "warp-specialised dX-only adjoint that writes its dY "
+                       "(mgcn_spmm_xw_bwd_dwl); the bottom layer runs no gather "
+                       "(tests/test_gpu_fused.py, tests/test_gpu_headline.py)"),
         "config": {"workload": head["workload"], "nodes": N, "edges": n_edges, "nnz": nnz,
                    "feat": F, "layers": L, "global_batch": world if mode == "replica" else 1,
                    "parallelism": head["parallelism"]},

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define MGCN_ABI_VERSION 17
+#define MGCN_ABI_VERSION 18
 
 /* return codes */
 #define MGCN_OK 0
@@ -413,6 +413,35 @@ int mgcn_spmm_xw_bwd(int64_t n_rows, int64_t n_cols, int32_t F_in, int32_t F_out
                      const float *row_div, float *colsum, const uint32_t *win_mask,
                      const int32_t *slot_map, void *workspace, size_t workspace_bytes,
                      void *stream);
+
+/* Bytes of scratch mgcn_spmm_xw_bwd_dwl needs (dWl split-K partials + column
+ * sums; ABI v18). */
+size_t mgcn_spmm_xw_bwd_dwl_workspace_bytes(int64_t n_rows);
+
+/*
+ * The dX-only adjoint of a 128 -> 128 layer l with the LOWER layer's weight
+ * gradient in the same launch (ABI v18; F = 128, bf16x6):
+ *   dX  = relu'(lower) ((A^T dY [* row_scale]) W^T) [/ row_div]
+ *         -- bit for bit mgcn_spmm_xw_bwd's dX-only form (layer l-1's dY)
+ *   colsum (+)= sum_rows dX            (layer l-1's bias gradient; accumulate_colsum)
+ *   dWl    (+)= Zl^T dX                (layer l-1's weight gradient; accumulate_dw)
+ * Zl [n_rows, 128] (ldz, 16-byte aligned rows) is layer l-1's aggregate as
+ * mgcn_spmm_xw_fwd returns it in Z (mean: the undivided sum, which pairs
+ * with the count-divided dX).  The reference's dW of layer l-1 is
+ * h^T (A^T dY_{l-1}) -- autograd of `x @ weight_node` and the gather /
+ * scatter_add (gcn_base_models.py:201-241) -- equal to (A h)^T dY_{l-1} for
+ * the linear aggregator; this replaces mgcn_gemm_bwd's dW-only Z^T dY pass
+ * over the dY this launch writes.  relu_mask needs colsum; row_div needs
+ * relu_mask.  dWl: deterministic split-K (one partial per workgroup, folded
+ * in order); within the fp64 |.|-bound of the reference product.
+ */
+int mgcn_spmm_xw_bwd_dwl(int64_t n_rows, int64_t n_cols, const int64_t *rowptr_t,
+                         const int32_t *col_t, const float *w_t, const float *row_scale,
+                         const float *dY, int64_t lddy, const float *W, int64_t ldw, float *dX,
+                         int64_t lddx, const uint32_t *relu_mask, const float *row_div,
+                         float *colsum, int accumulate_colsum, const float *Zl, int64_t ldz,
+                         float *dWl, int64_t lddw, int accumulate_dw, void *workspace,
+                         size_t workspace_bytes, void *stream);
 
 /* ---------------------------------------------------- edge weight adjoint */
 

@@ -246,6 +246,77 @@ __device__ __forceinline__ void gather_row_meta(const __amdgpu_buffer_rsrc_t rx,
   }
 }
 
+// Two rows per lane group at once (the warp-specialised adjoint's gather
+// waves): U slots of EACH row in flight per round, so a wave keeps four rows'
+// gathers in flight; each row folded in its own edge order, products and
+// sums rounded separately (gather_row_meta bit for bit).
+template <int U>
+__device__ __forceinline__ void gather_row2_meta(const __amdgpu_buffer_rsrc_t rx, uint32_t ldx_b,
+                                                 const int32_t *__restrict__ col,
+                                                 const float *__restrict__ w, const RowMeta &ma,
+                                                 const RowMeta &mb, int gl, int grp,
+                                                 float (&aa)[4], float (&ab)[4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) aa[j] = ab[j] = 0.0f;
+  const int64_t da = ma.deg, db = mb.deg;
+  int64_t dm = da > db ? da : db;
+  const int64_t odm = __shfl_xor(dm, 32, 64);
+  dm = dm > odm ? dm : odm;  // wave-uniform loop bound
+  int mca = ma.mc, mcb = mb.mc;
+  float mwa = ma.mw, mwb = mb.mw;
+  for (int64_t e0 = 0; e0 < dm; e0 += 32) {
+    if (e0 > 0) {  // rows longer than one metadata batch load the rest in place
+      const int64_t my = e0 + gl;
+      mca = mcb = 0;
+      mwa = mwb = 1.0f;
+      if (my < da) {
+        mca = col[ma.beg + my];
+        if (w != nullptr) mwa = w[ma.beg + my];
+      }
+      if (my < db) {
+        mcb = col[mb.beg + my];
+        if (w != nullptr) mwb = w[mb.beg + my];
+      }
+    }
+    const int64_t ra = da - e0, rb = db - e0;
+    const int na = ra <= 0 ? 0 : (ra < 32 ? (int)ra : 32);
+    const int nb = rb <= 0 ? 0 : (rb < 32 ? (int)rb : 32);
+    const int64_t remw = dm - e0;
+    const int nbmax = remw < 32 ? (int)remw : 32;  // wave-uniform
+    for (int k0 = 0; k0 < nbmax; k0 += U) {
+      float4 xa[U], xb[U];
+      float wa[U], wb[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = k0 + u;
+        const int ca = __shfl(mca, 32 * grp + (k & 31), 64);
+        const int cb = __shfl(mcb, 32 * grp + (k & 31), 64);
+        wa[u] = __shfl(mwa, 32 * grp + (k & 31), 64);
+        wb[u] = __shfl(mwb, 32 * grp + (k & 31), 64);
+        const uint32_t oa = k < na ? (uint32_t)ca * ldx_b + 16u * gl : 0xfffffff0u;
+        const uint32_t ob = k < nb ? (uint32_t)cb * ldx_b + 16u * gl : 0xfffffff0u;
+        xa[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, oa, 0, 0));
+        xb[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, ob, 0, 0));
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (k0 + u < na) {
+          aa[0] = __fadd_rn(aa[0], __fmul_rn(xa[u].x, wa[u]));
+          aa[1] = __fadd_rn(aa[1], __fmul_rn(xa[u].y, wa[u]));
+          aa[2] = __fadd_rn(aa[2], __fmul_rn(xa[u].z, wa[u]));
+          aa[3] = __fadd_rn(aa[3], __fmul_rn(xa[u].w, wa[u]));
+        }
+        if (k0 + u < nb) {
+          ab[0] = __fadd_rn(ab[0], __fmul_rn(xb[u].x, wb[u]));
+          ab[1] = __fadd_rn(ab[1], __fmul_rn(xb[u].y, wb[u]));
+          ab[2] = __fadd_rn(ab[2], __fmul_rn(xb[u].z, wb[u]));
+          ab[3] = __fadd_rn(ab[3], __fmul_rn(xb[u].w, wb[u]));
+        }
+      }
+    }
+  }
+}
+
 // The row sequence of one lane group in the chunk loop: row k is slot
 // 16 (k & 1) + 2 wave + grp of the workgroup's chunk k >> 1 (chunks
 // blockIdx.x + i gridDim.x).  Used by the forward (-2.5 %) and the dX-only
@@ -822,7 +893,432 @@ int launch_xb_u(const XbArgs &a, int epi, int grid, hipStream_t s) {
                                : launch_xb_m<U, false>(a, epi, grid, s);
 }
 
+// ===================== warp-specialised adjoint (round 5) =====================
+//
+// The dX-only adjoint above, re-cut by role as fused_wide.hip's F = 256
+// kernels, and optionally with the LOWER layer's weight gradient fused in:
+//
+//   dX = relu'(lower) ((A^T dY [* rs]) W^T) [/ row_div]   (= dY of layer l-1)
+//   colsum = sum_rows dX                                  (layer l-1's bias grad)
+//   dWl = Zl^T dX                                         (layer l-1's dW, DWL)
+//
+// with Zl the lower layer's aggregate A h (mgcn_spmm_xw_fwd's Z).  The
+// reference's dW of layer l-1 is h^T (A^T dY_{l-1}) (autograd of x @ weight
+// then the gather / scatter, gcn_base_models.py:201-241) = (A h)^T dY_{l-1}
+// for the linear aggregator -- the Z^T dY pass (mgcn_gemm_bwd dW-only), here
+// folded into the launch that PRODUCES dY_{l-1}: the dW pass's 1 GB re-read
+// of dY and its launch go away (config 2).
+//
+// One 1024-thread workgroup per CU: 8 GATHER waves aggregate dH rows (two
+// 32-lane groups per wave, gather_row_meta's edge order: bit for bit the
+// SpMM's adjoint), load the rows' Zl (DWL) and write both as bf16 term images
+// into a ring of two 48-KB chunk buffers; 8 MFMA waves hold W^T's fragments
+// of their 16 output columns (48 VGPRs, split once), form the chunk's dX
+// (W^T as the A operand: a lane's fragment is 4 consecutive columns of one
+// row, one 16-B store; the same six products in the same order as the
+// two-phase kernel, so dX is bit for bit its result), apply the epilogue,
+// write dX's term images, and after the eight waves' images are in (an LDS
+// counter) accumulate dWl += Zl^T dX on gemm_bwd's 32x32 tiles (two per
+// wave, transposed image reads) for the whole launch: one 128 x 128 partial
+// per workgroup, folded in workgroup order.  Hand-offs: LDS counters as in
+// fused_wide.hip (bounded spins, abort word).
+constexpr int kBsImgSet = 3 * kXwImg;          // one operand's three term images: 24 KB
+constexpr int kBsRingBuf = 2 * kBsImgSet;      // dH images + Zl images: 48 KB
+constexpr int kBsXOff = 2 * kBsRingBuf;        // two dX image sets (DWL)
+constexpr int kBsCtrOff = kBsXOff + 2 * kBsImgSet;
+constexpr int kBsLds = kBsCtrOff + 64;         // 144 KB + counters
+static_assert(kBsLds <= 160 * 1024, "one warp-specialised adjoint workgroup per CU");
+static_assert(16 * kXwF * 4 <= kBsXOff, "column-sum fold fits in the ring");
+constexpr int kBsNG = 8, kBsNM = 8;
+constexpr int kBsThreads = 64 * (kBsNG + kBsNM);
+constexpr uint32_t kBsSpinLimit = 1u << 25;
+#ifndef MGCN_BS_HOLDW
+#define MGCN_BS_HOLDW 0  // DWL: W^T fragments held in registers (0: re-read per chunk)
+#endif
+
+__device__ __forceinline__ int bs_lds_load(const int *p) {
+  return __builtin_amdgcn_readfirstlane(
+      __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+
+__device__ __forceinline__ bool bs_wait_ge(const int *p, int target, int *abort_word) {
+  for (uint32_t n = 0;; ++n) {
+    if (bs_lds_load(p) >= target) break;
+    if (bs_lds_load(abort_word) != 0) return false;
+    if (n >= kBsSpinLimit) {
+      __hip_atomic_store(abort_word, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  asm volatile("" ::: "memory");
+  return true;
+}
+
+__device__ __forceinline__ int bs_signal(int *p, int v, int lane) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  int old = 0;
+  if (lane == 0) old = __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  return __builtin_amdgcn_readfirstlane(old);
+}
+
+// the two-phase kernel's six products (dH_l W_h, dH_h W_l, dH_m W_m, dH_m W_h,
+// dH_h W_m, dH_h W_h) with W^T as the A operand
+__device__ __forceinline__ f32x4_t mfma16_x6_at(const bf16x8 (&w)[3], const bf16x8 &xh,
+                                               const bf16x8 &xm, const bf16x8 &xl, f32x4_t c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], xl, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[2], xh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[1], xm, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], xm, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[1], xh, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], xh, c, 0, 0, 0);
+}
+
+struct XbsArgs {
+  XbArgs b;             // rowptr .. row_div, colsum_partial (dX-only fields)
+  const float *Zl;      // DWL: the lower layer's aggregate [n_rows][128]
+  int64_t ldz;
+  float *dwl_partial;   // DWL: [grid][128][128]
+  int dbg;              // xw_ws_dbg (timing experiments only; 0 in production)
+};
+
+template <int U, int EPI, bool DWL>
+__global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArgs A) {
+  const XbArgs &a = A.b;
+  __shared__ __attribute__((aligned(16))) char lds[kBsLds];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int gl = lane & 31, grp = lane >> 5;
+  const int l16 = lane & 15, g4 = lane >> 4;
+  int *ctr = reinterpret_cast<int *>(lds + kBsCtrOff);
+  int *filled = ctr, *mdone = ctr + 2, *freed = ctr + 4, *xdone = ctr + 6, *abort_word = ctr + 8;
+  if (tid < 16) ctr[tid] = 0;
+  __syncthreads();
+
+  const int64_t n_chunks = (a.n_rows + kXwRows - 1) / kXwRows;
+  const int64_t n_my = my_chunks(n_chunks);
+  auto chunk_of = [&](int64_t i) { return (int64_t)blockIdx.x + i * gridDim.x; };
+  auto rows_in = [&](int64_t c) -> uint32_t {
+    const int64_t r = a.n_rows - c * kXwRows;
+    return (uint32_t)(r <= 0 ? 0 : r >= kXwRows ? kXwRows : r);
+  };
+
+  float cs[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // MFMA waves: column sums of their 4 columns
+  f32x16 accw[2];                          // MFMA waves (DWL): two 32 x 32 dWl tiles
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) accw[s][r] = 0.0f;
+
+  if (wave < kBsNG) {
+    // ------------------------------- gather waves ---------------------------
+    // the wave's k-th quad is q = wave + 8 k: chunk q >> 3, rows
+    // 4 (q & 7) + grp and 4 (q & 7) + 2 + grp for lane group grp
+    const int64_t n_quads = 8 * n_my;
+    auto row_of = [&](int64_t k, int second) -> int64_t {
+      const int64_t q = wave + kBsNG * k;
+      return chunk_of(q >> 3) * kXwRows + 4 * (q & 7) + 2 * second + grp;
+    };
+    const auto rdy = buf_rsrc(a.dY, (uint32_t)(a.n_cols * a.lddy * 4));
+    const uint32_t ldy_b = (uint32_t)a.lddy * 4u;
+    RowMeta cur[2] = {}, nxt[2] = {};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      meta_rowptr(a.rowptr, row_of(0, j), row_of(0, j) < a.n_rows && wave < n_quads, cur[j]);
+      meta_first(a.col, a.w, gl, cur[j]);
+      meta_rowptr(a.rowptr, row_of(1, j), row_of(1, j) < a.n_rows && wave + kBsNG < n_quads,
+                  nxt[j]);
+    }
+    int64_t k = 0;
+    for (int64_t q = wave; q < n_quads; q += kBsNG, ++k) {
+      RowMeta nn[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        meta_first(a.col, a.w, gl, nxt[j]);
+        const int64_t r2 = row_of(k + 2, j);
+        meta_rowptr(a.rowptr, r2, r2 < a.n_rows && q + 2 * kBsNG < n_quads, nn[j]);
+      }
+      const int64_t i = q >> 3;
+      const int64_t c = chunk_of(i);
+      const int64_t r0 = c * kXwRows;
+      const int lr0 = 4 * (int)(q & 7) + grp;
+      u32x4 zv[2] = {};
+      if (DWL && !(A.dbg & 4)) {  // the rows' Zl, under the gathers (streamed once)
+        const auto rz = buf_rsrc(A.Zl + r0 * A.ldz, rows_in(c) * (uint32_t)A.ldz * 4u);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          zv[j] = __builtin_amdgcn_raw_buffer_load_b128(
+              rz, 4 * (int)((lr0 + 2 * j) * A.ldz + 4 * gl), 0, MGCN_NT_AUX);
+      }
+      float acc[2][4];
+      gather_row2_meta<U>(rdy, ldy_b, a.col, a.w, cur[0], cur[1], gl, grp, acc[0], acc[1]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int64_t row = r0 + lr0 + 2 * j;
+        if (a.row_scale != nullptr && row < a.n_rows) {
+          const float sc = a.row_scale[row];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) acc[j][t] = __fmul_rn(acc[j][t], sc);
+        }
+      }
+      const int b = (int)(i & 1);
+      const int gen = (int)(i >> 1);
+      if (!bs_wait_ge(freed + b, gen, abort_word)) break;
+      char *buf = lds + b * kBsRingBuf;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        store_row_terms(buf, lr0 + 2 * j, gl, acc[j]);
+        if constexpr (DWL) {
+          const float4 zf = __builtin_bit_cast(float4, zv[j]);
+          const float zz[4] = {zf.x, zf.y, zf.z, zf.w};
+          store_row_terms(buf + kBsImgSet, lr0 + 2 * j, gl, zz);
+        }
+      }
+      bs_signal(filled + b, 4, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        cur[j] = nxt[j];
+        nxt[j] = nn[j];
+      }
+    }
+  } else {
+    // -------------------------------- MFMA waves ----------------------------
+    const int m = wave - kBsNG;  // dX columns 16 m .. 16 m + 15
+    // W^T fragments: A[c][k] = W[16 m + c][32 ks + 8 g4 + j] -- held for the
+    // launch (48 VGPRs) in the dX-only form; with the dWl accumulators (32)
+    // re-read from L2 and split per chunk instead (the MFMA waves have slack:
+    // ~3 k of ~19 k cycles per chunk)
+    const float *wp = a.W + (int64_t)(16 * m + l16) * a.ldw + 8 * g4;
+    constexpr bool kHoldW = !DWL || MGCN_BS_HOLDW;
+    bf16x8 wt[kHoldW ? 4 : 1][3];
+    if constexpr (kHoldW) {
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const float4 w0 = *reinterpret_cast<const float4 *>(wp + 32 * ks);
+        const float4 w1 = *reinterpret_cast<const float4 *>(wp + 32 * ks + 4);
+        const float v[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+        split3_bf16(v, wt[ks][0], wt[ks][1], wt[ks][2]);
+      }
+    }
+    // dWl tiles (gemm_bwd's mapping): rows 32 ti, columns 32 (tj0 + s)
+    const int h = lane >> 5, q = (lane >> 2) & 3, p4 = lane & 3;
+    auto frag_off = [&](int col0, int second) {
+      return img_off(8 * h + q + 4 * second, (col0 >> 3) + 2 * (g4 & 1) + (p4 >> 1)) + 8 * (p4 & 1);
+    };
+    const int ti = m >> 1, tj0 = 2 * (m & 1);
+    int offa[2], offb[2][2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      offa[r] = frag_off(32 * ti, r);
+      offb[0][r] = frag_off(32 * tj0, r);
+      offb[1][r] = frag_off(32 * (tj0 + 1), r);
+    }
+    auto read8 = [&](const char *base, const int (&o)[2]) {
+      const v4i16 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16_t *)(base + o[0]));
+      const v4i16 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16_t *)(base + o[1]));
+      const short y[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+      return __builtin_bit_cast(bf16x8, y);
+    };
+    const int bit = 4 * m + g4;  // mask bit of this lane's columns (word r: column 16 m + 4 g4 + r)
+    for (int64_t i = 0; i < n_my; ++i) {
+      const int b = (int)(i & 1);
+      const int gen = (int)(i >> 1);
+      const int64_t c = chunk_of(i);
+      const int64_t r0 = c * kXwRows;
+      const uint32_t rv = rows_in(c);
+      u32x4 mk[2] = {};
+      float dv[2] = {1.0f, 1.0f};
+      if constexpr (EPI != EPI_STORE) {
+        const auto rm = buf_rsrc(a.relu_mask + r0 * 4, rv * 16u);
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+          mk[rt] = __builtin_amdgcn_raw_buffer_load_b128(rm, 16 * (16 * rt + l16), 0, 0);
+        if constexpr (EPI == EPI_RELU_DIV) {
+          const auto rd = buf_rsrc(a.row_div + r0, rv * 4u);
+#pragma unroll
+          for (int rt = 0; rt < 2; ++rt)
+            dv[rt] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rd, 4 * (16 * rt + l16), 0, 0));
+        }
+      }
+      if (!bs_wait_ge(filled + b, kXwRows * (gen + 1), abort_word)) break;
+      if constexpr (EPI == EPI_RELU_DIV) {
+        // rows past the end read divisor 0: make it 1, so their zero rows stay
+        // 0 (not 0 / 0) in the dX images dWl reads
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+          if ((uint32_t)(16 * rt + l16) >= rv) dv[rt] = 1.0f;
+      }
+      const char *buf = lds + b * kBsRingBuf;
+      char *ximg = lds + kBsXOff + (int)(i & 1) * kBsImgSet;
+      const auto rx = buf_rsrc(a.dX + r0 * a.lddx, rv * (uint32_t)a.lddx * 4u);
+      f32x4_t acc2[2];
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc2[rt][r] = 0.0f;
+      float4 wn0{}, wn1{};
+      if constexpr (!kHoldW) {
+        wn0 = *reinterpret_cast<const float4 *>(wp);
+        wn1 = *reinterpret_cast<const float4 *>(wp + 4);
+      }
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        bf16x8 wk[3];
+        if constexpr (!kHoldW) {
+          const float v8[8] = {wn0.x, wn0.y, wn0.z, wn0.w, wn1.x, wn1.y, wn1.z, wn1.w};
+          if (ks + 1 < 4) {
+            wn0 = *reinterpret_cast<const float4 *>(wp + 32 * (ks + 1));
+            wn1 = *reinterpret_cast<const float4 *>(wp + 32 * (ks + 1) + 4);
+          }
+          split3_bf16(v8, wk[0], wk[1], wk[2]);
+        } else {
+#pragma unroll
+          for (int t = 0; t < 3; ++t) wk[t] = wt[ks][t];
+        }
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) {
+          const int off = img_off(16 * rt + l16, 4 * ks + g4);
+          const bf16x8 xh = *reinterpret_cast<const bf16x8 *>(buf + off);
+          const bf16x8 xm = *reinterpret_cast<const bf16x8 *>(buf + kXwImg + off);
+          const bf16x8 xl = *reinterpret_cast<const bf16x8 *>(buf + 2 * kXwImg + off);
+          acc2[rt] = mfma16_x6_at(wk, xh, xm, xl, acc2[rt]);
+        }
+      }
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+        const int row = 16 * rt + l16;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = acc2[rt][r];
+          if constexpr (EPI != EPI_STORE) {
+            v[r] = ((mk[rt][r] >> bit) & 1u) ? v[r] : 0.0f;
+            cs[r] = __fadd_rn(cs[r], v[r]);  // rows past the end: zero mask words
+            if constexpr (EPI == EPI_RELU_DIV) v[r] = __fdiv_rn(v[r], dv[rt]);
+          }
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(u32x4, make_float4(v[0], v[1], v[2], v[3])), rx,
+            4 * (int)(row * a.lddx + 16 * m + 4 * g4), 0, MGCN_NT_OUT);
+        if constexpr (DWL) store_row_terms(ximg, row, 4 * m + g4, v);
+      }
+      if (DWL && !(A.dbg & 1)) {
+        // every wave's 16 columns of the chunk's dX images are in
+        bs_signal(xdone + (int)(i & 1), 1, lane);
+        if (!bs_wait_ge(xdone + (int)(i & 1), kBsNM * (gen + 1), abort_word)) break;
+        if (!(A.dbg & 2)) {
+        const char *zimg = buf + kBsImgSet;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const char *za = zimg + ks * 16 * 256;
+          const char *xb = ximg + ks * 16 * 256;
+          bf16x8 fa[3];
+#pragma unroll
+          for (int t = 0; t < 3; ++t) fa[t] = read8(za + t * kXwImg, offa);
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            bf16x8 fb[3];
+#pragma unroll
+            for (int t = 0; t < 3; ++t) fb[t] = read8(xb + t * kXwImg, offb[s2]);
+            accw[s2] = mfma_x6(fa[0], fa[1], fa[2], fb[0], fb[1], fb[2], accw[s2]);
+          }
+        }
+        }
+      }
+      const int old = bs_signal(mdone + b, 1, lane);
+      if (old == kBsNM * gen + kBsNM - 1) bs_signal(freed + b, 1, lane);
+    }
+  }
+  __syncthreads();
+  if (wave >= kBsNG) {
+    const int m = wave - kBsNG;
+    if constexpr (DWL) {
+      const int h = lane >> 5, lc = lane & 31;
+      const int ti = m >> 1, tj0 = 2 * (m & 1);
+      float *slab = A.dwl_partial + (int64_t)blockIdx.x * kXwF * kXwF;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = 32 * ti + (r & 3) + 8 * (r >> 2) + 4 * h;
+          slab[row * kXwF + 32 * (tj0 + s2) + lc] = accw[s2][r];
+        }
+    }
+    if constexpr (EPI != EPI_STORE) {
+      float *red = reinterpret_cast<float *>(lds);  // [16 row lanes][128]
+      *reinterpret_cast<float4 *>(red + l16 * kXwF + 16 * m + 4 * g4) =
+          make_float4(cs[0], cs[1], cs[2], cs[3]);
+    }
+  }
+  if constexpr (EPI != EPI_STORE) {
+    __syncthreads();
+    if (tid < kXwF) {
+      const float *red = reinterpret_cast<const float *>(lds);
+      float s = 0.0f;
+#pragma unroll
+      for (int l = 0; l < 16; ++l) s = __fadd_rn(s, red[l * kXwF + tid]);
+      a.colsum_partial[(int64_t)blockIdx.x * kXwF + tid] = s;
+    }
+  }
+}
+
+int g_xw_ws = 0;  // mgcn_set_option("xw_ws"): the warp-specialised dX-only adjoint
+
+int bs_grid() {
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 256;
+  return cus;  // one workgroup per CU
+}
+
+template <int U, bool DWL>
+int launch_bs_u(const XbsArgs &a, int epi, int grid, hipStream_t s) {
+  if (epi == EPI_RELU_DIV)
+    hipLaunchKernelGGL((spmm_xw_bwd_ws_kernel<U, EPI_RELU_DIV, DWL>), dim3(grid), dim3(kBsThreads),
+                       0, s, a);
+  else if (epi == EPI_RELU)
+    hipLaunchKernelGGL((spmm_xw_bwd_ws_kernel<U, EPI_RELU, DWL>), dim3(grid), dim3(kBsThreads), 0,
+                       s, a);
+  else
+    hipLaunchKernelGGL((spmm_xw_bwd_ws_kernel<U, EPI_STORE, DWL>), dim3(grid), dim3(kBsThreads), 0,
+                       s, a);
+  return check_launch("spmm_xw_bwd_ws_kernel");
+}
+
+int g_bs_unroll = 4;
+// mgcn_set_option("xw_ws_dbg"): timing experiments (dWl WRONG when set): bit 0
+// skip the dW phase and its sync, bit 1 skip the dW products, bit 2 skip Zl loads
+int g_bs_dbg = 0;  // mgcn_set_option("xw_ws_unroll"): gathers in flight per row (4 / 8)
+
+template <bool DWL>
+int launch_bs(const XbsArgs &a, int epi, int grid, hipStream_t s) {
+  return g_bs_unroll == 4 ? launch_bs_u<4, DWL>(a, epi, grid, s) : launch_bs_u<8, DWL>(a, epi, grid, s);
+}
+
 }  // namespace
+
+int xw_set_ws(const char *name, int value) {
+  if (name[6] == 'd') {  // "xw_ws_dbg"
+    g_bs_dbg = value;
+    return MGCN_OK;
+  }
+  if (name[6] == 'u') {  // "xw_ws_unroll"
+    if (value != 4 && value != 8) {
+      set_error("xw_ws_unroll must be 4 or 8");
+      return MGCN_EINVAL;
+    }
+    g_bs_unroll = value;
+    return MGCN_OK;
+  }
+  if (value < 0 || value > 1) {
+    set_error("xw_ws must be 0 or 1");
+    return MGCN_EINVAL;
+  }
+  g_xw_ws = value;
+  return MGCN_OK;
+}
 
 int xw_set_unroll(int value) {
   if (value != 4 && value != 8) {
@@ -1028,6 +1524,14 @@ extern "C" int mgcn_spmm_xw_bwd(int64_t n_rows, int64_t n_cols, int32_t F_in, in
   a.colsum_partial = reinterpret_cast<float *>(static_cast<char *>(workspace) +
                                                align_up((size_t)xw_grid() * kXwF * kXwF * 4, 256));
   int rc;
+  if (dx_only && g_xw_ws) {  // the warp-specialised form (one workgroup per CU)
+    XbsArgs sa{};
+    sa.b = a;
+    const int64_t g = bs_grid() < n_chunks ? bs_grid() : n_chunks;
+    rc = launch_bs<false>(sa, epi, (int)g, s);
+    if (rc || epi == EPI_STORE) return rc;
+    return launch_fold(a.colsum_partial, g, kXwF, kXwF, colsum, kXwF, accumulate, s);
+  }
   if (dx_only) {
     rc = g_xw_unroll == 4 ? launch_xb_dx<4>(a, epi, grid, s) : launch_xb_dx<8>(a, epi, grid, s);
     if (rc || epi == EPI_STORE) return rc;
@@ -1049,3 +1553,83 @@ extern "C" int mgcn_debug_xw_prof(unsigned long long *host) {
   return MGCN_OK;
 }
 #endif
+
+extern "C" size_t mgcn_spmm_xw_bwd_dwl_workspace_bytes(int64_t n_rows) {
+  return mgcn_spmm_xw_bwd_workspace_bytes(n_rows, kXwF, kXwF);
+}
+
+extern "C" int mgcn_spmm_xw_bwd_dwl(int64_t n_rows, int64_t n_cols, const int64_t *rowptr_t,
+                                    const int32_t *col_t, const float *w_t, const float *row_scale,
+                                    const float *dY, int64_t lddy, const float *W, int64_t ldw,
+                                    float *dX, int64_t lddx, const uint32_t *relu_mask,
+                                    const float *row_div, float *colsum, int accumulate_colsum,
+                                    const float *Zl, int64_t ldz, float *dWl, int64_t lddw,
+                                    int accumulate_dw, void *workspace, size_t workspace_bytes,
+                                    void *stream) {
+  clear_error();
+  MGCN_REQUIRE(n_rows >= 0, "mgcn_spmm_xw_bwd_dwl: negative size");
+  MGCN_REQUIRE(gemm_precision_is_x6(), "mgcn_spmm_xw_bwd_dwl: needs the bf16x6 products");
+  MGCN_REQUIRE(dWl != nullptr && lddw >= kXwF, "mgcn_spmm_xw_bwd_dwl: bad dWl");
+  MGCN_REQUIRE(row_div == nullptr || relu_mask != nullptr,
+               "mgcn_spmm_xw_bwd_dwl: row_div needs relu_mask");
+  MGCN_REQUIRE(relu_mask == nullptr || colsum != nullptr,
+               "mgcn_spmm_xw_bwd_dwl: relu_mask needs colsum");
+  hipStream_t s = as_stream(stream);
+  if (n_rows == 0) {  // no rows: dWl (and the column sums) are zero contributions
+    if (!accumulate_dw)
+      for (int32_t r = 0; r < kXwF; ++r)
+        MGCN_HIP_TRY(hipMemsetAsync(dWl + r * lddw, 0, sizeof(float) * kXwF, s));
+    if (colsum && !accumulate_colsum) MGCN_HIP_TRY(hipMemsetAsync(colsum, 0, sizeof(float) * kXwF, s));
+    return MGCN_OK;
+  }
+  MGCN_REQUIRE(rowptr_t && dY && W && dX && Zl, "mgcn_spmm_xw_bwd_dwl: null array");
+  MGCN_REQUIRE(lddy >= kXwF && lddy % 4 == 0 && reinterpret_cast<uintptr_t>(dY) % 16 == 0,
+               "mgcn_spmm_xw_bwd_dwl: dY must have 16-byte aligned rows");
+  MGCN_REQUIRE(n_cols > 0 && (uint64_t)n_cols * (uint64_t)lddy * 4u <= 0xfffffff0ull,
+               "mgcn_spmm_xw_bwd_dwl: dY must hold 1 .. 4 GiB - 1 bytes (32-bit gather offsets)");
+  MGCN_REQUIRE(ldw >= kXwF && lddx >= kXwF && lddx % 4 == 0 &&
+                   reinterpret_cast<uintptr_t>(dX) % 16 == 0,
+               "mgcn_spmm_xw_bwd_dwl: bad W / dX (16-byte aligned dX rows)");
+  MGCN_REQUIRE(ldz >= kXwF && ldz % 4 == 0 && reinterpret_cast<uintptr_t>(Zl) % 16 == 0,
+               "mgcn_spmm_xw_bwd_dwl: Zl must have 16-byte aligned rows");
+  MGCN_REQUIRE((uint64_t)kXwRows * (uint64_t)(ldz > lddx ? ldz : lddx) * 4u < (1ull << 31),
+               "mgcn_spmm_xw_bwd_dwl: leading dimension too large");
+  MGCN_REQUIRE(relu_mask == nullptr || reinterpret_cast<uintptr_t>(relu_mask) % 16 == 0,
+               "mgcn_spmm_xw_bwd_dwl: relu_mask not 16-byte aligned");
+  const size_t need = mgcn_spmm_xw_bwd_dwl_workspace_bytes(n_rows);
+  if (workspace == nullptr || workspace_bytes < need) {
+    set_error("mgcn_spmm_xw_bwd_dwl: workspace %zu < %zu", workspace_bytes, need);
+    return MGCN_EWORKSPACE;
+  }
+  const int64_t n_chunks = (n_rows + kXwRows - 1) / kXwRows;
+  const int64_t g = bs_grid() < n_chunks ? bs_grid() : n_chunks;
+  XbsArgs sa{};
+  XbArgs &a = sa.b;
+  a.n_rows = n_rows;
+  a.rowptr = rowptr_t;
+  a.col = col_t;
+  a.w = w_t;
+  a.row_scale = row_scale;
+  a.dY = dY;
+  a.lddy = lddy;
+  a.n_cols = n_cols;
+  a.W = W;
+  a.ldw = ldw;
+  a.dX = dX;
+  a.lddx = lddx;
+  a.relu_mask = relu_mask;
+  a.row_div = row_div;
+  sa.Zl = Zl;
+  sa.ldz = ldz;
+  sa.dwl_partial = static_cast<float *>(workspace);
+  sa.dbg = g_bs_dbg;
+  a.colsum_partial = reinterpret_cast<float *>(
+      static_cast<char *>(workspace) + align_up((size_t)g * kXwF * kXwF * 4, 256));
+  const int epi = relu_mask == nullptr ? EPI_STORE : row_div != nullptr ? EPI_RELU_DIV : EPI_RELU;
+  int rc = launch_bs<true>(sa, epi, (int)g, s);
+  if (rc) return rc;
+  rc = launch_split_reduce(sa.dwl_partial, (int)g, (int64_t)kXwF * kXwF, kXwF, dWl, lddw,
+                           accumulate_dw, s);
+  if (rc || epi == EPI_STORE) return rc;
+  return launch_fold(a.colsum_partial, g, kXwF, kXwF, colsum, kXwF, accumulate_colsum, s);
+}

@@ -643,6 +643,7 @@ bool tn_lds(int M, int N) { return M % kTile == 0 && N % kTile == 0; }
 // K = 1M, M = N = 128: 0.321 / 0.335 / 0.337 ms): 0 = BK 64, one workgroup
 // per CU; 1 = BK 32, two; 2 = BK 16, three
 int g_tn_lds_variant = 0;
+int g_dw_ws = 0;  // mgcn_set_option("dw_ws"): gemm_dw_ws_kernel for mgcn_gemm_bwd's dW-only form
 int g_tn_staged = 1;  // M = 32, N = 32 / 64: gemm_tn_staged_kernel (0: gemm_tn_small_kernel)
 int tn_lds_wgs() { return g_tn_lds_variant == 1 ? 2 : g_tn_lds_variant == 2 ? 3 : 1; }
 
@@ -670,6 +671,12 @@ int gemm_splits(int64_t K, int M, int N) {
 int gemm_set_tn_variant(int value) {
   if (value < 0 || value > 2) return MGCN_EINVAL;
   g_tn_lds_variant = value;
+  return MGCN_OK;
+}
+
+int gemm_set_dw_ws(int value) {
+  if (value < 0 || value > 1) return MGCN_EINVAL;
+  g_dw_ws = value;
   return MGCN_OK;
 }
 
@@ -1887,6 +1894,205 @@ int launch_bwd(int grid, const float *X, int64_t ldx, const float *dH, int64_t l
   return check_launch("gemm_bwd_kernel");
 }
 
+// ----------------------------------------------------------------------------
+// dW-only pass (dW = X^T dH, optionally dH's column sums), warp-specialised
+// (round 5): gemm_bwd_kernel<.., false> serialises per chunk its loads'
+// arrival, the split VALU, the LDS writes, a barrier and the MFMAs of two
+// waves per SIMD (measured 4.3 k cycles per 32-row chunk against ~2.5 k of
+// HBM time).  Here one 1024-thread workgroup per CU: 8 LOADER waves stream
+// the chunks (two register banks ahead), split them into the three bf16 term
+// images and add the dH column sums; 8 MFMA waves take the images from a
+// ring of three 48-KB buffers (LDS counters, bounded spins -- fused.hip's
+// hand-off) and run gemm_bwd's 32x32 dW tiles.  Same products in the same
+// k-step order per workgroup as gemm_bwd_kernel; the chunk-to-workgroup map,
+// hence the split-K partials, is the same too (grid = kBwGrid).
+constexpr int kDwBuf = 6 * kBwImg;   // one chunk: X and dH, three terms each (48 KB)
+constexpr int kDwRing = 3;
+constexpr int kDwCtrOff = kDwRing * kDwBuf;
+constexpr int kDwLds = kDwCtrOff + 64;
+static_assert(kDwLds <= 160 * 1024, "one dW workgroup per CU");
+constexpr uint32_t kDwSpinLimit = 1u << 25;
+
+__device__ __forceinline__ int dw_lds_load(const int *p) {
+  return __builtin_amdgcn_readfirstlane(
+      __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+
+__device__ __forceinline__ bool dw_wait_ge(const int *p, int target, int *abort_word) {
+  for (uint32_t n = 0;; ++n) {
+    if (dw_lds_load(p) >= target) break;
+    if (dw_lds_load(abort_word) != 0) return false;
+    if (n >= kDwSpinLimit) {
+      __hip_atomic_store(abort_word, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  asm volatile("" ::: "memory");
+  return true;
+}
+
+__device__ __forceinline__ int dw_signal(int *p, int v, int lane) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  int old = 0;
+  if (lane == 0) old = __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  return __builtin_amdgcn_readfirstlane(old);
+}
+
+template <bool HCS>
+__global__ __launch_bounds__(1024) void gemm_dw_ws_kernel(
+    const float *__restrict__ X, int64_t ldx, const float *__restrict__ dH, int64_t lddh,
+    int64_t M, float *__restrict__ dw_partial, float *__restrict__ colsum_partial) {
+  __shared__ __attribute__((aligned(16))) char lds[kDwLds];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5, lc = lane & 31;
+  const int g4 = lane >> 4;
+  int *ctr = reinterpret_cast<int *>(lds + kDwCtrOff);
+  int *filled = ctr, *mdone = ctr + 3, *freed = ctr + 6, *abort_word = ctr + 9;
+  if (tid < 16) ctr[tid] = 0;
+  __syncthreads();
+  const int64_t n_chunks = (M + kBwRows - 1) / kBwRows;
+  const int64_t G = gridDim.x;
+  const int n_my = blockIdx.x < n_chunks ? (int)((n_chunks - 1 - blockIdx.x) / G) + 1 : 0;
+  auto rows_in = [&](int64_t chunk) -> uint32_t {
+    const int64_t r = M - chunk * kBwRows;
+    return (uint32_t)(r <= 0 ? 0 : r >= kBwRows ? kBwRows : r);
+  };
+  float hc[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // loaders (HCS): dH column sums of float4 t & 31
+  f32x16 accw[2];                          // MFMA waves
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) accw[s2][r] = 0.0f;
+  const int t = tid & 511;  // loader thread index (loaders are threads 0 .. 511)
+
+  if (wave < 8) {
+    // ------------------------------- loader waves ---------------------------
+    // thread t: float4 t & 31 of rows t >> 5 and 16 + (t >> 5), of X and dH
+    const int ld_off_x = 4 * (int)((t >> 5) * ldx + 4 * (t & 31));
+    const int ld_off_h = 4 * (int)((t >> 5) * lddh + 4 * (t & 31));
+    struct Bank {
+      u32x4 v[4];
+    };
+    auto load = [&](int i, Bank &b) {  // chunk i of this workgroup (past the end: zeros)
+      const int64_t chunk = blockIdx.x + (int64_t)i * G;
+      const int64_t r0 = chunk * kBwRows;
+      const uint32_t rv = i < n_my ? rows_in(chunk) : 0u;
+      const auto rx = buf_rsrc(X + (i < n_my ? r0 * ldx : 0), rv * (uint32_t)ldx * 4u);
+      const auto rh = buf_rsrc(dH + (i < n_my ? r0 * lddh : 0), rv * (uint32_t)lddh * 4u);
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        b.v[m] = __builtin_amdgcn_raw_buffer_load_b128(rx, ld_off_x + m * 64 * (int)ldx, 0,
+                                                       MGCN_NT_AUX);
+        b.v[2 + m] = __builtin_amdgcn_raw_buffer_load_b128(rh, ld_off_h + m * 64 * (int)lddh, 0, 0);
+      }
+    };
+    Bank bk[2];
+    load(0, bk[0]);
+    load(1, bk[1]);
+    for (int i = 0; i < n_my; i += 2) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int ii = i + j;
+        if (ii >= n_my) break;
+        const int b = ii % kDwRing, gen = ii / kDwRing;
+        if (!dw_wait_ge(freed + b, gen, abort_word)) goto loaders_done;
+        char *buf = lds + b * kDwBuf;
+        const int c4 = t & 31;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const int row = 16 * (m & 1) + (t >> 5);
+          const int off = img_off(row, c4 >> 1) + 8 * (c4 & 1);
+          const float4 v = __builtin_bit_cast(float4, bk[j].v[m]);
+          if constexpr (HCS) {
+            if (m >= 2) {  // rows q then 16 + q of every chunk: a fixed order
+              hc[0] = __fadd_rn(hc[0], v.x);
+              hc[1] = __fadd_rn(hc[1], v.y);
+              hc[2] = __fadd_rn(hc[2], v.z);
+              hc[3] = __fadd_rn(hc[3], v.w);
+            }
+          }
+          uint32_t hi[2], mid[2], lo[2];
+          split3_pair(f32x2{v.x, v.y}, hi[0], mid[0], lo[0]);
+          split3_pair(f32x2{v.z, v.w}, hi[1], mid[1], lo[1]);
+          char *img = buf + (m >> 1) * 3 * kBwImg + off;
+          *reinterpret_cast<uint2 *>(img) = make_uint2(hi[0], hi[1]);
+          *reinterpret_cast<uint2 *>(img + kBwImg) = make_uint2(mid[0], mid[1]);
+          *reinterpret_cast<uint2 *>(img + 2 * kBwImg) = make_uint2(lo[0], lo[1]);
+        }
+        load(ii + 2, bk[j]);  // the bank is free: two chunks ahead
+        dw_signal(filled + b, 1, lane);
+      }
+    }
+  loaders_done:;
+  } else {
+    // -------------------------------- MFMA waves ----------------------------
+    const int m = wave - 8;
+    const int q = (lane >> 2) & 3, p = lane & 3;
+    auto frag_off = [&](int col0, int second) {
+      return img_off(8 * h + q + 4 * second, (col0 >> 3) + 2 * (g4 & 1) + (p >> 1)) + 8 * (p & 1);
+    };
+    const int ti = m >> 1, tj0 = 2 * (m & 1);
+    int offa[2], offb[2][2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      offa[r] = frag_off(32 * ti, r);
+      offb[0][r] = 3 * kBwImg + frag_off(32 * tj0, r);
+      offb[1][r] = 3 * kBwImg + frag_off(32 * (tj0 + 1), r);
+    }
+    auto read8 = [&](const char *base, const int (&o)[2]) {
+      const v4i16 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16_t *)(base + o[0]));
+      const v4i16 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16_t *)(base + o[1]));
+      const short y[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+      return __builtin_bit_cast(bf16x8, y);
+    };
+    for (int i = 0; i < n_my; ++i) {
+      const int b = i % kDwRing, gen = i / kDwRing;
+      if (!dw_wait_ge(filled + b, 8 * (gen + 1), abort_word)) break;
+      const char *buf = lds + b * kDwBuf;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const char *kb = buf + ks * 16 * 256;
+        bf16x8 fa[3], fb[2][3];
+#pragma unroll
+        for (int tt = 0; tt < 3; ++tt) {
+          fa[tt] = read8(kb + tt * kBwImg, offa);
+          fb[0][tt] = read8(kb + tt * kBwImg, offb[0]);
+          fb[1][tt] = read8(kb + tt * kBwImg, offb[1]);
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+          accw[s2] = mfma_x6(fa[0], fa[1], fa[2], fb[s2][0], fb[s2][1], fb[s2][2], accw[s2]);
+      }
+      const int old = dw_signal(mdone + b, 1, lane);
+      if (old == 8 * gen + 7) dw_signal(freed + b, 1, lane);
+    }
+    float *slab = dw_partial + (int64_t)blockIdx.x * kBwF * kBwF;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = 32 * ti + (r & 3) + 8 * (r >> 2) + 4 * h;
+        slab[row * kBwF + 32 * (tj0 + s2) + lc] = accw[s2][r];
+      }
+  }
+  if constexpr (HCS) {
+    // fold the 16 row groups (t >> 5) of each column in fixed order
+    __syncthreads();
+    float *red = reinterpret_cast<float *>(lds);
+    if (wave < 8) *reinterpret_cast<float4 *>(red + 4 * t) = make_float4(hc[0], hc[1], hc[2], hc[3]);
+    __syncthreads();
+    if (tid < kBwF) {
+      float c = 0.0f;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) c = __fadd_rn(c, red[4 * (32 * g + (tid >> 2)) + (tid & 3)]);
+      colsum_partial[(int64_t)blockIdx.x * kBwF + tid] = c;
+    }
+  }
+}
+
 }  // namespace
 }  // namespace mgcn
 
@@ -1940,7 +2146,15 @@ extern "C" int mgcn_gemm_bwd(int64_t M, int32_t F_in, int32_t F_out, const float
   const int64_t n_chunks = (M + kBwRows - 1) / kBwRows;
   const int grid = (int)(n_chunks < kBwGrid ? n_chunks : kBwGrid);
   int rc;
-  if (dX == nullptr && hcs)
+  if (dX == nullptr && g_dw_ws) {
+    if (hcs)
+      hipLaunchKernelGGL((gemm_dw_ws_kernel<true>), dim3(grid), dim3(1024), 0, s, X, ldx, dH, lddh,
+                         M, dwp, csp);
+    else
+      hipLaunchKernelGGL((gemm_dw_ws_kernel<false>), dim3(grid), dim3(1024), 0, s, X, ldx, dH,
+                         lddh, M, dwp, csp);
+    rc = check_launch("gemm_dw_ws_kernel");
+  } else if (dX == nullptr && hcs)
     rc = launch_bwd<EPI_STORE, false, true>(grid, X, ldx, dH, lddh, W, ldw, M, dX, lddx,
                                             relu_mask, row_div, dwp, csp, s);
   else if (dX == nullptr)

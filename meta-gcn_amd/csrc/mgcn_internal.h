@@ -59,9 +59,11 @@ inline unsigned grid_for(int64_t work_items, int block) {
 // mgcn_set_option("gemm_tn_variant") -> gemm.hip
 int gemm_set_tn_variant(int value);
 int gemm_set_tn_staged(int value);  // mgcn_set_option("gemm_tn_staged")
+int gemm_set_dw_ws(int value);      // mgcn_set_option("dw_ws")
 int gemm_set_precision(int value);
 int gemm_precision_is_x6();  // 1 under bf16x6 (the fused kernels need it)
 int xw_set_unroll(int value);  // fused.hip
+int xw_set_ws(const char *name, int value);  // fused.hip: "xw_ws" / "xw_ws_unroll"
 extern int g_fused_mask;       // residual.hip: the stack's fused lower-layer mask pass
 extern int g_rl_cap;           // residual.hip: workgroups per light-row launch (grid-stride beyond)
 // deterministic folds of per-workgroup partials (gemm.hip)

@@ -779,6 +779,10 @@ extern "C" int mgcn_set_option(const char *name, int value) {
     MGCN_REQUIRE(value >= 0 && value <= 2, "gemm_tn_variant must be 0, 1 or 2");
     return gemm_set_tn_variant(value);
   }
+  if (n == "dw_ws") {
+    MGCN_REQUIRE(value == 0 || value == 1, "dw_ws must be 0 or 1");
+    return gemm_set_dw_ws(value);
+  }
   if (n == "gemm_tn_staged") {
     MGCN_REQUIRE(value == 0 || value == 1, "gemm_tn_staged must be 0 or 1");
     return gemm_set_tn_staged(value);
@@ -788,7 +792,7 @@ extern "C" int mgcn_set_option(const char *name, int value) {
     return gemm_set_precision(value);
   }
   if (n == "spmm_xw_unroll") return xw_set_unroll(value);
-  if (n == "xw_ws" || n == "xw_ws_unroll") return xw_set_ws(name, value);
+  if (n == "xw_ws" || n == "xw_ws_unroll" || n == "xw_ws_dbg") return xw_set_ws(name, value);
   if (n == "wide_pair" || n == "wide_unroll" || n == "wide_ws" || n == "wide_dbg" || n == "wide_mfma") return wide_set_option(name, value);
   if (n == "residual_blocks") {
     MGCN_REQUIRE(value >= 64 && value <= 65536, "residual_blocks must be in [64, 65536]");

@@ -40,6 +40,12 @@ _FUSE_XW = os.environ.get("MGCN_FUSE_XW", "1") != "0"
 # the dW pass) and the bottom layer (no gather at all) take the Z form.
 # MGCN_Z_MIDDLE=1 sends the middle layers through Z as well.
 _Z_MIDDLE = os.environ.get("MGCN_Z_MIDDLE", "0") != "0"
+# The lower layer's dW = Z^T dY fused into the adjoint that writes that dY
+# (mgcn_spmm_xw_bwd_dwl; every layer below a fused one keeps its Z): env
+# MGCN_DWL=1 / set_fused_dwl(True).  Off by default: measured at config 2 the
+# fused launch costs 1.17 ms against 0.87 + 0.22 ms for the dX-only adjoint
+# and the separate dW pass.
+_DWL = os.environ.get("MGCN_DWL", "0") != "0"
 
 
 def set_fused_layers(enabled: bool) -> None:
@@ -55,6 +61,14 @@ def set_z_middle(enabled: bool) -> None:
     gather kernel (False, the default)."""
     global _Z_MIDDLE
     _Z_MIDDLE = bool(enabled)
+
+
+def set_fused_dwl(enabled: bool) -> None:
+    """Fuse the lower layer's dW = Z^T dY into the dX-only adjoint that
+    produces its dY (True; mgcn_spmm_xw_bwd_dwl) or run the separate dense dW
+    pass (False, the default: faster at config 2)."""
+    global _DWL
+    _DWL = bool(enabled)
 
 
 def set_kernel_timer(timer) -> None:
@@ -314,6 +328,84 @@ def spmm_xw_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tens
         _TIMER(tname, False)
     L.check(rc, "mgcn_spmm_xw_bwd")
     return dW, dX, colsum
+
+
+def spmm_xw_bwd_dwl_supported(F_in: int, F_out: int) -> bool:
+    """The dX-only adjoint with the lower layer's dW fused
+    (:func:`spmm_xw_bwd_dwl`): 128 x 128, bf16x6."""
+    return int(F_in) == 128 and int(F_out) == 128 and \
+        bool(L.load().mgcn_spmm_xw_bwd_full_supported(128, 128))
+
+
+def spmm_xw_bwd_dwl(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tensor | None,
+                    dY: torch.Tensor, W: torch.Tensor, Zl: torch.Tensor,
+                    relu_mask: torch.Tensor | None = None, row_div: torch.Tensor | None = None,
+                    dx_out: torch.Tensor | None = None, colsum_acc: torch.Tensor | None = None,
+                    dw_out: torch.Tensor | None = None, accumulate_dw: bool = False):
+    """Layer l's dX-only adjoint and layer l-1's weight gradient in one launch
+    (``mgcn_spmm_xw_bwd_dwl``): dX = relu'(lower) ((A^T dY [* row_scale])
+    W^T) [/ row_div] (bit for bit :func:`spmm_xw_bwd`'s dX-only form), the
+    lower layer's bias column sums (added into ``colsum_acc`` when given) and
+    dWl = Zl^T dX with Zl the lower layer's aggregate (:func:`spmm_xw_fwd`'s
+    Z) -- the reference's h^T (A^T dY_{l-1}) (gcn_base_models.py:201-241).
+    Returns (dX, colsum or None, dWl)."""
+    lib = L.load()
+    dY = _contig_f32(dY, "dY")
+    if dY.stride(0) % 4 or dY.data_ptr() % 16:
+        dY = dY.contiguous()
+    Zl = _contig_f32(Zl, "Zl")
+    if Zl.stride(0) % 4 or Zl.data_ptr() % 16:
+        Zl = Zl.contiguous()
+    W = W.detach()
+    if W.dtype != torch.float32 or W.stride(1) != 1:
+        W = W.to(torch.float32).contiguous()
+    dev = L.require_device(dY, W, Zl, view_t.rowptr, w_t, row_scale, relu_mask, row_div)
+    F_in, F_out = W.shape
+    M = view_t.n_rows
+    if not spmm_xw_bwd_dwl_supported(F_in, F_out):
+        raise ValueError(f"spmm_xw_bwd_dwl: unsupported W {tuple(W.shape)} (128 x 128, bf16x6)")
+    if dY.size(0) != view_t.n_cols or dY.size(1) != F_out or tuple(Zl.shape) != (M, F_in):
+        raise ValueError(f"spmm_xw_bwd_dwl: dY {tuple(dY.shape)}, Zl {tuple(Zl.shape)} do not fit "
+                         f"the graph ({M} sources, {view_t.n_cols} destinations)")
+    dX = dx_out if dx_out is not None else torch.empty(M, F_in, dtype=torch.float32, device=dev)
+    if (dX.dtype != torch.float32 or dX.dim() != 2 or tuple(dX.shape) != (M, F_in) or
+            dX.stride(1) != 1 or dX.stride(0) < F_in or dX.stride(0) % 4 or dX.data_ptr() % 16):
+        raise ValueError(f"spmm_xw_bwd_dwl: dx_out must be float32 [{M}, {F_in}], 16-byte rows")
+    dW = dw_out if dw_out is not None else torch.empty(F_in, F_in, dtype=torch.float32,
+                                                         device=dev)
+    if dW.dtype != torch.float32 or tuple(dW.shape) != (F_in, F_in) or dW.stride(1) != 1:
+        raise ValueError(f"spmm_xw_bwd_dwl: dw_out must be float32 [{F_in}, {F_in}]")
+    colsum = None
+    if relu_mask is not None:
+        if relu_mask.shape != (M, mask_words(F_in)) or relu_mask.dtype != torch.int32:
+            raise ValueError(f"spmm_xw_bwd_dwl: relu_mask must be int32 [{M}, {mask_words(F_in)}]")
+        relu_mask = relu_mask.contiguous()
+        if colsum_acc is not None:
+            if colsum_acc.dtype != torch.float32 or tuple(colsum_acc.shape) != (F_in,) or \
+                    not colsum_acc.is_contiguous():
+                raise ValueError(f"spmm_xw_bwd_dwl: colsum_acc must be a contiguous float32 [{F_in}]")
+            L.require_device(colsum_acc)
+            colsum = colsum_acc
+        else:
+            colsum = torch.empty(F_in, dtype=torch.float32, device=dev)
+    elif colsum_acc is not None or row_div is not None:
+        raise ValueError("spmm_xw_bwd_dwl: colsum_acc / row_div need relu_mask")
+    ws_bytes = int(lib.mgcn_spmm_xw_bwd_dwl_workspace_bytes(M))
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    if _TIMER is not None:
+        _TIMER("spmm_xw_bwd_dwl", True, view_t.n_rows, view_t.edges)
+    with L.device_guard(dev):
+        rc = lib.mgcn_spmm_xw_bwd_dwl(M, view_t.n_cols, L.ptr(view_t.rowptr), L.ptr(view_t.col),
+                                      L.ptr(w_t), L.ptr(row_scale), L.ptr(dY), dY.stride(0),
+                                      L.ptr(W), W.stride(0), L.ptr(dX), dX.stride(0),
+                                      L.ptr(relu_mask), L.ptr(row_div), L.ptr(colsum),
+                                      1 if colsum_acc is not None else 0, L.ptr(Zl), Zl.stride(0),
+                                      L.ptr(dW), dW.stride(0), 1 if accumulate_dw else 0,
+                                      L.ptr(ws), ws_bytes, L.stream_of(dev))
+    if _TIMER is not None:
+        _TIMER("spmm_xw_bwd_dwl", False)
+    L.check(rc, "mgcn_spmm_xw_bwd_dwl")
+    return dX, colsum, dW
 
 
 def spmm_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tensor | None,
@@ -963,8 +1055,12 @@ class _GCNStack(torch.autograd.Function):
                 # middle layers keep the dW + dX gather kernel (_Z_MIDDLE)
                 below = i == 0 or (relus[i - 1] and rmasks[i - 1] is not None)
                 middle = 0 < i < len(Ws) - 1 and relus[i - 1]
+                dwl_next = (_DWL and nxt is not None and relu and
+                            spmm_xw_bwd_dwl_supported(*W.shape) and
+                            spmm_xw_bwd_dwl_supported(*nxt.shape))
                 want_z = (bool(ctx.needs_input_grad[5 + 2 * i]) and below and
-                          (_Z_MIDDLE or not middle or not xw_full_supported(*W.shape)) and
+                          (_Z_MIDDLE or dwl_next or not middle or
+                           not xw_full_supported(*W.shape)) and
                           dw_pass_supported(W.size(0), W.size(1)) and
                           spmm_xw_supported(plan.bwd, W.size(1), W.size(0), L.REDUCE_SUM))
                 h, am = spmm_xw_fwd(plan.fwd, norm.w_fwd, h, W, reduce, b, relu,
@@ -1022,6 +1118,24 @@ class _GCNStack(torch.autograd.Function):
                                      row_div=rd)
             gb[top] = db
         dx = None
+
+        def adjoint_dx(l, dY):
+            """Layer l's dX-only adjoint -> the lower layer's dY (with its ReLU
+            mask, bias gradient and mean divisor); the lower layer's dW from
+            the same launch when it takes the Z form (mgcn_spmm_xw_bwd_dwl)."""
+            W = Ws[l]
+            if (_DWL and ctx.needs_input_grad[5 + 2 * (l - 1)] and z_path(l - 1) and
+                    spmm_xw_bwd_dwl_supported(*W.shape) and
+                    spmm_xw_bwd_dwl_supported(*Ws[l - 1].shape)):
+                dYn, db, gW[l - 1] = spmm_xw_bwd_dwl(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY,
+                                                     W, zs[l - 1], relu_mask=rmasks[l - 1],
+                                                     row_div=rd)
+            else:
+                _, dYn, db = spmm_xw_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, None, W,
+                                         relu_mask=rmasks[l - 1], row_div=rd)
+            gb[l - 1] = db if ctx.has_bias[l - 1] else None
+            return dYn
+
         for l in range(top, -1, -1):
             am = args[l] if args[l].numel() else None
             W = Ws[l]
@@ -1035,9 +1149,7 @@ class _GCNStack(torch.autograd.Function):
                 if am is None and (fused or l == 0) and _FUSE_XW and \
                         spmm_xw_supported(plan.bwd, W.size(1), W.size(0), L.REDUCE_SUM):
                     if fused:
-                        _, dY, db = spmm_xw_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY,
-                                                None, W, relu_mask=rmasks[l - 1], row_div=rd)
-                        gb[l - 1] = db if ctx.has_bias[l - 1] else None
+                        dY = adjoint_dx(l, dY)
                     else:
                         dx = spmm_xw_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, None, W)[1]
                     continue
@@ -1048,13 +1160,12 @@ class _GCNStack(torch.autograd.Function):
                 # product.  The gather runs only for dX (+ the lower layer's
                 # ReLU / bias gradient); the bottom layer needs no gather at all.
                 hcs = bool(top_z and l == top and ctx.has_bias[top])
-                gW[l], cs = dw_pass(zs[l], dY, W, dh_colsum=hcs)
-                if hcs:
-                    gb[top] = cs
+                if gW[l] is None:  # (not already formed by the layer above's adjoint)
+                    gW[l], cs = dw_pass(zs[l], dY, W, dh_colsum=hcs)
+                    if hcs:
+                        gb[top] = cs
                 if fused:
-                    _, dY, db = spmm_xw_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, None,
-                                            W, relu_mask=rmasks[l - 1], row_div=rd)
-                    gb[l - 1] = db if ctx.has_bias[l - 1] else None
+                    dY = adjoint_dx(l, dY)
                 elif ctx.needs_input_grad[0]:
                     dx = spmm_xw_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, None, W)[1]
                 continue

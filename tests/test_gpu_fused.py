@@ -395,7 +395,9 @@ def test_z_dw_and_dx_only_backward(cuda, oracle, N, E, hub, deg_norm, aggr, epi)
     assert dWb is None
     assert torch.equal(dXa, dXb)
     if mask is not None:
-        assert torch.equal(csa, csb)
+        # (the warp-specialised dX-only form folds the column sums in its own
+        # order: within fp32 summation-order tolerance of the full form's)
+        torch.testing.assert_close(csa, csb, rtol=1e-5, atol=1e-4)
     with pytest.raises(ValueError, match="dX only"):
         ops.spmm_xw_bwd(plan.bwd, norm.w_bwd, None, dYp, None, W, want_dx=False)
 
