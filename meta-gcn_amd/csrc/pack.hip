@@ -140,6 +140,10 @@ __global__ __launch_bounds__(64 * kPkWaves) void pack_values_kernel(
   }
 }
 
+// Unpack, software-pipelined one row ahead (round 5): a row costs two
+// dependent round trips (its offset and mask word, then its values); the next
+// row's offset and first mask word are loaded while this row's values are in
+// flight, so a wave's rows cost about one round trip each (4.0 TB/s before).
 template <int G>
 __global__ __launch_bounds__(64 * kPkWaves) void unpack_kernel(int64_t n_seg, int64_t n, int F,
                                                                const uint32_t *__restrict__ buf,
@@ -151,32 +155,49 @@ __global__ __launch_bounds__(64 * kPkWaves) void unpack_kernel(int64_t n_seg, in
   const int64_t total = n_seg * n;
   const int64_t stride = (int64_t)gridDim.x * kPkWaves * RPW;
   const int words = F >> 5;
-  for (int64_t k = ((int64_t)blockIdx.x * kPkWaves + (threadIdx.x >> 6)) * RPW + p.grp;
-       k < total + p.grp; k += stride) {
+  const uint64_t lo = p.below >> (p.grp * G);
+  // header of row kk: its value offset and this lane's nibble of segment 0
+  auto header = [&](int64_t kk, int64_t &pos, uint32_t &nib) {
+    const bool rok = kk < total;
+    const int64_t sg = rok ? kk / n : 0, i = rok ? kk - sg * n : 0;
+    const uint32_t *seg = buf + sg * seg_words;
+    const int f = 4 * p.gl;
+    pos = rok ? reinterpret_cast<const int32_t *>(seg)[i] : 0;
+    nib = (rok && f < F) ? (seg[n + i * words + (f >> 5)] >> (f & 31)) & 0xfu : 0u;
+  };
+  int64_t k = ((int64_t)blockIdx.x * kPkWaves + (threadIdx.x >> 6)) * RPW + p.grp;
+  int64_t pos_n;
+  uint32_t nib_n;
+  header(k, pos_n, nib_n);
+  for (; k < total + p.grp; k += stride) {
     const bool rok = k < total;
+    int64_t pos = pos_n;
+    uint32_t nib0 = nib_n;
+    header(k + stride, pos_n, nib_n);  // the next row's header, under this row's values
     const int64_t sg = rok ? k / n : 0, i = rok ? k - sg * n : 0;
     const uint32_t *seg = buf + sg * seg_words;
     const uint32_t *mk = seg + n + i * words;
     const uint32_t *vals = seg + n + n * words;
-    int64_t pos = rok ? reinterpret_cast<const int32_t *>(seg)[i] : 0;
     uint32_t *t = reinterpret_cast<uint32_t *>(T + (rok ? k : 0) * ldt);
     for (int f0 = 0; f0 < F; f0 += 4 * G) {
       const int f = f0 + 4 * p.gl;
       const bool ok = rok && f < F;
       // this lane's nibble of its mask word: word f >> 5, bits (f & 31) .. + 3
-      const uint32_t nib = ok ? (mk[f >> 5] >> (f & 31)) & 0xfu : 0u;
+      const uint32_t nib = f0 == 0 ? nib0 : ok ? (mk[f >> 5] >> (f & 31)) & 0xfu : 0u;
       bool nz[4] = {(nib & 1u) != 0, (nib & 2u) != 0, (nib & 4u) != 0, (nib & 8u) != 0};
       uint64_t b[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) b[j] = (__ballot(nz[j]) & p.gmask) >> (p.grp * G);
-      const uint64_t lo = p.below >> (p.grp * G);
-      int64_t q = pos + __popcll(b[0] & lo) + __popcll(b[1] & lo) + __popcll(b[2] & lo) +
-                  __popcll(b[3] & lo);
-      uint4 v = make_uint4(0u, 0u, 0u, 0u);
-      if (nz[0]) v.x = vals[q++];
-      if (nz[1]) v.y = vals[q++];
-      if (nz[2]) v.z = vals[q++];
-      if (nz[3]) v.w = vals[q++];
+      const int64_t q = pos + __popcll(b[0] & lo) + __popcll(b[1] & lo) + __popcll(b[2] & lo) +
+                        __popcll(b[3] & lo);
+      // the four value loads issued together (a lane's values are consecutive)
+      const int64_t q1 = q + (nz[0] ? 1 : 0);
+      const int64_t q2 = q1 + (nz[1] ? 1 : 0);
+      const int64_t q3 = q2 + (nz[2] ? 1 : 0);
+      // (a zero word reads the segment's first header word: always in bounds)
+      const uint32_t x0 = *(nz[0] ? vals + q : seg), x1 = *(nz[1] ? vals + q1 : seg);
+      const uint32_t x2 = *(nz[2] ? vals + q2 : seg), x3 = *(nz[3] ? vals + q3 : seg);
+      const uint4 v = make_uint4(nz[0] ? x0 : 0u, nz[1] ? x1 : 0u, nz[2] ? x2 : 0u, nz[3] ? x3 : 0u);
       if (ok) *reinterpret_cast<uint4 *>(t + f) = v;
       pos += __popcll(b[0]) + __popcll(b[1]) + __popcll(b[2]) + __popcll(b[3]);
     }

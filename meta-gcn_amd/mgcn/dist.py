@@ -289,6 +289,18 @@ def new_table(shard: Shard, F: int, dtype, device, slot: str) -> torch.Tensor:
     return t
 
 
+_SIZE_STREAMS = {}
+
+
+def _size_stream(dev):
+    """Side stream (per device) of the packed exchange's size read-back."""
+    st = _SIZE_STREAMS.get(dev.index)
+    if st is None:
+        st = torch.cuda.Stream(device=dev)
+        _SIZE_STREAMS[dev.index] = st
+    return st
+
+
 def _wait(works):
     for w in works:
         if w is not None:
@@ -369,19 +381,41 @@ class _ChunkExchange:
         else:
             totals = torch.empty(P, dtype=torch.int64, device=dev)
             work = _gather_into(totals, total, P, self.group, True)
-        self.pending.append((c, rows, send, counts, totals, work))
+        # the sizes reach the host through a side stream that waits only for
+        # the size exchange: finish() then waits for THAT (an event), not for
+        # everything queued on the compute stream after it (`.item()` on the
+        # compute stream would drain the next chunk's kernels first, leaving
+        # the GPU idle until the host queued more)
+        host = ev = None
+        if dev.type == "cuda":
+            side = _size_stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                if work is not None:
+                    work.wait()
+                host = torch.empty(totals.numel(), dtype=torch.int64, pin_memory=True)
+                host.copy_(totals, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(side)
+            totals.record_stream(side)
+            work = None
+        self.pending.append((c, rows, send, counts, totals, work, host, ev))
 
     def finish(self, keep: int = 0) -> None:
         """Issue the payloads of all started chunks but the last ``keep``."""
         while len(self.pending) > keep:
             self._finish_one(*self.pending.pop(0))
 
-    def _finish_one(self, c, rows, send, counts, totals, work):
+    def _finish_one(self, c, rows, send, counts, totals, work, host, ev):
         sh = self.sh
         cr, P, F = sh.chunk_rows, sh.world, rows.size(1)
-        if work is not None:
-            work.wait()
-        cap = int(totals.max())  # the host waits for this chunk's pack
+        if ev is not None:
+            ev.synchronize()  # the size exchange (and its copy) only
+            cap = int(host.max())
+        else:
+            if work is not None:
+                work.wait()
+            cap = int(totals.max())
         head = cr * (1 + self.words)
         seg = head + cap
         self.stats["dense_words"] += cr * F * P
