@@ -466,6 +466,20 @@ int mgcn_edge_weight_grad(int64_t n_rows, int32_t F, const int64_t *rowptr, cons
 
 /* ------------------------------------------------------- pooling support */
 
+/*
+ * Batched dense product (ABI v18), DiffPool's dense operators (PyG 1.3
+ * DenseSAGEConv adj @ x @ weight and dense_diff_pool's S^T X, S^T A S, S S^T,
+ * reference kernel/diff_pool.py:13-14, 68, 76):
+ *   C[b][m][n] (+)= sum_k A[b][m][k] B[b][k][n]      (accumulate != 0: +=)
+ * every operand addressed through (batch, row, column) element strides, so
+ * transposed views need no copies; fp32 products and accumulation on MFMA.
+ * batch <= 65535.
+ */
+int mgcn_gemm_batched(int64_t batch, int32_t M, int32_t N, int32_t K, const float *A, int64_t sab,
+                      int64_t sam, int64_t sak, const float *B, int64_t sbb, int64_t sbk,
+                      int64_t sbn, float *C, int64_t scb, int64_t scm, int64_t scn,
+                      int accumulate, void *stream);
+
 /* Bytes of scratch mgcn_edge_merge_greedy needs. */
 size_t mgcn_edge_merge_workspace_bytes(int64_t n_nodes, int64_t n_edges);
 

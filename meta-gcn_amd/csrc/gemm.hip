@@ -631,6 +631,135 @@ gemm_tn_x6_wide_kernel(const float *__restrict__ A, int64_t lda, const float *__
       }
 }
 
+// The same dW with each split's C cut into two 256 x 128 column halves, one
+// workgroup per half (round 5): 64 accumulators per wave instead of 128, so
+// two workgroups fit a CU (72 KB of double-buffered images each) and one's
+// split / LDS work runs under the other's MFMAs (the single-workgroup form
+// serialises them: ~52 % of the MFMA rate).  Both halves read the split's A
+// rows; blocks b and b + 8 (one XCD under round-robin dispatch) are the two
+// halves of a split, so the second read comes from that XCD's L2.  Same
+// products per C element in the same k-step order: bit for bit the one-
+// workgroup form.
+constexpr int kTnWide2Chunk = 9 * kTnX6Img;  // A (two halves) + B half: 36 KB
+
+__global__ __launch_bounds__(512, 4) void gemm_tn_x6_wide2_kernel(
+    const float *__restrict__ A, int64_t lda, const float *__restrict__ B, int64_t ldb, int64_t K,
+    int64_t k_per_split, int n_splits, float *__restrict__ partial) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * kTnWide2Chunk];
+  const int bid = (int)blockIdx.x;
+  const int hh = (bid >> 3) & 1;
+  const int split = (bid >> 4) * 8 + (bid & 7);
+  if (split >= n_splits) return;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t kb = (int64_t)split * k_per_split;
+  const int64_t ke = (kb + k_per_split < K) ? kb + k_per_split : K;
+  const int h = lane >> 5, lc = lane & 31;
+  struct Regs {
+    float4 a[2], b;
+  };
+  const auto rsa = buf_rsrc(A + kb * lda, (uint32_t)((ke - kb) * lda * 4));
+  const auto rsb = buf_rsrc(B + kb * ldb + 128 * hh, (uint32_t)((ke - kb) * ldb * 4));
+  auto load_chunk = [&](int64_t k0, Regs &R) {
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int f = tid + 512 * m;
+      const int64_t row = k0 - kb + (f >> 6);
+      R.a[m] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                              rsa, (int)((row * lda + 4 * (f & 63)) * 4), 0, 0));
+    }
+    const int64_t row = k0 - kb + (tid >> 5);
+    R.b = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                         rsb, (int)((row * ldb + 4 * (tid & 31)) * 4), 0, 0));
+  };
+  auto put = [&](char *img, const float4 v) {
+    uint32_t hi[2], mid[2], lo[2];
+    split3_pair(f32x2{v.x, v.y}, hi[0], mid[0], lo[0]);
+    split3_pair(f32x2{v.z, v.w}, hi[1], mid[1], lo[1]);
+    *reinterpret_cast<uint2 *>(img) = make_uint2(hi[0], hi[1]);
+    *reinterpret_cast<uint2 *>(img + kTnX6Img) = make_uint2(mid[0], mid[1]);
+    *reinterpret_cast<uint2 *>(img + 2 * kTnX6Img) = make_uint2(lo[0], lo[1]);
+  };
+  auto store_chunk = [&](char *img0, const Regs &R) {
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int f = tid + 512 * m;
+      const int row = f >> 6, c4 = f & 63;
+      const int half = c4 >> 5, c = c4 & 31;
+      put(img0 + half * 3 * kTnX6Img + tn_x6_off(row, c >> 1) + 8 * (c & 1), R.a[m]);
+    }
+    const int row = tid >> 5, c = tid & 31;
+    put(img0 + 6 * kTnX6Img + tn_x6_off(row, c >> 1) + 8 * (c & 1), R.b);
+  };
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  auto frag_off = [&](int base_img, int col0, int second) {
+    const int row = 8 * h + q + 4 * second;
+    return base_img * kTnX6Img + tn_x6_off(row, (col0 >> 3) + 2 * (g & 1) + (p >> 1)) + 8 * (p & 1);
+  };
+  int offa[2][2], offb[2][2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int gcol = wm * 64 + 32 * t;  // A column (C row), 0 .. 255
+      offa[t][r] = frag_off((gcol >> 7) * 3, gcol & 127, r);
+      offb[t][r] = frag_off(6, wn * 64 + 32 * t, r);
+    }
+  }
+  auto read8 = [&](const char *img0, const int (&o)[2], int term) {
+    const v4i16 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_v4i16_t *)(img0 + o[0] + term * kTnX6Img));
+    const v4i16 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_v4i16_t *)(img0 + o[1] + term * kTnX6Img));
+    const short y[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+    return __builtin_bit_cast(bf16x8, y);
+  };
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][u][r] = 0.0f;
+  const int64_t nchunks = (ke - kb + kTnX6Rows - 1) / kTnX6Rows;
+  Regs R;
+  if (nchunks > 0) load_chunk(kb, R);
+  for (int64_t c = 0; c < nchunks; ++c) {
+    char *img0 = lds + (c & 1) * kTnWide2Chunk;
+    store_chunk(img0, R);
+    if (c + 1 < nchunks) load_chunk(kb + (c + 1) * kTnX6Rows, R);
+    __syncthreads();
+    bf16x8 fa[2][3];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int term = 0; term < 3; ++term) fa[t][term] = read8(img0, offa[t], term);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      bf16x8 fb[3];
+#pragma unroll
+      for (int term = 0; term < 3; ++term) fb[term] = read8(img0, offb[u], term);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        acc[t][u] = mfma_x6(fa[t][0], fa[t][1], fa[t][2], fb[0], fb[1], fb[2], acc[t][u]);
+    }
+  }
+  float *slab = partial + (int64_t)split * 256 * 256;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = wm * 64 + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        slab[(int64_t)row * 256 + 128 * hh + wn * 64 + u * 32 + lc] = acc[t][u][r];
+      }
+}
+
+int g_tn_wide2 = 0;  // mgcn_set_option("gemm_tn_wide2"): the two-half form at 256 x 256
+
 bool tn_wide(int M, int N) { return M == 256 && N == 256; }
 // gemm_tn_x6_wide_kernel addresses a split's rows with 32-bit buffer offsets
 bool tn_wide_fits(int64_t kps, int64_t lda, int64_t ldb) {
@@ -671,6 +800,12 @@ int gemm_splits(int64_t K, int M, int N) {
 int gemm_set_tn_variant(int value) {
   if (value < 0 || value > 2) return MGCN_EINVAL;
   g_tn_lds_variant = value;
+  return MGCN_OK;
+}
+
+int gemm_set_tn_wide2(int value) {
+  if (value < 0 || value > 1) return MGCN_EINVAL;
+  g_tn_wide2 = value;
   return MGCN_OK;
 }
 
@@ -757,7 +892,11 @@ int gemm_tn_core(int64_t K, int32_t M, int32_t N, const float *A, int64_t lda, c
              reinterpret_cast<uintptr_t>(B) % 16 == 0 && lda % 4 == 0 && ldb % 4 == 0) {
     // 1-D grids of tiles x splits in the kernels' XCD-aware order
     const dim3 grid(tiles_m * tiles_n * used);
-    if (g_gemm_precision == PREC_BF16X6 && tn_wide(M, N) && tn_wide_fits(kps, lda, ldb))
+    if (g_gemm_precision == PREC_BF16X6 && tn_wide(M, N) && tn_wide_fits(kps, lda, ldb) &&
+        g_tn_wide2)
+      hipLaunchKernelGGL(gemm_tn_x6_wide2_kernel, dim3(2 * ((used + 7) / 8) * 8), dim3(512), 0, s,
+                         A, lda, B, ldb, K, kps, used, partial);
+    else if (g_gemm_precision == PREC_BF16X6 && tn_wide(M, N) && tn_wide_fits(kps, lda, ldb))
       hipLaunchKernelGGL(gemm_tn_x6_wide_kernel, dim3(used), dim3(512), 0, s, A, lda, B, ldb, K,
                          kps, partial);
     else if (g_gemm_precision == PREC_BF16X6)

@@ -177,6 +177,46 @@ __global__ __launch_bounds__(kMgThreads) void edge_merge_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Batched dense product of DiffPool's dense operators (round 5): PyG 1.3's
+// DenseSAGEConv (adj @ x, @ weight) and dense_diff_pool (S^T X, S^T A S,
+// S S^T) as used by reference kernel/diff_pool.py:13-14, 68, 76 -- small
+// per-graph matrices (a padded mini-batch: B x N x N with N the largest
+// graph), so one wave per 16 x 16 output tile on v_mfma_f32_16x16x4_f32
+// (exact fp32 products, fp32 accumulation), operands read straight from
+// global memory through arbitrary (batch, row, column) strides, so
+// transposed operands -- the adjoints' A^T dC and dC B^T -- need no copies.
+//   C[b][m][n] (+)= sum_k A[b][m][k] B[b][k][n]
+__global__ __launch_bounds__(64) void gemm_batched_kernel(
+    int32_t M, int32_t N, int32_t K, const float *__restrict__ A, int64_t sab, int64_t sam,
+    int64_t sak, const float *__restrict__ B, int64_t sbb, int64_t sbk, int64_t sbn,
+    float *__restrict__ C, int64_t scb, int64_t scm, int64_t scn, int accumulate) {
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
+  const int lane = threadIdx.x;
+  const int64_t b = blockIdx.z;
+  const int m0 = 16 * (int)blockIdx.y, n0 = 16 * (int)blockIdx.x;
+  const int l16 = lane & 15, g4 = lane >> 4;
+  const float *a = A + b * sab + (int64_t)(m0 + l16) * sam;
+  const float *bb = B + b * sbb + (int64_t)(n0 + l16) * sbn;
+  const bool mok = m0 + l16 < M, nok = n0 + l16 < N;
+  f32x4v acc = {0.0f, 0.0f, 0.0f, 0.0f};
+  for (int k0 = 0; k0 < K; k0 += 4) {
+    const int k = k0 + g4;
+    const float av = (mok && k < K) ? a[(int64_t)k * sak] : 0.0f;
+    const float bv = (nok && k < K) ? bb[(int64_t)k * sbk] : 0.0f;
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
+  }
+  // lane (l16, g4) holds C[m0 + 4 g4 + r][n0 + l16]
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int m = m0 + 4 * g4 + r;
+    if (m < M && nok) {
+      float *c = C + b * scb + (int64_t)m * scm + (int64_t)(n0 + l16) * scn;
+      *c = accumulate ? __fadd_rn(*c, acc[r]) : acc[r];
+    }
+  }
+}
+
 }  // namespace
 }  // namespace mgcn
 
@@ -212,4 +252,21 @@ extern "C" int mgcn_edge_merge_greedy(int64_t n_nodes, int64_t n_edges, const in
                      (int32_t)n_edges, src, dst, order, rank, flag, best, freen, cluster, chosen,
                      counts);
   return check_launch("edge_merge_kernel");
+}
+
+extern "C" int mgcn_gemm_batched(int64_t batch, int32_t M, int32_t N, int32_t K, const float *A,
+                                 int64_t sab, int64_t sam, int64_t sak, const float *B,
+                                 int64_t sbb, int64_t sbk, int64_t sbn, float *C, int64_t scb,
+                                 int64_t scm, int64_t scn, int accumulate, void *stream) {
+  clear_error();
+  MGCN_REQUIRE(batch >= 0 && M >= 0 && N >= 0 && K >= 0, "mgcn_gemm_batched: negative size");
+  MGCN_REQUIRE(batch <= 65535, "mgcn_gemm_batched: batch %lld > 65535", (long long)batch);
+  if (batch == 0 || M == 0 || N == 0) return MGCN_OK;
+  MGCN_REQUIRE(C != nullptr && (K == 0 || (A != nullptr && B != nullptr)),
+               "mgcn_gemm_batched: null array");
+  hipStream_t s = as_stream(stream);
+  const dim3 grid((unsigned)((N + 15) / 16), (unsigned)((M + 15) / 16), (unsigned)batch);
+  hipLaunchKernelGGL(gemm_batched_kernel, grid, dim3(64), 0, s, M, N, K, A, sab, sam, sak, B, sbb,
+                     sbk, sbn, C, scb, scm, scn, accumulate);
+  return check_launch("gemm_batched_kernel");
 }

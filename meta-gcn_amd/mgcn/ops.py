@@ -728,6 +728,78 @@ def _mm_t(dH: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
     return torch.matmul(dH, W.detach().t())
 
 
+def _gemm_batched(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor,
+                  a_str, b_str, c_str, M: int, N: int, K: int, batch: int,
+                  accumulate: bool = False) -> None:
+    """C (+)= A B per batch through explicit (batch, row, col) element strides
+    (``mgcn_gemm_batched``)."""
+    lib = L.load()
+    dev = L.require_device(A, B, C)
+    with L.device_guard(dev):
+        rc = lib.mgcn_gemm_batched(batch, M, N, K, L.ptr(A), *a_str, L.ptr(B), *b_str, L.ptr(C),
+                                   *c_str, 1 if accumulate else 0, L.stream_of(dev))
+    L.check(rc, "mgcn_gemm_batched")
+
+
+def _bstr(t: torch.Tensor):
+    """(batch, row, col) strides of a 3-D tensor or a broadcast 2-D one."""
+    return (t.stride(0), t.stride(1), t.stride(2)) if t.dim() == 3 else (0, t.stride(0), t.stride(1))
+
+
+class _Bmm(torch.autograd.Function):
+    """a [B, M, K] @ b ([B, K, N] or a broadcast [K, N]) on mgcn_gemm_batched,
+    with its adjoints dA = dC b^T, db = a^T dC (summed over the batch for a
+    broadcast b) through transposed strides -- no copies."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        Bn, M, K = a.shape
+        N = b.shape[-1]
+        out = torch.empty(Bn, M, N, dtype=torch.float32, device=a.device)
+        _gemm_batched(a, b, out, _bstr(a), _bstr(b), _bstr(out), M, N, K, Bn)
+        ctx.save_for_backward(a, b)
+        return out
+
+    @staticmethod
+    def backward(ctx, dC):
+        a, b = ctx.saved_tensors
+        dC = dC.to(torch.float32)  # any strides: the kernel addresses them
+        Bn, M, K = a.shape
+        N = b.shape[-1]
+        da = db = None
+        if ctx.needs_input_grad[0]:
+            da = torch.empty_like(a, memory_format=torch.contiguous_format)
+            sb = _bstr(b)
+            _gemm_batched(dC, b, da, _bstr(dC), (sb[0], sb[2], sb[1]), _bstr(da), M, K, N, Bn)
+        if ctx.needs_input_grad[1]:
+            sa = _bstr(a)
+            if b.dim() == 3:
+                db = torch.empty(Bn, K, N, dtype=torch.float32, device=a.device)
+                _gemm_batched(a, dC, db, (sa[0], sa[2], sa[1]), _bstr(dC), _bstr(db), K, N, M, Bn)
+            else:  # broadcast weight: one product over the flattened batch rows
+                a2 = a.reshape(Bn * M, K)
+                d2 = dC.reshape(Bn * M, N)
+                db = torch.empty(K, N, dtype=torch.float32, device=a.device)
+                _gemm_batched(a2, d2, db, (0, a2.stride(1), a2.stride(0)), (0, d2.stride(0),
+                              d2.stride(1)), (0, db.stride(0), db.stride(1)), K, N, Bn * M, 1)
+        return da, db
+
+
+def bmm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """Batched dense product of DiffPool's dense operators (PyG 1.3
+    DenseSAGEConv / dense_diff_pool; reference kernel/diff_pool.py:13-14, 68,
+    76): a [B, M, K] @ b [B, K, N] (or a [K, N] weight broadcast over the
+    batch) on libmgcn's MFMA kernel, differentiable in both operands."""
+    if a.dtype != torch.float32 or b.dtype != torch.float32:
+        raise TypeError(f"bmm: float32 operands (the reference computes in fp32), got "
+                        f"{a.dtype} @ {b.dtype}")
+    if a.dim() != 3 or b.dim() not in (2, 3) or a.size(2) != b.size(-2) or \
+            (b.dim() == 3 and b.size(0) != a.size(0)):
+        raise ValueError(f"bmm: shapes {tuple(a.shape)} @ {tuple(b.shape)}")
+    L.require_device(a, b)
+    return _Bmm.apply(a, b)
+
+
 class _Linear(torch.autograd.Function):
     """H = x @ W (gcn_base_models.py:201) with all three products on libmgcn's
     MFMA kernels: forward on mgcn_gemm_nn (tall-skinny); backward dW = x^T dH

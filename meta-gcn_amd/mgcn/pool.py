@@ -34,7 +34,7 @@ from torch.nn import Parameter
 from . import _lib as L
 from .graph import build_view
 from .models import activation, glorot, zeros
-from .ops import scatter_, spmm_fwd
+from .ops import bmm, scatter_, spmm_fwd
 from .pyg import GraphConv, remove_self_loops, uniform
 
 EPS = 1e-15
@@ -526,9 +526,9 @@ class DenseSAGEConv(torch.nn.Module):
             adj = adj.clone()
             idx = torch.arange(N, dtype=torch.long, device=adj.device)
             adj[:, idx, idx] = 1
-        out = torch.matmul(adj, x)
+        out = bmm(adj, x)
         out = out / adj.sum(dim=-1, keepdim=True).clamp(min=1)
-        out = torch.matmul(out, self.weight)
+        out = bmm(out, self.weight)
         if self.bias is not None:
             out = out + self.bias
         if self.normalize:
@@ -552,9 +552,10 @@ def dense_diff_pool(x, adj, s, mask=None):
     if mask is not None:
         mask = mask.view(batch_size, num_nodes, 1).to(x.dtype)
         x, s = x * mask, s * mask
-    out = torch.matmul(s.transpose(1, 2), x)
-    out_adj = torch.matmul(torch.matmul(s.transpose(1, 2), adj), s)
-    link_loss = adj - torch.matmul(s, s.transpose(1, 2))
+    st = s.transpose(1, 2)  # (a strided view: the kernel reads it in place)
+    out = bmm(st, x)
+    out_adj = bmm(bmm(st, adj), s)
+    link_loss = adj - bmm(s, st)
     link_loss = torch.norm(link_loss, p=2) / adj.numel()
     ent_loss = (-s * torch.log(s + EPS)).sum(dim=-1).mean()
     return out, out_adj, link_loss, ent_loss

@@ -38,8 +38,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=6_243_575)
     ap.add_argument("--feat", type=int, default=256)
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="mgcn_set_option before the run (A/B)")
     args = ap.parse_args()
     from mgcn import ops
+    from mgcn import _lib as L
+    for kv in args.opt:
+        k, v = kv.split("=")
+        L.set_option(k, int(v))
     dev = torch.device("cuda:0")
     M, F = args.rows, args.feat
     g = torch.Generator(device=dev).manual_seed(0)

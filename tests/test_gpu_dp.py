@@ -35,6 +35,10 @@ def _init(rank, world, port):
     sys.path[:0] = [os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "meta-gcn_amd")]
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    # several ranks share cuda:0: two hardware queues each (HIP's default is
+    # 4), so the ranks' queues fit the device without the scheduler swapping
+    # them in and out (the r4g abort audit)
+    os.environ["GPU_MAX_HW_QUEUES"] = "2"
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
 

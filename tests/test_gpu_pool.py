@@ -363,6 +363,48 @@ def test_dense_sage_and_diff_pool(cuda):
     torch.testing.assert_close(ent.cpu(), (-S * torch.log(S + 1e-15)).sum(-1).mean())
 
 
+@pytest.mark.parametrize("B,N,C,K", [(3, 9, 4, 3), (5, 37, 20, 7), (1, 1, 1, 1)])
+def test_diff_pool_dense_products_on_libmgcn_with_gradients(cuda, B, N, C, K):
+    """DenseSAGEConv -> dense_diff_pool on mgcn_gemm_batched (ops.bmm, the
+    last vendor GEMM of a module path, round 5): forward values and the
+    gradients of x, s and the conv's weight / bias against fp64 torch autograd
+    on the CPU (the products are exact fp32 on MFMA; tolerance is fp32
+    summation order)."""
+    from mgcn import ops
+    from mgcn.pool import DenseSAGEConv, dense_diff_pool
+    torch.manual_seed(B * 100 + N)
+    x = torch.randn(B, N, C)
+    adj = (torch.rand(B, N, N) < 0.3).float()
+    mask = torch.ones(B, N, dtype=torch.bool)
+    if N > 2:
+        mask[0, N // 2:] = False
+    s0 = torch.randn(B, N, K)
+    conv = DenseSAGEConv(C, K).to(cuda)
+    ref_conv = DenseSAGEConv(C, K).double()
+    ref_conv.load_state_dict({k: v.double().cpu() for k, v in conv.state_dict().items()})
+    outs = []
+    for dev, m in ((cuda, conv), ("cpu", ref_conv)):
+        dt = torch.float32 if dev != "cpu" else torch.float64
+        xx = x.to(dev, dt).requires_grad_(True)
+        ss = s0.to(dev, dt).requires_grad_(True)
+        if dev == "cpu":
+            import mgcn.pool as P
+            saved = P.bmm
+            P.bmm = lambda a, b: torch.matmul(a, b)  # the fp64 reference products
+        try:
+            h = m(xx, adj.to(dev, dt), mask.to(dev))
+            out, out_adj, link, ent = dense_diff_pool(h, adj.to(dev, dt), ss, mask.to(dev))
+        finally:
+            if dev == "cpu":
+                P.bmm = saved
+        loss = out.sum() + (out_adj * out_adj).sum() + link + ent
+        loss.backward()
+        outs.append([out.detach(), out_adj.detach(), xx.grad, ss.grad, m.weight.grad, m.bias.grad])
+    for got, ref in zip(*outs):
+        torch.testing.assert_close(got.cpu().double(), ref, rtol=1e-4, atol=1e-4)
+    assert ops.bmm(torch.randn(2, 3, 4, device=cuda), torch.randn(4, 5, device=cuda)).shape == (2, 3, 5)
+
+
 @pytest.mark.parametrize("name", ["hardpool_add", "hardpool_add_bias", "hardpool_mean",
                                   "hardpool_sunk"])
 def test_hard_pooling_matches_reference(cuda, name):
