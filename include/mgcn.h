@@ -414,6 +414,30 @@ int mgcn_spmm_xw_bwd(int64_t n_rows, int64_t n_cols, int32_t F_in, int32_t F_out
                      const int32_t *slot_map, void *workspace, size_t workspace_bytes,
                      void *stream);
 
+/*
+ * A max layer with the NEXT layer's transform in one launch (ABI v18; F = 128,
+ * bf16x6, graphs without heavy rows):
+ *   Y  = relu(max_k H[col_k] * w_k + bias)  -- bit for bit mgcn_spmm_fwd
+ *        (MGCN_REDUCE_MAX with a winner-bit buffer): rows without edges 0,
+ *        `>=` so a later edge wins a tie (torch_scatter 1.x CPU)
+ *   relu_mask [n_rows][4] (nullable, needs relu), win_mask [nnz][4]: every
+ *        edge's winner bits at its fwd slot (mgcn_spmm_fwd's layout)
+ *   Hn = Y Wn  (the next layer's x @ weight_node, bf16x6)
+ * Replaces mgcn_spmm_fwd(MAX) + the next layer's mgcn_gemm_nn (the
+ * reference: x @ weight_node then gather / scatter max, gcn_base_models.py:
+ * 201, 223-237, common.py:59-64).  H [n_cols, 128] under 4 GiB, 16-byte rows.
+ * Scratch: mgcn_spmm_max_xw_fwd_workspace_bytes().
+ */
+int mgcn_spmm_max_xw_fwd(int64_t n_rows, int64_t n_cols, const int64_t *rowptr, const int32_t *col,
+                         const float *w, const float *H, int64_t ldh, const float *bias, int relu,
+                         float *Y, int64_t ldy, uint32_t *relu_mask, uint32_t *win_mask,
+                         const float *Wn, int64_t ldwn, float *Hn, int64_t ldhn, void *workspace,
+                         size_t workspace_bytes, void *stream);
+
+/* Bytes of scratch mgcn_spmm_max_xw_fwd needs (Wn split into its fragment
+ * image; 16-byte aligned). */
+size_t mgcn_spmm_max_xw_fwd_workspace_bytes(void);
+
 /* Bytes of scratch mgcn_spmm_xw_bwd_dwl needs (dWl split-K partials + column
  * sums; ABI v18). */
 size_t mgcn_spmm_xw_bwd_dwl_workspace_bytes(int64_t n_rows);

@@ -519,6 +519,270 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_fwd_kernel(c
 }
 
 // ---------------------------------------------------------------------------
+// Max layer with the NEXT layer's transform (round 5, config 4):
+//   Y  = relu(max_k H[col_k] w_k + b)   (+ ReLU mask words, + winner bits)
+//   Hn = Y Wn                           (the next layer's x @ W)
+// Max does not commute with W, so the layer's own product stays before it
+// (a GEMM or the previous call's Hn), but Y is complete in the gathering
+// workgroup: the next layer's product runs on it there, instead of a GEMM
+// that reads Y back (reference: x @ weight_node, gather, scatter max,
+// gcn_base_models.py:201, 223-237, common.py:59-64; torch_scatter 1.x's CPU
+// max: `>=`, a later edge wins a tie, rows without edges 0).  The chunk
+// structure is spmm_xw_fwd_kernel's: Phase A folds each row's edges in order
+// (mgcn_spmm_fwd's FWD_MAX arithmetic and winners, bit for bit), applies bias
+// and ReLU, stores Y, its mask words and every edge's winner bits (the
+// layout of mgcn_spmm_fwd with a winner-bit buffer: word f / 32 of the edge's
+// record at its fwd slot, bit f % 32) and writes Y's bf16 terms; Phase B
+// multiplies them by this wave's 16 columns of Wn (bf16x6) into Hn.
+struct XmArgs {
+  int64_t n_rows;
+  const int64_t *rowptr;
+  const int32_t *col;
+  const float *w;
+  const float *H;  // gathered rows [n_cols][128]
+  int64_t ldh;
+  int64_t n_cols;
+  const float *bias;
+  int relu;
+  float *Y;
+  int64_t ldy;
+  uint32_t *relu_mask;  // [n_rows][4], nullable
+  uint32_t *win_mask;   // [nnz][4]
+  const u32x4 *wimg;    // Wn's fragment image (xm_wimg_kernel): Hn = Y Wn
+  float *Hn;
+  int64_t ldhn;
+};
+
+// max fold of one row in the 32-lane group (gather_row_meta's loop): acc the
+// max of the separately rounded products, win the position (in the row) of
+// the edge that set it -- `>=`: a later edge wins a tie
+template <int U>
+__device__ __forceinline__ void gather_row_max(const __amdgpu_buffer_rsrc_t rx, uint32_t ldx_b,
+                                               const int32_t *__restrict__ col,
+                                               const float *__restrict__ w, const RowMeta &m,
+                                               int gl, int grp, float (&acc)[4], int (&win)[4]) {
+  const int64_t beg = m.beg, deg = m.deg;
+  const int64_t odeg = __shfl_xor(deg, 32, 64);
+  const int64_t maxdeg = deg > odeg ? deg : odeg;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    acc[j] = MGCN_MAX_FILL;
+    win[j] = -1;
+  }
+  int mc = m.mc;
+  float mw = m.mw;
+  for (int64_t e0 = 0; e0 < maxdeg; e0 += 32) {
+    if (e0 > 0) {
+      const int64_t my = e0 + gl;
+      mc = 0;
+      mw = 1.0f;
+      if (my < deg) {
+        mc = col[beg + my];
+        if (w != nullptr) mw = w[beg + my];
+      }
+    }
+    const int64_t rem = deg - e0;
+    const int nb = rem <= 0 ? 0 : (rem < 32 ? (int)rem : 32);
+    const int64_t remw = maxdeg - e0;
+    const int nbmax = remw < 32 ? (int)remw : 32;
+    for (int k0 = 0; k0 < nbmax; k0 += U) {
+      float4 xv[U];
+      float wk[U];
+      bool ok[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = k0 + u;
+        const int ck = __shfl(mc, 32 * grp + (k & 31), 64);
+        wk[u] = __shfl(mw, 32 * grp + (k & 31), 64);
+        ok[u] = k < nb;
+        const uint32_t off = ok[u] ? (uint32_t)ck * ldx_b + 16u * gl : 0xfffffff0u;
+        xv[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0));
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (ok[u]) {
+          const int e = (int)(e0 + k0 + u);
+          const float p[4] = {__fmul_rn(xv[u].x, wk[u]), __fmul_rn(xv[u].y, wk[u]),
+                              __fmul_rn(xv[u].z, wk[u]), __fmul_rn(xv[u].w, wk[u])};
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (p[j] >= acc[j]) {
+              acc[j] = p[j];
+              win[j] = e;
+            }
+        }
+      }
+    }
+  }
+}
+
+// LDS: the double-buffered chunk images (48 KB) and a 512-B winner-record
+// window per lane group (8 KB): 56 KB, two workgroups per CU.  Hn leaves
+// straight from the MFMA registers (Wn as the A operand: a lane holds four
+// consecutive columns of one row, one 16-B store), so no staging tile.
+constexpr int kXmWinOff = 2 * kXfBuf;
+constexpr int kXmLds = kXmWinOff + 16 * 32 * 16;
+static_assert(2 * kXmLds <= 160 * 1024, "two max+next workgroups per CU");
+
+// the six products of mfma16_x6(rows, W) with W as the A operand (same pairs,
+// same order)
+__device__ __forceinline__ f32x4_t mfma16_x6_wa(const bf16x8 (&w)[3], const bf16x8 &xh,
+                                               const bf16x8 &xm, const bf16x8 &xl, f32x4_t c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], xl, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[2], xh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[1], xm, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], xm, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[1], xh, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], xh, c, 0, 0, 0);
+}
+
+// Wn split once into bf16 terms in fragment order (a prep launch): fragment
+// ((ks * 8 + nt) * 3 + term) * 64 + lane holds Wn[32 ks + 8 g4 + j][16 nt + l16]
+// (lane = 16 g4 + l16, j < 8) -- the 48 VGPRs of held fragments would spill
+// the max gather, so each chunk's Phase B streams its wave's 12 fragments
+// from L2 (96 KB image), issued before the chunk barrier
+__global__ __launch_bounds__(256) void xm_wimg_kernel(const float *__restrict__ W, int64_t ldw,
+                                                      u32x4 *__restrict__ img) {
+  const int idx = (int)(blockIdx.x * 256 + threadIdx.x);
+  if (idx >= 4 * 8 * 64) return;
+  const int lane = idx & 63, nt = (idx >> 6) & 7, ks = idx >> 9;
+  const int l16 = lane & 15, g4 = lane >> 4;
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = W[(int64_t)(32 * ks + 8 * g4 + j) * ldw + 16 * nt + l16];
+  bf16x8 h, m, l;
+  split3_bf16(v, h, m, l);
+  u32x4 *o = img + ((ks * 8 + nt) * 3) * 64 + lane;
+  o[0] = __builtin_bit_cast(u32x4, h);
+  o[64] = __builtin_bit_cast(u32x4, m);
+  o[128] = __builtin_bit_cast(u32x4, l);
+}
+
+template <int U>
+__global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_max_xw_kernel(const XmArgs a) {
+  __shared__ __attribute__((aligned(16))) char lds[kXmLds];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int gl = lane & 31, grp = lane >> 5;
+  const int l16 = lane & 15, g4 = lane >> 4;
+  const int64_t n_chunks = (a.n_rows + kXwRows - 1) / kXwRows;
+  const auto rx = buf_rsrc(a.H, (uint32_t)(a.n_cols * a.ldh * 4));
+  const uint32_t ldx_b = (uint32_t)a.ldh * 4u;
+  // this wave's Wn fragments in the image (A operand: A[c][k] = Wn[k][16 wave + c])
+  const auto rw = buf_rsrc(a.wimg, 4 * 8 * 3 * 64 * 16);
+  uint32_t *rec = reinterpret_cast<uint32_t *>(lds + kXmWinOff) + (2 * wave + grp) * 32 * 4;
+  const int64_t n_my = my_chunks(n_chunks);
+  const RowSeq seq{(int64_t)blockIdx.x * kXwRows + 2 * wave + grp, (int64_t)gridDim.x * kXwRows,
+                   a.n_rows};
+  RowMeta cur, nxt;
+  meta_rowptr(a.rowptr, seq.row(0), seq.row(0) < a.n_rows, cur);
+  meta_first(a.col, a.w, gl, cur);
+  meta_rowptr(a.rowptr, seq.row(1), seq.row(1) < a.n_rows, nxt);
+  int it = 0;
+  for (int64_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x, ++it) {
+    char *buf = lds + (it & 1) * kXfBuf;
+    const int64_t r0 = chunk * kXwRows;
+    const int64_t left = a.n_rows - r0;
+    const uint32_t rows_in = (uint32_t)(left >= kXwRows ? kXwRows : left);
+#pragma unroll 1
+    for (int p = 0; p < 2; ++p) {
+      const int lr = 16 * p + 2 * wave + grp;
+      const int64_t k = 2 * it + p;
+      meta_first(a.col, a.w, gl, nxt);
+      RowMeta nn;
+      const int64_t r2 = seq.row(k + 2);
+      meta_rowptr(a.rowptr, r2, r2 < a.n_rows && k + 2 < 2 * n_my, nn);
+      float acc[4];
+      int win[4];
+      gather_row_max<U>(rx, ldx_b, a.col, a.w, cur, gl, grp, acc, win);
+      // epilogue (mgcn_spmm_fwd FWD_MAX): no edge -> 0, + bias, ReLU
+      float bb[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      if (a.bias != nullptr) *reinterpret_cast<float4 *>(bb) = *reinterpret_cast<const float4 *>(a.bias + 4 * gl);
+      float y[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float v = acc[j];
+        if (v == MGCN_MAX_FILL) {
+          v = 0.0f;
+          win[j] = -1;
+        }
+        if (a.bias != nullptr) v = __fadd_rn(v, bb[j]);
+        if (a.relu) v = (v < 0.0f) ? 0.0f : v;
+        y[j] = v;
+      }
+      const auto ry = buf_rsrc(a.Y + r0 * a.ldy, rows_in * (uint32_t)a.ldy * 4u);
+      __builtin_amdgcn_raw_buffer_store_b128(
+          __builtin_bit_cast(u32x4, make_float4(y[0], y[1], y[2], y[3])), ry,
+          4 * (int)(lr * a.ldy + 4 * gl), 0, MGCN_NT_OUT);
+      if (a.relu_mask != nullptr) {
+        const uint32_t m0 = (uint32_t)(__ballot(y[0] > 0.0f) >> (32 * grp));
+        const uint32_t m1 = (uint32_t)(__ballot(y[1] > 0.0f) >> (32 * grp));
+        const uint32_t m2 = (uint32_t)(__ballot(y[2] > 0.0f) >> (32 * grp));
+        const uint32_t m3 = (uint32_t)(__ballot(y[3] > 0.0f) >> (32 * grp));
+        if (gl == 0 && (uint32_t)lr < rows_in)
+          *reinterpret_cast<uint4 *>(a.relu_mask + (r0 + lr) * 4) = make_uint4(m0, m1, m2, m3);
+      }
+      // every edge's winner bits (mgcn_spmm_fwd's LDS windows): the group's
+      // 32-edge window of 16-B records, each lane ORs its four bits in (word
+      // gl / 8, bit 4 (gl % 8) + j), then lane gl writes record gl out.  One
+      // wave's LDS operations run in order: no barrier, only wave barriers.
+      {
+        const int64_t deg = cur.deg;
+        const int64_t odeg = __shfl_xor(deg, 32, 64);
+        const int64_t maxdeg = deg > odeg ? deg : odeg;
+        const int sh = (gl & 7) << 2;
+        for (int64_t w0 = 0; w0 < maxdeg; w0 += 32) {
+          *reinterpret_cast<uint4 *>(rec + 4 * gl) = make_uint4(0u, 0u, 0u, 0u);
+          __builtin_amdgcn_wave_barrier();
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int64_t pw = win[j] - w0;
+            if (win[j] >= 0 && pw >= 0 && pw < 32) atomicOr(rec + 4 * pw + (gl >> 3), 1u << (sh + j));
+          }
+          __builtin_amdgcn_wave_barrier();
+          const uint4 r = *reinterpret_cast<const uint4 *>(rec + 4 * gl);
+          if (w0 + gl < deg)
+            *reinterpret_cast<uint4 *>(a.win_mask + (cur.beg + w0 + gl) * 4) = r;
+          __builtin_amdgcn_wave_barrier();
+        }
+      }
+      store_row_terms(buf, lr, gl, y);
+      cur = nxt;
+      nxt = nn;
+    }
+    u32x4 wf[4][3];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int term = 0; term < 3; ++term)
+        wf[ks][term] = __builtin_amdgcn_raw_buffer_load_b128(
+            rw, 16 * (((ks * 8 + wave) * 3 + term) * 64 + lane), 0, 0);
+    __syncthreads();
+    // Hn = Y Wn: this wave's 16 columns of the chunk's 32 rows, D = Wn^T-frags
+    // x rows (lane: row l16 of the tile, columns 16 wave + 4 g4 .. + 3)
+    const auto rh = buf_rsrc(a.Hn + r0 * a.ldhn, rows_in * (uint32_t)a.ldhn * 4u);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      f32x4_t acc2 = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int off = img_off(16 * t + l16, 4 * ks + g4);
+        const bf16x8 xh = *reinterpret_cast<const bf16x8 *>(buf + off);
+        const bf16x8 xm = *reinterpret_cast<const bf16x8 *>(buf + kXwImg + off);
+        const bf16x8 xl = *reinterpret_cast<const bf16x8 *>(buf + 2 * kXwImg + off);
+        const bf16x8 wk[3] = {__builtin_bit_cast(bf16x8, wf[ks][0]), __builtin_bit_cast(bf16x8, wf[ks][1]),
+                              __builtin_bit_cast(bf16x8, wf[ks][2])};
+        acc2 = mfma16_x6_wa(wk, xh, xm, xl, acc2);
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(
+          __builtin_bit_cast(u32x4, make_float4(acc2[0], acc2[1], acc2[2], acc2[3])), rh,
+          4 * (int)((16 * t + l16) * a.ldhn + 16 * wave + 4 * g4), 0, MGCN_NT_OUT);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Backward.  LDS: X images, dH images (single-buffered: two barriers per
 // chunk), the chunk's mask / divisor words, the dX staging tile.  dX: wave w
 // owns columns 16 w .. +15; its W^T fragments are re-read from L2 (W is
@@ -1263,6 +1527,7 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
   }
 }
 
+int g_xm_unroll = 6;  // mgcn_set_option("xw_ws_xm_unroll"): max+next gathers in flight (4 / 6 / 8)
 int g_xw_ws = 0;  // mgcn_set_option("xw_ws"): the warp-specialised dX-only adjoint
 
 int bs_grid() {
@@ -1300,6 +1565,14 @@ int launch_bs(const XbsArgs &a, int epi, int grid, hipStream_t s) {
 }  // namespace
 
 int xw_set_ws(const char *name, int value) {
+  if (name[6] == 'x') {  // "xw_ws_xm_unroll"
+    if (value != 4 && value != 6 && value != 8) {
+      set_error("xw_ws_xm_unroll must be 4, 6 or 8");
+      return MGCN_EINVAL;
+    }
+    g_xm_unroll = value;
+    return MGCN_OK;
+  }
   if (name[6] == 'd') {  // "xw_ws_dbg"
     g_bs_dbg = value;
     return MGCN_OK;
@@ -1632,4 +1905,68 @@ extern "C" int mgcn_spmm_xw_bwd_dwl(int64_t n_rows, int64_t n_cols, const int64_
                            accumulate_dw, s);
   if (rc || epi == EPI_STORE) return rc;
   return launch_fold(a.colsum_partial, g, kXwF, kXwF, colsum, kXwF, accumulate_colsum, s);
+}
+
+extern "C" size_t mgcn_spmm_max_xw_fwd_workspace_bytes(void) { return 4 * 8 * 3 * 64 * 16; }
+
+extern "C" int mgcn_spmm_max_xw_fwd(int64_t n_rows, int64_t n_cols, const int64_t *rowptr,
+                                    const int32_t *col, const float *w, const float *H,
+                                    int64_t ldh, const float *bias, int relu, float *Y, int64_t ldy,
+                                    uint32_t *relu_mask, uint32_t *win_mask, const float *Wn,
+                                    int64_t ldwn, float *Hn, int64_t ldhn, void *workspace,
+                                    size_t workspace_bytes, void *stream) {
+  clear_error();
+  MGCN_REQUIRE(n_rows >= 0, "mgcn_spmm_max_xw_fwd: negative size");
+  MGCN_REQUIRE(gemm_precision_is_x6(), "mgcn_spmm_max_xw_fwd: needs the bf16x6 products");
+  MGCN_REQUIRE(relu_mask == nullptr || relu, "mgcn_spmm_max_xw_fwd: relu_mask needs relu");
+  if (n_rows == 0) return MGCN_OK;
+  MGCN_REQUIRE(rowptr && H && Y && win_mask && Wn && Hn, "mgcn_spmm_max_xw_fwd: null array");
+  MGCN_REQUIRE(ldh >= kXwF && ldh % 4 == 0 && reinterpret_cast<uintptr_t>(H) % 16 == 0,
+               "mgcn_spmm_max_xw_fwd: H must have 16-byte aligned rows");
+  MGCN_REQUIRE(n_cols > 0 && (uint64_t)n_cols * (uint64_t)ldh * 4u <= 0xfffffff0ull,
+               "mgcn_spmm_max_xw_fwd: H must hold 1 .. 4 GiB - 1 bytes (32-bit gather offsets)");
+  MGCN_REQUIRE(ldy >= kXwF && ldhn >= kXwF && ldwn >= kXwF &&
+                   (uint64_t)kXwRows * (uint64_t)(ldy > ldhn ? ldy : ldhn) * 4u < (1ull << 31),
+               "mgcn_spmm_max_xw_fwd: bad leading dimension");
+  MGCN_REQUIRE(bias == nullptr || reinterpret_cast<uintptr_t>(bias) % 16 == 0,
+               "mgcn_spmm_max_xw_fwd: bias not 16-byte aligned");
+  MGCN_REQUIRE(relu_mask == nullptr || reinterpret_cast<uintptr_t>(relu_mask) % 16 == 0,
+               "mgcn_spmm_max_xw_fwd: relu_mask not 16-byte aligned");
+  XmArgs a{};
+  a.n_rows = n_rows;
+  a.rowptr = rowptr;
+  a.col = col;
+  a.w = w;
+  a.H = H;
+  a.ldh = ldh;
+  a.n_cols = n_cols;
+  a.bias = bias;
+  a.relu = relu != 0;
+  a.Y = Y;
+  a.ldy = ldy;
+  a.relu_mask = relu_mask;
+  a.win_mask = win_mask;
+  a.Hn = Hn;
+  a.ldhn = ldhn;
+  if (workspace == nullptr || workspace_bytes < mgcn_spmm_max_xw_fwd_workspace_bytes() ||
+      reinterpret_cast<uintptr_t>(workspace) % 16 != 0) {
+    set_error("mgcn_spmm_max_xw_fwd: workspace %zu < %zu (16-byte aligned)", workspace_bytes,
+              mgcn_spmm_max_xw_fwd_workspace_bytes());
+    return MGCN_EWORKSPACE;
+  }
+  a.wimg = static_cast<const u32x4 *>(workspace);
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(xm_wimg_kernel, dim3(8), dim3(256), 0, s, Wn, ldwn,
+                     static_cast<u32x4 *>(workspace));
+  if (int rc = check_launch("xm_wimg_kernel")) return rc;
+  const int64_t n_chunks = (n_rows + kXwRows - 1) / kXwRows;
+  int64_t grid = xw_grid();
+  if (grid > n_chunks) grid = n_chunks;
+  if (g_xm_unroll == 8)
+    hipLaunchKernelGGL((spmm_max_xw_kernel<8>), dim3((unsigned)grid), dim3(kXwThreads), 0, s, a);
+  else if (g_xm_unroll == 4)
+    hipLaunchKernelGGL((spmm_max_xw_kernel<4>), dim3((unsigned)grid), dim3(kXwThreads), 0, s, a);
+  else
+    hipLaunchKernelGGL((spmm_max_xw_kernel<6>), dim3((unsigned)grid), dim3(kXwThreads), 0, s, a);
+  return check_launch("spmm_max_xw_kernel");
 }

@@ -63,6 +63,20 @@ def set_z_middle(enabled: bool) -> None:
     _Z_MIDDLE = bool(enabled)
 
 
+# Max layers followed by another 128 -> 128 layer write that layer's x @ W from
+# their own epilogue (mgcn_spmm_max_xw_fwd): MGCN_MAX_NEXT=1 / set_max_next(True).
+# Off by default: at config 4 the fused launch takes 1.19 ms against 0.95 +
+# 0.24 ms for the max SpMM and the GEMM, no step gain.
+_MAX_NEXT = os.environ.get("MGCN_MAX_NEXT", "0") != "0"
+
+
+def set_max_next(enabled: bool) -> None:
+    """Max layers write the next layer's x @ W from their epilogue (True;
+    mgcn_spmm_max_xw_fwd) or leave it to a GEMM launch (False, the default)."""
+    global _MAX_NEXT
+    _MAX_NEXT = bool(enabled)
+
+
 def set_fused_dwl(enabled: bool) -> None:
     """Fuse the lower layer's dW = Z^T dY into the dX-only adjoint that
     produces its dY (True; mgcn_spmm_xw_bwd_dwl) or run the separate dense dW
@@ -328,6 +342,59 @@ def spmm_xw_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tens
         _TIMER(tname, False)
     L.check(rc, "mgcn_spmm_xw_bwd")
     return dW, dX, colsum
+
+
+def spmm_max_xw_supported(view: CSRView, W: torch.Tensor, Wn: torch.Tensor,
+                          ld: int | None = None) -> bool:
+    """:func:`spmm_max_xw_fwd` takes a max layer (W) followed by Wn: both
+    128 x 128, bf16x6, no heavy rows, the gathered table within 32-bit
+    offsets."""
+    return (tuple(W.shape) == (128, 128) and tuple(Wn.shape) == (128, 128) and
+            spmm_xw_supported(view, 128, 128, L.REDUCE_SUM, ld))
+
+
+def spmm_max_xw_fwd(view: CSRView, w: torch.Tensor | None, H: torch.Tensor,
+                    bias: torch.Tensor | None, relu: bool, Wn: torch.Tensor, nnz: int,
+                    relu_mask: torch.Tensor | None = None):
+    """A max layer and the next layer's transform in one launch
+    (``mgcn_spmm_max_xw_fwd``): Y = relu(max_k H[col_k] w_k + b) -- bit for bit
+    :func:`spmm_fwd` (REDUCE_MAX) -- with its ReLU mask words and every
+    edge's winner bits ([nnz, 4], the ``mask_plan`` layout), and Hn = Y Wn
+    (the next layer's x @ weight_node, gcn_base_models.py:201).  Returns
+    (Y, winner bits, Hn)."""
+    lib = L.load()
+    H = _contig_f32(H, "H")
+    Wn = Wn.detach()
+    if Wn.dtype != torch.float32 or Wn.stride(1) != 1:
+        Wn = Wn.to(torch.float32).contiguous()
+    dev = L.require_device(H, view.rowptr, w, bias, Wn, relu_mask)
+    if H.size(0) != view.n_cols or H.size(1) != 128:
+        raise ValueError(f"spmm_max_xw_fwd: H {tuple(H.shape)} for {view.n_cols} sources, F = 128")
+    if bias is not None:
+        bias = bias.detach().to(torch.float32).contiguous()
+        if bias.numel() != 128:
+            raise ValueError(f"bias has {bias.numel()} entries, expected 128")
+    if relu_mask is not None and (relu_mask.shape != (view.n_rows, 4) or
+                                  relu_mask.dtype != torch.int32 or not relu):
+        raise ValueError(f"spmm_max_xw_fwd: relu_mask must be int32 [{view.n_rows}, 4] with relu")
+    Y = torch.empty(view.n_rows, 128, dtype=torch.float32, device=dev)
+    Hn = torch.empty(view.n_rows, 128, dtype=torch.float32, device=dev)
+    win = torch.empty(max(int(nnz), 1), 4, dtype=torch.int32, device=dev)
+    ws_bytes = int(lib.mgcn_spmm_max_xw_fwd_workspace_bytes())
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    if _TIMER is not None:
+        _TIMER("spmm_max_xw_fwd", True, view.n_rows, view.edges)
+    with L.device_guard(dev):
+        rc = lib.mgcn_spmm_max_xw_fwd(view.n_rows, view.n_cols, L.ptr(view.rowptr),
+                                      L.ptr(view.col), L.ptr(w), L.ptr(H), H.stride(0),
+                                      L.ptr(bias), int(bool(relu)), L.ptr(Y), Y.stride(0),
+                                      L.ptr(relu_mask), L.ptr(win), L.ptr(Wn), Wn.stride(0),
+                                      L.ptr(Hn), Hn.stride(0), L.ptr(ws), ws_bytes,
+                                      L.stream_of(dev))
+    if _TIMER is not None:
+        _TIMER("spmm_max_xw_fwd", False)
+    L.check(rc, "mgcn_spmm_max_xw_fwd")
+    return Y, win, Hn
 
 
 def spmm_xw_bwd_dwl_supported(F_in: int, F_out: int) -> bool:
@@ -1101,6 +1168,7 @@ class _GCNStack(torch.autograd.Function):
     def forward(ctx, x, plan, norm, reduce, relus, *params):
         Ws, bs = params[0::2], params[1::2]
         h = x
+        H_next = None  # the next layer's x @ W when a max layer's epilogue wrote it
         inputs, outs, args, rmasks, zs = [], [], [], [], []
         for i, (W, b, relu) in enumerate(zip(Ws, bs, relus)):
             z = None
@@ -1140,9 +1208,16 @@ class _GCNStack(torch.autograd.Function):
                 if want_z:
                     h, z = h
             else:
-                H = _mm(h, W)
-                h, am = spmm_fwd(plan.fwd, norm.w_fwd, H, reduce, b, relu, mask_plan=plan,
-                                 relu_mask=rm)
+                H = H_next if H_next is not None else _mm(h, W)
+                H_next = None
+                if (reduce == L.REDUCE_MAX and _MAX_NEXT and _FUSE_XW and nxt is not None and
+                        spmm_max_xw_supported(plan.fwd, W, nxt, H.stride(0))):
+                    # the next layer's x @ W from this layer's epilogue
+                    h, am, H_next = spmm_max_xw_fwd(plan.fwd, norm.w_fwd, H, b, relu, nxt,
+                                                    plan.nnz, relu_mask=rm)
+                else:
+                    h, am = spmm_fwd(plan.fwd, norm.w_fwd, H, reduce, b, relu, mask_plan=plan,
+                                     relu_mask=rm)
             outs.append(h)
             args.append(am)  # max: winner bits per edge (adjoint slot order)
             rmasks.append(rm)
