@@ -434,10 +434,11 @@ def main():
                        "bf16x6 (exact 3-term bf16 split of each fp32 operand, 6 MFMA products, "
                        "fp32 accumulate; error at fp32 level, tests/test_gpu_parity.py); "
                        "forward fused as (A x) W in one launch per layer, keeping Z = A x; "
-                       "backward: the top layer's dW = Z^T dY in one dense pass "
-                       "(mgcn_gemm_bwd), every other layer's dW = Z^T dY fused into the "
-                       "warp-specialised dX-only adjoint that writes its dY "
-                       "(mgcn_spmm_xw_bwd_dwl); the bottom layer runs no gather "
+                       "backward: the top layer's dX-only adjoint (mgcn_spmm_xw_bwd, X = NULL) "
+                       "plus dW = Z^T dY in one dense pass (mgcn_gemm_bwd); the middle layer's "
+                       "adjoint gathers dY and forms dW = X^T (A^T dY) and dX in one launch "
+                       "(mgcn_spmm_xw_bwd with X); the bottom layer runs no gather, its "
+                       "dW = Z^T dY is the dense pass alone "
                        "(tests/test_gpu_fused.py, tests/test_gpu_headline.py)"),
         "config": {"workload": head["workload"], "nodes": N, "edges": n_edges, "nnz": nnz,
                    "feat": F, "layers": L, "global_batch": world if mode == "replica" else 1,

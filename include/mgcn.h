@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define MGCN_ABI_VERSION 18
+#define MGCN_ABI_VERSION 19
 
 /* return codes */
 #define MGCN_OK 0
@@ -413,6 +413,27 @@ int mgcn_spmm_xw_bwd(int64_t n_rows, int64_t n_cols, int32_t F_in, int32_t F_out
                      const float *row_div, float *colsum, const uint32_t *win_mask,
                      const int32_t *slot_map, void *workspace, size_t workspace_bytes,
                      void *stream);
+
+/*
+ * The top layer's adjoint (ABI v19; F = 128, bf16x6): mgcn_spmm_xw_bwd's
+ * dW + dX form (X, dW and dX required; no max) that also returns
+ *   dy_colsum[128] = sum over the rows of dY   (the layer's own bias gradient,
+ *                    autograd of `+ self.bias`, gcn_base_models.py:240)
+ * from the launch that already streams dY -- each workgroup sums the dY rows
+ * of its own row chunks beside the gathers -- so the top layer of a stack
+ * needs neither a separate pass over dY nor the forward's Z and the dense
+ * Z^T dY pass.  Needs n_rows == n_cols (every dY row is a row of the view:
+ * a whole, square graph).  Runs the warp-specialised kernel (one workgroup
+ * per CU); dX bit for bit mgcn_spmm_xw_bwd's; dW and the column sums folded
+ * in a fixed order (deterministic).  Scratch: mgcn_spmm_xw_bwd_workspace_bytes.
+ */
+int mgcn_spmm_xw_bwd_hcs(int64_t n_rows, int64_t n_cols, const int64_t *rowptr_t,
+                         const int32_t *col_t, const float *w_t, const float *row_scale,
+                         const float *dY, int64_t lddy, const float *X, int64_t ldx,
+                         const float *W, int64_t ldw, float *dW, int64_t lddw, int accumulate,
+                         float *dX, int64_t lddx, const uint32_t *relu_mask, const float *row_div,
+                         float *colsum, float *dy_colsum, void *workspace, size_t workspace_bytes,
+                         void *stream);
 
 /*
  * A max layer with the NEXT layer's transform in one launch (ABI v18; F = 128,

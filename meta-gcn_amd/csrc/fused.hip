@@ -1186,6 +1186,15 @@ int launch_xb_u(const XbArgs &a, int epi, int grid, hipStream_t s) {
 // wave, transposed image reads) for the whole launch: one 128 x 128 partial
 // per workgroup, folded in workgroup order.  Hand-offs: LDS counters as in
 // fused_wide.hip (bounded spins, abort word).
+//
+// DWS (round 5, option xw_ws_full): the SAME layer's dW = X^T dH, the
+// two-phase full adjoint's product, from the chunk's own X rows: the gather
+// waves load them under the gathers (as DWL's Zl) into the ring beside the dH
+// images, and each MFMA wave folds its two 32x32 tiles of X^T dH straight from
+// the ring after its dX columns -- no hand-off between the MFMA waves, no dX
+// images.  dX is bit for bit the two-phase kernel's; dW folds the same
+// products per chunk over a one-workgroup-per-CU split-K grid.
+constexpr int kBsDx = 0, kBsDwl = 1, kBsDws = 2;  // spmm_xw_bwd_ws_kernel MODE
 constexpr int kBsImgSet = 3 * kXwImg;          // one operand's three term images: 24 KB
 constexpr int kBsRingBuf = 2 * kBsImgSet;      // dH images + Zl images: 48 KB
 constexpr int kBsXOff = 2 * kBsRingBuf;        // two dX image sets (DWL)
@@ -1193,6 +1202,18 @@ constexpr int kBsCtrOff = kBsXOff + 2 * kBsImgSet;
 constexpr int kBsLds = kBsCtrOff + 64;         // 144 KB + counters
 static_assert(kBsLds <= 160 * 1024, "one warp-specialised adjoint workgroup per CU");
 static_assert(16 * kXwF * 4 <= kBsXOff, "column-sum fold fits in the ring");
+// DWS layout: a ring of two (dH term images + X fp32 rows) chunk buffers and
+// W in fp32 (rows padded to 528 B: the 16 rows of a W^T fragment read and the
+// two row halves of an X^T fragment read fall on distinct banks); the MFMA
+// waves split W^T and X^T fragments as they read them
+constexpr int kDsXLd = kXwF + 4;                    // floats per padded row
+constexpr int kDsXOff = kBsImgSet;                  // X rows within a ring buffer
+constexpr int kDsRingBuf = kDsXOff + kXwRows * kDsXLd * 4;
+constexpr int kDsWOff = 2 * kDsRingBuf;
+constexpr int kDsCtrOff = kDsWOff + kXwF * kDsXLd * 4;
+constexpr int kDsLds = kDsCtrOff + 64;
+static_assert(kDsLds <= 160 * 1024, "one DWS workgroup per CU");
+static_assert(16 * kXwF * 4 <= kDsWOff, "column-sum fold fits in the ring");
 constexpr int kBsNG = 8, kBsNM = 8;
 constexpr int kBsThreads = 64 * (kBsNG + kBsNM);
 constexpr uint32_t kBsSpinLimit = 1u << 25;
@@ -1243,21 +1264,32 @@ struct XbsArgs {
   const float *Zl;      // DWL: the lower layer's aggregate [n_rows][128]
   int64_t ldz;
   float *dwl_partial;   // DWL: [grid][128][128]
+  float *hcs_partial;   // DWS (nullable): [grid][128] column sums of dY's own rows
   int dbg;              // xw_ws_dbg (timing experiments only; 0 in production)
 };
 
-template <int U, int EPI, bool DWL>
+template <int U, int EPI, int MODE>
 __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArgs A) {
+  constexpr bool DWL = MODE == kBsDwl, DWS = MODE == kBsDws;
+  constexpr int kRing = DWS ? kDsRingBuf : kBsRingBuf;
   const XbArgs &a = A.b;
-  __shared__ __attribute__((aligned(16))) char lds[kBsLds];
+  __shared__ __attribute__((aligned(16))) char lds[DWS ? kDsLds : kBsLds];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int gl = lane & 31, grp = lane >> 5;
   const int l16 = lane & 15, g4 = lane >> 4;
-  int *ctr = reinterpret_cast<int *>(lds + kBsCtrOff);
+  int *ctr = reinterpret_cast<int *>(lds + (DWS ? kDsCtrOff : kBsCtrOff));
   int *filled = ctr, *mdone = ctr + 2, *freed = ctr + 4, *xdone = ctr + 6, *abort_word = ctr + 8;
   if (tid < 16) ctr[tid] = 0;
+  if constexpr (DWS) {  // W (64 KB) into LDS once: four float4 per thread
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int e = tid + kBsThreads * j;  // float4 e: row e >> 5, columns 4 (e & 31) ..
+      const float4 v = *reinterpret_cast<const float4 *>(a.W + (int64_t)(e >> 5) * a.ldw + 4 * (e & 31));
+      *reinterpret_cast<float4 *>(lds + kDsWOff + 4 * ((e >> 5) * kDsXLd + 4 * (e & 31))) = v;
+    }
+  }
   __syncthreads();
 
   const int64_t n_chunks = (a.n_rows + kXwRows - 1) / kXwRows;
@@ -1269,7 +1301,8 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
   };
 
   float cs[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // MFMA waves: column sums of their 4 columns
-  f32x16 accw[2];                          // MFMA waves (DWL): two 32 x 32 dWl tiles
+  float hc[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // gather waves (DWS, hcs_partial): dY column sums
+  f32x16 accw[2];                          // MFMA waves (DWL / DWS): two 32 x 32 dW tiles
 #pragma unroll
   for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -1308,15 +1341,36 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
       const int64_t r0 = c * kXwRows;
       const int lr0 = 4 * (int)(q & 7) + grp;
       u32x4 zv[2] = {};
-      if (DWL && !(A.dbg & 4)) {  // the rows' Zl, under the gathers (streamed once)
+      if ((DWL || DWS) && !(A.dbg & 4)) {  // the rows' Zl / X, under the gathers (streamed once)
         const auto rz = buf_rsrc(A.Zl + r0 * A.ldz, rows_in(c) * (uint32_t)A.ldz * 4u);
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           zv[j] = __builtin_amdgcn_raw_buffer_load_b128(
               rz, 4 * (int)((lr0 + 2 * j) * A.ldz + 4 * gl), 0, MGCN_NT_AUX);
       }
+      // DWS + hcs_partial (n_cols == n_rows): the rows' own dY rows, whose
+      // column sums are the layer's bias gradient -- every dY row once, rows
+      // q then q + 2 of every quad: a fixed order
+      u32x4 yv[2] = {};
+      if (DWS && A.hcs_partial != nullptr) {
+        const auto ry = buf_rsrc(a.dY + r0 * a.lddy, rows_in(c) * (uint32_t)a.lddy * 4u);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          yv[j] = __builtin_amdgcn_raw_buffer_load_b128(
+              ry, 4 * (int)((lr0 + 2 * j) * a.lddy + 4 * gl), 0, 0);
+      }
       float acc[2][4];
       gather_row2_meta<U>(rdy, ldy_b, a.col, a.w, cur[0], cur[1], gl, grp, acc[0], acc[1]);
+      if (DWS && A.hcs_partial != nullptr) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const float4 y = __builtin_bit_cast(float4, yv[j]);
+          hc[0] = __fadd_rn(hc[0], y.x);
+          hc[1] = __fadd_rn(hc[1], y.y);
+          hc[2] = __fadd_rn(hc[2], y.z);
+          hc[3] = __fadd_rn(hc[3], y.w);
+        }
+      }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int64_t row = r0 + lr0 + 2 * j;
@@ -1329,10 +1383,12 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
       const int b = (int)(i & 1);
       const int gen = (int)(i >> 1);
       if (!bs_wait_ge(freed + b, gen, abort_word)) break;
-      char *buf = lds + b * kBsRingBuf;
+      char *buf = lds + b * kRing;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         store_row_terms(buf, lr0 + 2 * j, gl, acc[j]);
+        if constexpr (DWS)  // the X rows as they are (split by the MFMA waves)
+          *reinterpret_cast<u32x4 *>(buf + kDsXOff + 4 * ((lr0 + 2 * j) * kDsXLd + 4 * gl)) = zv[j];
         if constexpr (DWL) {
           const float4 zf = __builtin_bit_cast(float4, zv[j]);
           const float zz[4] = {zf.x, zf.y, zf.z, zf.w};
@@ -1354,7 +1410,7 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
     // re-read from L2 and split per chunk instead (the MFMA waves have slack:
     // ~3 k of ~19 k cycles per chunk)
     const float *wp = a.W + (int64_t)(16 * m + l16) * a.ldw + 8 * g4;
-    constexpr bool kHoldW = !DWL || MGCN_BS_HOLDW;
+    constexpr bool kHoldW = MODE == kBsDx || MGCN_BS_HOLDW;
     bf16x8 wt[kHoldW ? 4 : 1][3];
     if constexpr (kHoldW) {
 #pragma unroll
@@ -1413,7 +1469,7 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
         for (int rt = 0; rt < 2; ++rt)
           if ((uint32_t)(16 * rt + l16) >= rv) dv[rt] = 1.0f;
       }
-      const char *buf = lds + b * kBsRingBuf;
+      const char *buf = lds + b * kRing;
       char *ximg = lds + kBsXOff + (int)(i & 1) * kBsImgSet;
       const auto rx = buf_rsrc(a.dX + r0 * a.lddx, rv * (uint32_t)a.lddx * 4u);
       f32x4_t acc2[2];
@@ -1421,19 +1477,50 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
       for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc2[rt][r] = 0.0f;
+      // W^T fragment rows: global (L2) or, DWS, the LDS copy
+      const float *wq = DWS ? reinterpret_cast<const float *>(lds + kDsWOff) +
+                                  (16 * m + l16) * kDsXLd + 8 * g4
+                            : wp;
       float4 wn0{}, wn1{};
       if constexpr (!kHoldW) {
-        wn0 = *reinterpret_cast<const float4 *>(wp);
-        wn1 = *reinterpret_cast<const float4 *>(wp + 4);
+        if (!(A.dbg & 8)) {  // dbg 8: no W^T loads (timing only: dX wrong)
+          wn0 = *reinterpret_cast<const float4 *>(wq);
+          wn1 = *reinterpret_cast<const float4 *>(wq + 4);
+        }
       }
+      if constexpr (DWS) {
+        // dW += X^T dH: X^T fragments (lane: column 32 ti + lc of rows
+        // 16 ks + 8 h + j) read from the fp32 rows and split here, dH^T
+        // fragments from the term images
+        if (!(A.dbg & 1)) {
+          const float *xr = reinterpret_cast<const float *>(buf + kDsXOff) + 32 * ti + (lane & 31);
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) {
+            float xv[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) xv[j] = xr[(16 * ks + 8 * h + j) * kDsXLd];
+            bf16x8 fa[3];
+            split3_bf16(xv, fa[0], fa[1], fa[2]);
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+              bf16x8 fb[3];
+#pragma unroll
+              for (int t = 0; t < 3; ++t) fb[t] = read8(buf + ks * 16 * 256 + t * kXwImg, offb[s2]);
+              accw[s2] = mfma_x6(fa[0], fa[1], fa[2], fb[0], fb[1], fb[2], accw[s2]);
+            }
+          }
+        }
+      }
+      // DWS with dX == NULL: dW alone (the same partials as with dX)
+      if (!DWS || a.dX != nullptr) {
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         bf16x8 wk[3];
         if constexpr (!kHoldW) {
           const float v8[8] = {wn0.x, wn0.y, wn0.z, wn0.w, wn1.x, wn1.y, wn1.z, wn1.w};
-          if (ks + 1 < 4) {
-            wn0 = *reinterpret_cast<const float4 *>(wp + 32 * (ks + 1));
-            wn1 = *reinterpret_cast<const float4 *>(wp + 32 * (ks + 1) + 4);
+          if (ks + 1 < 4 && !(A.dbg & 8)) {
+            wn0 = *reinterpret_cast<const float4 *>(wq + 32 * (ks + 1));
+            wn1 = *reinterpret_cast<const float4 *>(wq + 32 * (ks + 1) + 4);
           }
           split3_bf16(v8, wk[0], wk[1], wk[2]);
         } else {
@@ -1467,6 +1554,7 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
             4 * (int)(row * a.lddx + 16 * m + 4 * g4), 0, MGCN_NT_OUT);
         if constexpr (DWL) store_row_terms(ximg, row, 4 * m + g4, v);
       }
+      }
       if (DWL && !(A.dbg & 1)) {
         // every wave's 16 columns of the chunk's dX images are in
         bs_signal(xdone + (int)(i & 1), 1, lane);
@@ -1497,7 +1585,7 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
   __syncthreads();
   if (wave >= kBsNG) {
     const int m = wave - kBsNG;
-    if constexpr (DWL) {
+    if constexpr (DWL || DWS) {
       const int h = lane >> 5, lc = lane & 31;
       const int ti = m >> 1, tj0 = 2 * (m & 1);
       float *slab = A.dwl_partial + (int64_t)blockIdx.x * kXwF * kXwF;
@@ -1515,20 +1603,39 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
           make_float4(cs[0], cs[1], cs[2], cs[3]);
     }
   }
-  if constexpr (EPI != EPI_STORE) {
+  if constexpr (DWS) {
+    if (A.hcs_partial != nullptr) {  // (past the dX column sums' [16][128] in LDS)
+      float *red2 = reinterpret_cast<float *>(lds) + 16 * kXwF;
+      if (wave < kBsNG)
+        *reinterpret_cast<float4 *>(red2 + (2 * wave + grp) * kXwF + 4 * gl) =
+            make_float4(hc[0], hc[1], hc[2], hc[3]);
+    }
+  }
+  if (EPI != EPI_STORE || (DWS && A.hcs_partial != nullptr)) {
     __syncthreads();
-    if (tid < kXwF) {
-      const float *red = reinterpret_cast<const float *>(lds);
+    if constexpr (EPI != EPI_STORE) {
+      if (tid < kXwF) {
+        const float *red = reinterpret_cast<const float *>(lds);
+        float s = 0.0f;
+#pragma unroll
+        for (int l = 0; l < 16; ++l) s = __fadd_rn(s, red[l * kXwF + tid]);
+        a.colsum_partial[(int64_t)blockIdx.x * kXwF + tid] = s;
+      }
+    }
+    if (DWS && A.hcs_partial != nullptr && tid >= kXwF && tid < 2 * kXwF) {
+      const int f = tid - kXwF;
+      const float *red2 = reinterpret_cast<const float *>(lds) + 16 * kXwF;
       float s = 0.0f;
 #pragma unroll
-      for (int l = 0; l < 16; ++l) s = __fadd_rn(s, red[l * kXwF + tid]);
-      a.colsum_partial[(int64_t)blockIdx.x * kXwF + tid] = s;
+      for (int l = 0; l < 16; ++l) s = __fadd_rn(s, red2[l * kXwF + f]);
+      A.hcs_partial[(int64_t)blockIdx.x * kXwF + f] = s;
     }
   }
 }
 
 int g_xm_unroll = 6;  // mgcn_set_option("xw_ws_xm_unroll"): max+next gathers in flight (4 / 6 / 8)
 int g_xw_ws = 0;  // mgcn_set_option("xw_ws"): the warp-specialised dX-only adjoint
+int g_xw_ws_full = 1;  // mgcn_set_option("xw_ws_full"): the warp-specialised dW + dX adjoint (DWS)
 
 int bs_grid() {
   int dev = 0, cus = 256;
@@ -1538,16 +1645,16 @@ int bs_grid() {
   return cus;  // one workgroup per CU
 }
 
-template <int U, bool DWL>
+template <int U, int MODE>
 int launch_bs_u(const XbsArgs &a, int epi, int grid, hipStream_t s) {
   if (epi == EPI_RELU_DIV)
-    hipLaunchKernelGGL((spmm_xw_bwd_ws_kernel<U, EPI_RELU_DIV, DWL>), dim3(grid), dim3(kBsThreads),
+    hipLaunchKernelGGL((spmm_xw_bwd_ws_kernel<U, EPI_RELU_DIV, MODE>), dim3(grid), dim3(kBsThreads),
                        0, s, a);
   else if (epi == EPI_RELU)
-    hipLaunchKernelGGL((spmm_xw_bwd_ws_kernel<U, EPI_RELU, DWL>), dim3(grid), dim3(kBsThreads), 0,
+    hipLaunchKernelGGL((spmm_xw_bwd_ws_kernel<U, EPI_RELU, MODE>), dim3(grid), dim3(kBsThreads), 0,
                        s, a);
   else
-    hipLaunchKernelGGL((spmm_xw_bwd_ws_kernel<U, EPI_STORE, DWL>), dim3(grid), dim3(kBsThreads), 0,
+    hipLaunchKernelGGL((spmm_xw_bwd_ws_kernel<U, EPI_STORE, MODE>), dim3(grid), dim3(kBsThreads), 0,
                        s, a);
   return check_launch("spmm_xw_bwd_ws_kernel");
 }
@@ -1557,9 +1664,9 @@ int g_bs_unroll = 4;
 // skip the dW phase and its sync, bit 1 skip the dW products, bit 2 skip Zl loads
 int g_bs_dbg = 0;  // mgcn_set_option("xw_ws_unroll"): gathers in flight per row (4 / 8)
 
-template <bool DWL>
+template <int MODE>
 int launch_bs(const XbsArgs &a, int epi, int grid, hipStream_t s) {
-  return g_bs_unroll == 4 ? launch_bs_u<4, DWL>(a, epi, grid, s) : launch_bs_u<8, DWL>(a, epi, grid, s);
+  return g_bs_unroll == 4 ? launch_bs_u<4, MODE>(a, epi, grid, s) : launch_bs_u<8, MODE>(a, epi, grid, s);
 }
 
 }  // namespace
@@ -1571,6 +1678,14 @@ int xw_set_ws(const char *name, int value) {
       return MGCN_EINVAL;
     }
     g_xm_unroll = value;
+    return MGCN_OK;
+  }
+  if (name[6] == 'f') {  // "xw_ws_full"
+    if (value < 0 || value > 1) {
+      set_error("xw_ws_full must be 0 or 1");
+      return MGCN_EINVAL;
+    }
+    g_xw_ws_full = value;
     return MGCN_OK;
   }
   if (name[6] == 'd') {  // "xw_ws_dbg"
@@ -1699,15 +1814,15 @@ extern "C" size_t mgcn_spmm_xw_bwd_workspace_bytes(int64_t n_rows, int32_t F_in,
   return align_up(g * kXwF * kXwF * 4, 256) + align_up(g * kXwF * 4, 256);
 }
 
-extern "C" int mgcn_spmm_xw_bwd(int64_t n_rows, int64_t n_cols, int32_t F_in, int32_t F_out,
-                                const int64_t *rowptr_t, const int32_t *col_t, const float *w_t,
-                                const float *row_scale, const float *dY, int64_t lddy,
-                                const float *X, int64_t ldx, const float *W, int64_t ldw,
-                                float *dW, int64_t lddw, int accumulate, float *dX, int64_t lddx,
-                                const uint32_t *relu_mask, const float *row_div, float *colsum,
-                                const uint32_t *win_mask, const int32_t *slot_map,
-                                void *workspace, size_t workspace_bytes, void *stream) {
-  clear_error();
+namespace {
+// mgcn_spmm_xw_bwd and (dy_colsum != NULL) mgcn_spmm_xw_bwd_hcs
+int xw_bwd_impl(int64_t n_rows, int64_t n_cols, int32_t F_in, int32_t F_out,
+                const int64_t *rowptr_t, const int32_t *col_t, const float *w_t,
+                const float *row_scale, const float *dY, int64_t lddy, const float *X,
+                int64_t ldx, const float *W, int64_t ldw, float *dW, int64_t lddw, int accumulate,
+                float *dX, int64_t lddx, const uint32_t *relu_mask, const float *row_div,
+                float *colsum, const uint32_t *win_mask, const int32_t *slot_map,
+                float *dy_colsum, void *workspace, size_t workspace_bytes, void *stream) {
   MGCN_REQUIRE(n_rows >= 0, "mgcn_spmm_xw_bwd: negative size");
   MGCN_REQUIRE((win_mask == nullptr) == (slot_map == nullptr),
                "mgcn_spmm_xw_bwd: win_mask and slot_map go together (max adjoint)");
@@ -1724,6 +1839,7 @@ extern "C" int mgcn_spmm_xw_bwd(int64_t n_rows, int64_t n_cols, int32_t F_in, in
                "mgcn_spmm_xw_bwd: row_div needs relu_mask");
   hipStream_t s = as_stream(stream);
   if (n_rows == 0) {  // an empty row range (a sharded chunk): no dX rows to write
+    if (dy_colsum) MGCN_HIP_TRY(hipMemsetAsync(dy_colsum, 0, sizeof(float) * F_out, s));
     if (!accumulate && dW != nullptr)
       for (int32_t r = 0; r < F_in; ++r)
         MGCN_HIP_TRY(hipMemsetAsync(dW + r * lddw, 0, sizeof(float) * F_out, s));
@@ -1801,7 +1917,7 @@ extern "C" int mgcn_spmm_xw_bwd(int64_t n_rows, int64_t n_cols, int32_t F_in, in
     XbsArgs sa{};
     sa.b = a;
     const int64_t g = bs_grid() < n_chunks ? bs_grid() : n_chunks;
-    rc = launch_bs<false>(sa, epi, (int)g, s);
+    rc = launch_bs<kBsDx>(sa, epi, (int)g, s);
     if (rc || epi == EPI_STORE) return rc;
     return launch_fold(a.colsum_partial, g, kXwF, kXwF, colsum, kXwF, accumulate, s);
   }
@@ -1812,11 +1928,62 @@ extern "C" int mgcn_spmm_xw_bwd(int64_t n_rows, int64_t n_cols, int32_t F_in, in
     // of one adjoint fold their bias gradient on the device)
     return launch_fold(a.colsum_partial, grid, kXwF, kXwF, colsum, kXwF, accumulate, s);
   }
-  rc = g_xw_unroll == 4 ? launch_xb_u<4>(a, epi, grid, s) : launch_xb_u<8>(a, epi, grid, s);
+  float *hcs_partial = nullptr;
+  if ((g_xw_ws_full || dy_colsum) && win_mask == nullptr) {
+    // the warp-specialised dW + dX (or dW-only) form (one workgroup per CU; DWS)
+    XbsArgs sa{};
+    sa.b = a;
+    sa.Zl = X;
+    sa.ldz = ldx;
+    sa.dwl_partial = a.dw_partial;
+    sa.dbg = g_bs_dbg;
+    grid = bs_grid() < n_chunks ? bs_grid() : (int)n_chunks;
+    // dY's column sums: [grid][128] partials past the grid's dW slabs (the
+    // dW partial area holds xw_grid() = 2 x CUs slabs, this grid <= CUs)
+    if (dy_colsum) hcs_partial = a.dw_partial + (size_t)grid * kXwF * kXwF;
+    sa.hcs_partial = hcs_partial;
+    rc = launch_bs<kBsDws>(sa, epi, grid, s);
+  } else {
+    rc = g_xw_unroll == 4 ? launch_xb_u<4>(a, epi, grid, s) : launch_xb_u<8>(a, epi, grid, s);
+  }
   if (rc) return rc;
   rc = launch_split_reduce(a.dw_partial, grid, (int64_t)kXwF * kXwF, kXwF, dW, lddw, accumulate, s);
+  if (rc == MGCN_OK && hcs_partial) rc = launch_colsum_fold(hcs_partial, grid, kXwF, dy_colsum, s);
   if (rc || epi == EPI_STORE) return rc;
   return launch_colsum_fold(a.colsum_partial, grid, kXwF, colsum, s);
+}
+}  // namespace
+
+extern "C" int mgcn_spmm_xw_bwd(int64_t n_rows, int64_t n_cols, int32_t F_in, int32_t F_out,
+                                const int64_t *rowptr_t, const int32_t *col_t, const float *w_t,
+                                const float *row_scale, const float *dY, int64_t lddy,
+                                const float *X, int64_t ldx, const float *W, int64_t ldw,
+                                float *dW, int64_t lddw, int accumulate, float *dX, int64_t lddx,
+                                const uint32_t *relu_mask, const float *row_div, float *colsum,
+                                const uint32_t *win_mask, const int32_t *slot_map,
+                                void *workspace, size_t workspace_bytes, void *stream) {
+  clear_error();
+  return xw_bwd_impl(n_rows, n_cols, F_in, F_out, rowptr_t, col_t, w_t, row_scale, dY, lddy, X,
+                     ldx, W, ldw, dW, lddw, accumulate, dX, lddx, relu_mask, row_div, colsum,
+                     win_mask, slot_map, nullptr, workspace, workspace_bytes, stream);
+}
+
+extern "C" int mgcn_spmm_xw_bwd_hcs(int64_t n_rows, int64_t n_cols, const int64_t *rowptr_t,
+                                    const int32_t *col_t, const float *w_t,
+                                    const float *row_scale, const float *dY, int64_t lddy,
+                                    const float *X, int64_t ldx, const float *W, int64_t ldw,
+                                    float *dW, int64_t lddw, int accumulate, float *dX,
+                                    int64_t lddx, const uint32_t *relu_mask,
+                                    const float *row_div, float *colsum, float *dy_colsum,
+                                    void *workspace, size_t workspace_bytes, void *stream) {
+  clear_error();
+  MGCN_REQUIRE(n_rows == n_cols, "mgcn_spmm_xw_bwd_hcs: needs n_rows == n_cols (%lld, %lld): "
+               "every dY row a row of the view", (long long)n_rows, (long long)n_cols);
+  MGCN_REQUIRE(X != nullptr && dW != nullptr && dX != nullptr && dy_colsum != nullptr,
+               "mgcn_spmm_xw_bwd_hcs: X, dW, dX and dy_colsum are required");
+  return xw_bwd_impl(n_rows, n_cols, kXwF, kXwF, rowptr_t, col_t, w_t, row_scale, dY, lddy, X,
+                     ldx, W, ldw, dW, lddw, accumulate, dX, lddx, relu_mask, row_div, colsum,
+                     nullptr, nullptr, dy_colsum, workspace, workspace_bytes, stream);
 }
 
 #ifdef MGCN_XW_PROFILE
@@ -1899,7 +2066,7 @@ extern "C" int mgcn_spmm_xw_bwd_dwl(int64_t n_rows, int64_t n_cols, const int64_
   a.colsum_partial = reinterpret_cast<float *>(
       static_cast<char *>(workspace) + align_up((size_t)g * kXwF * kXwF * 4, 256));
   const int epi = relu_mask == nullptr ? EPI_STORE : row_div != nullptr ? EPI_RELU_DIV : EPI_RELU;
-  int rc = launch_bs<true>(sa, epi, (int)g, s);
+  int rc = launch_bs<kBsDwl>(sa, epi, (int)g, s);
   if (rc) return rc;
   rc = launch_split_reduce(sa.dwl_partial, (int)g, (int64_t)kXwF * kXwF, kXwF, dWl, lddw,
                            accumulate_dw, s);

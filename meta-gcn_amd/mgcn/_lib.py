@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmgcn.so")
 
 # constants mirrored from include/mgcn.h
-ABI_VERSION = 18
+ABI_VERSION = 19
 OK, EINVAL, EINDEX, EHIP, EWORKSPACE = 0, 1, 2, 3, 4
 REDUCE_SUM, REDUCE_MEAN, REDUCE_MAX = 0, 1, 2
 NORM_NONE, NORM_SM, NORM_RW = 0, 1, 2
@@ -79,6 +79,9 @@ SIGNATURES = {
     "mgcn_spmm_xw_bwd": (_int, [_i64, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64,
                                 _vp, _i64, _vp, _i64, _int, _vp, _i64, _vp, _vp, _vp, _vp, _vp,
                                 _vp, _sz, _vp]),
+    "mgcn_spmm_xw_bwd_hcs": (_int, [_i64, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp,
+                                    _i64, _vp, _i64, _int, _vp, _i64, _vp, _vp, _vp, _vp, _vp,
+                                    _sz, _vp]),
     "mgcn_spmm_xw_bwd_dwl_workspace_bytes": (_sz, [_i64]),
     "mgcn_spmm_xw_bwd_dwl": (_int, [_i64, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp,
                                     _i64, _vp, _vp, _vp, _int, _vp, _i64, _vp, _i64, _int, _vp,

@@ -46,6 +46,10 @@ _Z_MIDDLE = os.environ.get("MGCN_Z_MIDDLE", "0") != "0"
 # fused launch costs 1.17 ms against 0.87 + 0.22 ms for the dX-only adjoint
 # and the separate dW pass.
 _DWL = os.environ.get("MGCN_DWL", "0") != "0"
+# the top 128-wide layer of a stack (sum, no ReLU) takes the dW + dX adjoint
+# with its bias gradient from the same launch (mgcn_spmm_xw_bwd_hcs) instead of
+# keeping Z for the dense Z^T dY pass: env MGCN_TOP_FULL=0 turns it off
+_TOP_FULL = os.environ.get("MGCN_TOP_FULL", "1") != "0"
 
 
 def set_fused_layers(enabled: bool) -> None:
@@ -261,13 +265,17 @@ def spmm_xw_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tens
                 dY: torch.Tensor, X: torch.Tensor, W: torch.Tensor, want_dx: bool = True,
                 relu_mask: torch.Tensor | None = None, row_div: torch.Tensor | None = None,
                 win_mask: torch.Tensor | None = None, slot_map: torch.Tensor | None = None,
-                dx_out: torch.Tensor | None = None, colsum_acc: torch.Tensor | None = None):
+                dx_out: torch.Tensor | None = None, colsum_acc: torch.Tensor | None = None,
+                dy_colsum_out: torch.Tensor | None = None):
     """Both adjoints of a 128 -> 128 layer from one pass (``mgcn_spmm_xw_bwd``):
     dH = A^T dY [* row_scale] stays on chip, and dW = X^T dH, dX = dH W^T
     (with the lower layer's ReLU mask / row divisor / bias column sums, as
     :func:`gemm_bwd`) are formed from it.  Max: ``win_mask`` (the forward's
     winner bits, :func:`spmm_fwd` with ``mask_plan``) and the plan's
-    ``slot_map`` route dY as :func:`spmm_bwd` does.  Returns
+    ``slot_map`` route dY as :func:`spmm_bwd` does.  ``dy_colsum_out`` (a
+    float32 [F_out] tensor; the dW + dX form of a whole square graph, no max)
+    receives the column sums of dY itself -- the layer's own bias gradient --
+    from the same launch (``mgcn_spmm_xw_bwd_hcs``).  Returns
     (dW, dX or None, colsum or None)."""
     lib = L.load()
     dY = _contig_f32(dY, "dY")
@@ -324,11 +332,31 @@ def spmm_xw_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tens
     elif colsum_acc is not None:
         raise ValueError("spmm_xw_bwd: colsum_acc needs relu_mask")
     acc_flag = 1 if colsum_acc is not None else 0
+    if dy_colsum_out is not None:
+        if (dx_only or not want_dx or win_mask is not None or view_t.n_rows != view_t.n_cols or
+                dy_colsum_out.dtype != torch.float32 or
+                tuple(dy_colsum_out.shape) != (F_out,) or not dy_colsum_out.is_contiguous()):
+            raise ValueError("spmm_xw_bwd: dy_colsum_out needs the dW + dX form of a square "
+                             f"graph (no max) and a contiguous float32 [{F_out}] tensor")
+        L.require_device(dy_colsum_out)
     ws_bytes = int(lib.mgcn_spmm_xw_bwd_workspace_bytes(M, F_in, F_out))
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
     tname = "spmm_xw_bwd_dx" if dx_only else "spmm_xw_bwd" if want_dx else "spmm_xw_bwd_dw"
     if _TIMER is not None:
         _TIMER(tname, True, view_t.n_rows, view_t.edges)
+    if dy_colsum_out is not None:
+        with L.device_guard(dev):
+            rc = lib.mgcn_spmm_xw_bwd_hcs(M, view_t.n_cols, L.ptr(view_t.rowptr), L.ptr(view_t.col),
+                                          L.ptr(w_t), L.ptr(row_scale), L.ptr(dY), dY.stride(0),
+                                          L.ptr(X), X.stride(0), L.ptr(W), W.stride(0), L.ptr(dW),
+                                          dW.stride(0), 0, L.ptr(dX), dX.stride(0),
+                                          L.ptr(relu_mask), L.ptr(row_div), L.ptr(colsum),
+                                          L.ptr(dy_colsum_out), L.ptr(ws), ws_bytes,
+                                          L.stream_of(dev))
+        if _TIMER is not None:
+            _TIMER(tname, False)
+        L.check(rc, "mgcn_spmm_xw_bwd_hcs")
+        return dW, dX, colsum
     with L.device_guard(dev):
         rc = lib.mgcn_spmm_xw_bwd(M, view_t.n_cols, F_in, F_out, L.ptr(view_t.rowptr),
                                   L.ptr(view_t.col), L.ptr(w_t), L.ptr(row_scale), L.ptr(dY),
@@ -1198,7 +1226,11 @@ class _GCNStack(torch.autograd.Function):
                 dwl_next = (_DWL and nxt is not None and relu and
                             spmm_xw_bwd_dwl_supported(*W.shape) and
                             spmm_xw_bwd_dwl_supported(*nxt.shape))
-                want_z = (bool(ctx.needs_input_grad[5 + 2 * i]) and below and
+                top_full = (_TOP_FULL and i == len(Ws) - 1 and i > 0 and relus[i - 1] and
+                            rmasks[i - 1] is not None and not relu and
+                            reduce == L.REDUCE_SUM and plan.bwd.n_rows == plan.bwd.n_cols and
+                            xw_full_supported(*W.shape))
+                want_z = (bool(ctx.needs_input_grad[5 + 2 * i]) and below and not top_full and
                           (_Z_MIDDLE or dwl_next or not middle or
                            not xw_full_supported(*W.shape)) and
                           dw_pass_supported(W.size(0), W.size(1)) and
@@ -1256,9 +1288,18 @@ class _GCNStack(torch.autograd.Function):
                                           L.REDUCE_SUM))
 
         top_z = z_path(top) and not relus[top] and rd is None
-        if top_z:
+        # the top layer's bias gradient from its dW + dX adjoint (mgcn_spmm_xw_bwd_hcs):
+        # the forward kept no Z for it (top_full there); same predicate here
+        top_hcs = (_TOP_FULL and not zs[top].numel() and top > 0 and not relus[top] and
+                   rd is None and args[top].numel() == 0 and relus[top - 1] and
+                   rmasks[top - 1].numel() > 0 and ctx.needs_input_grad[5 + 2 * top] and
+                   ctx.has_bias[top] and plan.bwd.n_rows == plan.bwd.n_cols and
+                   _FUSE_XW and xw_full_supported(*Ws[top].shape) and
+                   spmm_xw_supported(plan.bwd, Ws[top].size(0), Ws[top].size(1), L.REDUCE_SUM))
+        if top_z or top_hcs:
             # dY = dZ as it is: its column sums (the top bias gradient) come
-            # from the dW = Z^T dY pass below, no separate read of dZ
+            # from the dW = Z^T dY pass below or from the top layer's dW + dX
+            # adjoint (top_hcs), no separate read of dZ
             dY = dZ.contiguous()
         else:
             dY, db = relu_bwd_colsum(dZ.contiguous(), outs[top], relus[top], ctx.has_bias[top],
@@ -1325,9 +1366,14 @@ class _GCNStack(torch.autograd.Function):
                 # 1.42 ms at config 4, so max fuses only the dW-only layer)
                 sm = plan.slot_map() if am is not None else None
                 if fused and am is None:
+                    hcs = None
+                    if top_hcs and l == top:
+                        hcs = gb[top] = torch.empty(W.size(1), dtype=torch.float32,
+                                                    device=dY.device)
                     gW[l], dY, db = spmm_xw_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY,
                                                 inputs[l], W, relu_mask=rmasks[l - 1],
-                                                row_div=rd, win_mask=am, slot_map=sm)
+                                                row_div=rd, win_mask=am, slot_map=sm,
+                                                dy_colsum_out=hcs)
                     gb[l - 1] = db if ctx.has_bias[l - 1] else None
                     continue
                 if l == 0 and not ctx.needs_input_grad[0]:

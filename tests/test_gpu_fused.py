@@ -406,7 +406,9 @@ def test_z_dw_and_dx_only_backward(cuda, oracle, N, E, hub, deg_norm, aggr, epi)
 def test_gcn_stack_keeps_z_only_where_the_backward_reads_it(cuda, acts):
     """The forward stores the aggregate Z of a layer only when the backward
     forms that layer's dW as Z^T dY: the bottom layer, or a layer whose lower
-    layer ends in a ReLU (its mask feeds the dX-only gather's epilogue).  A
+    layer ends in a ReLU (its mask feeds the dX-only gather's epilogue) --
+    except the top layer, which by default (ops._TOP_FULL) takes the dW + dX
+    adjoint with its bias gradient in the same launch and keeps no Z.  A
     layer above a 'none' layer keeps no N x F Z (and its gradients still
     match the two-launch stack)."""
     from mgcn import ops
@@ -423,7 +425,7 @@ def test_gcn_stack_keeps_z_only_where_the_backward_reads_it(cuda, acts):
     y = stack(x, ei)
     zs = y.grad_fn.saved_tensors[5 * n:6 * n]
     for i in range(n):
-        want = i == 0 or (acts[i - 1] == "relu" and i == n - 1)
+        want = i == 0 or (acts[i - 1] == "relu" and i == n - 1 and not ops._TOP_FULL)
         assert (zs[i].numel() > 0) == want, (i, acts)
     y.backward(dZ)
     got = [x.grad.clone()] + [p.grad.clone() for p in stack.parameters()]
