@@ -1194,7 +1194,10 @@ int launch_xb_u(const XbArgs &a, int epi, int grid, hipStream_t s) {
 // the ring after its dX columns -- no hand-off between the MFMA waves, no dX
 // images.  dX is bit for bit the two-phase kernel's; dW folds the same
 // products per chunk over a one-workgroup-per-CU split-K grid.
-constexpr int kBsDx = 0, kBsDwl = 1, kBsDws = 2;  // spmm_xw_bwd_ws_kernel MODE
+constexpr int kBsDx = 0, kBsDwl = 1, kBsDws = 2, kBsDwsH = 3;  // spmm_xw_bwd_ws_kernel MODE
+#ifndef MGCN_DS_MASK_RING
+#define MGCN_DS_MASK_RING 1  // DWS: ReLU mask words / divisors through the ring (0: MFMA waves load them)
+#endif
 constexpr int kBsImgSet = 3 * kXwImg;          // one operand's three term images: 24 KB
 constexpr int kBsRingBuf = 2 * kBsImgSet;      // dH images + Zl images: 48 KB
 constexpr int kBsXOff = 2 * kBsRingBuf;        // two dX image sets (DWL)
@@ -1208,7 +1211,9 @@ static_assert(16 * kXwF * 4 <= kBsXOff, "column-sum fold fits in the ring");
 // waves split W^T and X^T fragments as they read them
 constexpr int kDsXLd = kXwF + 4;                    // floats per padded row
 constexpr int kDsXOff = kBsImgSet;                  // X rows within a ring buffer
-constexpr int kDsRingBuf = kDsXOff + kXwRows * kDsXLd * 4;
+constexpr int kDsMaskOff = kDsXOff + kXwRows * kDsXLd * 4;  // [32][4] mask words
+constexpr int kDsDivOff = kDsMaskOff + kXwRows * 16;         // [32] row divisors
+constexpr int kDsRingBuf = kDsDivOff + kXwRows * 4;
 constexpr int kDsWOff = 2 * kDsRingBuf;
 constexpr int kDsCtrOff = kDsWOff + kXwF * kDsXLd * 4;
 constexpr int kDsLds = kDsCtrOff + 64;
@@ -1270,7 +1275,9 @@ struct XbsArgs {
 
 template <int U, int EPI, int MODE>
 __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArgs A) {
-  constexpr bool DWL = MODE == kBsDwl, DWS = MODE == kBsDws;
+  constexpr bool DWL = MODE == kBsDwl, DWS = MODE == kBsDws || MODE == kBsDwsH;
+  constexpr bool HCS = MODE == kBsDwsH;  // DWS + dY's column sums (hcs_partial)
+  constexpr bool MRING = DWS && MGCN_DS_MASK_RING;
   constexpr int kRing = DWS ? kDsRingBuf : kBsRingBuf;
   const XbArgs &a = A.b;
   __shared__ __attribute__((aligned(16))) char lds[DWS ? kDsLds : kBsLds];
@@ -1351,8 +1358,23 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
       // DWS + hcs_partial (n_cols == n_rows): the rows' own dY rows, whose
       // column sums are the layer's bias gradient -- every dY row once, rows
       // q then q + 2 of every quad: a fixed order
+      // DWS: the rows' ReLU mask words (lanes 0-3) and divisor (lane 4) ride
+      // through the ring to the MFMA waves' epilogue (no registers held there)
+      uint32_t mv[2] = {0u, 0u};
+      if constexpr (MRING && EPI != EPI_STORE) {
+        const auto rm = buf_rsrc(a.relu_mask + r0 * 4, rows_in(c) * 16u);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          if (gl < 4) mv[j] = __builtin_amdgcn_raw_buffer_load_b32(rm, 4 * ((lr0 + 2 * j) * 4 + gl), 0, 0);
+        if constexpr (EPI == EPI_RELU_DIV) {
+          const auto rd = buf_rsrc(a.row_div + r0, rows_in(c) * 4u);
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            if (gl == 4) mv[j] = __builtin_amdgcn_raw_buffer_load_b32(rd, 4 * (lr0 + 2 * j), 0, 0);
+        }
+      }
       u32x4 yv[2] = {};
-      if (DWS && A.hcs_partial != nullptr) {
+      if constexpr (HCS) {
         const auto ry = buf_rsrc(a.dY + r0 * a.lddy, rows_in(c) * (uint32_t)a.lddy * 4u);
 #pragma unroll
         for (int j = 0; j < 2; ++j)
@@ -1361,7 +1383,7 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
       }
       float acc[2][4];
       gather_row2_meta<U>(rdy, ldy_b, a.col, a.w, cur[0], cur[1], gl, grp, acc[0], acc[1]);
-      if (DWS && A.hcs_partial != nullptr) {
+      if constexpr (HCS) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const float4 y = __builtin_bit_cast(float4, yv[j]);
@@ -1389,6 +1411,12 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
         store_row_terms(buf, lr0 + 2 * j, gl, acc[j]);
         if constexpr (DWS)  // the X rows as they are (split by the MFMA waves)
           *reinterpret_cast<u32x4 *>(buf + kDsXOff + 4 * ((lr0 + 2 * j) * kDsXLd + 4 * gl)) = zv[j];
+        if constexpr (MRING && EPI != EPI_STORE) {
+          if (gl < 4)
+            *reinterpret_cast<uint32_t *>(buf + kDsMaskOff + 4 * ((lr0 + 2 * j) * 4 + gl)) = mv[j];
+          if (EPI == EPI_RELU_DIV && gl == 4)
+            *reinterpret_cast<uint32_t *>(buf + kDsDivOff + 4 * (lr0 + 2 * j)) = mv[j];
+        }
         if constexpr (DWL) {
           const float4 zf = __builtin_bit_cast(float4, zv[j]);
           const float zz[4] = {zf.x, zf.y, zf.z, zf.w};
@@ -1442,6 +1470,23 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
     };
     const int bit = 4 * m + g4;  // mask bit of this lane's columns (word r: column 16 m + 4 g4 + r)
     for (int64_t i = 0; i < n_my; ++i) {
+      // the lane-derived LDS offsets, recomputed per chunk from an opaque copy
+      // of the lane id: hoisted out of the loop they were spilled, and every
+      // scratch reload waited behind s_waitcnt vmcnt(0) -- i.e. for the
+      // previous chunk's dX stores too
+      int lane_o = lane;
+      asm volatile("" : "+v"(lane_o));
+      const int l16 = lane_o & 15, g4 = lane_o >> 4, h = lane_o >> 5;
+      int offb[2][2];
+      {
+        const int q = (lane_o >> 2) & 3, p4 = lane_o & 3;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int r = 0; r < 2; ++r)
+            offb[s2][r] = img_off(8 * h + q + 4 * r, 4 * (tj0 + s2) + 2 * (g4 & 1) + (p4 >> 1)) +
+                          8 * (p4 & 1);
+      }
       const int b = (int)(i & 1);
       const int gen = (int)(i >> 1);
       const int64_t c = chunk_of(i);
@@ -1449,7 +1494,7 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
       const uint32_t rv = rows_in(c);
       u32x4 mk[2] = {};
       float dv[2] = {1.0f, 1.0f};
-      if constexpr (EPI != EPI_STORE) {
+      if constexpr (EPI != EPI_STORE && !MRING) {
         const auto rm = buf_rsrc(a.relu_mask + r0 * 4, rv * 16u);
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt)
@@ -1462,6 +1507,17 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
         }
       }
       if (!bs_wait_ge(filled + b, kXwRows * (gen + 1), abort_word)) break;
+      uint32_t mbits[2] = {0u, 0u};  // MRING: this lane's 4 mask bits per row tile
+      if constexpr (EPI != EPI_STORE && MRING) {  // from the ring (the gather waves loaded them)
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) {
+          const u32x4 w4 = *reinterpret_cast<const u32x4 *>(lds + b * kRing + kDsMaskOff + 16 * (16 * rt + l16));
+#pragma unroll
+          for (int r = 0; r < 4; ++r) mbits[rt] |= ((w4[r] >> bit) & 1u) << r;
+          if constexpr (EPI == EPI_RELU_DIV)
+            dv[rt] = *reinterpret_cast<const float *>(lds + b * kRing + kDsDivOff + 4 * (16 * rt + l16));
+        }
+      }
       if constexpr (EPI == EPI_RELU_DIV) {
         // rows past the end read divisor 0: make it 1, so their zero rows stay
         // 0 (not 0 / 0) in the dX images dWl reads
@@ -1471,29 +1527,13 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
       }
       const char *buf = lds + b * kRing;
       char *ximg = lds + kBsXOff + (int)(i & 1) * kBsImgSet;
-      const auto rx = buf_rsrc(a.dX + r0 * a.lddx, rv * (uint32_t)a.lddx * 4u);
-      f32x4_t acc2[2];
-#pragma unroll
-      for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc2[rt][r] = 0.0f;
-      // W^T fragment rows: global (L2) or, DWS, the LDS copy
-      const float *wq = DWS ? reinterpret_cast<const float *>(lds + kDsWOff) +
-                                  (16 * m + l16) * kDsXLd + 8 * g4
-                            : wp;
-      float4 wn0{}, wn1{};
-      if constexpr (!kHoldW) {
-        if (!(A.dbg & 8)) {  // dbg 8: no W^T loads (timing only: dX wrong)
-          wn0 = *reinterpret_cast<const float4 *>(wq);
-          wn1 = *reinterpret_cast<const float4 *>(wq + 4);
-        }
-      }
       if constexpr (DWS) {
+        // (first: nothing but the dW accumulators is live across it)
         // dW += X^T dH: X^T fragments (lane: column 32 ti + lc of rows
         // 16 ks + 8 h + j) read from the fp32 rows and split here, dH^T
         // fragments from the term images
         if (!(A.dbg & 1)) {
-          const float *xr = reinterpret_cast<const float *>(buf + kDsXOff) + 32 * ti + (lane & 31);
+          const float *xr = reinterpret_cast<const float *>(buf + kDsXOff) + 32 * ti + (lane_o & 31);
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks) {
             float xv[8];
@@ -1509,6 +1549,23 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
               accw[s2] = mfma_x6(fa[0], fa[1], fa[2], fb[0], fb[1], fb[2], accw[s2]);
             }
           }
+        }
+      }
+      const auto rx = buf_rsrc(a.dX + r0 * a.lddx, rv * (uint32_t)a.lddx * 4u);
+      f32x4_t acc2[2];
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc2[rt][r] = 0.0f;
+      // W^T fragment rows: global (L2) or, DWS, the LDS copy
+      const float *wq = DWS ? reinterpret_cast<const float *>(lds + kDsWOff) +
+                                  (16 * m + l16) * kDsXLd + 8 * g4
+                            : wp;
+      float4 wn0{}, wn1{};
+      if constexpr (!kHoldW) {
+        if (!(A.dbg & 8)) {  // dbg 8: no W^T loads (timing only: dX wrong)
+          wn0 = *reinterpret_cast<const float4 *>(wq);
+          wn1 = *reinterpret_cast<const float4 *>(wq + 4);
         }
       }
       // DWS with dX == NULL: dW alone (the same partials as with dX)
@@ -1544,7 +1601,8 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
         for (int r = 0; r < 4; ++r) {
           v[r] = acc2[rt][r];
           if constexpr (EPI != EPI_STORE) {
-            v[r] = ((mk[rt][r] >> bit) & 1u) ? v[r] : 0.0f;
+            const uint32_t on = MRING ? (mbits[rt] >> r) & 1u : (mk[rt][r] >> bit) & 1u;
+            v[r] = on ? v[r] : 0.0f;
             cs[r] = __fadd_rn(cs[r], v[r]);  // rows past the end: zero mask words
             if constexpr (EPI == EPI_RELU_DIV) v[r] = __fdiv_rn(v[r], dv[rt]);
           }
@@ -1604,14 +1662,14 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
     }
   }
   if constexpr (DWS) {
-    if (A.hcs_partial != nullptr) {  // (past the dX column sums' [16][128] in LDS)
+    if constexpr (HCS) {  // (past the dX column sums' [16][128] in LDS)
       float *red2 = reinterpret_cast<float *>(lds) + 16 * kXwF;
       if (wave < kBsNG)
         *reinterpret_cast<float4 *>(red2 + (2 * wave + grp) * kXwF + 4 * gl) =
             make_float4(hc[0], hc[1], hc[2], hc[3]);
     }
   }
-  if (EPI != EPI_STORE || (DWS && A.hcs_partial != nullptr)) {
+  if (EPI != EPI_STORE || HCS) {
     __syncthreads();
     if constexpr (EPI != EPI_STORE) {
       if (tid < kXwF) {
@@ -1622,7 +1680,7 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
         a.colsum_partial[(int64_t)blockIdx.x * kXwF + tid] = s;
       }
     }
-    if (DWS && A.hcs_partial != nullptr && tid >= kXwF && tid < 2 * kXwF) {
+    if (HCS && tid >= kXwF && tid < 2 * kXwF) {
       const int f = tid - kXwF;
       const float *red2 = reinterpret_cast<const float *>(lds) + 16 * kXwF;
       float s = 0.0f;
@@ -1942,7 +2000,7 @@ int xw_bwd_impl(int64_t n_rows, int64_t n_cols, int32_t F_in, int32_t F_out,
     // dW partial area holds xw_grid() = 2 x CUs slabs, this grid <= CUs)
     if (dy_colsum) hcs_partial = a.dw_partial + (size_t)grid * kXwF * kXwF;
     sa.hcs_partial = hcs_partial;
-    rc = launch_bs<kBsDws>(sa, epi, grid, s);
+    rc = hcs_partial ? launch_bs<kBsDwsH>(sa, epi, grid, s) : launch_bs<kBsDws>(sa, epi, grid, s);
   } else {
     rc = g_xw_unroll == 4 ? launch_xb_u<4>(a, epi, grid, s) : launch_xb_u<8>(a, epi, grid, s);
   }

@@ -48,8 +48,10 @@ _Z_MIDDLE = os.environ.get("MGCN_Z_MIDDLE", "0") != "0"
 _DWL = os.environ.get("MGCN_DWL", "0") != "0"
 # the top 128-wide layer of a stack (sum, no ReLU) takes the dW + dX adjoint
 # with its bias gradient from the same launch (mgcn_spmm_xw_bwd_hcs) instead of
-# keeping Z for the dense Z^T dY pass: env MGCN_TOP_FULL=0 turns it off
-_TOP_FULL = os.environ.get("MGCN_TOP_FULL", "1") != "0"
+# keeping Z for the dense Z^T dY pass: env MGCN_TOP_FULL=1.  Off by default:
+# measured equal at config 2 (5.072 vs 5.072 ms/step; the dY row reads and
+# their registers cost the hcs launch ~0.1 ms over the plain one)
+_TOP_FULL = os.environ.get("MGCN_TOP_FULL", "0") != "0"
 
 
 def set_fused_layers(enabled: bool) -> None:

@@ -407,8 +407,8 @@ def test_gcn_stack_keeps_z_only_where_the_backward_reads_it(cuda, acts):
     """The forward stores the aggregate Z of a layer only when the backward
     forms that layer's dW as Z^T dY: the bottom layer, or a layer whose lower
     layer ends in a ReLU (its mask feeds the dX-only gather's epilogue) --
-    except the top layer, which by default (ops._TOP_FULL) takes the dW + dX
-    adjoint with its bias gradient in the same launch and keeps no Z.  A
+    except the top layer when ops._TOP_FULL is set (it then takes the dW + dX
+    adjoint with its bias gradient in the same launch and keeps no Z).  A
     layer above a 'none' layer keeps no N x F Z (and its gradients still
     match the two-launch stack)."""
     from mgcn import ops

@@ -423,7 +423,7 @@ def test_ws_full_hcs_column_sums(cuda, N, E):
 @pytest.mark.parametrize("layers", [2, 3])
 def test_stack_top_full_vs_z_form(cuda, monkeypatch, layers):
     """The stack's top layer on the dW + dX adjoint with its bias gradient in
-    the same launch (ops._TOP_FULL, the default) against the Z form (Z kept,
+    the same launch (ops._TOP_FULL, MGCN_TOP_FULL=1) against the Z form (Z kept,
     dX-only adjoint + dense Z^T dY pass): y and x.grad bit for bit, every
     dW / db within tolerance."""
     from mgcn import ops
