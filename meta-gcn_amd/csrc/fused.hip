@@ -174,15 +174,17 @@ __device__ __forceinline__ void gather_row(const __amdgpu_buffer_rsrc_t rx, uint
 // are loaded while row k's feature rows are gathered, so a row costs one
 // gather round trip instead of three dependent ones (rowptr -> col -> row).
 struct RowMeta {
-  int64_t beg, deg;
+  int64_t beg;
+  int32_t deg;  // a row's degree fits 32 bits (the slots are addressed from beg)
   int mc;
   float mw;
+  int ms;  // max adjoint (meta_first_m): fwd slot of the lane's edge
 };
 
 __device__ __forceinline__ void meta_rowptr(const int64_t *__restrict__ rowptr, int64_t row,
                                             bool ok, RowMeta &m) {
   m.beg = ok ? rowptr[row] : 0;
-  m.deg = ok ? rowptr[row + 1] - m.beg : 0;
+  m.deg = ok ? (int32_t)(rowptr[row + 1] - m.beg) : 0;
 }
 
 __device__ __forceinline__ void meta_first(const int32_t *__restrict__ col,
@@ -193,6 +195,15 @@ __device__ __forceinline__ void meta_first(const int32_t *__restrict__ col,
     m.mc = col[m.beg + gl];
     if (w != nullptr) m.mw = w[m.beg + gl];
   }
+}
+
+// meta_first plus the lane's edge's fwd slot (the max adjoint's slot_map)
+__device__ __forceinline__ void meta_first_m(const int32_t *__restrict__ col,
+                                             const float *__restrict__ w,
+                                             const int32_t *__restrict__ slot_map, int gl,
+                                             RowMeta &m) {
+  meta_first(col, w, gl, m);
+  m.ms = gl < m.deg ? slot_map[m.beg + gl] : 0;
 }
 
 template <int U>
@@ -250,12 +261,14 @@ __device__ __forceinline__ void gather_row_meta(const __amdgpu_buffer_rsrc_t rx,
 // waves): U slots of EACH row in flight per round, so a wave keeps four rows'
 // gathers in flight; each row folded in its own edge order, products and
 // sums rounded separately (gather_row_meta bit for bit).
-template <int U>
+template <int U, bool MAXM = false>
 __device__ __forceinline__ void gather_row2_meta(const __amdgpu_buffer_rsrc_t rx, uint32_t ldx_b,
                                                  const int32_t *__restrict__ col,
                                                  const float *__restrict__ w, const RowMeta &ma,
                                                  const RowMeta &mb, int gl, int grp,
-                                                 float (&aa)[4], float (&ab)[4]) {
+                                                 float (&aa)[4], float (&ab)[4],
+                                                 const uint32_t *__restrict__ win = nullptr,
+                                                 const int32_t *__restrict__ slot_map = nullptr) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) aa[j] = ab[j] = 0.0f;
   const int64_t da = ma.deg, db = mb.deg;
@@ -264,6 +277,11 @@ __device__ __forceinline__ void gather_row2_meta(const __amdgpu_buffer_rsrc_t rx
   dm = dm > odm ? dm : odm;  // wave-uniform loop bound
   int mca = ma.mc, mcb = mb.mc;
   float mwa = ma.mw, mwb = mb.mw;
+  int msa = 0, msb = 0;
+  if constexpr (MAXM) {
+    msa = ma.ms;
+    msb = mb.ms;
+  }
   for (int64_t e0 = 0; e0 < dm; e0 += 32) {
     if (e0 > 0) {  // rows longer than one metadata batch load the rest in place
       const int64_t my = e0 + gl;
@@ -272,10 +290,12 @@ __device__ __forceinline__ void gather_row2_meta(const __amdgpu_buffer_rsrc_t rx
       if (my < da) {
         mca = col[ma.beg + my];
         if (w != nullptr) mwa = w[ma.beg + my];
+        if constexpr (MAXM) msa = slot_map[ma.beg + my];
       }
       if (my < db) {
         mcb = col[mb.beg + my];
         if (w != nullptr) mwb = w[mb.beg + my];
+        if constexpr (MAXM) msb = slot_map[mb.beg + my];
       }
     }
     const int64_t ra = da - e0, rb = db - e0;
@@ -286,6 +306,7 @@ __device__ __forceinline__ void gather_row2_meta(const __amdgpu_buffer_rsrc_t rx
     for (int k0 = 0; k0 < nbmax; k0 += U) {
       float4 xa[U], xb[U];
       float wa[U], wb[U];
+      uint32_t ba[U], bb[U];  // MAXM: the edges' winner words (word gl / 8 of the record)
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int k = k0 + u;
@@ -297,9 +318,27 @@ __device__ __forceinline__ void gather_row2_meta(const __amdgpu_buffer_rsrc_t rx
         const uint32_t ob = k < nb ? (uint32_t)cb * ldx_b + 16u * gl : 0xfffffff0u;
         xa[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, oa, 0, 0));
         xb[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, ob, 0, 0));
+        if constexpr (MAXM) {
+          // loaded unconditionally (masked edges read word 0, never used)
+          const int sa = __shfl(msa, 32 * grp + (k & 31), 64);
+          const int sb = __shfl(msb, 32 * grp + (k & 31), 64);
+          ba[u] = win[k < na ? (int64_t)sa * 4 + (gl >> 3) : 0];
+          bb[u] = win[k < nb ? (int64_t)sb * 4 + (gl >> 3) : 0];
+        }
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
+        if constexpr (MAXM) {  // each edge's dY counts only where it won (gather_row's select)
+          const uint32_t qa = ba[u] >> (4 * (gl & 7)), qb = bb[u] >> (4 * (gl & 7));
+          xa[u].x = (qa & 1u) ? xa[u].x : 0.0f;
+          xa[u].y = (qa & 2u) ? xa[u].y : 0.0f;
+          xa[u].z = (qa & 4u) ? xa[u].z : 0.0f;
+          xa[u].w = (qa & 8u) ? xa[u].w : 0.0f;
+          xb[u].x = (qb & 1u) ? xb[u].x : 0.0f;
+          xb[u].y = (qb & 2u) ? xb[u].y : 0.0f;
+          xb[u].z = (qb & 4u) ? xb[u].z : 0.0f;
+          xb[u].w = (qb & 8u) ? xb[u].w : 0.0f;
+        }
         if (k0 + u < na) {
           aa[0] = __fadd_rn(aa[0], __fmul_rn(xa[u].x, wa[u]));
           aa[1] = __fadd_rn(aa[1], __fmul_rn(xa[u].y, wa[u]));
@@ -1194,7 +1233,7 @@ int launch_xb_u(const XbArgs &a, int epi, int grid, hipStream_t s) {
 // the ring after its dX columns -- no hand-off between the MFMA waves, no dX
 // images.  dX is bit for bit the two-phase kernel's; dW folds the same
 // products per chunk over a one-workgroup-per-CU split-K grid.
-constexpr int kBsDx = 0, kBsDwl = 1, kBsDws = 2, kBsDwsH = 3;  // spmm_xw_bwd_ws_kernel MODE
+constexpr int kBsDx = 0, kBsDwl = 1, kBsDws = 2, kBsDwsH = 3, kBsDwsM = 4;  // spmm_xw_bwd_ws_kernel MODE
 #ifndef MGCN_DS_MASK_RING
 #define MGCN_DS_MASK_RING 1  // DWS: ReLU mask words / divisors through the ring (0: MFMA waves load them)
 #endif
@@ -1275,8 +1314,9 @@ struct XbsArgs {
 
 template <int U, int EPI, int MODE>
 __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArgs A) {
-  constexpr bool DWL = MODE == kBsDwl, DWS = MODE == kBsDws || MODE == kBsDwsH;
+  constexpr bool DWL = MODE == kBsDwl, DWS = MODE == kBsDws || MODE == kBsDwsH || MODE == kBsDwsM;
   constexpr bool HCS = MODE == kBsDwsH;  // DWS + dY's column sums (hcs_partial)
+  constexpr bool MAXM = MODE == kBsDwsM;  // DWS on the max adjoint (win_mask + slot_map)
   constexpr bool MRING = DWS && MGCN_DS_MASK_RING;
   constexpr int kRing = DWS ? kDsRingBuf : kBsRingBuf;
   const XbArgs &a = A.b;
@@ -1330,7 +1370,10 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       meta_rowptr(a.rowptr, row_of(0, j), row_of(0, j) < a.n_rows && wave < n_quads, cur[j]);
-      meta_first(a.col, a.w, gl, cur[j]);
+      if constexpr (MAXM)
+        meta_first_m(a.col, a.w, a.slot_map, gl, cur[j]);
+      else
+        meta_first(a.col, a.w, gl, cur[j]);
       meta_rowptr(a.rowptr, row_of(1, j), row_of(1, j) < a.n_rows && wave + kBsNG < n_quads,
                   nxt[j]);
     }
@@ -1339,7 +1382,10 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
       RowMeta nn[2];
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        meta_first(a.col, a.w, gl, nxt[j]);
+        if constexpr (MAXM)
+          meta_first_m(a.col, a.w, a.slot_map, gl, nxt[j]);
+        else
+          meta_first(a.col, a.w, gl, nxt[j]);
         const int64_t r2 = row_of(k + 2, j);
         meta_rowptr(a.rowptr, r2, r2 < a.n_rows && q + 2 * kBsNG < n_quads, nn[j]);
       }
@@ -1382,7 +1428,8 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
               ry, 4 * (int)((lr0 + 2 * j) * a.lddy + 4 * gl), 0, 0);
       }
       float acc[2][4];
-      gather_row2_meta<U>(rdy, ldy_b, a.col, a.w, cur[0], cur[1], gl, grp, acc[0], acc[1]);
+      gather_row2_meta<U, MAXM>(rdy, ldy_b, a.col, a.w, cur[0], cur[1], gl, grp, acc[0], acc[1],
+                                a.win_mask, a.slot_map);
       if constexpr (HCS) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
@@ -1694,6 +1741,7 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
 int g_xm_unroll = 6;  // mgcn_set_option("xw_ws_xm_unroll"): max+next gathers in flight (4 / 6 / 8)
 int g_xw_ws = 0;  // mgcn_set_option("xw_ws"): the warp-specialised dX-only adjoint
 int g_xw_ws_full = 1;  // mgcn_set_option("xw_ws_full"): the warp-specialised dW + dX adjoint (DWS)
+int g_xw_ws_max = 1;   // mgcn_set_option("xw_ws_max"): ... and its max adjoint (DWS + win_mask)
 
 int bs_grid() {
   int dev = 0, cus = 256;
@@ -1724,7 +1772,11 @@ int g_bs_dbg = 0;  // mgcn_set_option("xw_ws_unroll"): gathers in flight per row
 
 template <int MODE>
 int launch_bs(const XbsArgs &a, int epi, int grid, hipStream_t s) {
-  return g_bs_unroll == 4 ? launch_bs_u<4, MODE>(a, epi, grid, s) : launch_bs_u<8, MODE>(a, epi, grid, s);
+  if constexpr (MODE == kBsDwsM)  // the winner words take registers: 3 slots per row
+    return launch_bs_u<3, MODE>(a, epi, grid, s);
+  else
+    return g_bs_unroll == 4 ? launch_bs_u<4, MODE>(a, epi, grid, s)
+                            : launch_bs_u<8, MODE>(a, epi, grid, s);
 }
 
 }  // namespace
@@ -1736,6 +1788,14 @@ int xw_set_ws(const char *name, int value) {
       return MGCN_EINVAL;
     }
     g_xm_unroll = value;
+    return MGCN_OK;
+  }
+  if (name[6] == 'm') {  // "xw_ws_max"
+    if (value < 0 || value > 1) {
+      set_error("xw_ws_max must be 0 or 1");
+      return MGCN_EINVAL;
+    }
+    g_xw_ws_max = value;
     return MGCN_OK;
   }
   if (name[6] == 'f') {  // "xw_ws_full"
@@ -1987,7 +2047,8 @@ int xw_bwd_impl(int64_t n_rows, int64_t n_cols, int32_t F_in, int32_t F_out,
     return launch_fold(a.colsum_partial, grid, kXwF, kXwF, colsum, kXwF, accumulate, s);
   }
   float *hcs_partial = nullptr;
-  if ((g_xw_ws_full || dy_colsum) && win_mask == nullptr) {
+  // (the max adjoint's dW-only form stays two-phase: 1.10 vs 1.22 ms at config 4)
+  if ((g_xw_ws_full || dy_colsum) && (win_mask == nullptr || (g_xw_ws_max && dX != nullptr))) {
     // the warp-specialised dW + dX (or dW-only) form (one workgroup per CU; DWS)
     XbsArgs sa{};
     sa.b = a;
@@ -2000,7 +2061,9 @@ int xw_bwd_impl(int64_t n_rows, int64_t n_cols, int32_t F_in, int32_t F_out,
     // dW partial area holds xw_grid() = 2 x CUs slabs, this grid <= CUs)
     if (dy_colsum) hcs_partial = a.dw_partial + (size_t)grid * kXwF * kXwF;
     sa.hcs_partial = hcs_partial;
-    rc = hcs_partial ? launch_bs<kBsDwsH>(sa, epi, grid, s) : launch_bs<kBsDws>(sa, epi, grid, s);
+    rc = hcs_partial ? launch_bs<kBsDwsH>(sa, epi, grid, s)
+         : win_mask  ? launch_bs<kBsDwsM>(sa, epi, grid, s)
+                     : launch_bs<kBsDws>(sa, epi, grid, s);
   } else {
     rc = g_xw_unroll == 4 ? launch_xb_u<4>(a, epi, grid, s) : launch_xb_u<8>(a, epi, grid, s);
   }

@@ -52,6 +52,10 @@ _DWL = os.environ.get("MGCN_DWL", "0") != "0"
 # measured equal at config 2 (5.072 vs 5.072 ms/step; the dY row reads and
 # their registers cost the hcs launch ~0.1 ms over the plain one)
 _TOP_FULL = os.environ.get("MGCN_TOP_FULL", "0") != "0"
+# max layers with dX: the dW + dX adjoint with the winner-bit routing in one
+# launch (mgcn_spmm_xw_bwd with win_mask: the warp-specialised kernel) instead
+# of mgcn_spmm_bwd + mgcn_gemm_bwd: env MGCN_MAX_FULL=0 turns it off
+_MAX_FULL = os.environ.get("MGCN_MAX_FULL", "1") != "0"
 
 
 def set_fused_layers(enabled: bool) -> None:
@@ -1364,10 +1368,11 @@ class _GCNStack(torch.autograd.Function):
                 # adjoint SpMM + dW + dX (+ the lower layer's ReLU / bias
                 # gradient) in one pass: dH never leaves the chip (max: the
                 # adjoint routes dY through the forward's winner bits; with dX
-                # that form measured slower than the two launches, 1.53 vs
-                # 1.42 ms at config 4, so max fuses only the dW-only layer)
+                # the two-phase kernel measured slower than the two launches,
+                # 1.53 vs 1.42 ms at config 4; the warp-specialised one is
+                # faster, _MAX_FULL)
                 sm = plan.slot_map() if am is not None else None
-                if fused and am is None:
+                if fused and (am is None or _MAX_FULL):
                     hcs = None
                     if top_hcs and l == top:
                         hcs = gb[top] = torch.empty(W.size(1), dtype=torch.float32,
