@@ -48,6 +48,8 @@
 //   backward the same + 4 N F (X) (+ 16 N mask)
 // and 2 N F^2 (forward) / 4 N F^2 (backward) x 6 bf16 MFMA flops under it.
 
+#include <string>
+
 #include "mgcn_internal.h"
 #include "x6.h"
 
@@ -1770,60 +1772,55 @@ int g_bs_unroll = 4;
 // skip the dW phase and its sync, bit 1 skip the dW products, bit 2 skip Zl loads
 int g_bs_dbg = 0;  // mgcn_set_option("xw_ws_unroll"): gathers in flight per row (4 / 8)
 
+int g_bs_full_unroll = 5;  // mgcn_set_option("xw_ws_full_unroll"): DWS gathers in flight per row (5: 0.984-0.991 vs 1.000-1.012 ms at 4)
+
 template <int MODE>
 int launch_bs(const XbsArgs &a, int epi, int grid, hipStream_t s) {
-  if constexpr (MODE == kBsDwsM)  // the winner words take registers: 3 slots per row
+  if constexpr (MODE == kBsDwsM) {  // the winner words take registers: 3 slots per row
     return launch_bs_u<3, MODE>(a, epi, grid, s);
-  else
+  } else if constexpr (MODE == kBsDws || MODE == kBsDwsH) {
+    return g_bs_full_unroll == 4 ? launch_bs_u<4, MODE>(a, epi, grid, s)
+         : g_bs_full_unroll == 5 ? launch_bs_u<5, MODE>(a, epi, grid, s)
+                                 : launch_bs_u<6, MODE>(a, epi, grid, s);
+  } else {
     return g_bs_unroll == 4 ? launch_bs_u<4, MODE>(a, epi, grid, s)
+         : g_bs_unroll == 5 ? launch_bs_u<5, MODE>(a, epi, grid, s)
+         : g_bs_unroll == 6 ? launch_bs_u<6, MODE>(a, epi, grid, s)
                             : launch_bs_u<8, MODE>(a, epi, grid, s);
+  }
 }
 
 }  // namespace
 
 int xw_set_ws(const char *name, int value) {
-  if (name[6] == 'x') {  // "xw_ws_xm_unroll"
-    if (value != 4 && value != 6 && value != 8) {
-      set_error("xw_ws_xm_unroll must be 4, 6 or 8");
-      return MGCN_EINVAL;
-    }
-    g_xm_unroll = value;
-    return MGCN_OK;
-  }
-  if (name[6] == 'm') {  // "xw_ws_max"
+  const std::string n(name);
+  auto flag = [&](int &g) {
     if (value < 0 || value > 1) {
-      set_error("xw_ws_max must be 0 or 1");
-      return MGCN_EINVAL;
+      set_error("%s must be 0 or 1", name);
+      return (int)MGCN_EINVAL;
     }
-    g_xw_ws_max = value;
-    return MGCN_OK;
-  }
-  if (name[6] == 'f') {  // "xw_ws_full"
-    if (value < 0 || value > 1) {
-      set_error("xw_ws_full must be 0 or 1");
-      return MGCN_EINVAL;
-    }
-    g_xw_ws_full = value;
-    return MGCN_OK;
-  }
-  if (name[6] == 'd') {  // "xw_ws_dbg"
+    g = value;
+    return (int)MGCN_OK;
+  };
+  auto unroll = [&](int &g, std::initializer_list<int> ok) {
+    for (int v : ok)
+      if (v == value) {
+        g = value;
+        return (int)MGCN_OK;
+      }
+    set_error("%s: unsupported value %d", name, value);
+    return (int)MGCN_EINVAL;
+  };
+  if (n == "xw_ws_xm_unroll") return unroll(g_xm_unroll, {4, 6, 8});
+  if (n == "xw_ws_max") return flag(g_xw_ws_max);
+  if (n == "xw_ws_full") return flag(g_xw_ws_full);
+  if (n == "xw_ws_dbg") {
     g_bs_dbg = value;
     return MGCN_OK;
   }
-  if (name[6] == 'u') {  // "xw_ws_unroll"
-    if (value != 4 && value != 8) {
-      set_error("xw_ws_unroll must be 4 or 8");
-      return MGCN_EINVAL;
-    }
-    g_bs_unroll = value;
-    return MGCN_OK;
-  }
-  if (value < 0 || value > 1) {
-    set_error("xw_ws must be 0 or 1");
-    return MGCN_EINVAL;
-  }
-  g_xw_ws = value;
-  return MGCN_OK;
+  if (n == "xw_ws_unroll") return unroll(g_bs_unroll, {4, 5, 6, 8});        // dX-only / DWL
+  if (n == "xw_ws_full_unroll") return unroll(g_bs_full_unroll, {4, 5, 6});  // DWS
+  return flag(g_xw_ws);  // "xw_ws"
 }
 
 int xw_set_unroll(int value) {
