@@ -21,7 +21,7 @@ from bench import spmm_bytes  # noqa: E402
 
 N, NNZ, F = 1_000_000, 11_000_000, 128
 KERNELS = {"fwd": "spmm_xw_fwd_kernel", "fwd_z": "spmm_xw_fwd_kernel",
-           "bwd": "spmm_xw_bwd_kernel", "bwd_dw": "spmm_xw_bwd_kernel",
+           "bwd": "spmm_xw_bwd_ws_kernel", "bwd_dw": "spmm_xw_bwd_ws_kernel",
            "bwd_dx": "spmm_xw_bwd_kernel", "gemm_dw": "gemm_bwd_kernel"}
 
 
