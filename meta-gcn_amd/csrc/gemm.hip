@@ -772,7 +772,8 @@ bool tn_lds(int M, int N) { return M % kTile == 0 && N % kTile == 0; }
 // K = 1M, M = N = 128: 0.321 / 0.335 / 0.337 ms): 0 = BK 64, one workgroup
 // per CU; 1 = BK 32, two; 2 = BK 16, three
 int g_tn_lds_variant = 0;
-int g_dw_ws = 0;  // mgcn_set_option("dw_ws"): gemm_dw_ws_kernel for mgcn_gemm_bwd's dW-only form
+int g_dw_ws = 0;  // mgcn_set_option("dw_ws"): gemm_dw_ws_kernel (1) / gemm_dw_direct_kernel (2) for mgcn_gemm_bwd's dW-only form
+int g_dw_direct_ni = 2;  // mgcn_set_option("dw_direct_ni"): 2 or 4 (see gemm_dw_direct_kernel)
 int g_tn_staged = 1;  // M = 32, N = 32 / 64: gemm_tn_staged_kernel (0: gemm_tn_small_kernel)
 int tn_lds_wgs() { return g_tn_lds_variant == 1 ? 2 : g_tn_lds_variant == 2 ? 3 : 1; }
 
@@ -810,8 +811,14 @@ int gemm_set_tn_wide2(int value) {
 }
 
 int gemm_set_dw_ws(int value) {
-  if (value < 0 || value > 1) return MGCN_EINVAL;
+  if (value < 0 || value > 2) return MGCN_EINVAL;
   g_dw_ws = value;
+  return MGCN_OK;
+}
+
+int gemm_set_dw_direct_ni(int value) {
+  if (value != 2 && value != 4) return MGCN_EINVAL;
+  g_dw_direct_ni = value;
   return MGCN_OK;
 }
 
@@ -2232,6 +2239,194 @@ __global__ __launch_bounds__(1024) void gemm_dw_ws_kernel(
   }
 }
 
+// ----------------------------------------------------------------------------
+// dW-only pass with no LDS (round 5, mgcn_set_option "dw_ws" 2): each wave
+// streams its rows of X (one 64-column half) and all of dH straight into
+// MFMA-layout registers -- lane (lc, h) of a 16-row k-step loads column lc
+// of rows 8 h .. 8 h + 7 (one dword per row; each instruction two 128-B row
+// segments) -- splits them into their bf16 terms in registers and
+// accumulates its 64 x 128 half of dW in eight 32x32 tiles (128
+// accumulators).  256-thread workgroups, one per CU, each over a contiguous
+// K range: waves 2 p + c (c: the column half) take the range's k-steps
+// p, p + 2, ...; the two pairs' tiles are added in LDS, one partial per
+// workgroup (folded in workgroup order).  D k-steps of raw loads in flight.
+constexpr int kDdThreads = 256;
+
+// NI = 2: waves 2 p + c take X's column half c over k-steps p, p + 2, ...
+// (128 accumulators); NI = 4: each wave the whole 128 x 128 over k-steps
+// w, w + 4, ... (256 accumulators, AGPRs: the VALU split of 64 loads per
+// k-step hides under 96 MFMAs instead of 48 loads under 48)
+template <bool HCS, int D, int NI>
+__global__ __launch_bounds__(kDdThreads, 1) void gemm_dw_direct_kernel(
+    const float *__restrict__ X, int64_t ldx, const float *__restrict__ dH, int64_t lddh,
+    int64_t M, int64_t rows_per_wg, float *__restrict__ dw_partial,
+    float *__restrict__ colsum_partial) {
+  constexpr int NP = NI;  // waves sharing a column range (k-step interleave): 2 or 4
+  __shared__ __attribute__((aligned(16))) float red[2 * NI * 4 * 16 * 64];
+  __shared__ float cred[4][kBwF];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lc = lane & 31, h = lane >> 5;
+  const int half = NI == 2 ? (wave & 1) : 0;
+  const int pair = NI == 2 ? (wave >> 1) : wave;
+  const int64_t wb = (int64_t)blockIdx.x * rows_per_wg;
+  int64_t we = wb + rows_per_wg;
+  if (we > M) we = M;
+  const int64_t nrows = we > wb ? we - wb : 0;
+  const auto rx = buf_rsrc(X + wb * ldx, (uint32_t)(nrows * ldx * 4));
+  const auto rh = buf_rsrc(dH + wb * lddh, (uint32_t)(nrows * lddh * 4));
+  const int n_steps = (int)((nrows + 15) / 16);
+  const int my_steps = n_steps > pair ? (n_steps - pair + NP - 1) / NP : 0;
+  const uint32_t xstep = (uint32_t)(16 * NP * ldx * 4), hstep = (uint32_t)(16 * NP * lddh * 4);
+  const uint32_t x0 = (uint32_t)(16 * pair * ldx * 4), h0 = (uint32_t)(16 * pair * lddh * 4);
+  const int va = 4 * (int)(8 * h * ldx + 64 * half + lc);
+  const int vb = 4 * (int)(8 * h * lddh + lc);
+
+  struct Raw {
+    float a[NI][8];
+    float b[4][8];
+  };
+  auto load = [&](int t, Raw &r) {  // k-step t of this wave (past the range: zeros)
+    const uint32_t so_x = x0 + (uint32_t)t * xstep, so_h = h0 + (uint32_t)t * hstep;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+#pragma unroll
+      for (int ib = 0; ib < NI; ++ib)
+        r.a[ib][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+            rx, va + 4 * (int)(j * ldx + 32 * ib), so_x, MGCN_NT_AUX));
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb)
+        r.b[nb][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+            rh, vb + 4 * (int)(j * lddh + 32 * nb), so_h, 0));
+    }
+  };
+  f32x16 acc[NI][4];
+#pragma unroll
+  for (int ib = 0; ib < NI; ++ib)
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[ib][nb][r] = 0.0f;
+  float hc[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // HCS (half 0): dH column sums, columns 32 nb + lc
+
+  Raw ring[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) load(d, ring[d]);
+  for (int t0 = 0; t0 < my_steps; t0 += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int t = t0 + d;
+      if (t >= my_steps) break;
+      Raw cur = ring[d];
+      load(t + D, ring[d]);
+      bf16x8 fa[NI][3], fb[4][3];
+#pragma unroll
+      for (int ib = 0; ib < NI; ++ib) split3_bf16(cur.a[ib], fa[ib][0], fa[ib][1], fa[ib][2]);
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        split3_bf16(cur.b[nb], fb[nb][0], fb[nb][1], fb[nb][2]);
+        if constexpr (HCS) {
+          if (half == 0)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) hc[nb] = __fadd_rn(hc[nb], cur.b[nb][j]);
+        }
+      }
+#pragma unroll
+      for (int ib = 0; ib < NI; ++ib)
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb)
+          acc[ib][nb] = mfma_x6(fa[ib][0], fa[ib][1], fa[ib][2], fb[nb][0], fb[nb][1], fb[nb][2],
+                                acc[ib][nb]);
+    }
+  }
+  if constexpr (HCS) {
+    if (half == 0) {
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        const float v = __fadd_rn(hc[nb], __shfl_xor(hc[nb], 32, 64));  // rows 8 h ..: both halves
+        if (h == 0) cred[pair][32 * nb + lc] = v;
+      }
+    }
+  }
+  // fold the waves sharing a column range through LDS ([slot][tile][r][lane]):
+  // NI = 2, pair 1 into pair 0; NI = 4, waves 2, 3 into 0, 1, then 1 into 0
+  auto put = [&](int slot) {
+#pragma unroll
+    for (int ib = 0; ib < NI; ++ib)
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) red[((slot * NI + ib) * 4 + nb) * 1024 + r * 64 + lane] = acc[ib][nb][r];
+  };
+  auto add = [&](int slot) {
+#pragma unroll
+    for (int ib = 0; ib < NI; ++ib)
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          acc[ib][nb][r] = __fadd_rn(acc[ib][nb][r], red[((slot * NI + ib) * 4 + nb) * 1024 + r * 64 + lane]);
+  };
+  bool writer;
+  if constexpr (NI == 2) {
+    if (pair == 1) put(half);
+    __syncthreads();
+    if (pair == 0) add(half);
+    writer = pair == 0;
+  } else {
+    if (wave >= 2) put(wave - 2);
+    __syncthreads();
+    if (wave < 2) add(wave);
+    __syncthreads();
+    if (wave == 1) put(0);
+    __syncthreads();
+    if (wave == 0) add(0);
+    writer = wave == 0;
+  }
+  if (writer) {
+    float *slab = dw_partial + (int64_t)blockIdx.x * kBwF * kBwF;
+#pragma unroll
+    for (int ib = 0; ib < NI; ++ib)
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = 32 * (NI == 2 ? 2 * half + ib : ib) + (r & 3) + 8 * (r >> 2) + 4 * h;
+          slab[row * kBwF + 32 * nb + lc] = acc[ib][nb][r];
+        }
+  }
+  if constexpr (HCS) {
+    __syncthreads();
+    if (threadIdx.x < kBwF) {
+      float c = 0.0f;
+#pragma unroll
+      for (int q = 0; q < NP; ++q) c = __fadd_rn(c, cred[q][threadIdx.x]);
+      colsum_partial[(int64_t)blockIdx.x * kBwF + threadIdx.x] = c;
+    }
+  }
+}
+
+template <bool HCS>
+int launch_dw_direct(const float *X, int64_t ldx, const float *dH, int64_t lddh, int64_t M,
+                     float *dwp, float *csp, int *grid_out, hipStream_t s) {
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 256;
+  if (cus > kBwGrid) cus = kBwGrid;  // the workspace holds kBwGrid partials
+  int64_t rows = (M + cus - 1) / cus;
+  rows = (rows + 63) / 64 * 64;  // whole 16-row k-steps for every wave
+  const int grid = (int)((M + rows - 1) / rows);
+  *grid_out = grid;
+  if (g_dw_direct_ni == 2)
+    hipLaunchKernelGGL((gemm_dw_direct_kernel<HCS, 2, 2>), dim3(grid), dim3(kDdThreads), 0, s, X,
+                       ldx, dH, lddh, M, rows, dwp, csp);
+  else
+    hipLaunchKernelGGL((gemm_dw_direct_kernel<HCS, 1, 4>), dim3(grid), dim3(kDdThreads), 0, s, X,
+                       ldx, dH, lddh, M, rows, dwp, csp);
+  return check_launch("gemm_dw_direct_kernel");
+}
+
 }  // namespace
 }  // namespace mgcn
 
@@ -2285,7 +2480,12 @@ extern "C" int mgcn_gemm_bwd(int64_t M, int32_t F_in, int32_t F_out, const float
   const int64_t n_chunks = (M + kBwRows - 1) / kBwRows;
   const int grid = (int)(n_chunks < kBwGrid ? n_chunks : kBwGrid);
   int rc;
-  if (dX == nullptr && g_dw_ws) {
+  int fold_grid = grid;
+  if (dX == nullptr && g_dw_ws == 2 &&
+      (uint64_t)((M + 255) / 256 + 32) * (uint64_t)(ldx > lddh ? ldx : lddh) * 4u < (1ull << 32)) {
+    rc = hcs ? launch_dw_direct<true>(X, ldx, dH, lddh, M, dwp, csp, &fold_grid, s)
+             : launch_dw_direct<false>(X, ldx, dH, lddh, M, dwp, csp, &fold_grid, s);
+  } else if (dX == nullptr && g_dw_ws) {
     if (hcs)
       hipLaunchKernelGGL((gemm_dw_ws_kernel<true>), dim3(grid), dim3(1024), 0, s, X, ldx, dH, lddh,
                          M, dwp, csp);
@@ -2310,8 +2510,8 @@ extern "C" int mgcn_gemm_bwd(int64_t M, int32_t F_in, int32_t F_out, const float
                                      row_div, dwp, csp, s);
   if (rc) return rc;
   const int64_t MN = (int64_t)F_in * F_out;
-  if (int rc2 = launch_fold(dwp, grid, MN, F_out, dW, lddw, accumulate, s)) return rc2;
-  if (hcs) return launch_colsum_fold(csp, grid, F_out, colsum, s);
+  if (int rc2 = launch_fold(dwp, fold_grid, MN, F_out, dW, lddw, accumulate, s)) return rc2;
+  if (hcs) return launch_colsum_fold(csp, fold_grid, F_out, colsum, s);
   if (epi == EPI_STORE) return MGCN_OK;
   return launch_colsum_fold(csp, grid, F_in, colsum, s);
 }

@@ -783,8 +783,12 @@ extern "C" int mgcn_set_option(const char *name, int value) {
     MGCN_REQUIRE(value == 0 || value == 1, "gemm_tn_wide2 must be 0 or 1");
     return gemm_set_tn_wide2(value);
   }
+  if (n == "dw_direct_ni") {
+    MGCN_REQUIRE(value == 2 || value == 4, "dw_direct_ni must be 2 or 4");
+    return gemm_set_dw_direct_ni(value);
+  }
   if (n == "dw_ws") {
-    MGCN_REQUIRE(value == 0 || value == 1, "dw_ws must be 0 or 1");
+    MGCN_REQUIRE(value >= 0 && value <= 2, "dw_ws must be 0, 1 or 2");
     return gemm_set_dw_ws(value);
   }
   if (n == "gemm_tn_staged") {

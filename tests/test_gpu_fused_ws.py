@@ -450,3 +450,32 @@ def test_stack_top_full_vs_z_form(cuda, monkeypatch, layers):
     assert torch.equal(ya, yb) and torch.equal(xa, xb)
     for a, b in zip(ga, gb):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("M", [1, 31, 33, 4097, 300000])
+@pytest.mark.parametrize("hcs", [False, True])
+def test_dw_pass_direct(cuda, M, hcs):
+    """mgcn_gemm_bwd's dW-only form on the LDS-free kernel (mgcn_set_option
+    "dw_ws" 2: X and dH straight into MFMA-layout registers): dW within the
+    fp64 |.|-bound of Z^T dY and within twice it of the default kernel (a
+    different split-K); dH's column sums within fp32 summation tolerance."""
+    from mgcn import _lib as L
+    from mgcn import ops
+    g = torch.Generator(device=cuda).manual_seed(M + 7)
+    Z = torch.randn(M, F, device=cuda, generator=g)
+    dY = torch.randn(M, F, device=cuda, generator=g)
+    W = torch.randn(F, F, device=cuda, generator=g)
+    out = {}
+    try:
+        for form in (2, 0):
+            L.set_option("dw_ws", form)
+            out[form] = ops.gemm_bwd(Z, dY, W, want_dx=False, dh_colsum=hcs)
+    finally:
+        L.set_option("dw_ws", 0)
+    ref = Z.double().t() @ dY.double()
+    bound = Z.double().abs().t() @ dY.double().abs()
+    assert ((out[2][0].double() - ref).abs() <= 4e-5 * bound + 1e-6).all()
+    assert ((out[2][0].double() - out[0][0].double()).abs() <= 8e-5 * bound + 1e-6).all()
+    if hcs:
+        cb = dY.double().abs().sum(0)
+        assert ((out[2][2].double() - dY.double().sum(0)).abs() <= 1e-5 * cb + 1e-6).all()
