@@ -1,4 +1,6 @@
-# Round-5 profile pass (the second half of scripts/round_final.sh)
+# Profile pass + config-3 / config-4 workloads: the second half of
+# scripts/round_final.sh, as its own gpurun call
+#   bash scripts/round_final_profile.sh <tag>
 set -e -o pipefail
 T=${1:?tag}; O=gpurun_out/$T; mkdir -p $O
 bash scripts/profile_round.sh $T

@@ -1,4 +1,5 @@
-# Round-5 GPU suite + smoke (the first half of scripts/round_final.sh)
+# GPU suite + smoke: the first half of scripts/round_final.sh, as its own gpurun call
+#   bash scripts/round_final_tests.sh <tag>
 set -e -o pipefail
 T=${1:?tag}; O=gpurun_out/$T; mkdir -p $O
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread \
