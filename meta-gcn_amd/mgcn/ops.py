@@ -52,6 +52,9 @@ _DWL = os.environ.get("MGCN_DWL", "0") != "0"
 # measured equal at config 2 (5.072 vs 5.072 ms/step; the dY row reads and
 # their registers cost the hcs launch ~0.1 ms over the plain one)
 _TOP_FULL = os.environ.get("MGCN_TOP_FULL", "0") != "0"
+# (with _TOP_FULL: the top bias gradient from the adjoint launch (1) or from a
+# separate column-sum pass over dY (0); timing experiments)
+_TOP_HCS = os.environ.get("MGCN_TOP_HCS", "1") != "0"
 # max layers with dX: the dW + dX adjoint with the winner-bit routing in one
 # launch (mgcn_spmm_xw_bwd with win_mask: the warp-specialised kernel) instead
 # of mgcn_spmm_bwd + mgcn_gemm_bwd: env MGCN_MAX_FULL=0 turns it off
@@ -553,11 +556,15 @@ def relu_bwd_colsum(dZ: torch.Tensor, Z: torch.Tensor | None, relu: bool, want_d
         return dY, None
     ws_bytes = int(lib.mgcn_colsum_workspace_bytes(n, F)) if want_db else 0
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev) if want_db else None
+    if _TIMER is not None:
+        _TIMER("relu_bwd_colsum", True, n)
     with L.device_guard(dev):
         rc = lib.mgcn_relu_bwd_colsum(n, F, L.ptr(dZ), L.ptr(Z.contiguous() if relu else None),
                                       int(bool(relu)), L.ptr(row_div), L.ptr(dY if write else None),
                                       L.ptr(db),
                                       L.ptr(ws), ws_bytes, L.stream_of(dev))
+    if _TIMER is not None:
+        _TIMER("relu_bwd_colsum", False)
     L.check(rc, "mgcn_relu_bwd_colsum")
     return dY, db
 
@@ -1296,7 +1303,7 @@ class _GCNStack(torch.autograd.Function):
         top_z = z_path(top) and not relus[top] and rd is None
         # the top layer's bias gradient from its dW + dX adjoint (mgcn_spmm_xw_bwd_hcs):
         # the forward kept no Z for it (top_full there); same predicate here
-        top_hcs = (_TOP_FULL and not zs[top].numel() and top > 0 and not relus[top] and
+        top_hcs = (_TOP_FULL and _TOP_HCS and not zs[top].numel() and top > 0 and not relus[top] and
                    rd is None and args[top].numel() == 0 and relus[top - 1] and
                    rmasks[top - 1].numel() > 0 and ctx.needs_input_grad[5 + 2 * top] and
                    ctx.has_bias[top] and plan.bwd.n_rows == plan.bwd.n_cols and
