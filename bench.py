@@ -435,12 +435,13 @@ def main():
         "arithmetic": ("aggregation fp32 (bitwise = reference); dense x@W / dW / dX products as "
                        "bf16x6 (exact 3-term bf16 split of each fp32 operand, 6 MFMA products, "
                        "fp32 accumulate; error at fp32 level, tests/test_gpu_parity.py); "
-                       "forward fused as (A x) W in one launch per layer, keeping Z = A x; "
-                       "backward: the top layer's dX-only adjoint (mgcn_spmm_xw_bwd, X = NULL) "
-                       "plus dW = Z^T dY in one dense pass (mgcn_gemm_bwd); the middle layer's "
-                       "adjoint gathers dY and forms dW = X^T (A^T dY) and dX in one launch "
-                       "(mgcn_spmm_xw_bwd with X); the bottom layer runs no gather, its "
-                       "dW = Z^T dY is the dense pass alone "
+                       "forward fused as (A x) W in one launch per layer, keeping Z = A x where the "
+                       "backward reads it (the bottom layer); "
+                       "backward: the top and middle layers' adjoints gather dY and form "
+                       "dW = X^T (A^T dY) and dX in one launch (mgcn_spmm_xw_bwd, the "
+                       "warp-specialised kernel), the top bias gradient from a column-sum pass "
+                       "over dY; the bottom layer keeps Z = A x from its forward and forms "
+                       "dW = Z^T dY in one dense pass (mgcn_gemm_bwd), no gather "
                        "(tests/test_gpu_fused.py, tests/test_gpu_headline.py)"),
         "config": {"workload": head["workload"], "nodes": N, "edges": n_edges, "nnz": nnz,
                    "feat": F, "layers": L, "global_batch": world if mode == "replica" else 1,

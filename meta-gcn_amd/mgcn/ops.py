@@ -47,14 +47,14 @@ _Z_MIDDLE = os.environ.get("MGCN_Z_MIDDLE", "0") != "0"
 # and the separate dW pass.
 _DWL = os.environ.get("MGCN_DWL", "0") != "0"
 # the top 128-wide layer of a stack (sum, no ReLU) takes the dW + dX adjoint
-# with its bias gradient from the same launch (mgcn_spmm_xw_bwd_hcs) instead of
-# keeping Z for the dense Z^T dY pass: env MGCN_TOP_FULL=1.  Off by default:
-# measured equal at config 2 (5.072 vs 5.072 ms/step; the dY row reads and
-# their registers cost the hcs launch ~0.1 ms over the plain one)
-_TOP_FULL = os.environ.get("MGCN_TOP_FULL", "0") != "0"
-# (with _TOP_FULL: the top bias gradient from the adjoint launch (1) or from a
-# separate column-sum pass over dY (0); timing experiments)
-_TOP_HCS = os.environ.get("MGCN_TOP_HCS", "1") != "0"
+# (the DWS kernel) instead of keeping Z for the dense Z^T dY pass: env
+# MGCN_TOP_FULL=0 turns it off.  Its bias gradient (dY's column sums) comes
+# from a column-sum pass over dY (0.095 ms) -- config 2: 5.02 vs 5.04-5.07
+# ms/step (A/B on one box) -- or, MGCN_TOP_HCS=1, from the adjoint launch
+# itself (mgcn_spmm_xw_bwd_hcs: its dY row reads and their registers cost
+# that launch ~0.25 ms, 5.16-5.19)
+_TOP_FULL = os.environ.get("MGCN_TOP_FULL", "1") != "0"
+_TOP_HCS = os.environ.get("MGCN_TOP_HCS", "0") != "0"
 # max layers with dX: the dW + dX adjoint with the winner-bit routing in one
 # launch (mgcn_spmm_xw_bwd with win_mask: the warp-specialised kernel) instead
 # of mgcn_spmm_bwd + mgcn_gemm_bwd: env MGCN_MAX_FULL=0 turns it off

@@ -420,10 +420,12 @@ def test_ws_full_hcs_column_sums(cuda, N, E):
             ops.spmm_xw_bwd(v, norm.w_bwd, None, dY, X[:N // 2], W, dy_colsum_out=hc)
 
 
+@pytest.mark.parametrize("hcs", [False, True])
 @pytest.mark.parametrize("layers", [2, 3])
-def test_stack_top_full_vs_z_form(cuda, monkeypatch, layers):
-    """The stack's top layer on the dW + dX adjoint with its bias gradient in
-    the same launch (ops._TOP_FULL, MGCN_TOP_FULL=1) against the Z form (Z kept,
+def test_stack_top_full_vs_z_form(cuda, monkeypatch, layers, hcs):
+    """The stack's top layer on the dW + dX adjoint (ops._TOP_FULL, the
+    default), its bias gradient from a column-sum pass or (hcs) from the same
+    launch (ops._TOP_HCS), against the Z form (Z kept,
     dX-only adjoint + dense Z^T dY pass): y and x.grad bit for bit, every
     dW / db within tolerance."""
     from mgcn import ops
@@ -438,6 +440,7 @@ def test_stack_top_full_vs_z_form(cuda, monkeypatch, layers):
     x = torch.randn(N, F, device=cuda, requires_grad=True)
     dZ = torch.randn(N, F, device=cuda)
     res = []
+    monkeypatch.setattr(ops, "_TOP_HCS", hcs)
     for top_full in (True, False):
         monkeypatch.setattr(ops, "_TOP_FULL", top_full)
         x.grad = None
