@@ -83,7 +83,16 @@ const char *mgcn_last_error(void);
  *                   1 = bf16x6 (default; fp32 operands split exactly into
  *                   three bf16 terms, six products on bf16 MFMA, fp32
  *                   accumulate -- fp32-level error), 0 = f32
- *                   MFMA (v_mfma_f32_32x32x2_f32)                          */
+ *                   MFMA (v_mfma_f32_32x32x2_f32)
+ *   "spmm_xw_unroll": gathers in flight per row of the fused 128-wide layer
+ *                   forward, 4 / 5 (default) / 6 / 8 (the two-phase adjoints:
+ *                   8, else 4); every value folds in edge order (same bits)
+ *   "xw_ws_full"  : 1 (default) = mgcn_spmm_xw_bwd's dW (+ dX) form on the
+ *                   warp-specialised kernel (DWS), 0 = the two-phase kernel
+ *   "xw_ws_max"   : 1 (default) = the max adjoint with dX on DWS as well
+ *   "xw_ws_full_unroll": DWS gathers in flight per row, 4 / 5 (default) / 6
+ *   "xw_ws", "xw_ws_unroll", "dw_ws", "dw_direct_ni", "gemm_tn_wide2",
+ *   "wide_ws", "wide_mfma": round-5 kernel forms, see INTEGRATION.md      */
 int mgcn_set_option(const char *name, int value);
 
 /* ------------------------------------------------------------------ graph */

@@ -1150,7 +1150,7 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
   }
 }
 
-int g_xw_unroll = 4;
+int g_xw_unroll = 5;  // forward gathers in flight per row (5: config 2 5.06 -> 5.005 ms/step; 6 spills)
 
 int xw_grid() {
   int dev = 0, cus = 256;
@@ -1824,8 +1824,8 @@ int xw_set_ws(const char *name, int value) {
 }
 
 int xw_set_unroll(int value) {
-  if (value != 4 && value != 8) {
-    set_error("spmm_xw_unroll must be 4 or 8");
+  if (value != 4 && value != 5 && value != 6 && value != 8) {
+    set_error("spmm_xw_unroll must be 4, 5, 6 or 8 (5 / 6: the forward only)");
     return MGCN_EINVAL;
   }
   g_xw_unroll = value;
@@ -1919,7 +1919,10 @@ extern "C" int mgcn_spmm_xw_fwd(int64_t n_rows, int64_t n_cols, int32_t F_in, in
   a.mean = reduce == MGCN_REDUCE_MEAN;
   a.relu = relu != 0;
   hipStream_t s = as_stream(stream);
-  return g_xw_unroll == 4 ? launch_xw<4>(a, s) : launch_xw<8>(a, s);
+  return g_xw_unroll == 4 ? launch_xw<4>(a, s)
+       : g_xw_unroll == 5 ? launch_xw<5>(a, s)
+       : g_xw_unroll == 6 ? launch_xw<6>(a, s)
+                          : launch_xw<8>(a, s);
 }
 
 extern "C" size_t mgcn_spmm_xw_bwd_workspace_bytes(int64_t n_rows, int32_t F_in, int32_t F_out) {
@@ -2037,7 +2040,7 @@ int xw_bwd_impl(int64_t n_rows, int64_t n_cols, int32_t F_in, int32_t F_out,
     return launch_fold(a.colsum_partial, g, kXwF, kXwF, colsum, kXwF, accumulate, s);
   }
   if (dx_only) {
-    rc = g_xw_unroll == 4 ? launch_xb_dx<4>(a, epi, grid, s) : launch_xb_dx<8>(a, epi, grid, s);
+    rc = g_xw_unroll == 8 ? launch_xb_dx<8>(a, epi, grid, s) : launch_xb_dx<4>(a, epi, grid, s);
     if (rc || epi == EPI_STORE) return rc;
     // dX only: accumulate != 0 adds the column sums into colsum (row chunks
     // of one adjoint fold their bias gradient on the device)
@@ -2062,7 +2065,7 @@ int xw_bwd_impl(int64_t n_rows, int64_t n_cols, int32_t F_in, int32_t F_out,
          : win_mask  ? launch_bs<kBsDwsM>(sa, epi, grid, s)
                      : launch_bs<kBsDws>(sa, epi, grid, s);
   } else {
-    rc = g_xw_unroll == 4 ? launch_xb_u<4>(a, epi, grid, s) : launch_xb_u<8>(a, epi, grid, s);
+    rc = g_xw_unroll == 8 ? launch_xb_u<8>(a, epi, grid, s) : launch_xb_u<4>(a, epi, grid, s);
   }
   if (rc) return rc;
   rc = launch_split_reduce(a.dw_partial, grid, (int64_t)kXwF * kXwF, kXwF, dW, lddw, accumulate, s);

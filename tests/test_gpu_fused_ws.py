@@ -482,3 +482,40 @@ def test_dw_pass_direct(cuda, M, hcs):
     if hcs:
         cb = dY.double().abs().sum(0)
         assert ((out[2][2].double() - dY.double().sum(0)).abs() <= 1e-5 * cb + 1e-6).all()
+
+
+@pytest.mark.parametrize("N,E,hub", [(20000, 200000, 0), (3000, 20000, 700), (33, 100, 0)])
+def test_gather_unroll_forms_bitwise(cuda, N, E, hub):
+    """The gathers in flight per row (forward spmm_xw_unroll 4 / 5 / 6, DWS
+    xw_ws_full_unroll 4 / 5 / 6) change only the load schedule: every row is
+    still folded in edge order, so Y, Z, the masks, dX, dW and the column
+    sums are bit for bit the same."""
+    from mgcn import _lib as L
+    from mgcn import ops
+    rng = np.random.default_rng(N + 41)
+    ei = _graph(rng, N, E, hub)
+    plan, norm = _plan(cuda, ei, N, "sm")
+    g = torch.Generator(device=cuda).manual_seed(N + 43)
+    X = torch.randn(N, F, device=cuda, generator=g)
+    W = torch.randn(F, F, device=cuda, generator=g) * 0.1
+    b = torch.randn(F, device=cuda, generator=g) * 0.1
+    dY = torch.randn(N, F, device=cuda, generator=g)
+    rm = ops.make_relu_mask(torch.randn(N, F, device=cuda, generator=g))
+    fwd, bwd = {}, {}
+    try:
+        for u in (4, 5, 6):
+            L.set_option("spmm_xw_unroll", u)
+            rmo = torch.empty_like(rm)
+            y, z = ops.spmm_xw_fwd(plan.fwd, norm.w_fwd, X, W, L.REDUCE_SUM, b, True,
+                                   relu_mask=rmo, want_z=True)
+            fwd[u] = (y, z, rmo)
+            L.set_option("xw_ws_full_unroll", u)
+            bwd[u] = ops.spmm_xw_bwd(plan.bwd, norm.w_bwd, None, dY, X, W, relu_mask=rm)
+    finally:  # the defaults
+        L.set_option("spmm_xw_unroll", 5)
+        L.set_option("xw_ws_full_unroll", 5)
+    for u in (5, 6):
+        for a, c in zip(fwd[u], fwd[4]):
+            assert torch.equal(a, c)
+        for a, c in zip(bwd[u], bwd[4]):
+            assert torch.equal(a, c)
