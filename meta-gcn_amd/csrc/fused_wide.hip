@@ -93,8 +93,8 @@ int wide_set_option(const char *name, int value) {
     return MGCN_OK;
   }
   const bool pair = name[5] == 'p';
-  if (pair ? (value < 0 || value > 3) : (value != 4 && value != 8)) {
-    set_error(pair ? "wide_pair must be 0 .. 3" : "wide_unroll must be 4 or 8");
+  if (pair ? (value < 0 || value > 3) : (value != 4 && value != 5 && value != 6 && value != 8)) {
+    set_error(pair ? "wide_pair must be 0 .. 3" : "wide_unroll must be 4, 5, 6 or 8 (5 / 6: the warp-specialised kernels)");
     return MGCN_EINVAL;
   }
   (pair ? g_wide_pair : g_wide_unroll) = value;
@@ -995,6 +995,8 @@ int launch_wide(const WideArgs &a, bool bwd, int epi, int *grid, hipStream_t s) 
     const int64_t cus = wide_grid() / 2;  // one workgroup per CU
     *grid = (int)(cus < n_chunks ? cus : n_chunks);
     return g_wide_unroll == 8 ? launch_wide_ws_u<8>(a, bwd, epi, *grid, s)
+         : g_wide_unroll == 6 ? launch_wide_ws_u<6>(a, bwd, epi, *grid, s)
+         : g_wide_unroll == 5 ? launch_wide_ws_u<5>(a, bwd, epi, *grid, s)
                               : launch_wide_ws_u<4>(a, bwd, epi, *grid, s);
   }
   const int64_t n_chunks = (a.n_rows + kWRows - 1) / kWRows;
