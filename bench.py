@@ -227,6 +227,8 @@ def launch_bytes(name: str, rows: int, edges: int, F: int):
         return (12 * F + 16) * rows, 4.0 * rows * F * F
     if name == "gemm_bwd_dw":     # dW alone: X (or Z), dH read
         return 8 * F * rows, 2.0 * rows * F * F
+    if name == "gemm_bwd_dw_cs":  # dW alone + the column sums of a third [rows, F] stream
+        return 12 * F * rows, 2.0 * rows * F * F
     if name == "relu_bwd_colsum":  # dZ read (+ Z read and dY written under ReLU): lower bound
         return 4 * F * rows, 0.0
     return 8 * F * rows, 2.0 * rows * F * F  # F x F transforms: read + write [rows, F]

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define MGCN_ABI_VERSION 19
+#define MGCN_ABI_VERSION 20
 
 /* return codes */
 #define MGCN_OK 0
@@ -339,6 +339,23 @@ int mgcn_gemm_bwd(int64_t M, int32_t F_in, int32_t F_out, const float *X, int64_
                   float *dW, int64_t lddw, int accumulate, float *dX, int64_t lddx,
                   const uint32_t *relu_mask, const float *row_div, float *colsum,
                   void *workspace, size_t workspace_bytes, void *stream);
+
+/* Bytes of scratch mgcn_gemm_bwd_dw_cs needs (ABI v20). */
+size_t mgcn_gemm_bwd_dw_cs_workspace_bytes(int64_t M);
+
+/*
+ * mgcn_gemm_bwd's dW-only form at 128 x 128 (ABI v20) that also returns
+ *   s_colsum[128] = sum over the M rows of S   (S [M, 128], lds, 16-byte rows)
+ * streamed in the same pass: dW (+)= X^T dH, colsum (nullable) = dH's column
+ * sums as mgcn_gemm_bwd.  A GCN stack folds its TOP layer's bias gradient
+ * (the column sums of the upstream gradient, gcn_base_models.py:240) into the
+ * BOTTOM layer's dW = Z^T dY pass this way, instead of a separate pass over
+ * the upstream gradient.  Deterministic (fixed-order folds).
+ */
+int mgcn_gemm_bwd_dw_cs(int64_t M, const float *X, int64_t ldx, const float *dH, int64_t lddh,
+                        float *dW, int64_t lddw, int accumulate, float *colsum, const float *S,
+                        int64_t lds, float *s_colsum, void *workspace, size_t workspace_bytes,
+                        void *stream);
 
 /* ------------------------------------------------- fused layer forward */
 

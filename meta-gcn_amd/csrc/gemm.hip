@@ -1779,17 +1779,22 @@ struct BwBank {
   u32x4 v[4];  // X rows q, 16 + q and dH rows q, 16 + q (q = tid >> 5), float4 tid & 31
   u32x4 mk;    // mask words of row tid & 31
   uint32_t rd; // row divisor of row tid & 31
+  u32x4 sv[2]; // SCS: rows q, 16 + q of S
 };
 
 // HCS (dW only): also the column sums of dH -- the bias gradient of the
 // layer whose output gradient dH is (gcn_base_models.py:240) -- from the
 // staged rows, so that pass needs no second read of dH.
-template <int EPI, bool DX, bool HCS = false>
+// SCS (dW only, ABI v20): also the column sums of another [M, 128] matrix S
+// streamed beside X and dH (a stack's top-layer bias gradient folded into the
+// bottom layer's pass) into s_partial.
+template <int EPI, bool DX, bool HCS = false, bool SCS = false>
 __global__ __launch_bounds__(kBwThreads, 1) void gemm_bwd_kernel(
     const float *__restrict__ X, int64_t ldx, const float *__restrict__ dH, int64_t lddh,
     const float *__restrict__ W, int64_t ldw, int64_t M, float *__restrict__ dX, int64_t lddx,
     const uint32_t *__restrict__ relu_mask, const float *__restrict__ row_div,
-    float *__restrict__ dw_partial, float *__restrict__ colsum_partial) {
+    float *__restrict__ dw_partial, float *__restrict__ colsum_partial,
+    const float *__restrict__ S = nullptr, int64_t lds_ = 0, float *__restrict__ s_partial = nullptr) {
   __shared__ __attribute__((aligned(16))) char lds[2 * kBwBuf];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1828,6 +1833,13 @@ __global__ __launch_bounds__(kBwThreads, 1) void gemm_bwd_kernel(
                                                      MGCN_NT_AUX);
       b.v[2 + m] = __builtin_amdgcn_raw_buffer_load_b128(rh, ld_off_h + m * 64 * (int)lddh, 0, 0);
     }
+    if constexpr (SCS) {
+      const auto rs = buf_rsrc(S + r0 * lds_, rv * (uint32_t)lds_ * 4u);
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+        b.sv[m] = __builtin_amdgcn_raw_buffer_load_b128(
+            rs, 4 * (int)((tid >> 5) * lds_ + 4 * (tid & 31)) + m * 64 * (int)lds_, 0, MGCN_NT_AUX);
+    }
     if constexpr (DX && EPI != EPI_STORE) {
       const auto rm = buf_rsrc(relu_mask + r0 * 4, rv * 16u);
       b.mk = __builtin_amdgcn_raw_buffer_load_b128(rm, 16 * (tid & 31), 0, 0);
@@ -1843,11 +1855,21 @@ __global__ __launch_bounds__(kBwThreads, 1) void gemm_bwd_kernel(
   // MFMA steps of the previous chunk so the split VALU work and the LDS
   // writes run under them
   float hc[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // HCS: dH column sums of float4 tid & 31
+  float sc[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // SCS: S column sums of float4 tid & 31
   auto stage_part = [&](const BwBank &b, char *buf, int m) {
     const int c4 = tid & 31;
     const int row = 16 * (m & 1) + (tid >> 5);
     const int off = img_off(row, c4 >> 1) + 8 * (c4 & 1);
     const float4 v = __builtin_bit_cast(float4, b.v[m]);
+    if constexpr (SCS) {
+      if (m >= 2) {  // rows q then 16 + q of every chunk, as hc
+        const float4 u = __builtin_bit_cast(float4, b.sv[m - 2]);
+        sc[0] = __fadd_rn(sc[0], u.x);
+        sc[1] = __fadd_rn(sc[1], u.y);
+        sc[2] = __fadd_rn(sc[2], u.z);
+        sc[3] = __fadd_rn(sc[3], u.w);
+      }
+    }
     if constexpr (HCS) {
       // every chunk is staged once (chunks past the end as zeros), rows q
       // then 16 + q: a fixed summation order
@@ -2021,6 +2043,18 @@ chunks_done:
 #pragma unroll
       for (int g = 0; g < 16; ++g) c = __fadd_rn(c, red[4 * (32 * g + (tid >> 2)) + (tid & 3)]);
       colsum_partial[(int64_t)blockIdx.x * kBwF + tid] = c;
+    }
+  }
+  if constexpr (SCS) {
+    __syncthreads();  // (HCS's fold, if any, has read its LDS)
+    float *red = reinterpret_cast<float *>(lds);
+    *reinterpret_cast<float4 *>(red + 4 * tid) = make_float4(sc[0], sc[1], sc[2], sc[3]);
+    __syncthreads();
+    if (tid < kBwF) {
+      float c = 0.0f;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) c = __fadd_rn(c, red[4 * (32 * g + (tid >> 2)) + (tid & 3)]);
+      s_partial[(int64_t)blockIdx.x * kBwF + tid] = c;
     }
   }
   if constexpr (DX && EPI != EPI_STORE) {
@@ -2514,6 +2548,60 @@ extern "C" int mgcn_gemm_bwd(int64_t M, int32_t F_in, int32_t F_out, const float
   if (hcs) return launch_colsum_fold(csp, fold_grid, F_out, colsum, s);
   if (epi == EPI_STORE) return MGCN_OK;
   return launch_colsum_fold(csp, grid, F_in, colsum, s);
+}
+
+extern "C" size_t mgcn_gemm_bwd_dw_cs_workspace_bytes(int64_t M) {
+  return mgcn_gemm_bwd_workspace_bytes(M, kBwF, kBwF) + align_up((size_t)kBwGrid * kBwF * 4, 256);
+}
+
+extern "C" int mgcn_gemm_bwd_dw_cs(int64_t M, const float *X, int64_t ldx, const float *dH,
+                                   int64_t lddh, float *dW, int64_t lddw, int accumulate,
+                                   float *colsum, const float *S, int64_t lds, float *s_colsum,
+                                   void *workspace, size_t workspace_bytes, void *stream) {
+  clear_error();
+  MGCN_REQUIRE(M >= 0, "mgcn_gemm_bwd_dw_cs: negative size");
+  MGCN_REQUIRE(g_gemm_precision == PREC_BF16X6, "mgcn_gemm_bwd_dw_cs: needs the bf16x6 products");
+  MGCN_REQUIRE(dW != nullptr && lddw >= kBwF && s_colsum != nullptr,
+               "mgcn_gemm_bwd_dw_cs: bad dW / s_colsum");
+  hipStream_t s = as_stream(stream);
+  if (M == 0) {
+    if (!accumulate)
+      for (int32_t r = 0; r < kBwF; ++r)
+        MGCN_HIP_TRY(hipMemsetAsync(dW + r * lddw, 0, sizeof(float) * kBwF, s));
+    if (colsum) MGCN_HIP_TRY(hipMemsetAsync(colsum, 0, sizeof(float) * kBwF, s));
+    MGCN_HIP_TRY(hipMemsetAsync(s_colsum, 0, sizeof(float) * kBwF, s));
+    return MGCN_OK;
+  }
+  MGCN_REQUIRE(X && dH && S && ldx >= kBwF && lddh >= kBwF && lds >= kBwF && ldx % 4 == 0 &&
+                   lddh % 4 == 0 && lds % 4 == 0 && reinterpret_cast<uintptr_t>(X) % 16 == 0 &&
+                   reinterpret_cast<uintptr_t>(dH) % 16 == 0 &&
+                   reinterpret_cast<uintptr_t>(S) % 16 == 0,
+               "mgcn_gemm_bwd_dw_cs: X / dH / S must be 16-byte aligned rows");
+  const size_t need = mgcn_gemm_bwd_dw_cs_workspace_bytes(M);
+  if (workspace == nullptr || workspace_bytes < need) {
+    set_error("mgcn_gemm_bwd_dw_cs: workspace %zu < %zu", workspace_bytes, need);
+    return MGCN_EWORKSPACE;
+  }
+  float *dwp = static_cast<float *>(workspace);
+  float *csp = reinterpret_cast<float *>(static_cast<char *>(workspace) +
+                                         align_up((size_t)kBwGrid * kBwF * kBwF * 4, 256));
+  float *ssp = reinterpret_cast<float *>(static_cast<char *>(workspace) +
+                                         mgcn_gemm_bwd_workspace_bytes(M, kBwF, kBwF));
+  const int64_t n_chunks = (M + kBwRows - 1) / kBwRows;
+  const int grid = (int)(n_chunks < kBwGrid ? n_chunks : kBwGrid);
+  if (colsum)
+    hipLaunchKernelGGL((gemm_bwd_kernel<EPI_STORE, false, true, true>), dim3(grid),
+                       dim3(kBwThreads), 0, s, X, ldx, dH, lddh, nullptr, 0, M, nullptr, 0,
+                       nullptr, nullptr, dwp, csp, S, lds, ssp);
+  else
+    hipLaunchKernelGGL((gemm_bwd_kernel<EPI_STORE, false, false, true>), dim3(grid),
+                       dim3(kBwThreads), 0, s, X, ldx, dH, lddh, nullptr, 0, M, nullptr, 0,
+                       nullptr, nullptr, dwp, csp, S, lds, ssp);
+  if (int rc = check_launch("gemm_bwd_kernel")) return rc;
+  if (int rc = launch_fold(dwp, grid, (int64_t)kBwF * kBwF, kBwF, dW, lddw, accumulate, s)) return rc;
+  if (colsum)
+    if (int rc = launch_colsum_fold(csp, grid, kBwF, colsum, s)) return rc;
+  return launch_colsum_fold(ssp, grid, kBwF, s_colsum, s);
 }
 
 namespace mgcn {

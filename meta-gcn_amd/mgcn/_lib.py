@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmgcn.so")
 
 # constants mirrored from include/mgcn.h
-ABI_VERSION = 19
+ABI_VERSION = 20
 OK, EINVAL, EINDEX, EHIP, EWORKSPACE = 0, 1, 2, 3, 4
 REDUCE_SUM, REDUCE_MEAN, REDUCE_MAX = 0, 1, 2
 NORM_NONE, NORM_SM, NORM_RW = 0, 1, 2
@@ -67,6 +67,9 @@ SIGNATURES = {
     "mgcn_gemm_bwd_workspace_bytes": (_sz, [_i64, _i32, _i32]),
     "mgcn_gemm_bwd": (_int, [_i64, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _int,
                              _vp, _i64, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "mgcn_gemm_bwd_dw_cs_workspace_bytes": (_sz, [_i64]),
+    "mgcn_gemm_bwd_dw_cs": (_int, [_i64, _vp, _i64, _vp, _i64, _vp, _i64, _int, _vp, _vp, _i64, _vp,
+                                   _vp, _sz, _vp]),
     "mgcn_edge_weight_grad": (_int, [_i64, _i32, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp]),
     "mgcn_edge_merge_workspace_bytes": (_sz, [_i64, _i64]),
     "mgcn_edge_merge_greedy": (_int, [_i64, _i64, _vp, _vp, _vp, _vp, _sz, _vp, _vp, _vp, _vp]),

@@ -55,6 +55,10 @@ _DWL = os.environ.get("MGCN_DWL", "0") != "0"
 # that launch ~0.25 ms, 5.16-5.19)
 _TOP_FULL = os.environ.get("MGCN_TOP_FULL", "1") != "0"
 _TOP_HCS = os.environ.get("MGCN_TOP_HCS", "0") != "0"
+# (with _TOP_FULL: the top bias gradient from the bottom layer's dW pass, which
+# streams dY beside its own operands -- mgcn_gemm_bwd_dw_cs; env
+# MGCN_TOP_CS_DEFER=0: a column-sum pass of its own)
+_TOP_CS_DEFER = os.environ.get("MGCN_TOP_CS_DEFER", "1") != "0"
 # max layers with dX: the dW + dX adjoint with the winner-bit routing in one
 # launch (mgcn_spmm_xw_bwd with win_mask: the warp-specialised kernel) instead
 # of mgcn_spmm_bwd + mgcn_gemm_bwd: env MGCN_MAX_FULL=0 turns it off
@@ -762,6 +766,37 @@ def dw_pass_supported(F_in: int, F_out: int) -> bool:
     return gemm_bwd_supported(F_in, F_out) or (int(F_in) % 128 == 0 and int(F_out) % 128 == 0)
 
 
+def dw_pass_cs(Z: torch.Tensor, dY: torch.Tensor, S: torch.Tensor):
+    """(dW = Z^T dY, the column sums of S) in one pass (``mgcn_gemm_bwd_dw_cs``,
+    128 x 128): S [M, 128] is streamed beside Z and dY -- a stack's top-layer
+    bias gradient folded into its bottom layer's dW pass."""
+    lib = L.load()
+    Z = _contig_f32(Z, "Z")
+    dY = _contig_f32(dY, "dY")
+    S = _contig_f32(S, "S")
+    for name, t in (("Z", Z), ("dY", dY), ("S", S)):
+        if t.dim() != 2 or t.size(1) != 128 or t.stride(0) % 4 or t.data_ptr() % 16:
+            raise ValueError(f"dw_pass_cs: {name} must be a [M, 128] float32 with 16-byte rows")
+    M = Z.size(0)
+    if dY.size(0) != M or S.size(0) != M:
+        raise ValueError(f"dw_pass_cs: Z, dY, S rows {M}, {dY.size(0)}, {S.size(0)}")
+    dev = L.require_device(Z, dY, S)
+    dW = torch.empty(128, 128, dtype=torch.float32, device=dev)
+    scs = torch.empty(128, dtype=torch.float32, device=dev)
+    ws_bytes = int(lib.mgcn_gemm_bwd_dw_cs_workspace_bytes(M))
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    if _TIMER is not None:
+        _TIMER("gemm_bwd_dw_cs", True, M)
+    with L.device_guard(dev):
+        rc = lib.mgcn_gemm_bwd_dw_cs(M, L.ptr(Z), Z.stride(0), L.ptr(dY), dY.stride(0), L.ptr(dW),
+                                     dW.stride(0), 0, None, L.ptr(S), S.stride(0), L.ptr(scs),
+                                     L.ptr(ws), ws_bytes, L.stream_of(dev))
+    if _TIMER is not None:
+        _TIMER("gemm_bwd_dw_cs", False)
+    L.check(rc, "mgcn_gemm_bwd_dw_cs")
+    return dW, scs
+
+
 def dw_pass(Z: torch.Tensor, dY: torch.Tensor, W: torch.Tensor, dh_colsum: bool = False):
     """(dW = Z^T dY, the column sums of dY or None) -- :func:`dw_pass_supported`."""
     if gemm_bwd_supported(W.size(0), W.size(1)):
@@ -1241,8 +1276,8 @@ class _GCNStack(torch.autograd.Function):
                             spmm_xw_bwd_dwl_supported(*nxt.shape))
                 top_full = (_TOP_FULL and i == len(Ws) - 1 and i > 0 and relus[i - 1] and
                             rmasks[i - 1] is not None and not relu and
-                            reduce == L.REDUCE_SUM and plan.bwd.n_rows == plan.bwd.n_cols and
-                            xw_full_supported(*W.shape))
+                            reduce in (L.REDUCE_SUM, L.REDUCE_MEAN) and
+                            plan.bwd.n_rows == plan.bwd.n_cols and xw_full_supported(*W.shape))
                 want_z = (bool(ctx.needs_input_grad[5 + 2 * i]) and below and not top_full and
                           (_Z_MIDDLE or dwl_next or not middle or
                            not xw_full_supported(*W.shape)) and
@@ -1309,11 +1344,21 @@ class _GCNStack(torch.autograd.Function):
                    ctx.has_bias[top] and plan.bwd.n_rows == plan.bwd.n_cols and
                    _FUSE_XW and xw_full_supported(*Ws[top].shape) and
                    spmm_xw_supported(plan.bwd, Ws[top].size(0), Ws[top].size(1), L.REDUCE_SUM))
-        if top_z or top_hcs:
+        # or from the bottom layer's dW = Z^T dY pass, which streams dZ beside
+        # its own operands (mgcn_gemm_bwd_dw_cs): no separate pass over dZ
+        top_defer = (not top_z and not top_hcs and _TOP_CS_DEFER and not _DWL and top > 0 and
+                     not relus[top] and rd is None and ctx.has_bias[top] and
+                     ctx.needs_input_grad[5] and z_path(0) and
+                     gemm_bwd_supported(*Ws[0].shape) and tuple(dZ.shape) == (zs[0].size(0), 128))
+        top_S = None
+        if top_z or top_hcs or top_defer:
             # dY = dZ as it is: its column sums (the top bias gradient) come
-            # from the dW = Z^T dY pass below or from the top layer's dW + dX
-            # adjoint (top_hcs), no separate read of dZ
+            # from the dW = Z^T dY pass below, from the top layer's dW + dX
+            # adjoint (top_hcs) or from the bottom layer's dW pass (top_defer),
+            # no separate read of dZ
             dY = dZ.contiguous()
+            if top_defer:
+                top_S = dY
         else:
             dY, db = relu_bwd_colsum(dZ.contiguous(), outs[top], relus[top], ctx.has_bias[top],
                                      row_div=rd)
@@ -1361,7 +1406,9 @@ class _GCNStack(torch.autograd.Function):
                 # product.  The gather runs only for dX (+ the lower layer's
                 # ReLU / bias gradient); the bottom layer needs no gather at all.
                 hcs = bool(top_z and l == top and ctx.has_bias[top])
-                if gW[l] is None:  # (not already formed by the layer above's adjoint)
+                if gW[l] is None and top_S is not None and l == 0:
+                    gW[l], gb[top] = dw_pass_cs(zs[l], dY, top_S)  # + the top bias gradient
+                elif gW[l] is None:  # (not already formed by the layer above's adjoint)
                     gW[l], cs = dw_pass(zs[l], dY, W, dh_colsum=hcs)
                     if hcs:
                         gb[top] = cs

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Parametrised A/B run on the GPU box (repo root), replacing the one-off
 # per-experiment wrappers of earlier rounds:
-#   TESTS="tests/test_gpu_x.py -k y" bash scripts/gpu_ab.sh <tag> <workload> <reps> "<arm 1>" "<arm 2>" ...
+#   TESTS="tests/test_gpu_x.py" TESTS_K="y or z" bash scripts/gpu_ab.sh <tag> <workload> <reps> "<arm 1>" "<arm 2>" ...
 # workload: bench | config3 | config4 | config4max | config5rank | cmd:<command>
 # an arm is a space-separated list of VAR=value settings ("" = defaults), e.g.
 #   "MGCN_LIB=$PWD/meta-gcn_amd/mgcn/libmgcn_x.so"  (an alternative build)
@@ -11,8 +11,10 @@
 set -e -o pipefail
 O=$PWD/gpurun_out/$1; W=$2; N=$3; shift 3
 mkdir -p "$O"
+KARG=()
+if [ -n "$TESTS_K" ]; then KARG=(-k "$TESTS_K"); fi
 if [ -n "$TESTS" ]; then
-  timeout -k 10 600 python -u -m pytest $TESTS -x -q --timeout 150 --timeout-method thread \
+  timeout -k 10 600 python -u -m pytest $TESTS "${KARG[@]}" -x -q --timeout 150 --timeout-method thread \
     > "$O/tests.log" 2>&1 || { tail -40 "$O/tests.log"; exit 1; }
   tail -1 "$O/tests.log"
 fi

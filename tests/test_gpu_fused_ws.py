@@ -420,9 +420,10 @@ def test_ws_full_hcs_column_sums(cuda, N, E):
             ops.spmm_xw_bwd(v, norm.w_bwd, None, dY, X[:N // 2], W, dy_colsum_out=hc)
 
 
-@pytest.mark.parametrize("hcs", [False, True])
+@pytest.mark.parametrize("aggr,deg_norm", [("add", "sm"), ("mean", "rw")])
+@pytest.mark.parametrize("hcs,defer", [(False, True), (False, False), (True, False)])
 @pytest.mark.parametrize("layers", [2, 3])
-def test_stack_top_full_vs_z_form(cuda, monkeypatch, layers, hcs):
+def test_stack_top_full_vs_z_form(cuda, monkeypatch, layers, hcs, defer, aggr, deg_norm):
     """The stack's top layer on the dW + dX adjoint (ops._TOP_FULL, the
     default), its bias gradient from a column-sum pass or (hcs) from the same
     launch (ops._TOP_HCS), against the Z form (Z kept,
@@ -434,13 +435,14 @@ def test_stack_top_full_vs_z_form(cuda, monkeypatch, layers, hcs):
     rng = np.random.default_rng(31)
     N = 8000
     ei = _t(_graph(rng, N, 80000), cuda)
-    stack = GCNStack([GCNLayer(F, F, deg_norm="sm", aggr="add", bias=True,
+    stack = GCNStack([GCNLayer(F, F, deg_norm=deg_norm, aggr=aggr, bias=True,
                                non_linear="relu" if i < layers - 1 else "none").to(cuda)
                       for i in range(layers)])
     x = torch.randn(N, F, device=cuda, requires_grad=True)
     dZ = torch.randn(N, F, device=cuda)
     res = []
     monkeypatch.setattr(ops, "_TOP_HCS", hcs)
+    monkeypatch.setattr(ops, "_TOP_CS_DEFER", defer)
     for top_full in (True, False):
         monkeypatch.setattr(ops, "_TOP_FULL", top_full)
         x.grad = None
@@ -519,3 +521,43 @@ def test_gather_unroll_forms_bitwise(cuda, N, E, hub):
             assert torch.equal(a, c)
         for a, c in zip(bwd[u], bwd[4]):
             assert torch.equal(a, c)
+
+
+@pytest.mark.parametrize("M", [1, 31, 33, 4097, 300000])
+@pytest.mark.parametrize("hcs", [False, True])
+def test_dw_pass_with_third_stream_colsum(cuda, M, hcs):
+    """mgcn_gemm_bwd_dw_cs: dW (and dH's column sums) bit for bit mgcn_gemm_bwd's
+    dW-only pass (the same kernel, chunk map and fold), plus the column sums of
+    a third matrix S streamed in the same pass, within fp32 summation
+    tolerance of the fp64 sums; an empty M zeroes every output."""
+    from mgcn import _lib as L
+    from mgcn import ops
+    lib = L.load()
+    g = torch.Generator(device=cuda).manual_seed(M + 3)
+    Z = torch.randn(M, F, device=cuda, generator=g)
+    dY = torch.randn(M, F, device=cuda, generator=g)
+    S = torch.randn(M, F, device=cuda, generator=g)
+    W = torch.randn(F, F, device=cuda, generator=g)
+    ref_dw, _, ref_cs = ops.gemm_bwd(Z, dY, W, want_dx=False, dh_colsum=hcs)
+    dW = torch.empty(F, F, device=cuda)
+    cs = torch.empty(F, device=cuda) if hcs else None
+    scs = torch.empty(F, device=cuda)
+    wsb = int(lib.mgcn_gemm_bwd_dw_cs_workspace_bytes(M))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=cuda)
+    with L.device_guard(cuda):
+        rc = lib.mgcn_gemm_bwd_dw_cs(M, L.ptr(Z), F, L.ptr(dY), F, L.ptr(dW), F, 0, L.ptr(cs),
+                                     L.ptr(S), F, L.ptr(scs), L.ptr(ws), wsb, L.stream_of(cuda))
+    L.check(rc, "mgcn_gemm_bwd_dw_cs")
+    assert torch.equal(dW, ref_dw)
+    if hcs:
+        assert torch.equal(cs, ref_cs)
+    bound = S.double().abs().sum(0)
+    assert ((scs.double() - S.double().sum(0)).abs() <= 1e-5 * bound + 1e-6).all()
+    dW2, scs2 = ops.dw_pass_cs(Z, dY, S)
+    assert torch.equal(dW2, dW) and torch.equal(scs2, scs)
+    z = torch.full((F,), float("nan"), device=cuda)
+    with L.device_guard(cuda):
+        rc = lib.mgcn_gemm_bwd_dw_cs(0, L.ptr(Z), F, L.ptr(dY), F, L.ptr(dW), F, 0, None,
+                                     L.ptr(S), F, L.ptr(z), L.ptr(ws), wsb, L.stream_of(cuda))
+    L.check(rc, "mgcn_gemm_bwd_dw_cs")
+    assert (z == 0).all() and (dW == 0).all()
