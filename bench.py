@@ -441,9 +441,9 @@ def main():
                        "backward reads it (the bottom layer); "
                        "backward: the top and middle layers' adjoints gather dY and form "
                        "dW = X^T (A^T dY) and dX in one launch (mgcn_spmm_xw_bwd, the "
-                       "warp-specialised kernel), the top bias gradient from a column-sum pass "
-                       "over dY; the bottom layer keeps Z = A x from its forward and forms "
-                       "dW = Z^T dY in one dense pass (mgcn_gemm_bwd), no gather "
+                       "warp-specialised kernel); the bottom layer keeps Z = A x from its "
+                       "forward and forms dW = Z^T dY in one dense pass that also streams the "
+                       "top layer's dY for the top bias gradient (mgcn_gemm_bwd_dw_cs), no gather "
                        "(tests/test_gpu_fused.py, tests/test_gpu_headline.py)"),
         "config": {"workload": head["workload"], "nodes": N, "edges": n_edges, "nnz": nnz,
                    "feat": F, "layers": L, "global_batch": world if mode == "replica" else 1,
