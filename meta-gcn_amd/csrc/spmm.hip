@@ -476,6 +476,10 @@ int g_force_vec = 0;  // tuning knobs (mgcn_set_option)
 int g_unroll = 8;
 bool g_unroll_set = false;  // spmm_unroll given explicitly: every mode takes it
 int g_heavy_side = 1;  // heavy-row launch on a side stream (concurrent)
+// mgcn_set_option("heavy_mid_side"): heavy_rows() also puts the non-giant heavy
+// rows on the side stream (after the giant ones), so the caller's light-row
+// pass starts at once on its stream
+int g_heavy_mid_side = 0;
 
 template <int VEC, int G, int U, int MODE>
 int launch_one(const SpmmArgs &a, hipStream_t stream) {
@@ -701,8 +705,14 @@ int heavy_rows(int bwd, int64_t n_rows, int32_t F, const int64_t *rowptr, const 
       const int rc = bwd ? launch_heavy_v<BWD_SUM>(a, vec, true, side->stream)
                          : launch_heavy_v<FWD_SUM>(a, vec, true, side->stream);
       if (rc) return rc;
+      if (g_heavy_mid_side && n_heavy > n_giant) {
+        const int rc2 = bwd ? launch_heavy_v<BWD_SUM>(a, vec, false, side->stream)
+                            : launch_heavy_v<FWD_SUM>(a, vec, false, side->stream);
+        if (rc2) return rc2;
+      }
       MGCN_HIP_TRY(hipEventRecord(side->join, side->stream));
       *side_used = true;
+      if (g_heavy_mid_side) return MGCN_OK;  // (the mid heavy rows went with them)
     } else {
       const int rc = bwd ? launch_heavy_v<BWD_SUM>(a, vec, true, stream)
                          : launch_heavy_v<FWD_SUM>(a, vec, true, stream);
@@ -815,6 +825,11 @@ extern "C" int mgcn_set_option(const char *name, int value) {
   if (n == "heavy_side_fence") {
     MGCN_REQUIRE(value == 0 || value == 1, "heavy_side_fence must be 0 or 1");
     g_side_fence = value;
+    return MGCN_OK;
+  }
+  if (n == "heavy_mid_side") {
+    MGCN_REQUIRE(value == 0 || value == 1, "heavy_mid_side must be 0 or 1");
+    g_heavy_mid_side = value;
     return MGCN_OK;
   }
   if (n == "heavy_side_stream") {
