@@ -171,6 +171,24 @@ __device__ __forceinline__ void gather_row(const __amdgpu_buffer_rsrc_t rx, uint
   deg_out = deg;
 }
 
+// Broadcast of lane 32 grp + k (k wave-uniform) to its 32-lane group: two
+// v_readlane and a select instead of a ds_bpermute (MGCN_BCAST_READLANE; no
+// LDS traffic beside the warp-specialised kernels' image reads)
+#ifndef MGCN_BCAST_READLANE
+#define MGCN_BCAST_READLANE 0
+#endif
+__device__ __forceinline__ int bcast_g(int v, int grp, int k) {
+#if MGCN_BCAST_READLANE
+  const int lo = __builtin_amdgcn_readlane(v, k), hi = __builtin_amdgcn_readlane(v, 32 + k);
+  return grp ? hi : lo;
+#else
+  return __shfl(v, 32 * grp + k, 64);
+#endif
+}
+__device__ __forceinline__ float bcast_g(float v, int grp, int k) {
+  return __int_as_float(bcast_g(__float_as_int(v), grp, k));
+}
+
 // Pipelined form for a wave that walks a known sequence of rows: the row
 // pointer pair of row k + 2 and the first 32 edge slots (col, w) of row k + 1
 // are loaded while row k's feature rows are gathered, so a row costs one
@@ -240,8 +258,8 @@ __device__ __forceinline__ void gather_row_meta(const __amdgpu_buffer_rsrc_t rx,
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int k = k0 + u;
-        const int ck = __shfl(mc, 32 * grp + (k & 31), 64);
-        wk[u] = __shfl(mw, 32 * grp + (k & 31), 64);
+        const int ck = bcast_g(mc, grp, k & 31);
+        wk[u] = bcast_g(mw, grp, k & 31);
         ok[u] = k < nb;
         const uint32_t off = ok[u] ? (uint32_t)ck * ldx_b + 16u * gl : 0xfffffff0u;
         xv[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0));
@@ -312,18 +330,18 @@ __device__ __forceinline__ void gather_row2_meta(const __amdgpu_buffer_rsrc_t rx
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int k = k0 + u;
-        const int ca = __shfl(mca, 32 * grp + (k & 31), 64);
-        const int cb = __shfl(mcb, 32 * grp + (k & 31), 64);
-        wa[u] = __shfl(mwa, 32 * grp + (k & 31), 64);
-        wb[u] = __shfl(mwb, 32 * grp + (k & 31), 64);
+        const int ca = bcast_g(mca, grp, k & 31);
+        const int cb = bcast_g(mcb, grp, k & 31);
+        wa[u] = bcast_g(mwa, grp, k & 31);
+        wb[u] = bcast_g(mwb, grp, k & 31);
         const uint32_t oa = k < na ? (uint32_t)ca * ldx_b + 16u * gl : 0xfffffff0u;
         const uint32_t ob = k < nb ? (uint32_t)cb * ldx_b + 16u * gl : 0xfffffff0u;
         xa[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, oa, 0, 0));
         xb[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, ob, 0, 0));
         if constexpr (MAXM) {
           // loaded unconditionally (masked edges read word 0, never used)
-          const int sa = __shfl(msa, 32 * grp + (k & 31), 64);
-          const int sb = __shfl(msb, 32 * grp + (k & 31), 64);
+          const int sa = bcast_g(msa, grp, k & 31);
+          const int sb = bcast_g(msb, grp, k & 31);
           ba[u] = win[k < na ? (int64_t)sa * 4 + (gl >> 3) : 0];
           bb[u] = win[k < nb ? (int64_t)sb * 4 + (gl >> 3) : 0];
         }
@@ -633,8 +651,8 @@ __device__ __forceinline__ void gather_row_max(const __amdgpu_buffer_rsrc_t rx, 
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int k = k0 + u;
-        const int ck = __shfl(mc, 32 * grp + (k & 31), 64);
-        wk[u] = __shfl(mw, 32 * grp + (k & 31), 64);
+        const int ck = bcast_g(mc, grp, k & 31);
+        wk[u] = bcast_g(mw, grp, k & 31);
         ok[u] = k < nb;
         const uint32_t off = ok[u] ? (uint32_t)ck * ldx_b + 16u * gl : 0xfffffff0u;
         xv[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0));
