@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define MGCN_ABI_VERSION 20
+#define MGCN_ABI_VERSION 21
 
 /* return codes */
 #define MGCN_OK 0
@@ -45,6 +45,9 @@ extern "C" {
 #define MGCN_EINDEX 2   /* an edge index is outside [0, n)                    */
 #define MGCN_EHIP 3     /* a HIP runtime call or kernel launch failed          */
 #define MGCN_EWORKSPACE 4 /* caller-provided workspace is too small            */
+#define MGCN_EDEVICE 5  /* a kernel reported a failure from the device: the
+                           outputs of that launch are invalid (see
+                           mgcn_check_device)                                 */
 
 /* reductions (common.py:54 `name in ['add', 'mean', 'max']`) */
 #define MGCN_REDUCE_SUM 0
@@ -61,6 +64,18 @@ extern "C" {
 
 int mgcn_abi_version(void);
 const char *mgcn_last_error(void);
+
+/* Device-side failures (ABI 21).  The warp-specialised kernels (the 128-wide
+ * adjoint behind mgcn_spmm_xw_bwd, the 256-wide layer kernels behind
+ * mgcn_spmm_xw_fwd / _bwd) hand chunks between their waves through LDS
+ * counters with bounded spins; a spin that runs past its bound makes every
+ * wave leave, and the kernel then stores a code into a host-mapped error
+ * word instead of finishing silently.  That word is reported as MGCN_EDEVICE
+ * (+ mgcn_last_error naming the kernel) by the next mgcn_spmm_xw_* call, or
+ * here: sync != 0 synchronises `stream` first, so every launch issued on it
+ * before this call is covered.  Reading the word clears it.  No reference
+ * counterpart (torch_scatter reports nothing from the device either). */
+int mgcn_check_device(void *stream, int sync);
 
 /* Tuning knobs (process-wide; default 0 = automatic):
  *   "spmm_vec"    : cap the floats per lane of the SpMM gathers (1, 2, 4)

@@ -1280,7 +1280,6 @@ static_assert(kDsLds <= 160 * 1024, "one DWS workgroup per CU");
 static_assert(16 * kXwF * 4 <= kDsWOff, "column-sum fold fits in the ring");
 constexpr int kBsNG = 8, kBsNM = 8;
 constexpr int kBsThreads = 64 * (kBsNG + kBsNM);
-constexpr uint32_t kBsSpinLimit = 1u << 25;
 #ifndef MGCN_BS_HOLDW
 #define MGCN_BS_HOLDW 0  // DWL: W^T fragments held in registers (0: re-read per chunk)
 #endif
@@ -1290,11 +1289,12 @@ __device__ __forceinline__ int bs_lds_load(const int *p) {
       __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
 }
 
-__device__ __forceinline__ bool bs_wait_ge(const int *p, int target, int *abort_word) {
+__device__ __forceinline__ bool bs_wait_ge(const int *p, int target, int *abort_word,
+                                           uint32_t limit) {
   for (uint32_t n = 0;; ++n) {
     if (bs_lds_load(p) >= target) break;
     if (bs_lds_load(abort_word) != 0) return false;
-    if (n >= kBsSpinLimit) {
+    if (n >= limit) {
       __hip_atomic_store(abort_word, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       return false;
     }
@@ -1329,7 +1329,9 @@ struct XbsArgs {
   int64_t ldz;
   float *dwl_partial;   // DWL: [grid][128][128]
   float *hcs_partial;   // DWS (nullable): [grid][128] column sums of dY's own rows
-  int dbg;              // xw_ws_dbg (timing experiments only; 0 in production)
+  int dbg;              // xw_ws_dbg (experiment builds only; masked by kDbgMask)
+  uint32_t spin;        // hand-off spin bound (g_spin_limit)
+  unsigned *err;        // device error word: kDevErrDws when a hand-off gave up
 };
 
 template <int U, int EPI, int MODE>
@@ -1414,7 +1416,7 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
       const int64_t r0 = c * kXwRows;
       const int lr0 = 4 * (int)(q & 7) + grp;
       u32x4 zv[2] = {};
-      if ((DWL || DWS) && !(A.dbg & 4)) {  // the rows' Zl / X, under the gathers (streamed once)
+      if ((DWL || DWS) && !(A.dbg & kDbgMask & 4)) {  // the rows' Zl / X, under the gathers (streamed once)
         const auto rz = buf_rsrc(A.Zl + r0 * A.ldz, rows_in(c) * (uint32_t)A.ldz * 4u);
 #pragma unroll
         for (int j = 0; j < 2; ++j)
@@ -1471,7 +1473,7 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
       }
       const int b = (int)(i & 1);
       const int gen = (int)(i >> 1);
-      if (!bs_wait_ge(freed + b, gen, abort_word)) break;
+      if (!bs_wait_ge(freed + b, gen, abort_word, A.spin)) break;
       char *buf = lds + b * kRing;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -1573,7 +1575,7 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
             dv[rt] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rd, 4 * (16 * rt + l16), 0, 0));
         }
       }
-      if (!bs_wait_ge(filled + b, kXwRows * (gen + 1), abort_word)) break;
+      if (!bs_wait_ge(filled + b, kXwRows * (gen + 1), abort_word, A.spin)) break;
       uint32_t mbits[2] = {0u, 0u};  // MRING: this lane's 4 mask bits per row tile
       if constexpr (EPI != EPI_STORE && MRING) {  // from the ring (the gather waves loaded them)
 #pragma unroll
@@ -1599,7 +1601,7 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
         // dW += X^T dH: X^T fragments (lane: column 32 ti + lc of rows
         // 16 ks + 8 h + j) read from the fp32 rows and split here, dH^T
         // fragments from the term images
-        if (!(A.dbg & 1)) {
+        if (!(A.dbg & kDbgMask & 1)) {
           const float *xr = reinterpret_cast<const float *>(buf + kDsXOff) + 32 * ti + (lane_o & 31);
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks) {
@@ -1630,7 +1632,7 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
                             : wp;
       float4 wn0{}, wn1{};
       if constexpr (!kHoldW) {
-        if (!(A.dbg & 8)) {  // dbg 8: no W^T loads (timing only: dX wrong)
+        if (!(A.dbg & kDbgMask & 8)) {  // dbg 8: no W^T loads (timing only: dX wrong)
           wn0 = *reinterpret_cast<const float4 *>(wq);
           wn1 = *reinterpret_cast<const float4 *>(wq + 4);
         }
@@ -1642,7 +1644,7 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
         bf16x8 wk[3];
         if constexpr (!kHoldW) {
           const float v8[8] = {wn0.x, wn0.y, wn0.z, wn0.w, wn1.x, wn1.y, wn1.z, wn1.w};
-          if (ks + 1 < 4 && !(A.dbg & 8)) {
+          if (ks + 1 < 4 && !(A.dbg & kDbgMask & 8)) {
             wn0 = *reinterpret_cast<const float4 *>(wq + 32 * (ks + 1));
             wn1 = *reinterpret_cast<const float4 *>(wq + 32 * (ks + 1) + 4);
           }
@@ -1680,11 +1682,11 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
         if constexpr (DWL) store_row_terms(ximg, row, 4 * m + g4, v);
       }
       }
-      if (DWL && !(A.dbg & 1)) {
+      if (DWL && !(A.dbg & kDbgMask & 1)) {
         // every wave's 16 columns of the chunk's dX images are in
         bs_signal(xdone + (int)(i & 1), 1, lane);
-        if (!bs_wait_ge(xdone + (int)(i & 1), kBsNM * (gen + 1), abort_word)) break;
-        if (!(A.dbg & 2)) {
+        if (!bs_wait_ge(xdone + (int)(i & 1), kBsNM * (gen + 1), abort_word, A.spin)) break;
+        if (!(A.dbg & kDbgMask & 2)) {
         const char *zimg = buf + kBsImgSet;
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
@@ -1708,6 +1710,9 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
     }
   }
   __syncthreads();
+  // a hand-off gave up: this launch's dX / dW are incomplete -- say so (the
+  // host turns the word into MGCN_EDEVICE) instead of returning them silently
+  if (wave == 0 && bs_lds_load(abort_word) != 0) report_device_error(A.err, kDevErrDws);
   if (wave >= kBsNG) {
     const int m = wave - kBsNG;
     if constexpr (DWL || DWS) {
@@ -1808,6 +1813,14 @@ int launch_bs(const XbsArgs &a, int epi, int grid, hipStream_t s) {
   }
 }
 
+// the warp-specialised launch's failure plumbing: spin bound, error word
+int bs_prepare(XbsArgs &sa) {
+  sa.dbg = g_bs_dbg;
+  sa.spin = g_spin_limit;
+  sa.err = device_error_word();
+  return sa.err == nullptr ? MGCN_EHIP : MGCN_OK;
+}
+
 }  // namespace
 
 int xw_set_ws(const char *name, int value) {
@@ -1832,7 +1845,11 @@ int xw_set_ws(const char *name, int value) {
   if (n == "xw_ws_xm_unroll") return unroll(g_xm_unroll, {4, 6, 8});
   if (n == "xw_ws_max") return flag(g_xw_ws_max);
   if (n == "xw_ws_full") return flag(g_xw_ws_full);
-  if (n == "xw_ws_dbg") {
+  if (n == "xw_ws_dbg") {  // (timing experiments: results WRONG when set)
+    if (!MGCN_EXPERIMENT) {
+      set_error("xw_ws_dbg: experiment builds only (make exp -> libmgcn_exp.so)");
+      return MGCN_EINVAL;
+    }
     g_bs_dbg = value;
     return MGCN_OK;
   }
@@ -1876,6 +1893,7 @@ extern "C" int mgcn_spmm_xw_fwd(int64_t n_rows, int64_t n_cols, int32_t F_in, in
                                 uint32_t *relu_mask, float *Z, int64_t ldz, void *workspace,
                                 size_t workspace_bytes, void *stream) {
   clear_error();
+  if (int rc = take_device_error()) return rc;  // a previous launch failed on the device
   MGCN_REQUIRE(n_rows >= 0, "mgcn_spmm_xw_fwd: negative size");
   MGCN_REQUIRE(mgcn_spmm_xw_supported(F_in, F_out, reduce),
                "mgcn_spmm_xw_fwd: unsupported F_in=%d F_out=%d reduce=%d (needs 128 x 128 or "
@@ -1959,6 +1977,7 @@ int xw_bwd_impl(int64_t n_rows, int64_t n_cols, int32_t F_in, int32_t F_out,
                 float *dX, int64_t lddx, const uint32_t *relu_mask, const float *row_div,
                 float *colsum, const uint32_t *win_mask, const int32_t *slot_map,
                 float *dy_colsum, void *workspace, size_t workspace_bytes, void *stream) {
+  if (int rc = take_device_error()) return rc;  // a previous launch failed on the device
   MGCN_REQUIRE(n_rows >= 0, "mgcn_spmm_xw_bwd: negative size");
   MGCN_REQUIRE((win_mask == nullptr) == (slot_map == nullptr),
                "mgcn_spmm_xw_bwd: win_mask and slot_map go together (max adjoint)");
@@ -2016,6 +2035,9 @@ int xw_bwd_impl(int64_t n_rows, int64_t n_cols, int32_t F_in, int32_t F_out,
                "mgcn_spmm_xw_bwd: leading dimension too large");
   MGCN_REQUIRE(dX == nullptr || (W != nullptr && ldw >= F_out && lddx >= F_in),
                "mgcn_spmm_xw_bwd: bad W/dX");
+  // the warp-specialised adjoint copies W into LDS with 16-byte loads
+  MGCN_REQUIRE(W == nullptr || (ldw % 4 == 0 && reinterpret_cast<uintptr_t>(W) % 16 == 0),
+               "mgcn_spmm_xw_bwd: W must have 16-byte aligned rows");
   MGCN_REQUIRE(relu_mask == nullptr || reinterpret_cast<uintptr_t>(relu_mask) % 16 == 0,
                "mgcn_spmm_xw_bwd: relu_mask not 16-byte aligned");
   const size_t need = mgcn_spmm_xw_bwd_workspace_bytes(n_rows, F_in, F_out);
@@ -2052,6 +2074,7 @@ int xw_bwd_impl(int64_t n_rows, int64_t n_cols, int32_t F_in, int32_t F_out,
   if (dx_only && g_xw_ws) {  // the warp-specialised form (one workgroup per CU)
     XbsArgs sa{};
     sa.b = a;
+    if (int rc2 = bs_prepare(sa)) return rc2;
     const int64_t g = bs_grid() < n_chunks ? bs_grid() : n_chunks;
     rc = launch_bs<kBsDx>(sa, epi, (int)g, s);
     if (rc || epi == EPI_STORE) return rc;
@@ -2073,7 +2096,7 @@ int xw_bwd_impl(int64_t n_rows, int64_t n_cols, int32_t F_in, int32_t F_out,
     sa.Zl = X;
     sa.ldz = ldx;
     sa.dwl_partial = a.dw_partial;
-    sa.dbg = g_bs_dbg;
+    if (int rc2 = bs_prepare(sa)) return rc2;
     grid = bs_grid() < n_chunks ? bs_grid() : (int)n_chunks;
     // dY's column sums: [grid][128] partials past the grid's dW slabs (the
     // dW partial area holds xw_grid() = 2 x CUs slabs, this grid <= CUs)
@@ -2201,7 +2224,7 @@ extern "C" int mgcn_spmm_xw_bwd_dwl(int64_t n_rows, int64_t n_cols, const int64_
   sa.Zl = Zl;
   sa.ldz = ldz;
   sa.dwl_partial = static_cast<float *>(workspace);
-  sa.dbg = g_bs_dbg;
+  if (int rc2 = bs_prepare(sa)) return rc2;
   a.colsum_partial = reinterpret_cast<float *>(
       static_cast<char *>(workspace) + align_up((size_t)g * kXwF * kXwF * 4, 256));
   const int epi = relu_mask == nullptr ? EPI_STORE : row_div != nullptr ? EPI_RELU_DIV : EPI_RELU;

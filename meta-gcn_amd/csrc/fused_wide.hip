@@ -80,7 +80,11 @@ int wide_set_option(const char *name, int value) {
     g_wide_mfma = value;
     return MGCN_OK;
   }
-  if (name[5] == 'd') {
+  if (name[5] == 'd') {  // (timing experiments: results WRONG when set)
+    if (!MGCN_EXPERIMENT) {
+      set_error("wide_dbg: experiment builds only (make exp -> libmgcn_exp.so)");
+      return MGCN_EINVAL;
+    }
     g_wide_dbg = value;
     return MGCN_OK;
   }
@@ -176,7 +180,9 @@ struct WideArgs {
   const float *row_div;        // backward mean divisor
   float *colsum_partial;       // backward: [grid][256]
   int mean, relu;
-  int dbg;                     // wide_dbg (timing experiments only; 0 in production)
+  int dbg;                     // wide_dbg (experiment builds only; masked by kDbgMask)
+  uint32_t spin;               // warp-specialised hand-off spin bound (g_spin_limit)
+  unsigned *err;               // device error word: kDevErrWide when a hand-off gave up
 };
 
 // a row's edge slots: [beg, beg + deg) (wave-uniform), and lane l's slot
@@ -597,7 +603,7 @@ __global__ __launch_bounds__(kWThreads, 4) void spmm_xw_wide_kernel(const WideAr
 // Hand-offs are LDS counters inside the workgroup (monotonic per buffer; a
 // wave's LDS operations complete in order, so its image writes land before
 // its counter add), polled with s_sleep and bounded: a spin that exceeds
-// kSpinLimit sets the abort word and every wave leaves its loop.  The MFMA
+// the bound (g_spin_limit) sets the abort word and every wave leaves its loop.  The MFMA
 // term order is the 16-row kernel's with the operands swapped (the same six
 // products per k-step in the same order), so Y / dX equal its results.
 constexpr int kSRows = 32;
@@ -610,7 +616,6 @@ constexpr int kSCtrOff = kSMaskOff + kSBufs * kSRows * kWMaskWords * 4;  // coun
 constexpr int kSLds = kSCtrOff + 64;
 static_assert(kSLds <= 160 * 1024, "one warp-specialised workgroup per CU");
 static_assert(16 * kWF * 4 <= kSMaskOff, "column-sum fold fits in the image ring");
-constexpr uint32_t kSpinLimit = 1u << 25;
 
 // the 16-row kernel's six products (rows_l W_h, rows_h W_l, rows_m W_m,
 // rows_m W_h, rows_h W_m, rows_h W_h) with W as the A operand
@@ -633,11 +638,12 @@ __device__ __forceinline__ int lds_load(const int *p) {
 }
 
 // wait until *p >= target (false: the abort word is set, leave)
-__device__ __forceinline__ bool lds_wait_ge(const int *p, int target, int *abort_word) {
+__device__ __forceinline__ bool lds_wait_ge(const int *p, int target, int *abort_word,
+                                            uint32_t limit) {
   for (uint32_t n = 0;; ++n) {
     if (lds_load(p) >= target) break;
     if (lds_load(abort_word) != 0) return false;
-    if (n >= kSpinLimit) {
+    if (n >= limit) {
       __hip_atomic_store(abort_word, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       return false;
     }
@@ -689,7 +695,7 @@ __global__ __launch_bounds__(kSThreads) void spmm_xw_wide_ws_kernel(const WideAr
 
   if (wave < NG) {
     // ------------------------------- gather waves ---------------------------
-    if (a.dbg & 8) __builtin_amdgcn_s_setprio(2);
+    if (a.dbg & kDbgMask & 8) __builtin_amdgcn_s_setprio(2);
     const int64_t n_pairs = 16 * n_my;
     auto pair_row = [&](int64_t p) { return chunk_of(p >> 4) * kSRows + 2 * (p & 15); };
     WRow cur, cur2, nxt, nxt2;
@@ -712,7 +718,7 @@ __global__ __launch_bounds__(kSThreads) void spmm_xw_wide_ws_kernel(const WideAr
       wrow_ptr(a.rowptr, rq, q < n_pairs && rq < a.n_rows, nn);
       wrow_ptr(a.rowptr, rq + 1, q < n_pairs && rq + 1 < a.n_rows, nn2);
       float acc[2][4];
-      if (a.dbg & 4) {
+      if (a.dbg & kDbgMask & 4) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[0][j] = acc[1][j] = 0.0f;
       } else {
@@ -755,7 +761,7 @@ __global__ __launch_bounds__(kSThreads) void spmm_xw_wide_ws_kernel(const WideAr
         split3_pair(f32x2{acc[k][2], acc[k][3]}, hi[k][1], mid[k][1], lo[k][1]);
       }
       // the buffer's previous chunk has left the MFMA waves
-      if (!lds_wait_ge(freed + b, gen, abort_word)) break;
+      if (!lds_wait_ge(freed + b, gen, abort_word, a.spin)) break;
       char *buf = lds + b * kSBuf;
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
@@ -775,7 +781,7 @@ __global__ __launch_bounds__(kSThreads) void spmm_xw_wide_ws_kernel(const WideAr
     }
   } else {
     // -------------------------------- MFMA waves ----------------------------
-    if (a.dbg & 16) __builtin_amdgcn_s_setprio(2);
+    if (a.dbg & kDbgMask & 16) __builtin_amdgcn_s_setprio(2);
     const int m = wave - NG;
     const int nt0 = NT * m;
     const int h = nt0 >> 3;  // 128-column half: mask words 4 h .. 4 h + 3
@@ -814,8 +820,8 @@ __global__ __launch_bounds__(kSThreads) void spmm_xw_wide_ws_kernel(const WideAr
             dv[rt] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rd, 4 * (16 * rt + l16), 0, 0));
         }
       }
-      if (!lds_wait_ge(filled + b, kSRows * (gen + 1), abort_word)) break;
-      if (a.dbg & 2) {
+      if (!lds_wait_ge(filled + b, kSRows * (gen + 1), abort_word, a.spin)) break;
+      if (a.dbg & kDbgMask & 2) {
         const int old = lds_signal(mdone + b, 1, lane);
         if (old == NM * gen + NM - 1) lds_signal(freed + b, 1, lane);
         continue;
@@ -844,7 +850,7 @@ __global__ __launch_bounds__(kSThreads) void spmm_xw_wide_ws_kernel(const WideAr
 #pragma unroll
           for (int t = 0; t < NT; ++t) {
             const int q = kk * NT + t;  // step within the ring turn: ring slot q
-            if (!(a.dbg & 1)) load_step((NT * ks + t + 2) % kSteps, wf[(q + 2) & 3]);
+            if (!(a.dbg & kDbgMask & 1)) load_step((NT * ks + t + 2) % kSteps, wf[(q + 2) & 3]);
 #pragma unroll
             for (int rt = 0; rt < 2; ++rt)
               acc[t][rt] = mfma16_x6_wt(wf[q], xf[rt][0], xf[rt][1], xf[rt][2], acc[t][rt]);
@@ -917,9 +923,12 @@ __global__ __launch_bounds__(kSThreads) void spmm_xw_wide_ws_kernel(const WideAr
       }
     }
   }
+  __syncthreads();
+  // a hand-off gave up: this launch's rows are incomplete -- say so (the host
+  // turns the word into MGCN_EDEVICE) instead of returning them silently
+  if (wave == 0 && lds_load(abort_word) != 0) report_device_error(a.err, kDevErrWide);
   if constexpr (BWD && EPI != WEPI_STORE) {
     // column sums: each column's 16 row lanes (one MFMA wave) folded in lane order
-    __syncthreads();
     float *red = reinterpret_cast<float *>(lds);  // [16 row lanes][256]
     if (wave >= NG) {
       const int m = wave - NG;
@@ -1049,6 +1058,9 @@ int xw_wide_fwd(int64_t n_rows, const int64_t *rowptr, const int32_t *col, const
   a.mean = mean;
   a.relu = relu;
   a.dbg = g_wide_dbg;
+  a.spin = g_spin_limit;
+  a.err = device_error_word();
+  if (a.err == nullptr) return MGCN_EHIP;
   int grid = 0;
   return launch_wide(a, false, WEPI_STORE, &grid, s);
 }
@@ -1061,6 +1073,7 @@ int xw_wide_bwd_dx(int64_t n_rows, const int64_t *rowptr_t, const int32_t *col_t
   u32x4 *img = static_cast<u32x4 *>(workspace);
   float *partial = reinterpret_cast<float *>(static_cast<char *>(workspace) +
                                              align_up((size_t)kWImgFrags * 16, 256));
+  if (int rc = take_device_error()) return rc;  // a previous launch failed on the device
   if (int rc = launch_wimg(W, ldw, true, img, s)) return rc;
   const int epi = relu_mask == nullptr ? WEPI_STORE : row_div != nullptr ? WEPI_RELU_DIV : WEPI_RELU;
   WideArgs a{};
@@ -1078,6 +1091,9 @@ int xw_wide_bwd_dx(int64_t n_rows, const int64_t *rowptr_t, const int32_t *col_t
   a.row_div = row_div;
   a.colsum_partial = partial;
   a.dbg = g_wide_dbg;
+  a.spin = g_spin_limit;
+  a.err = device_error_word();
+  if (a.err == nullptr) return MGCN_EHIP;
   int grid = 0;
   int rc = launch_wide(a, true, epi, &grid, s);
   if (rc || epi == WEPI_STORE) return rc;

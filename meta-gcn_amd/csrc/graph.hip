@@ -35,6 +35,59 @@ void set_error(const char *fmt, ...) {
 
 void clear_error() { g_last_error.clear(); }
 
+// warp-specialised hand-off spin bound (mgcn_internal.h; settable in experiment builds)
+uint32_t g_spin_limit = kSpinLimitDefault;
+
+// Device-side failure word (round 6).  One 64-B line of pinned, coherent,
+// portable host memory mapped into every device's address space: a kernel
+// that fails after launch (a warp-specialised kernel whose LDS hand-off spin
+// ran past its bound) stores its code there with one vector store, and the
+// host reads it with a plain load -- no copy, no synchronisation.
+
+namespace {
+std::once_flag g_dev_err_once;
+volatile unsigned *g_dev_err_host = nullptr;
+unsigned *g_dev_err_dev = nullptr;
+hipError_t g_dev_err_status = hipSuccess;
+}  // namespace
+
+unsigned *device_error_word() {
+  std::call_once(g_dev_err_once, [] {
+    void *p = nullptr;
+    g_dev_err_status = hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent |
+                                                 hipHostMallocPortable);
+    if (g_dev_err_status != hipSuccess) return;
+    std::memset(p, 0, 64);
+    void *d = nullptr;
+    g_dev_err_status = hipHostGetDevicePointer(&d, p, 0);
+    if (g_dev_err_status != hipSuccess) return;
+    g_dev_err_host = static_cast<volatile unsigned *>(p);
+    g_dev_err_dev = static_cast<unsigned *>(d);
+  });
+  if (g_dev_err_dev == nullptr)
+    set_error("device error word: %s", hipGetErrorString(g_dev_err_status));
+  return g_dev_err_dev;
+}
+
+const char *device_error_what(unsigned code) {
+  switch (code) {
+    case kDevErrDws: return "spmm_xw_bwd_ws_kernel (128-wide adjoint)";
+    case kDevErrWide: return "spmm_xw_wide_ws_kernel (256-wide layer)";
+    default: return "unknown kernel";
+  }
+}
+
+int take_device_error() {
+  if (g_dev_err_host == nullptr) return MGCN_OK;
+  const unsigned code = *g_dev_err_host;
+  if (code == 0) return MGCN_OK;
+  *g_dev_err_host = 0u;
+  set_error("device: %s stopped at a warp-specialised hand-off that exceeded its spin bound; "
+            "the outputs of that launch are invalid (code %u)",
+            device_error_what(code), code);
+  return MGCN_EDEVICE;
+}
+
 namespace {
 
 constexpr int kBlock = 256;
@@ -186,6 +239,12 @@ using namespace mgcn;
 extern "C" int mgcn_abi_version(void) { return MGCN_ABI_VERSION; }
 
 extern "C" const char *mgcn_last_error(void) { return g_last_error.c_str(); }
+
+extern "C" int mgcn_check_device(void *stream, int sync) {
+  clear_error();
+  if (sync) MGCN_HIP_TRY(hipStreamSynchronize(as_stream(stream)));
+  return take_device_error();
+}
 
 extern "C" size_t mgcn_csr_workspace_bytes(int64_t nnz, int64_t n) {
   return sort_scratch(nnz, n).total;

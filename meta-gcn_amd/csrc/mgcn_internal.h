@@ -17,6 +17,35 @@ void clear_error();
 
 inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Experiment builds (make exp -> libmgcn_exp.so, -DMGCN_EXPERIMENT=1) accept
+// the timing-only switches that change results (wide_dbg, xw_ws_dbg) and a
+// settable hand-off spin bound (ws_spin_limit); the product library compiles
+// those switches out and rejects their names.
+#ifndef MGCN_EXPERIMENT
+#define MGCN_EXPERIMENT 0
+#endif
+constexpr int kDbgMask = MGCN_EXPERIMENT ? ~0 : 0;  // (a.dbg & kDbgMask): constant 0 in the product
+constexpr uint32_t kSpinLimitDefault = 1u << 25;    // ~1 s of s_sleep(1) polls per hand-off
+extern uint32_t g_spin_limit;                       // kSpinLimitDefault unless an experiment build sets it
+
+// Device-side failure reporting (round 6): the host-mapped error word
+// (graph.hip).  A kernel that cannot finish its work correctly stores a code
+// there; take_device_error() turns a stored code into MGCN_EDEVICE + the
+// message (and clears it).  The launchers of such kernels call it first, so a
+// failed launch fails the next call at the latest; mgcn_check_device() reads
+// it after a stream sync.
+constexpr unsigned kDevErrDws = 1;   // spmm_xw_bwd_ws_kernel: hand-off spin bound exceeded
+constexpr unsigned kDevErrWide = 2;  // spmm_xw_wide_ws_kernel: hand-off spin bound exceeded
+unsigned *device_error_word();       // device pointer (nullptr + set_error on failure)
+int take_device_error();
+
+// lane 0 of the calling wave stores `code` into the error word (a vector
+// store to host-coherent memory at system scope)
+__device__ inline void report_device_error(unsigned *err, unsigned code) {
+  if (err != nullptr && (threadIdx.x & 63) == 0)
+    __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Check the last launch on this thread; record the HIP error string on failure.
 inline int check_launch(const char *what) {
   hipError_t e = hipGetLastError();

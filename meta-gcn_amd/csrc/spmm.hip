@@ -832,6 +832,15 @@ extern "C" int mgcn_set_option(const char *name, int value) {
     g_heavy_mid_side = value;
     return MGCN_OK;
   }
+  if (n == "ws_spin_limit") {  // the warp-specialised kernels' hand-off bound (abort-path tests)
+    if (!MGCN_EXPERIMENT) {
+      set_error("ws_spin_limit: experiment builds only (make exp -> libmgcn_exp.so)");
+      return MGCN_EINVAL;
+    }
+    MGCN_REQUIRE(value >= 1, "ws_spin_limit must be >= 1");
+    g_spin_limit = (uint32_t)value;
+    return MGCN_OK;
+  }
   if (n == "heavy_side_stream") {
     MGCN_REQUIRE(value == 0 || value == 1, "heavy_side_stream must be 0 or 1");
     g_heavy_side = value;

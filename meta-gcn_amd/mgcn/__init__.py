@@ -14,11 +14,11 @@ All compute goes through libmgcn.so (include/mgcn.h); there is no CPU path.
 import torch  # noqa: F401  -- must be imported before libmgcn binds libamdhip64
 
 from . import _lib
-from ._lib import MgcnError, load, set_option
+from ._lib import MgcnError, check_device, load, set_option
 from .graph import GraphPlan, build_plan, clear_cache, plan_for
 from .ops import aggregate, scatter_, segment_mean
 
 __version__ = "0.1.0"
 
-__all__ = ["MgcnError", "load", "set_option", "GraphPlan", "build_plan", "plan_for",
+__all__ = ["MgcnError", "check_device", "load", "set_option", "GraphPlan", "build_plan", "plan_for",
            "clear_cache", "aggregate", "scatter_", "segment_mean", "_lib"]

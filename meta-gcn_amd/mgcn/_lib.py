@@ -16,8 +16,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmgcn.so")
 
 # constants mirrored from include/mgcn.h
-ABI_VERSION = 20
-OK, EINVAL, EINDEX, EHIP, EWORKSPACE = 0, 1, 2, 3, 4
+ABI_VERSION = 21
+OK, EINVAL, EINDEX, EHIP, EWORKSPACE, EDEVICE = 0, 1, 2, 3, 4, 5
 REDUCE_SUM, REDUCE_MEAN, REDUCE_MAX = 0, 1, 2
 NORM_NONE, NORM_SM, NORM_RW = 0, 1, 2
 MAX_FILL = -1e38
@@ -36,6 +36,7 @@ SIGNATURES = {
     "mgcn_abi_version": (_int, []),
     "mgcn_last_error": (ctypes.c_char_p, []),
     "mgcn_set_option": (_int, [ctypes.c_char_p, _int]),
+    "mgcn_check_device": (_int, [_vp, _int]),
     "mgcn_csr_workspace_bytes": (_sz, [_i64, _i64]),
     "mgcn_csr_build": (_int, [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _sz, _vp]),
     "mgcn_degree_norm": (_int, [_i64, _vp, _vp, _vp, _vp, _int, _vp, _vp, _vp]),
@@ -229,6 +230,17 @@ def device_guard(device: torch.device):
     if device.index is None or device.index == torch._C._cuda_getDevice():
         return _NO_GUARD
     return torch.cuda.device(device)
+
+
+def check_device(device: torch.device | None = None, sync: bool = True) -> None:
+    """Raise if a libmgcn kernel reported a failure from the device
+    (``mgcn_check_device``; MGCN_EDEVICE: a warp-specialised kernel left a
+    hand-off at its spin bound, so that launch's outputs are invalid).
+    ``sync`` first synchronises the current stream of ``device`` (default:
+    the current device), covering every launch issued on it so far."""
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device())
+    check(load().mgcn_check_device(stream_of(device), 1 if sync else 0), "mgcn_check_device")
 
 
 def set_option(name: str, value: int) -> None:

@@ -300,7 +300,8 @@ def spmm_xw_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tens
         if X.stride(0) % 4 or X.data_ptr() % 16:
             X = X.contiguous()
     W = W.detach()
-    if W.dtype != torch.float32 or W.stride(1) != 1:
+    # (the warp-specialised adjoint copies W into LDS with 16-byte loads)
+    if W.dtype != torch.float32 or W.stride(1) != 1 or W.stride(0) % 4 or W.data_ptr() % 16:
         W = W.to(torch.float32).contiguous()
     dev = L.require_device(dY, X, W, view_t.rowptr, w_t, row_scale, relu_mask, row_div)
     F_in, F_out = W.shape

@@ -42,3 +42,19 @@ def cuda():
     import mgcn
     mgcn.load()
     return torch.device("cuda:0")
+
+
+@pytest.fixture(autouse=True)
+def _device_errors(request):
+    """After every GPU test: a kernel that reported a failure from the device
+    (mgcn_check_device, MGCN_EDEVICE) fails the test that launched it."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    import torch
+    if not torch.cuda.is_available():
+        return
+    from mgcn import _lib as L
+    if L._lib is None:
+        return
+    L.check_device(sync=True)

@@ -33,9 +33,14 @@ def test_library_exports_every_header_symbol():
 def test_abi_version_and_option_errors():
     import mgcn
     lib = mgcn.load()
-    assert lib.mgcn_abi_version() == mgcn._lib.ABI_VERSION == 20
+    assert lib.mgcn_abi_version() == mgcn._lib.ABI_VERSION == 21
     assert lib.mgcn_set_option(b"no_such_option", 1) == 1
     assert b"unknown option" in lib.mgcn_last_error()
+    # the switches that change results (timing experiments) and the spin bound
+    # of the warp-specialised kernels exist only in libmgcn_exp.so
+    for name in (b"ws_spin_limit", b"wide_dbg", b"xw_ws_dbg"):
+        assert lib.mgcn_set_option(name, 1) == 1
+        assert b"experiment builds only" in lib.mgcn_last_error()
     with pytest.raises(mgcn.MgcnError):
         mgcn.set_option("spmm_unroll", 3)
     mgcn.set_option("spmm_unroll", 8)
