@@ -196,9 +196,6 @@ def launch_bytes(name: str, rows: int, edges: int, F: int):
             b += 4 * rows * F     # the aggregate Z written beside Y
         elif name == "spmm_xw_bwd_dx":
             b += 16 * rows        # the lower layer's ReLU mask words
-        elif name == "spmm_xw_bwd_dwl":
-            b += 16 * rows + 4 * rows * F   # masks + the lower layer's Z rows read
-            fl *= 2                         # + dWl = Z^T dX
         return b, fl
     if name.startswith("spmm"):
         return spmm_bytes(rows, edges, F), 0.0

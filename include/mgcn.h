@@ -77,23 +77,34 @@ const char *mgcn_last_error(void);
  * counterpart (torch_scatter reports nothing from the device either). */
 int mgcn_check_device(void *stream, int sync);
 
-/* Tuning knobs (process-wide; default 0 = automatic):
+/* Tuning knobs (ABI 21: only knobs that keep every result within its tested
+ * bound -- bit for bit, except gemm_precision).  Process-wide settings meant
+ * to be set once at start-up (MGCN_OPTIONS="name=value,..." does that from
+ * the environment), not per call; the defaults are the measured-fastest
+ * forms.  Switches that change results (timing experiments: wide_dbg,
+ * xw_ws_dbg) and the warp-specialised spin bound (ws_spin_limit) exist only
+ * in the experiment build libmgcn_exp.so (make -C meta-gcn_amd/csrc exp);
+ * this library rejects them (MGCN_EINVAL).
  *   "spmm_vec"    : cap the floats per lane of the SpMM gathers (1, 2, 4)
  *   "spmm_unroll" : gathers in flight per lane group (4, 8 or 16)
  *   "heavy_side_stream": 1 (default) runs the heavy-row launch on a side
  *                   stream concurrently with the lane-group launch; 0 serial
+ *   "heavy_side_fence": 1 = system-scope events on that side stream
  *   "heavy_lds_kb": LDS per giant-row workgroup, 16..160 (default 160)
  *   "heavy_block" : threads per giant-row workgroup, 256/512/1024 (1024)
  *   "heavy_mid_lds_kb": LDS per (non-giant) heavy-row workgroup (default 40)
- *   "residual_blocks": workgroup cap of the fused residual layer's launches
- *                   (default 8192; the backward's is also capped at 4096)
  *   "heavy_mid_q1": 1 (default) = one edge quad in flight per producer in the
  *                   non-giant heavy-row workgroups when a row is <= 32 floats
  *                   wide (fewer registers, more workgroups per CU); 0 = four
  *   "heavy_giant_thr" : degree above which a heavy row is giant, read by
  *                   mgcn_row_schedule (default 512)
+ *   "residual_blocks": workgroup cap of the fused residual layer's launches
+ *                   (default 8192; the backward's is also capped at 4096)
+ *   "residual_fused_mask": 1 (default) the residual stack's lower-layer mask
+ *                   pass fused into its launches
  *   "gemm_tn_variant": LDS-staged dW kernel chunk depth (M, N multiples of
  *                   128): 0 = 64 rows (default), 1 = 32, 2 = 16
+ *   "gemm_tn_staged": 1 (default) the staged small-C kernel at M = 32
  *   "gemm_precision": product arithmetic of mgcn_gemm_nn / mgcn_gemm_tn:
  *                   1 = bf16x6 (default; fp32 operands split exactly into
  *                   three bf16 terms, six products on bf16 MFMA, fp32
@@ -106,8 +117,14 @@ int mgcn_check_device(void *stream, int sync);
  *                   warp-specialised kernel (DWS), 0 = the two-phase kernel
  *   "xw_ws_max"   : 1 (default) = the max adjoint with dX on DWS as well
  *   "xw_ws_full_unroll": DWS gathers in flight per row, 4 / 5 (default) / 6
- *   "xw_ws", "xw_ws_unroll", "dw_ws", "dw_direct_ni", "gemm_tn_wide2",
- *   "wide_ws", "wide_mfma": round-5 kernel forms, see INTEGRATION.md      */
+ *   "wide_ws"     : the 256-wide layer kernels: bit 0 the forward, bit 1 the
+ *                   adjoint on the warp-specialised form (default 3), else
+ *                   the 16-row two-phase form
+ *   "wide_pair"   : the two-phase 256-wide form gathers a wave's two rows
+ *                   together (bit 0 forward, bit 1 adjoint; default 3)
+ *   "wide_mfma"   : MFMA waves of the warp-specialised 256-wide kernels, 4 / 8
+ *                   (default)
+ * (Measured-slower forms removed in round 6 live as patches under exp/.) */
 int mgcn_set_option(const char *name, int value);
 
 /* ------------------------------------------------------------------ graph */
@@ -475,59 +492,6 @@ int mgcn_spmm_xw_bwd_hcs(int64_t n_rows, int64_t n_cols, const int64_t *rowptr_t
                          float *dX, int64_t lddx, const uint32_t *relu_mask, const float *row_div,
                          float *colsum, float *dy_colsum, void *workspace, size_t workspace_bytes,
                          void *stream);
-
-/*
- * A max layer with the NEXT layer's transform in one launch (ABI v18; F = 128,
- * bf16x6, graphs without heavy rows):
- *   Y  = relu(max_k H[col_k] * w_k + bias)  -- bit for bit mgcn_spmm_fwd
- *        (MGCN_REDUCE_MAX with a winner-bit buffer): rows without edges 0,
- *        `>=` so a later edge wins a tie (torch_scatter 1.x CPU)
- *   relu_mask [n_rows][4] (nullable, needs relu), win_mask [nnz][4]: every
- *        edge's winner bits at its fwd slot (mgcn_spmm_fwd's layout)
- *   Hn = Y Wn  (the next layer's x @ weight_node, bf16x6)
- * Replaces mgcn_spmm_fwd(MAX) + the next layer's mgcn_gemm_nn (the
- * reference: x @ weight_node then gather / scatter max, gcn_base_models.py:
- * 201, 223-237, common.py:59-64).  H [n_cols, 128] under 4 GiB, 16-byte rows.
- * Scratch: mgcn_spmm_max_xw_fwd_workspace_bytes().
- */
-int mgcn_spmm_max_xw_fwd(int64_t n_rows, int64_t n_cols, const int64_t *rowptr, const int32_t *col,
-                         const float *w, const float *H, int64_t ldh, const float *bias, int relu,
-                         float *Y, int64_t ldy, uint32_t *relu_mask, uint32_t *win_mask,
-                         const float *Wn, int64_t ldwn, float *Hn, int64_t ldhn, void *workspace,
-                         size_t workspace_bytes, void *stream);
-
-/* Bytes of scratch mgcn_spmm_max_xw_fwd needs (Wn split into its fragment
- * image; 16-byte aligned). */
-size_t mgcn_spmm_max_xw_fwd_workspace_bytes(void);
-
-/* Bytes of scratch mgcn_spmm_xw_bwd_dwl needs (dWl split-K partials + column
- * sums; ABI v18). */
-size_t mgcn_spmm_xw_bwd_dwl_workspace_bytes(int64_t n_rows);
-
-/*
- * The dX-only adjoint of a 128 -> 128 layer l with the LOWER layer's weight
- * gradient in the same launch (ABI v18; F = 128, bf16x6):
- *   dX  = relu'(lower) ((A^T dY [* row_scale]) W^T) [/ row_div]
- *         -- bit for bit mgcn_spmm_xw_bwd's dX-only form (layer l-1's dY)
- *   colsum (+)= sum_rows dX            (layer l-1's bias gradient; accumulate_colsum)
- *   dWl    (+)= Zl^T dX                (layer l-1's weight gradient; accumulate_dw)
- * Zl [n_rows, 128] (ldz, 16-byte aligned rows) is layer l-1's aggregate as
- * mgcn_spmm_xw_fwd returns it in Z (mean: the undivided sum, which pairs
- * with the count-divided dX).  The reference's dW of layer l-1 is
- * h^T (A^T dY_{l-1}) -- autograd of `x @ weight_node` and the gather /
- * scatter_add (gcn_base_models.py:201-241) -- equal to (A h)^T dY_{l-1} for
- * the linear aggregator; this replaces mgcn_gemm_bwd's dW-only Z^T dY pass
- * over the dY this launch writes.  relu_mask needs colsum; row_div needs
- * relu_mask.  dWl: deterministic split-K (one partial per workgroup, folded
- * in order); within the fp64 |.|-bound of the reference product.
- */
-int mgcn_spmm_xw_bwd_dwl(int64_t n_rows, int64_t n_cols, const int64_t *rowptr_t,
-                         const int32_t *col_t, const float *w_t, const float *row_scale,
-                         const float *dY, int64_t lddy, const float *W, int64_t ldw, float *dX,
-                         int64_t lddx, const uint32_t *relu_mask, const float *row_div,
-                         float *colsum, int accumulate_colsum, const float *Zl, int64_t ldz,
-                         float *dWl, int64_t lddw, int accumulate_dw, void *workspace,
-                         size_t workspace_bytes, void *stream);
 
 /* ---------------------------------------------------- edge weight adjoint */
 

@@ -171,19 +171,10 @@ __device__ __forceinline__ void gather_row(const __amdgpu_buffer_rsrc_t rx, uint
   deg_out = deg;
 }
 
-// Broadcast of lane 32 grp + k (k wave-uniform) to its 32-lane group: two
-// v_readlane and a select instead of a ds_bpermute (MGCN_BCAST_READLANE; no
-// LDS traffic beside the warp-specialised kernels' image reads)
-#ifndef MGCN_BCAST_READLANE
-#define MGCN_BCAST_READLANE 0
-#endif
+// Broadcast of lane 32 grp + k (k wave-uniform) to its 32-lane group
+// (ds_bpermute; the two-v_readlane form measured slower, exp/ in git history)
 __device__ __forceinline__ int bcast_g(int v, int grp, int k) {
-#if MGCN_BCAST_READLANE
-  const int lo = __builtin_amdgcn_readlane(v, k), hi = __builtin_amdgcn_readlane(v, 32 + k);
-  return grp ? hi : lo;
-#else
   return __shfl(v, 32 * grp + k, 64);
-#endif
 }
 __device__ __forceinline__ float bcast_g(float v, int grp, int k) {
   return __int_as_float(bcast_g(__float_as_int(v), grp, k));
@@ -578,270 +569,6 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_fwd_kernel(c
 }
 
 // ---------------------------------------------------------------------------
-// Max layer with the NEXT layer's transform (round 5, config 4):
-//   Y  = relu(max_k H[col_k] w_k + b)   (+ ReLU mask words, + winner bits)
-//   Hn = Y Wn                           (the next layer's x @ W)
-// Max does not commute with W, so the layer's own product stays before it
-// (a GEMM or the previous call's Hn), but Y is complete in the gathering
-// workgroup: the next layer's product runs on it there, instead of a GEMM
-// that reads Y back (reference: x @ weight_node, gather, scatter max,
-// gcn_base_models.py:201, 223-237, common.py:59-64; torch_scatter 1.x's CPU
-// max: `>=`, a later edge wins a tie, rows without edges 0).  The chunk
-// structure is spmm_xw_fwd_kernel's: Phase A folds each row's edges in order
-// (mgcn_spmm_fwd's FWD_MAX arithmetic and winners, bit for bit), applies bias
-// and ReLU, stores Y, its mask words and every edge's winner bits (the
-// layout of mgcn_spmm_fwd with a winner-bit buffer: word f / 32 of the edge's
-// record at its fwd slot, bit f % 32) and writes Y's bf16 terms; Phase B
-// multiplies them by this wave's 16 columns of Wn (bf16x6) into Hn.
-struct XmArgs {
-  int64_t n_rows;
-  const int64_t *rowptr;
-  const int32_t *col;
-  const float *w;
-  const float *H;  // gathered rows [n_cols][128]
-  int64_t ldh;
-  int64_t n_cols;
-  const float *bias;
-  int relu;
-  float *Y;
-  int64_t ldy;
-  uint32_t *relu_mask;  // [n_rows][4], nullable
-  uint32_t *win_mask;   // [nnz][4]
-  const u32x4 *wimg;    // Wn's fragment image (xm_wimg_kernel): Hn = Y Wn
-  float *Hn;
-  int64_t ldhn;
-};
-
-// max fold of one row in the 32-lane group (gather_row_meta's loop): acc the
-// max of the separately rounded products, win the position (in the row) of
-// the edge that set it -- `>=`: a later edge wins a tie
-template <int U>
-__device__ __forceinline__ void gather_row_max(const __amdgpu_buffer_rsrc_t rx, uint32_t ldx_b,
-                                               const int32_t *__restrict__ col,
-                                               const float *__restrict__ w, const RowMeta &m,
-                                               int gl, int grp, float (&acc)[4], int (&win)[4]) {
-  const int64_t beg = m.beg, deg = m.deg;
-  const int64_t odeg = __shfl_xor(deg, 32, 64);
-  const int64_t maxdeg = deg > odeg ? deg : odeg;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    acc[j] = MGCN_MAX_FILL;
-    win[j] = -1;
-  }
-  int mc = m.mc;
-  float mw = m.mw;
-  for (int64_t e0 = 0; e0 < maxdeg; e0 += 32) {
-    if (e0 > 0) {
-      const int64_t my = e0 + gl;
-      mc = 0;
-      mw = 1.0f;
-      if (my < deg) {
-        mc = col[beg + my];
-        if (w != nullptr) mw = w[beg + my];
-      }
-    }
-    const int64_t rem = deg - e0;
-    const int nb = rem <= 0 ? 0 : (rem < 32 ? (int)rem : 32);
-    const int64_t remw = maxdeg - e0;
-    const int nbmax = remw < 32 ? (int)remw : 32;
-    for (int k0 = 0; k0 < nbmax; k0 += U) {
-      float4 xv[U];
-      float wk[U];
-      bool ok[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int k = k0 + u;
-        const int ck = bcast_g(mc, grp, k & 31);
-        wk[u] = bcast_g(mw, grp, k & 31);
-        ok[u] = k < nb;
-        const uint32_t off = ok[u] ? (uint32_t)ck * ldx_b + 16u * gl : 0xfffffff0u;
-        xv[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0));
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (ok[u]) {
-          const int e = (int)(e0 + k0 + u);
-          const float p[4] = {__fmul_rn(xv[u].x, wk[u]), __fmul_rn(xv[u].y, wk[u]),
-                              __fmul_rn(xv[u].z, wk[u]), __fmul_rn(xv[u].w, wk[u])};
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (p[j] >= acc[j]) {
-              acc[j] = p[j];
-              win[j] = e;
-            }
-        }
-      }
-    }
-  }
-}
-
-// LDS: the double-buffered chunk images (48 KB) and a 512-B winner-record
-// window per lane group (8 KB): 56 KB, two workgroups per CU.  Hn leaves
-// straight from the MFMA registers (Wn as the A operand: a lane holds four
-// consecutive columns of one row, one 16-B store), so no staging tile.
-constexpr int kXmWinOff = 2 * kXfBuf;
-constexpr int kXmLds = kXmWinOff + 16 * 32 * 16;
-static_assert(2 * kXmLds <= 160 * 1024, "two max+next workgroups per CU");
-
-// the six products of mfma16_x6(rows, W) with W as the A operand (same pairs,
-// same order)
-__device__ __forceinline__ f32x4_t mfma16_x6_wa(const bf16x8 (&w)[3], const bf16x8 &xh,
-                                               const bf16x8 &xm, const bf16x8 &xl, f32x4_t c) {
-  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], xl, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[2], xh, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[1], xm, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], xm, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[1], xh, c, 0, 0, 0);
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], xh, c, 0, 0, 0);
-}
-
-// Wn split once into bf16 terms in fragment order (a prep launch): fragment
-// ((ks * 8 + nt) * 3 + term) * 64 + lane holds Wn[32 ks + 8 g4 + j][16 nt + l16]
-// (lane = 16 g4 + l16, j < 8) -- the 48 VGPRs of held fragments would spill
-// the max gather, so each chunk's Phase B streams its wave's 12 fragments
-// from L2 (96 KB image), issued before the chunk barrier
-__global__ __launch_bounds__(256) void xm_wimg_kernel(const float *__restrict__ W, int64_t ldw,
-                                                      u32x4 *__restrict__ img) {
-  const int idx = (int)(blockIdx.x * 256 + threadIdx.x);
-  if (idx >= 4 * 8 * 64) return;
-  const int lane = idx & 63, nt = (idx >> 6) & 7, ks = idx >> 9;
-  const int l16 = lane & 15, g4 = lane >> 4;
-  float v[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = W[(int64_t)(32 * ks + 8 * g4 + j) * ldw + 16 * nt + l16];
-  bf16x8 h, m, l;
-  split3_bf16(v, h, m, l);
-  u32x4 *o = img + ((ks * 8 + nt) * 3) * 64 + lane;
-  o[0] = __builtin_bit_cast(u32x4, h);
-  o[64] = __builtin_bit_cast(u32x4, m);
-  o[128] = __builtin_bit_cast(u32x4, l);
-}
-
-template <int U>
-__global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_max_xw_kernel(const XmArgs a) {
-  __shared__ __attribute__((aligned(16))) char lds[kXmLds];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int gl = lane & 31, grp = lane >> 5;
-  const int l16 = lane & 15, g4 = lane >> 4;
-  const int64_t n_chunks = (a.n_rows + kXwRows - 1) / kXwRows;
-  const auto rx = buf_rsrc(a.H, (uint32_t)(a.n_cols * a.ldh * 4));
-  const uint32_t ldx_b = (uint32_t)a.ldh * 4u;
-  // this wave's Wn fragments in the image (A operand: A[c][k] = Wn[k][16 wave + c])
-  const auto rw = buf_rsrc(a.wimg, 4 * 8 * 3 * 64 * 16);
-  uint32_t *rec = reinterpret_cast<uint32_t *>(lds + kXmWinOff) + (2 * wave + grp) * 32 * 4;
-  const int64_t n_my = my_chunks(n_chunks);
-  const RowSeq seq{(int64_t)blockIdx.x * kXwRows + 2 * wave + grp, (int64_t)gridDim.x * kXwRows,
-                   a.n_rows};
-  RowMeta cur, nxt;
-  meta_rowptr(a.rowptr, seq.row(0), seq.row(0) < a.n_rows, cur);
-  meta_first(a.col, a.w, gl, cur);
-  meta_rowptr(a.rowptr, seq.row(1), seq.row(1) < a.n_rows, nxt);
-  int it = 0;
-  for (int64_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x, ++it) {
-    char *buf = lds + (it & 1) * kXfBuf;
-    const int64_t r0 = chunk * kXwRows;
-    const int64_t left = a.n_rows - r0;
-    const uint32_t rows_in = (uint32_t)(left >= kXwRows ? kXwRows : left);
-#pragma unroll 1
-    for (int p = 0; p < 2; ++p) {
-      const int lr = 16 * p + 2 * wave + grp;
-      const int64_t k = 2 * it + p;
-      meta_first(a.col, a.w, gl, nxt);
-      RowMeta nn;
-      const int64_t r2 = seq.row(k + 2);
-      meta_rowptr(a.rowptr, r2, r2 < a.n_rows && k + 2 < 2 * n_my, nn);
-      float acc[4];
-      int win[4];
-      gather_row_max<U>(rx, ldx_b, a.col, a.w, cur, gl, grp, acc, win);
-      // epilogue (mgcn_spmm_fwd FWD_MAX): no edge -> 0, + bias, ReLU
-      float bb[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-      if (a.bias != nullptr) *reinterpret_cast<float4 *>(bb) = *reinterpret_cast<const float4 *>(a.bias + 4 * gl);
-      float y[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float v = acc[j];
-        if (v == MGCN_MAX_FILL) {
-          v = 0.0f;
-          win[j] = -1;
-        }
-        if (a.bias != nullptr) v = __fadd_rn(v, bb[j]);
-        if (a.relu) v = (v < 0.0f) ? 0.0f : v;
-        y[j] = v;
-      }
-      const auto ry = buf_rsrc(a.Y + r0 * a.ldy, rows_in * (uint32_t)a.ldy * 4u);
-      __builtin_amdgcn_raw_buffer_store_b128(
-          __builtin_bit_cast(u32x4, make_float4(y[0], y[1], y[2], y[3])), ry,
-          4 * (int)(lr * a.ldy + 4 * gl), 0, MGCN_NT_OUT);
-      if (a.relu_mask != nullptr) {
-        const uint32_t m0 = (uint32_t)(__ballot(y[0] > 0.0f) >> (32 * grp));
-        const uint32_t m1 = (uint32_t)(__ballot(y[1] > 0.0f) >> (32 * grp));
-        const uint32_t m2 = (uint32_t)(__ballot(y[2] > 0.0f) >> (32 * grp));
-        const uint32_t m3 = (uint32_t)(__ballot(y[3] > 0.0f) >> (32 * grp));
-        if (gl == 0 && (uint32_t)lr < rows_in)
-          *reinterpret_cast<uint4 *>(a.relu_mask + (r0 + lr) * 4) = make_uint4(m0, m1, m2, m3);
-      }
-      // every edge's winner bits (mgcn_spmm_fwd's LDS windows): the group's
-      // 32-edge window of 16-B records, each lane ORs its four bits in (word
-      // gl / 8, bit 4 (gl % 8) + j), then lane gl writes record gl out.  One
-      // wave's LDS operations run in order: no barrier, only wave barriers.
-      {
-        const int64_t deg = cur.deg;
-        const int64_t odeg = __shfl_xor(deg, 32, 64);
-        const int64_t maxdeg = deg > odeg ? deg : odeg;
-        const int sh = (gl & 7) << 2;
-        for (int64_t w0 = 0; w0 < maxdeg; w0 += 32) {
-          *reinterpret_cast<uint4 *>(rec + 4 * gl) = make_uint4(0u, 0u, 0u, 0u);
-          __builtin_amdgcn_wave_barrier();
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int64_t pw = win[j] - w0;
-            if (win[j] >= 0 && pw >= 0 && pw < 32) atomicOr(rec + 4 * pw + (gl >> 3), 1u << (sh + j));
-          }
-          __builtin_amdgcn_wave_barrier();
-          const uint4 r = *reinterpret_cast<const uint4 *>(rec + 4 * gl);
-          if (w0 + gl < deg)
-            *reinterpret_cast<uint4 *>(a.win_mask + (cur.beg + w0 + gl) * 4) = r;
-          __builtin_amdgcn_wave_barrier();
-        }
-      }
-      store_row_terms(buf, lr, gl, y);
-      cur = nxt;
-      nxt = nn;
-    }
-    u32x4 wf[4][3];
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
-#pragma unroll
-      for (int term = 0; term < 3; ++term)
-        wf[ks][term] = __builtin_amdgcn_raw_buffer_load_b128(
-            rw, 16 * (((ks * 8 + wave) * 3 + term) * 64 + lane), 0, 0);
-    __syncthreads();
-    // Hn = Y Wn: this wave's 16 columns of the chunk's 32 rows, D = Wn^T-frags
-    // x rows (lane: row l16 of the tile, columns 16 wave + 4 g4 .. + 3)
-    const auto rh = buf_rsrc(a.Hn + r0 * a.ldhn, rows_in * (uint32_t)a.ldhn * 4u);
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      f32x4_t acc2 = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const int off = img_off(16 * t + l16, 4 * ks + g4);
-        const bf16x8 xh = *reinterpret_cast<const bf16x8 *>(buf + off);
-        const bf16x8 xm = *reinterpret_cast<const bf16x8 *>(buf + kXwImg + off);
-        const bf16x8 xl = *reinterpret_cast<const bf16x8 *>(buf + 2 * kXwImg + off);
-        const bf16x8 wk[3] = {__builtin_bit_cast(bf16x8, wf[ks][0]), __builtin_bit_cast(bf16x8, wf[ks][1]),
-                              __builtin_bit_cast(bf16x8, wf[ks][2])};
-        acc2 = mfma16_x6_wa(wk, xh, xm, xl, acc2);
-      }
-      __builtin_amdgcn_raw_buffer_store_b128(
-          __builtin_bit_cast(u32x4, make_float4(acc2[0], acc2[1], acc2[2], acc2[3])), rh,
-          4 * (int)((16 * t + l16) * a.ldhn + 16 * wave + 4 * g4), 0, MGCN_NT_OUT);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
 // Backward.  LDS: X images, dH images (single-buffered: two barriers per
 // chunk), the chunk's mask / divisor words, the dX staging tile.  dX: wave w
 // owns columns 16 w .. +15; its W^T fragments are re-read from L2 (W is
@@ -1218,53 +945,31 @@ int launch_xb_u(const XbArgs &a, int epi, int grid, hipStream_t s) {
 
 // ===================== warp-specialised adjoint (round 5) =====================
 //
-// The dX-only adjoint above, re-cut by role as fused_wide.hip's F = 256
-// kernels, and optionally with the LOWER layer's weight gradient fused in:
-//
-//   dX = relu'(lower) ((A^T dY [* rs]) W^T) [/ row_div]   (= dY of layer l-1)
-//   colsum = sum_rows dX                                  (layer l-1's bias grad)
-//   dWl = Zl^T dX                                         (layer l-1's dW, DWL)
-//
-// with Zl the lower layer's aggregate A h (mgcn_spmm_xw_fwd's Z).  The
-// reference's dW of layer l-1 is h^T (A^T dY_{l-1}) (autograd of x @ weight
-// then the gather / scatter, gcn_base_models.py:201-241) = (A h)^T dY_{l-1}
-// for the linear aggregator -- the Z^T dY pass (mgcn_gemm_bwd dW-only), here
-// folded into the launch that PRODUCES dY_{l-1}: the dW pass's 1 GB re-read
-// of dY and its launch go away (config 2).
+// DWS: the layer's whole adjoint re-cut by role as fused_wide.hip's F = 256
+// kernels (dW = X^T dH and dX = relu'(lower) (dH W^T) [/ row_div], dH =
+// A^T dY [* rs] never leaving the chip):
 //
 // One 1024-thread workgroup per CU: 8 GATHER waves aggregate dH rows (two
 // 32-lane groups per wave, gather_row_meta's edge order: bit for bit the
-// SpMM's adjoint), load the rows' Zl (DWL) and write both as bf16 term images
-// into a ring of two 48-KB chunk buffers; 8 MFMA waves hold W^T's fragments
-// of their 16 output columns (48 VGPRs, split once), form the chunk's dX
-// (W^T as the A operand: a lane's fragment is 4 consecutive columns of one
-// row, one 16-B store; the same six products in the same order as the
-// two-phase kernel, so dX is bit for bit its result), apply the epilogue,
-// write dX's term images, and after the eight waves' images are in (an LDS
-// counter) accumulate dWl += Zl^T dX on gemm_bwd's 32x32 tiles (two per
-// wave, transposed image reads) for the whole launch: one 128 x 128 partial
-// per workgroup, folded in workgroup order.  Hand-offs: LDS counters as in
-// fused_wide.hip (bounded spins, abort word).
-//
-// DWS (round 5, option xw_ws_full): the SAME layer's dW = X^T dH, the
-// two-phase full adjoint's product, from the chunk's own X rows: the gather
-// waves load them under the gathers (as DWL's Zl) into the ring beside the dH
-// images, and each MFMA wave folds its two 32x32 tiles of X^T dH straight from
-// the ring after its dX columns -- no hand-off between the MFMA waves, no dX
-// images.  dX is bit for bit the two-phase kernel's; dW folds the same
-// products per chunk over a one-workgroup-per-CU split-K grid.
-constexpr int kBsDx = 0, kBsDwl = 1, kBsDws = 2, kBsDwsH = 3, kBsDwsM = 4;  // spmm_xw_bwd_ws_kernel MODE
+// SpMM's adjoint), write them as bf16 term images into a ring of two chunk
+// buffers and load the chunk's own X rows (fp32) beside them under the
+// gathers; 8 MFMA waves form the chunk's dX (W^T as the A operand from an LDS
+// copy of W: a lane's fragment is 4 consecutive columns of one row, one 16-B
+// store; the same six products in the same order as the two-phase kernel, so
+// dX is bit for bit its result), apply the epilogue, and fold their two 32x32
+// tiles of X^T dH straight from the ring -- one 128 x 128 partial per
+// workgroup over a one-workgroup-per-CU split-K grid, folded in workgroup
+// order.  Hand-offs: LDS counters as in fused_wide.hip (bounded spins, abort
+// word, reported through the device error word).  (The dX-only form of this
+// kernel and DWL -- the lower layer's dW fused into the dX-only adjoint --
+// measured slower than the two-phase kernel / the separate dW pass, round 5,
+// and are removed.)
+constexpr int kBsDws = 2, kBsDwsH = 3, kBsDwsM = 4;  // spmm_xw_bwd_ws_kernel MODE
 #ifndef MGCN_DS_MASK_RING
 #define MGCN_DS_MASK_RING 1  // DWS: ReLU mask words / divisors through the ring (0: MFMA waves load them)
 #endif
-constexpr int kBsImgSet = 3 * kXwImg;          // one operand's three term images: 24 KB
-constexpr int kBsRingBuf = 2 * kBsImgSet;      // dH images + Zl images: 48 KB
-constexpr int kBsXOff = 2 * kBsRingBuf;        // two dX image sets (DWL)
-constexpr int kBsCtrOff = kBsXOff + 2 * kBsImgSet;
-constexpr int kBsLds = kBsCtrOff + 64;         // 144 KB + counters
-static_assert(kBsLds <= 160 * 1024, "one warp-specialised adjoint workgroup per CU");
-static_assert(16 * kXwF * 4 <= kBsXOff, "column-sum fold fits in the ring");
-// DWS layout: a ring of two (dH term images + X fp32 rows) chunk buffers and
+constexpr int kBsImgSet = 3 * kXwImg;          // dH's three term images: 24 KB
+// Layout: a ring of two (dH term images + X fp32 rows) chunk buffers and
 // W in fp32 (rows padded to 528 B: the 16 rows of a W^T fragment read and the
 // two row halves of an X^T fragment read fall on distinct banks); the MFMA
 // waves split W^T and X^T fragments as they read them
@@ -1280,9 +985,6 @@ static_assert(kDsLds <= 160 * 1024, "one DWS workgroup per CU");
 static_assert(16 * kXwF * 4 <= kDsWOff, "column-sum fold fits in the ring");
 constexpr int kBsNG = 8, kBsNM = 8;
 constexpr int kBsThreads = 64 * (kBsNG + kBsNM);
-#ifndef MGCN_BS_HOLDW
-#define MGCN_BS_HOLDW 0  // DWL: W^T fragments held in registers (0: re-read per chunk)
-#endif
 
 __device__ __forceinline__ int bs_lds_load(const int *p) {
   return __builtin_amdgcn_readfirstlane(
@@ -1324,10 +1026,7 @@ __device__ __forceinline__ f32x4_t mfma16_x6_at(const bf16x8 (&w)[3], const bf16
 }
 
 struct XbsArgs {
-  XbArgs b;             // rowptr .. row_div, colsum_partial (dX-only fields)
-  const float *Zl;      // DWL: the lower layer's aggregate [n_rows][128]
-  int64_t ldz;
-  float *dwl_partial;   // DWL: [grid][128][128]
+  XbArgs b;             // rowptr .. colsum_partial; X, dw_partial: [grid][128][128]
   float *hcs_partial;   // DWS (nullable): [grid][128] column sums of dY's own rows
   int dbg;              // xw_ws_dbg (experiment builds only; masked by kDbgMask)
   uint32_t spin;        // hand-off spin bound (g_spin_limit)
@@ -1336,28 +1035,26 @@ struct XbsArgs {
 
 template <int U, int EPI, int MODE>
 __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArgs A) {
-  constexpr bool DWL = MODE == kBsDwl, DWS = MODE == kBsDws || MODE == kBsDwsH || MODE == kBsDwsM;
   constexpr bool HCS = MODE == kBsDwsH;  // DWS + dY's column sums (hcs_partial)
   constexpr bool MAXM = MODE == kBsDwsM;  // DWS on the max adjoint (win_mask + slot_map)
-  constexpr bool MRING = DWS && MGCN_DS_MASK_RING;
-  constexpr int kRing = DWS ? kDsRingBuf : kBsRingBuf;
+  constexpr bool MRING = MGCN_DS_MASK_RING;
+  constexpr int kRing = kDsRingBuf;
   const XbArgs &a = A.b;
-  __shared__ __attribute__((aligned(16))) char lds[DWS ? kDsLds : kBsLds];
+  __shared__ __attribute__((aligned(16))) char lds[kDsLds];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int gl = lane & 31, grp = lane >> 5;
   const int l16 = lane & 15, g4 = lane >> 4;
-  int *ctr = reinterpret_cast<int *>(lds + (DWS ? kDsCtrOff : kBsCtrOff));
-  int *filled = ctr, *mdone = ctr + 2, *freed = ctr + 4, *xdone = ctr + 6, *abort_word = ctr + 8;
+  int *ctr = reinterpret_cast<int *>(lds + kDsCtrOff);
+  int *filled = ctr, *mdone = ctr + 2, *freed = ctr + 4, *abort_word = ctr + 8;
   if (tid < 16) ctr[tid] = 0;
-  if constexpr (DWS) {  // W (64 KB) into LDS once: four float4 per thread
+  // W (64 KB) into LDS once: four float4 per thread
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int e = tid + kBsThreads * j;  // float4 e: row e >> 5, columns 4 (e & 31) ..
-      const float4 v = *reinterpret_cast<const float4 *>(a.W + (int64_t)(e >> 5) * a.ldw + 4 * (e & 31));
-      *reinterpret_cast<float4 *>(lds + kDsWOff + 4 * ((e >> 5) * kDsXLd + 4 * (e & 31))) = v;
-    }
+  for (int j = 0; j < 4; ++j) {
+    const int e = tid + kBsThreads * j;  // float4 e: row e >> 5, columns 4 (e & 31) ..
+    const float4 v = *reinterpret_cast<const float4 *>(a.W + (int64_t)(e >> 5) * a.ldw + 4 * (e & 31));
+    *reinterpret_cast<float4 *>(lds + kDsWOff + 4 * ((e >> 5) * kDsXLd + 4 * (e & 31))) = v;
   }
   __syncthreads();
 
@@ -1370,8 +1067,8 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
   };
 
   float cs[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // MFMA waves: column sums of their 4 columns
-  float hc[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // gather waves (DWS, hcs_partial): dY column sums
-  f32x16 accw[2];                          // MFMA waves (DWL / DWS): two 32 x 32 dW tiles
+  float hc[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // gather waves (hcs_partial): dY column sums
+  f32x16 accw[2];                          // MFMA waves: two 32 x 32 dW tiles
 #pragma unroll
   for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -1416,12 +1113,12 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
       const int64_t r0 = c * kXwRows;
       const int lr0 = 4 * (int)(q & 7) + grp;
       u32x4 zv[2] = {};
-      if ((DWL || DWS) && !(A.dbg & kDbgMask & 4)) {  // the rows' Zl / X, under the gathers (streamed once)
-        const auto rz = buf_rsrc(A.Zl + r0 * A.ldz, rows_in(c) * (uint32_t)A.ldz * 4u);
+      if (!(A.dbg & kDbgMask & 4)) {  // the rows' X, under the gathers (streamed once)
+        const auto rz = buf_rsrc(a.X + r0 * a.ldx, rows_in(c) * (uint32_t)a.ldx * 4u);
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           zv[j] = __builtin_amdgcn_raw_buffer_load_b128(
-              rz, 4 * (int)((lr0 + 2 * j) * A.ldz + 4 * gl), 0, MGCN_NT_AUX);
+              rz, 4 * (int)((lr0 + 2 * j) * a.ldx + 4 * gl), 0, MGCN_NT_AUX);
       }
       // DWS + hcs_partial (n_cols == n_rows): the rows' own dY rows, whose
       // column sums are the layer's bias gradient -- every dY row once, rows
@@ -1478,18 +1175,13 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         store_row_terms(buf, lr0 + 2 * j, gl, acc[j]);
-        if constexpr (DWS)  // the X rows as they are (split by the MFMA waves)
-          *reinterpret_cast<u32x4 *>(buf + kDsXOff + 4 * ((lr0 + 2 * j) * kDsXLd + 4 * gl)) = zv[j];
+        // the X rows as they are (split by the MFMA waves)
+        *reinterpret_cast<u32x4 *>(buf + kDsXOff + 4 * ((lr0 + 2 * j) * kDsXLd + 4 * gl)) = zv[j];
         if constexpr (MRING && EPI != EPI_STORE) {
           if (gl < 4)
             *reinterpret_cast<uint32_t *>(buf + kDsMaskOff + 4 * ((lr0 + 2 * j) * 4 + gl)) = mv[j];
           if (EPI == EPI_RELU_DIV && gl == 4)
             *reinterpret_cast<uint32_t *>(buf + kDsDivOff + 4 * (lr0 + 2 * j)) = mv[j];
-        }
-        if constexpr (DWL) {
-          const float4 zf = __builtin_bit_cast(float4, zv[j]);
-          const float zz[4] = {zf.x, zf.y, zf.z, zf.w};
-          store_row_terms(buf + kBsImgSet, lr0 + 2 * j, gl, zz);
         }
       }
       bs_signal(filled + b, 4, lane);
@@ -1502,35 +1194,8 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
   } else {
     // -------------------------------- MFMA waves ----------------------------
     const int m = wave - kBsNG;  // dX columns 16 m .. 16 m + 15
-    // W^T fragments: A[c][k] = W[16 m + c][32 ks + 8 g4 + j] -- held for the
-    // launch (48 VGPRs) in the dX-only form; with the dWl accumulators (32)
-    // re-read from L2 and split per chunk instead (the MFMA waves have slack:
-    // ~3 k of ~19 k cycles per chunk)
-    const float *wp = a.W + (int64_t)(16 * m + l16) * a.ldw + 8 * g4;
-    constexpr bool kHoldW = MODE == kBsDx || MGCN_BS_HOLDW;
-    bf16x8 wt[kHoldW ? 4 : 1][3];
-    if constexpr (kHoldW) {
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const float4 w0 = *reinterpret_cast<const float4 *>(wp + 32 * ks);
-        const float4 w1 = *reinterpret_cast<const float4 *>(wp + 32 * ks + 4);
-        const float v[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-        split3_bf16(v, wt[ks][0], wt[ks][1], wt[ks][2]);
-      }
-    }
-    // dWl tiles (gemm_bwd's mapping): rows 32 ti, columns 32 (tj0 + s)
-    const int h = lane >> 5, q = (lane >> 2) & 3, p4 = lane & 3;
-    auto frag_off = [&](int col0, int second) {
-      return img_off(8 * h + q + 4 * second, (col0 >> 3) + 2 * (g4 & 1) + (p4 >> 1)) + 8 * (p4 & 1);
-    };
+    // dW tiles (gemm_bwd's mapping): rows 32 ti, columns 32 (tj0 + s)
     const int ti = m >> 1, tj0 = 2 * (m & 1);
-    int offa[2], offb[2][2];
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      offa[r] = frag_off(32 * ti, r);
-      offb[0][r] = frag_off(32 * tj0, r);
-      offb[1][r] = frag_off(32 * (tj0 + 1), r);
-    }
     auto read8 = [&](const char *base, const int (&o)[2]) {
       const v4i16 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16_t *)(base + o[0]));
       const v4i16 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16_t *)(base + o[1]));
@@ -1595,8 +1260,7 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
           if ((uint32_t)(16 * rt + l16) >= rv) dv[rt] = 1.0f;
       }
       const char *buf = lds + b * kRing;
-      char *ximg = lds + kBsXOff + (int)(i & 1) * kBsImgSet;
-      if constexpr (DWS) {
+      {
         // (first: nothing but the dW accumulators is live across it)
         // dW += X^T dH: X^T fragments (lane: column 32 ti + lc of rows
         // 16 ks + 8 h + j) read from the fp32 rows and split here, dH^T
@@ -1626,32 +1290,25 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
       for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc2[rt][r] = 0.0f;
-      // W^T fragment rows: global (L2) or, DWS, the LDS copy
-      const float *wq = DWS ? reinterpret_cast<const float *>(lds + kDsWOff) +
-                                  (16 * m + l16) * kDsXLd + 8 * g4
-                            : wp;
+      // W^T fragment rows from the LDS copy
+      const float *wq = reinterpret_cast<const float *>(lds + kDsWOff) + (16 * m + l16) * kDsXLd + 8 * g4;
       float4 wn0{}, wn1{};
-      if constexpr (!kHoldW) {
-        if (!(A.dbg & kDbgMask & 8)) {  // dbg 8: no W^T loads (timing only: dX wrong)
-          wn0 = *reinterpret_cast<const float4 *>(wq);
-          wn1 = *reinterpret_cast<const float4 *>(wq + 4);
-        }
+      if (!(A.dbg & kDbgMask & 8)) {  // dbg 8: no W^T loads (timing only: dX wrong)
+        wn0 = *reinterpret_cast<const float4 *>(wq);
+        wn1 = *reinterpret_cast<const float4 *>(wq + 4);
       }
-      // DWS with dX == NULL: dW alone (the same partials as with dX)
-      if (!DWS || a.dX != nullptr) {
+      // dX == NULL: dW alone (the same partials as with dX)
+      if (a.dX != nullptr) {
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         bf16x8 wk[3];
-        if constexpr (!kHoldW) {
+        {
           const float v8[8] = {wn0.x, wn0.y, wn0.z, wn0.w, wn1.x, wn1.y, wn1.z, wn1.w};
           if (ks + 1 < 4 && !(A.dbg & kDbgMask & 8)) {
             wn0 = *reinterpret_cast<const float4 *>(wq + 32 * (ks + 1));
             wn1 = *reinterpret_cast<const float4 *>(wq + 32 * (ks + 1) + 4);
           }
           split3_bf16(v8, wk[0], wk[1], wk[2]);
-        } else {
-#pragma unroll
-          for (int t = 0; t < 3; ++t) wk[t] = wt[ks][t];
         }
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt) {
@@ -1679,31 +1336,7 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
         __builtin_amdgcn_raw_buffer_store_b128(
             __builtin_bit_cast(u32x4, make_float4(v[0], v[1], v[2], v[3])), rx,
             4 * (int)(row * a.lddx + 16 * m + 4 * g4), 0, MGCN_NT_OUT);
-        if constexpr (DWL) store_row_terms(ximg, row, 4 * m + g4, v);
       }
-      }
-      if (DWL && !(A.dbg & kDbgMask & 1)) {
-        // every wave's 16 columns of the chunk's dX images are in
-        bs_signal(xdone + (int)(i & 1), 1, lane);
-        if (!bs_wait_ge(xdone + (int)(i & 1), kBsNM * (gen + 1), abort_word, A.spin)) break;
-        if (!(A.dbg & kDbgMask & 2)) {
-        const char *zimg = buf + kBsImgSet;
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          const char *za = zimg + ks * 16 * 256;
-          const char *xb = ximg + ks * 16 * 256;
-          bf16x8 fa[3];
-#pragma unroll
-          for (int t = 0; t < 3; ++t) fa[t] = read8(za + t * kXwImg, offa);
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) {
-            bf16x8 fb[3];
-#pragma unroll
-            for (int t = 0; t < 3; ++t) fb[t] = read8(xb + t * kXwImg, offb[s2]);
-            accw[s2] = mfma_x6(fa[0], fa[1], fa[2], fb[0], fb[1], fb[2], accw[s2]);
-          }
-        }
-        }
       }
       const int old = bs_signal(mdone + b, 1, lane);
       if (old == kBsNM * gen + kBsNM - 1) bs_signal(freed + b, 1, lane);
@@ -1715,10 +1348,10 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
   if (wave == 0 && bs_lds_load(abort_word) != 0) report_device_error(A.err, kDevErrDws);
   if (wave >= kBsNG) {
     const int m = wave - kBsNG;
-    if constexpr (DWL || DWS) {
+    {
       const int h = lane >> 5, lc = lane & 31;
       const int ti = m >> 1, tj0 = 2 * (m & 1);
-      float *slab = A.dwl_partial + (int64_t)blockIdx.x * kXwF * kXwF;
+      float *slab = a.dw_partial + (int64_t)blockIdx.x * kXwF * kXwF;
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
@@ -1733,13 +1366,11 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
           make_float4(cs[0], cs[1], cs[2], cs[3]);
     }
   }
-  if constexpr (DWS) {
-    if constexpr (HCS) {  // (past the dX column sums' [16][128] in LDS)
-      float *red2 = reinterpret_cast<float *>(lds) + 16 * kXwF;
-      if (wave < kBsNG)
-        *reinterpret_cast<float4 *>(red2 + (2 * wave + grp) * kXwF + 4 * gl) =
-            make_float4(hc[0], hc[1], hc[2], hc[3]);
-    }
+  if constexpr (HCS) {  // (past the dX column sums' [16][128] in LDS)
+    float *red2 = reinterpret_cast<float *>(lds) + 16 * kXwF;
+    if (wave < kBsNG)
+      *reinterpret_cast<float4 *>(red2 + (2 * wave + grp) * kXwF + 4 * gl) =
+          make_float4(hc[0], hc[1], hc[2], hc[3]);
   }
   if (EPI != EPI_STORE || HCS) {
     __syncthreads();
@@ -1763,8 +1394,6 @@ __global__ __launch_bounds__(kBsThreads) void spmm_xw_bwd_ws_kernel(const XbsArg
   }
 }
 
-int g_xm_unroll = 6;  // mgcn_set_option("xw_ws_xm_unroll"): max+next gathers in flight (4 / 6 / 8)
-int g_xw_ws = 0;  // mgcn_set_option("xw_ws"): the warp-specialised dX-only adjoint
 int g_xw_ws_full = 1;  // mgcn_set_option("xw_ws_full"): the warp-specialised dW + dX adjoint (DWS)
 int g_xw_ws_max = 1;   // mgcn_set_option("xw_ws_max"): ... and its max adjoint (DWS + win_mask)
 
@@ -1790,10 +1419,10 @@ int launch_bs_u(const XbsArgs &a, int epi, int grid, hipStream_t s) {
   return check_launch("spmm_xw_bwd_ws_kernel");
 }
 
-int g_bs_unroll = 4;
-// mgcn_set_option("xw_ws_dbg"): timing experiments (dWl WRONG when set): bit 0
-// skip the dW phase and its sync, bit 1 skip the dW products, bit 2 skip Zl loads
-int g_bs_dbg = 0;  // mgcn_set_option("xw_ws_unroll"): gathers in flight per row (4 / 8)
+// mgcn_set_option("xw_ws_dbg") (experiment builds): timing experiments (dW / dX
+// WRONG when set): bit 0 skip the dW products, bit 2 skip the X loads, bit 3
+// skip the W^T reads
+int g_bs_dbg = 0;
 
 int g_bs_full_unroll = 5;  // mgcn_set_option("xw_ws_full_unroll"): DWS gathers in flight per row (5: 0.984-0.991 vs 1.000-1.012 ms at 4)
 
@@ -1801,15 +1430,10 @@ template <int MODE>
 int launch_bs(const XbsArgs &a, int epi, int grid, hipStream_t s) {
   if constexpr (MODE == kBsDwsM) {  // the winner words take registers: 3 slots per row
     return launch_bs_u<3, MODE>(a, epi, grid, s);
-  } else if constexpr (MODE == kBsDws || MODE == kBsDwsH) {
+  } else {
     return g_bs_full_unroll == 4 ? launch_bs_u<4, MODE>(a, epi, grid, s)
          : g_bs_full_unroll == 5 ? launch_bs_u<5, MODE>(a, epi, grid, s)
                                  : launch_bs_u<6, MODE>(a, epi, grid, s);
-  } else {
-    return g_bs_unroll == 4 ? launch_bs_u<4, MODE>(a, epi, grid, s)
-         : g_bs_unroll == 5 ? launch_bs_u<5, MODE>(a, epi, grid, s)
-         : g_bs_unroll == 6 ? launch_bs_u<6, MODE>(a, epi, grid, s)
-                            : launch_bs_u<8, MODE>(a, epi, grid, s);
   }
 }
 
@@ -1842,7 +1466,6 @@ int xw_set_ws(const char *name, int value) {
     set_error("%s: unsupported value %d", name, value);
     return (int)MGCN_EINVAL;
   };
-  if (n == "xw_ws_xm_unroll") return unroll(g_xm_unroll, {4, 6, 8});
   if (n == "xw_ws_max") return flag(g_xw_ws_max);
   if (n == "xw_ws_full") return flag(g_xw_ws_full);
   if (n == "xw_ws_dbg") {  // (timing experiments: results WRONG when set)
@@ -1853,9 +1476,7 @@ int xw_set_ws(const char *name, int value) {
     g_bs_dbg = value;
     return MGCN_OK;
   }
-  if (n == "xw_ws_unroll") return unroll(g_bs_unroll, {4, 5, 6, 8});        // dX-only / DWL
-  if (n == "xw_ws_full_unroll") return unroll(g_bs_full_unroll, {4, 5, 6});  // DWS
-  return flag(g_xw_ws);  // "xw_ws"
+  return unroll(g_bs_full_unroll, {4, 5, 6});  // "xw_ws_full_unroll"
 }
 
 int xw_set_unroll(int value) {
@@ -2071,15 +1692,6 @@ int xw_bwd_impl(int64_t n_rows, int64_t n_cols, int32_t F_in, int32_t F_out,
   a.colsum_partial = reinterpret_cast<float *>(static_cast<char *>(workspace) +
                                                align_up((size_t)xw_grid() * kXwF * kXwF * 4, 256));
   int rc;
-  if (dx_only && g_xw_ws) {  // the warp-specialised form (one workgroup per CU)
-    XbsArgs sa{};
-    sa.b = a;
-    if (int rc2 = bs_prepare(sa)) return rc2;
-    const int64_t g = bs_grid() < n_chunks ? bs_grid() : n_chunks;
-    rc = launch_bs<kBsDx>(sa, epi, (int)g, s);
-    if (rc || epi == EPI_STORE) return rc;
-    return launch_fold(a.colsum_partial, g, kXwF, kXwF, colsum, kXwF, accumulate, s);
-  }
   if (dx_only) {
     rc = g_xw_unroll == 8 ? launch_xb_dx<8>(a, epi, grid, s) : launch_xb_dx<4>(a, epi, grid, s);
     if (rc || epi == EPI_STORE) return rc;
@@ -2093,9 +1705,6 @@ int xw_bwd_impl(int64_t n_rows, int64_t n_cols, int32_t F_in, int32_t F_out,
     // the warp-specialised dW + dX (or dW-only) form (one workgroup per CU; DWS)
     XbsArgs sa{};
     sa.b = a;
-    sa.Zl = X;
-    sa.ldz = ldx;
-    sa.dwl_partial = a.dw_partial;
     if (int rc2 = bs_prepare(sa)) return rc2;
     grid = bs_grid() < n_chunks ? bs_grid() : (int)n_chunks;
     // dY's column sums: [grid][128] partials past the grid's dW slabs (the
@@ -2156,146 +1765,3 @@ extern "C" int mgcn_debug_xw_prof(unsigned long long *host) {
 }
 #endif
 
-extern "C" size_t mgcn_spmm_xw_bwd_dwl_workspace_bytes(int64_t n_rows) {
-  return mgcn_spmm_xw_bwd_workspace_bytes(n_rows, kXwF, kXwF);
-}
-
-extern "C" int mgcn_spmm_xw_bwd_dwl(int64_t n_rows, int64_t n_cols, const int64_t *rowptr_t,
-                                    const int32_t *col_t, const float *w_t, const float *row_scale,
-                                    const float *dY, int64_t lddy, const float *W, int64_t ldw,
-                                    float *dX, int64_t lddx, const uint32_t *relu_mask,
-                                    const float *row_div, float *colsum, int accumulate_colsum,
-                                    const float *Zl, int64_t ldz, float *dWl, int64_t lddw,
-                                    int accumulate_dw, void *workspace, size_t workspace_bytes,
-                                    void *stream) {
-  clear_error();
-  MGCN_REQUIRE(n_rows >= 0, "mgcn_spmm_xw_bwd_dwl: negative size");
-  MGCN_REQUIRE(gemm_precision_is_x6(), "mgcn_spmm_xw_bwd_dwl: needs the bf16x6 products");
-  MGCN_REQUIRE(dWl != nullptr && lddw >= kXwF, "mgcn_spmm_xw_bwd_dwl: bad dWl");
-  MGCN_REQUIRE(row_div == nullptr || relu_mask != nullptr,
-               "mgcn_spmm_xw_bwd_dwl: row_div needs relu_mask");
-  MGCN_REQUIRE(relu_mask == nullptr || colsum != nullptr,
-               "mgcn_spmm_xw_bwd_dwl: relu_mask needs colsum");
-  hipStream_t s = as_stream(stream);
-  if (n_rows == 0) {  // no rows: dWl (and the column sums) are zero contributions
-    if (!accumulate_dw)
-      for (int32_t r = 0; r < kXwF; ++r)
-        MGCN_HIP_TRY(hipMemsetAsync(dWl + r * lddw, 0, sizeof(float) * kXwF, s));
-    if (colsum && !accumulate_colsum) MGCN_HIP_TRY(hipMemsetAsync(colsum, 0, sizeof(float) * kXwF, s));
-    return MGCN_OK;
-  }
-  MGCN_REQUIRE(rowptr_t && dY && W && dX && Zl, "mgcn_spmm_xw_bwd_dwl: null array");
-  MGCN_REQUIRE(lddy >= kXwF && lddy % 4 == 0 && reinterpret_cast<uintptr_t>(dY) % 16 == 0,
-               "mgcn_spmm_xw_bwd_dwl: dY must have 16-byte aligned rows");
-  MGCN_REQUIRE(n_cols > 0 && (uint64_t)n_cols * (uint64_t)lddy * 4u <= 0xfffffff0ull,
-               "mgcn_spmm_xw_bwd_dwl: dY must hold 1 .. 4 GiB - 1 bytes (32-bit gather offsets)");
-  MGCN_REQUIRE(ldw >= kXwF && lddx >= kXwF && lddx % 4 == 0 &&
-                   reinterpret_cast<uintptr_t>(dX) % 16 == 0,
-               "mgcn_spmm_xw_bwd_dwl: bad W / dX (16-byte aligned dX rows)");
-  MGCN_REQUIRE(ldz >= kXwF && ldz % 4 == 0 && reinterpret_cast<uintptr_t>(Zl) % 16 == 0,
-               "mgcn_spmm_xw_bwd_dwl: Zl must have 16-byte aligned rows");
-  MGCN_REQUIRE((uint64_t)kXwRows * (uint64_t)(ldz > lddx ? ldz : lddx) * 4u < (1ull << 31),
-               "mgcn_spmm_xw_bwd_dwl: leading dimension too large");
-  MGCN_REQUIRE(relu_mask == nullptr || reinterpret_cast<uintptr_t>(relu_mask) % 16 == 0,
-               "mgcn_spmm_xw_bwd_dwl: relu_mask not 16-byte aligned");
-  const size_t need = mgcn_spmm_xw_bwd_dwl_workspace_bytes(n_rows);
-  if (workspace == nullptr || workspace_bytes < need) {
-    set_error("mgcn_spmm_xw_bwd_dwl: workspace %zu < %zu", workspace_bytes, need);
-    return MGCN_EWORKSPACE;
-  }
-  const int64_t n_chunks = (n_rows + kXwRows - 1) / kXwRows;
-  const int64_t g = bs_grid() < n_chunks ? bs_grid() : n_chunks;
-  XbsArgs sa{};
-  XbArgs &a = sa.b;
-  a.n_rows = n_rows;
-  a.rowptr = rowptr_t;
-  a.col = col_t;
-  a.w = w_t;
-  a.row_scale = row_scale;
-  a.dY = dY;
-  a.lddy = lddy;
-  a.n_cols = n_cols;
-  a.W = W;
-  a.ldw = ldw;
-  a.dX = dX;
-  a.lddx = lddx;
-  a.relu_mask = relu_mask;
-  a.row_div = row_div;
-  sa.Zl = Zl;
-  sa.ldz = ldz;
-  sa.dwl_partial = static_cast<float *>(workspace);
-  if (int rc2 = bs_prepare(sa)) return rc2;
-  a.colsum_partial = reinterpret_cast<float *>(
-      static_cast<char *>(workspace) + align_up((size_t)g * kXwF * kXwF * 4, 256));
-  const int epi = relu_mask == nullptr ? EPI_STORE : row_div != nullptr ? EPI_RELU_DIV : EPI_RELU;
-  int rc = launch_bs<kBsDwl>(sa, epi, (int)g, s);
-  if (rc) return rc;
-  rc = launch_split_reduce(sa.dwl_partial, (int)g, (int64_t)kXwF * kXwF, kXwF, dWl, lddw,
-                           accumulate_dw, s);
-  if (rc || epi == EPI_STORE) return rc;
-  return launch_fold(a.colsum_partial, g, kXwF, kXwF, colsum, kXwF, accumulate_colsum, s);
-}
-
-extern "C" size_t mgcn_spmm_max_xw_fwd_workspace_bytes(void) { return 4 * 8 * 3 * 64 * 16; }
-
-extern "C" int mgcn_spmm_max_xw_fwd(int64_t n_rows, int64_t n_cols, const int64_t *rowptr,
-                                    const int32_t *col, const float *w, const float *H,
-                                    int64_t ldh, const float *bias, int relu, float *Y, int64_t ldy,
-                                    uint32_t *relu_mask, uint32_t *win_mask, const float *Wn,
-                                    int64_t ldwn, float *Hn, int64_t ldhn, void *workspace,
-                                    size_t workspace_bytes, void *stream) {
-  clear_error();
-  MGCN_REQUIRE(n_rows >= 0, "mgcn_spmm_max_xw_fwd: negative size");
-  MGCN_REQUIRE(gemm_precision_is_x6(), "mgcn_spmm_max_xw_fwd: needs the bf16x6 products");
-  MGCN_REQUIRE(relu_mask == nullptr || relu, "mgcn_spmm_max_xw_fwd: relu_mask needs relu");
-  if (n_rows == 0) return MGCN_OK;
-  MGCN_REQUIRE(rowptr && H && Y && win_mask && Wn && Hn, "mgcn_spmm_max_xw_fwd: null array");
-  MGCN_REQUIRE(ldh >= kXwF && ldh % 4 == 0 && reinterpret_cast<uintptr_t>(H) % 16 == 0,
-               "mgcn_spmm_max_xw_fwd: H must have 16-byte aligned rows");
-  MGCN_REQUIRE(n_cols > 0 && (uint64_t)n_cols * (uint64_t)ldh * 4u <= 0xfffffff0ull,
-               "mgcn_spmm_max_xw_fwd: H must hold 1 .. 4 GiB - 1 bytes (32-bit gather offsets)");
-  MGCN_REQUIRE(ldy >= kXwF && ldhn >= kXwF && ldwn >= kXwF &&
-                   (uint64_t)kXwRows * (uint64_t)(ldy > ldhn ? ldy : ldhn) * 4u < (1ull << 31),
-               "mgcn_spmm_max_xw_fwd: bad leading dimension");
-  MGCN_REQUIRE(bias == nullptr || reinterpret_cast<uintptr_t>(bias) % 16 == 0,
-               "mgcn_spmm_max_xw_fwd: bias not 16-byte aligned");
-  MGCN_REQUIRE(relu_mask == nullptr || reinterpret_cast<uintptr_t>(relu_mask) % 16 == 0,
-               "mgcn_spmm_max_xw_fwd: relu_mask not 16-byte aligned");
-  XmArgs a{};
-  a.n_rows = n_rows;
-  a.rowptr = rowptr;
-  a.col = col;
-  a.w = w;
-  a.H = H;
-  a.ldh = ldh;
-  a.n_cols = n_cols;
-  a.bias = bias;
-  a.relu = relu != 0;
-  a.Y = Y;
-  a.ldy = ldy;
-  a.relu_mask = relu_mask;
-  a.win_mask = win_mask;
-  a.Hn = Hn;
-  a.ldhn = ldhn;
-  if (workspace == nullptr || workspace_bytes < mgcn_spmm_max_xw_fwd_workspace_bytes() ||
-      reinterpret_cast<uintptr_t>(workspace) % 16 != 0) {
-    set_error("mgcn_spmm_max_xw_fwd: workspace %zu < %zu (16-byte aligned)", workspace_bytes,
-              mgcn_spmm_max_xw_fwd_workspace_bytes());
-    return MGCN_EWORKSPACE;
-  }
-  a.wimg = static_cast<const u32x4 *>(workspace);
-  hipStream_t s = as_stream(stream);
-  hipLaunchKernelGGL(xm_wimg_kernel, dim3(8), dim3(256), 0, s, Wn, ldwn,
-                     static_cast<u32x4 *>(workspace));
-  if (int rc = check_launch("xm_wimg_kernel")) return rc;
-  const int64_t n_chunks = (n_rows + kXwRows - 1) / kXwRows;
-  int64_t grid = xw_grid();
-  if (grid > n_chunks) grid = n_chunks;
-  if (g_xm_unroll == 8)
-    hipLaunchKernelGGL((spmm_max_xw_kernel<8>), dim3((unsigned)grid), dim3(kXwThreads), 0, s, a);
-  else if (g_xm_unroll == 4)
-    hipLaunchKernelGGL((spmm_max_xw_kernel<4>), dim3((unsigned)grid), dim3(kXwThreads), 0, s, a);
-  else
-    hipLaunchKernelGGL((spmm_max_xw_kernel<6>), dim3((unsigned)grid), dim3(kXwThreads), 0, s, a);
-  return check_launch("spmm_max_xw_kernel");
-}

@@ -54,12 +54,12 @@
 
 namespace mgcn {
 
-// mgcn_set_option("wide_pair") / ("wide_unroll"): both rows of a wave's pair
-// gathered together or one after the other -- bit 0 the forward, bit 1 the
-// adjoint (default 3: both paired); gathered rows in flight per row and
-// round (4 or 8)
+// mgcn_set_option("wide_pair"): both rows of a wave's pair gathered together
+// or one after the other -- bit 0 the forward, bit 1 the adjoint (default 3:
+// both paired).  Gathered rows in flight per row and round: 4 (5 / 6 / 8
+// measured slower, round 5, and removed)
 int g_wide_pair = 3;
-int g_wide_unroll = 4;
+constexpr int kWideU = 4;
 // mgcn_set_option("wide_ws"): the warp-specialised kernels (below) -- bit 0
 // the forward, bit 1 the adjoint
 int g_wide_ws = 3;
@@ -96,12 +96,11 @@ int wide_set_option(const char *name, int value) {
     g_wide_ws = value;
     return MGCN_OK;
   }
-  const bool pair = name[5] == 'p';
-  if (pair ? (value < 0 || value > 3) : (value != 4 && value != 5 && value != 6 && value != 8)) {
-    set_error(pair ? "wide_pair must be 0 .. 3" : "wide_unroll must be 4, 5, 6 or 8 (5 / 6: the warp-specialised kernels)");
+  if (value < 0 || value > 3) {  // "wide_pair"
+    set_error("wide_pair must be 0 .. 3");
     return MGCN_EINVAL;
   }
-  (pair ? g_wide_pair : g_wide_unroll) = value;
+  g_wide_pair = value;
   return MGCN_OK;
 }
 
@@ -1003,10 +1002,7 @@ int launch_wide(const WideArgs &a, bool bwd, int epi, int *grid, hipStream_t s) 
     const int64_t n_chunks = (a.n_rows + kSRows - 1) / kSRows;
     const int64_t cus = wide_grid() / 2;  // one workgroup per CU
     *grid = (int)(cus < n_chunks ? cus : n_chunks);
-    return g_wide_unroll == 8 ? launch_wide_ws_u<8>(a, bwd, epi, *grid, s)
-         : g_wide_unroll == 6 ? launch_wide_ws_u<6>(a, bwd, epi, *grid, s)
-         : g_wide_unroll == 5 ? launch_wide_ws_u<5>(a, bwd, epi, *grid, s)
-                              : launch_wide_ws_u<4>(a, bwd, epi, *grid, s);
+    return launch_wide_ws_u<kWideU>(a, bwd, epi, *grid, s);
   }
   const int64_t n_chunks = (a.n_rows + kWRows - 1) / kWRows;
   const int64_t g = wide_grid();
@@ -1015,11 +1011,8 @@ int launch_wide(const WideArgs &a, bool bwd, int epi, int *grid, hipStream_t s) 
 }
 
 int launch_wide_legacy(const WideArgs &a, bool bwd, int epi, int grid, hipStream_t s) {
-  if (g_wide_pair & (bwd ? 2 : 1))
-    return g_wide_unroll == 8 ? launch_wide_p<8, true>(a, bwd, epi, grid, s)
-                              : launch_wide_p<4, true>(a, bwd, epi, grid, s);
-  return g_wide_unroll == 8 ? launch_wide_p<8, false>(a, bwd, epi, grid, s)
-                            : launch_wide_p<4, false>(a, bwd, epi, grid, s);
+  if (g_wide_pair & (bwd ? 2 : 1)) return launch_wide_p<kWideU, true>(a, bwd, epi, grid, s);
+  return launch_wide_p<kWideU, false>(a, bwd, epi, grid, s);
 }
 
 int launch_wimg(const float *W, int64_t ldw, bool trans, u32x4 *img, hipStream_t s) {

@@ -631,134 +631,6 @@ gemm_tn_x6_wide_kernel(const float *__restrict__ A, int64_t lda, const float *__
       }
 }
 
-// The same dW with each split's C cut into two 256 x 128 column halves, one
-// workgroup per half (round 5): 64 accumulators per wave instead of 128, so
-// two workgroups fit a CU (72 KB of double-buffered images each) and one's
-// split / LDS work runs under the other's MFMAs (the single-workgroup form
-// serialises them: ~52 % of the MFMA rate).  Both halves read the split's A
-// rows; blocks b and b + 8 (one XCD under round-robin dispatch) are the two
-// halves of a split, so the second read comes from that XCD's L2.  Same
-// products per C element in the same k-step order: bit for bit the one-
-// workgroup form.
-constexpr int kTnWide2Chunk = 9 * kTnX6Img;  // A (two halves) + B half: 36 KB
-
-__global__ __launch_bounds__(512, 4) void gemm_tn_x6_wide2_kernel(
-    const float *__restrict__ A, int64_t lda, const float *__restrict__ B, int64_t ldb, int64_t K,
-    int64_t k_per_split, int n_splits, float *__restrict__ partial) {
-  __shared__ __attribute__((aligned(16))) char lds[2 * kTnWide2Chunk];
-  const int bid = (int)blockIdx.x;
-  const int hh = (bid >> 3) & 1;
-  const int split = (bid >> 4) * 8 + (bid & 7);
-  if (split >= n_splits) return;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  const int64_t kb = (int64_t)split * k_per_split;
-  const int64_t ke = (kb + k_per_split < K) ? kb + k_per_split : K;
-  const int h = lane >> 5, lc = lane & 31;
-  struct Regs {
-    float4 a[2], b;
-  };
-  const auto rsa = buf_rsrc(A + kb * lda, (uint32_t)((ke - kb) * lda * 4));
-  const auto rsb = buf_rsrc(B + kb * ldb + 128 * hh, (uint32_t)((ke - kb) * ldb * 4));
-  auto load_chunk = [&](int64_t k0, Regs &R) {
-#pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      const int f = tid + 512 * m;
-      const int64_t row = k0 - kb + (f >> 6);
-      R.a[m] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                              rsa, (int)((row * lda + 4 * (f & 63)) * 4), 0, 0));
-    }
-    const int64_t row = k0 - kb + (tid >> 5);
-    R.b = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                         rsb, (int)((row * ldb + 4 * (tid & 31)) * 4), 0, 0));
-  };
-  auto put = [&](char *img, const float4 v) {
-    uint32_t hi[2], mid[2], lo[2];
-    split3_pair(f32x2{v.x, v.y}, hi[0], mid[0], lo[0]);
-    split3_pair(f32x2{v.z, v.w}, hi[1], mid[1], lo[1]);
-    *reinterpret_cast<uint2 *>(img) = make_uint2(hi[0], hi[1]);
-    *reinterpret_cast<uint2 *>(img + kTnX6Img) = make_uint2(mid[0], mid[1]);
-    *reinterpret_cast<uint2 *>(img + 2 * kTnX6Img) = make_uint2(lo[0], lo[1]);
-  };
-  auto store_chunk = [&](char *img0, const Regs &R) {
-#pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      const int f = tid + 512 * m;
-      const int row = f >> 6, c4 = f & 63;
-      const int half = c4 >> 5, c = c4 & 31;
-      put(img0 + half * 3 * kTnX6Img + tn_x6_off(row, c >> 1) + 8 * (c & 1), R.a[m]);
-    }
-    const int row = tid >> 5, c = tid & 31;
-    put(img0 + 6 * kTnX6Img + tn_x6_off(row, c >> 1) + 8 * (c & 1), R.b);
-  };
-  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-  auto frag_off = [&](int base_img, int col0, int second) {
-    const int row = 8 * h + q + 4 * second;
-    return base_img * kTnX6Img + tn_x6_off(row, (col0 >> 3) + 2 * (g & 1) + (p >> 1)) + 8 * (p & 1);
-  };
-  int offa[2][2], offb[2][2];
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int gcol = wm * 64 + 32 * t;  // A column (C row), 0 .. 255
-      offa[t][r] = frag_off((gcol >> 7) * 3, gcol & 127, r);
-      offb[t][r] = frag_off(6, wn * 64 + 32 * t, r);
-    }
-  }
-  auto read8 = [&](const char *img0, const int (&o)[2], int term) {
-    const v4i16 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (lds_v4i16_t *)(img0 + o[0] + term * kTnX6Img));
-    const v4i16 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (lds_v4i16_t *)(img0 + o[1] + term * kTnX6Img));
-    const short y[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
-    return __builtin_bit_cast(bf16x8, y);
-  };
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[t][u][r] = 0.0f;
-  const int64_t nchunks = (ke - kb + kTnX6Rows - 1) / kTnX6Rows;
-  Regs R;
-  if (nchunks > 0) load_chunk(kb, R);
-  for (int64_t c = 0; c < nchunks; ++c) {
-    char *img0 = lds + (c & 1) * kTnWide2Chunk;
-    store_chunk(img0, R);
-    if (c + 1 < nchunks) load_chunk(kb + (c + 1) * kTnX6Rows, R);
-    __syncthreads();
-    bf16x8 fa[2][3];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int term = 0; term < 3; ++term) fa[t][term] = read8(img0, offa[t], term);
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      bf16x8 fb[3];
-#pragma unroll
-      for (int term = 0; term < 3; ++term) fb[term] = read8(img0, offb[u], term);
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-        acc[t][u] = mfma_x6(fa[t][0], fa[t][1], fa[t][2], fb[0], fb[1], fb[2], acc[t][u]);
-    }
-  }
-  float *slab = partial + (int64_t)split * 256 * 256;
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = wm * 64 + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        slab[(int64_t)row * 256 + 128 * hh + wn * 64 + u * 32 + lc] = acc[t][u][r];
-      }
-}
-
-int g_tn_wide2 = 0;  // mgcn_set_option("gemm_tn_wide2"): the two-half form at 256 x 256
 
 bool tn_wide(int M, int N) { return M == 256 && N == 256; }
 // gemm_tn_x6_wide_kernel addresses a split's rows with 32-bit buffer offsets
@@ -772,8 +644,6 @@ bool tn_lds(int M, int N) { return M % kTile == 0 && N % kTile == 0; }
 // K = 1M, M = N = 128: 0.321 / 0.335 / 0.337 ms): 0 = BK 64, one workgroup
 // per CU; 1 = BK 32, two; 2 = BK 16, three
 int g_tn_lds_variant = 0;
-int g_dw_ws = 0;  // mgcn_set_option("dw_ws"): gemm_dw_ws_kernel (1) / gemm_dw_direct_kernel (2) for mgcn_gemm_bwd's dW-only form
-int g_dw_direct_ni = 2;  // mgcn_set_option("dw_direct_ni"): 2 or 4 (see gemm_dw_direct_kernel)
 int g_tn_staged = 1;  // M = 32, N = 32 / 64: gemm_tn_staged_kernel (0: gemm_tn_small_kernel)
 int tn_lds_wgs() { return g_tn_lds_variant == 1 ? 2 : g_tn_lds_variant == 2 ? 3 : 1; }
 
@@ -801,24 +671,6 @@ int gemm_splits(int64_t K, int M, int N) {
 int gemm_set_tn_variant(int value) {
   if (value < 0 || value > 2) return MGCN_EINVAL;
   g_tn_lds_variant = value;
-  return MGCN_OK;
-}
-
-int gemm_set_tn_wide2(int value) {
-  if (value < 0 || value > 1) return MGCN_EINVAL;
-  g_tn_wide2 = value;
-  return MGCN_OK;
-}
-
-int gemm_set_dw_ws(int value) {
-  if (value < 0 || value > 2) return MGCN_EINVAL;
-  g_dw_ws = value;
-  return MGCN_OK;
-}
-
-int gemm_set_dw_direct_ni(int value) {
-  if (value != 2 && value != 4) return MGCN_EINVAL;
-  g_dw_direct_ni = value;
   return MGCN_OK;
 }
 
@@ -899,11 +751,7 @@ int gemm_tn_core(int64_t K, int32_t M, int32_t N, const float *A, int64_t lda, c
              reinterpret_cast<uintptr_t>(B) % 16 == 0 && lda % 4 == 0 && ldb % 4 == 0) {
     // 1-D grids of tiles x splits in the kernels' XCD-aware order
     const dim3 grid(tiles_m * tiles_n * used);
-    if (g_gemm_precision == PREC_BF16X6 && tn_wide(M, N) && tn_wide_fits(kps, lda, ldb) &&
-        g_tn_wide2)
-      hipLaunchKernelGGL(gemm_tn_x6_wide2_kernel, dim3(2 * ((used + 7) / 8) * 8), dim3(512), 0, s,
-                         A, lda, B, ldb, K, kps, used, partial);
-    else if (g_gemm_precision == PREC_BF16X6 && tn_wide(M, N) && tn_wide_fits(kps, lda, ldb))
+    if (g_gemm_precision == PREC_BF16X6 && tn_wide(M, N) && tn_wide_fits(kps, lda, ldb))
       hipLaunchKernelGGL(gemm_tn_x6_wide_kernel, dim3(used), dim3(512), 0, s, A, lda, B, ldb, K,
                          kps, partial);
     else if (g_gemm_precision == PREC_BF16X6)
@@ -2075,392 +1923,6 @@ int launch_bwd(int grid, const float *X, int64_t ldx, const float *dH, int64_t l
 }
 
 // ----------------------------------------------------------------------------
-// dW-only pass (dW = X^T dH, optionally dH's column sums), warp-specialised
-// (round 5): gemm_bwd_kernel<.., false> serialises per chunk its loads'
-// arrival, the split VALU, the LDS writes, a barrier and the MFMAs of two
-// waves per SIMD (measured 4.3 k cycles per 32-row chunk against ~2.5 k of
-// HBM time).  Here one 1024-thread workgroup per CU: 8 LOADER waves stream
-// the chunks (two register banks ahead), split them into the three bf16 term
-// images and add the dH column sums; 8 MFMA waves take the images from a
-// ring of three 48-KB buffers (LDS counters, bounded spins -- fused.hip's
-// hand-off) and run gemm_bwd's 32x32 dW tiles.  Same products in the same
-// k-step order per workgroup as gemm_bwd_kernel; the chunk-to-workgroup map,
-// hence the split-K partials, is the same too (grid = kBwGrid).
-constexpr int kDwBuf = 6 * kBwImg;   // one chunk: X and dH, three terms each (48 KB)
-constexpr int kDwRing = 3;
-constexpr int kDwCtrOff = kDwRing * kDwBuf;
-constexpr int kDwLds = kDwCtrOff + 64;
-static_assert(kDwLds <= 160 * 1024, "one dW workgroup per CU");
-constexpr uint32_t kDwSpinLimit = 1u << 25;
-
-__device__ __forceinline__ int dw_lds_load(const int *p) {
-  return __builtin_amdgcn_readfirstlane(
-      __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-}
-
-__device__ __forceinline__ bool dw_wait_ge(const int *p, int target, int *abort_word) {
-  for (uint32_t n = 0;; ++n) {
-    if (dw_lds_load(p) >= target) break;
-    if (dw_lds_load(abort_word) != 0) return false;
-    if (n >= kDwSpinLimit) {
-      __hip_atomic_store(abort_word, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-  asm volatile("" ::: "memory");
-  return true;
-}
-
-__device__ __forceinline__ int dw_signal(int *p, int v, int lane) {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  int old = 0;
-  if (lane == 0) old = __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  return __builtin_amdgcn_readfirstlane(old);
-}
-
-template <bool HCS>
-__global__ __launch_bounds__(1024) void gemm_dw_ws_kernel(
-    const float *__restrict__ X, int64_t ldx, const float *__restrict__ dH, int64_t lddh,
-    int64_t M, float *__restrict__ dw_partial, float *__restrict__ colsum_partial) {
-  __shared__ __attribute__((aligned(16))) char lds[kDwLds];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int h = lane >> 5, lc = lane & 31;
-  const int g4 = lane >> 4;
-  int *ctr = reinterpret_cast<int *>(lds + kDwCtrOff);
-  int *filled = ctr, *mdone = ctr + 3, *freed = ctr + 6, *abort_word = ctr + 9;
-  if (tid < 16) ctr[tid] = 0;
-  __syncthreads();
-  const int64_t n_chunks = (M + kBwRows - 1) / kBwRows;
-  const int64_t G = gridDim.x;
-  const int n_my = blockIdx.x < n_chunks ? (int)((n_chunks - 1 - blockIdx.x) / G) + 1 : 0;
-  auto rows_in = [&](int64_t chunk) -> uint32_t {
-    const int64_t r = M - chunk * kBwRows;
-    return (uint32_t)(r <= 0 ? 0 : r >= kBwRows ? kBwRows : r);
-  };
-  float hc[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // loaders (HCS): dH column sums of float4 t & 31
-  f32x16 accw[2];                          // MFMA waves
-#pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) accw[s2][r] = 0.0f;
-  const int t = tid & 511;  // loader thread index (loaders are threads 0 .. 511)
-
-  if (wave < 8) {
-    // ------------------------------- loader waves ---------------------------
-    // thread t: float4 t & 31 of rows t >> 5 and 16 + (t >> 5), of X and dH
-    const int ld_off_x = 4 * (int)((t >> 5) * ldx + 4 * (t & 31));
-    const int ld_off_h = 4 * (int)((t >> 5) * lddh + 4 * (t & 31));
-    struct Bank {
-      u32x4 v[4];
-    };
-    auto load = [&](int i, Bank &b) {  // chunk i of this workgroup (past the end: zeros)
-      const int64_t chunk = blockIdx.x + (int64_t)i * G;
-      const int64_t r0 = chunk * kBwRows;
-      const uint32_t rv = i < n_my ? rows_in(chunk) : 0u;
-      const auto rx = buf_rsrc(X + (i < n_my ? r0 * ldx : 0), rv * (uint32_t)ldx * 4u);
-      const auto rh = buf_rsrc(dH + (i < n_my ? r0 * lddh : 0), rv * (uint32_t)lddh * 4u);
-#pragma unroll
-      for (int m = 0; m < 2; ++m) {
-        b.v[m] = __builtin_amdgcn_raw_buffer_load_b128(rx, ld_off_x + m * 64 * (int)ldx, 0,
-                                                       MGCN_NT_AUX);
-        b.v[2 + m] = __builtin_amdgcn_raw_buffer_load_b128(rh, ld_off_h + m * 64 * (int)lddh, 0, 0);
-      }
-    };
-    Bank bk[2];
-    load(0, bk[0]);
-    load(1, bk[1]);
-    for (int i = 0; i < n_my; i += 2) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int ii = i + j;
-        if (ii >= n_my) break;
-        const int b = ii % kDwRing, gen = ii / kDwRing;
-        if (!dw_wait_ge(freed + b, gen, abort_word)) goto loaders_done;
-        char *buf = lds + b * kDwBuf;
-        const int c4 = t & 31;
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-          const int row = 16 * (m & 1) + (t >> 5);
-          const int off = img_off(row, c4 >> 1) + 8 * (c4 & 1);
-          const float4 v = __builtin_bit_cast(float4, bk[j].v[m]);
-          if constexpr (HCS) {
-            if (m >= 2) {  // rows q then 16 + q of every chunk: a fixed order
-              hc[0] = __fadd_rn(hc[0], v.x);
-              hc[1] = __fadd_rn(hc[1], v.y);
-              hc[2] = __fadd_rn(hc[2], v.z);
-              hc[3] = __fadd_rn(hc[3], v.w);
-            }
-          }
-          uint32_t hi[2], mid[2], lo[2];
-          split3_pair(f32x2{v.x, v.y}, hi[0], mid[0], lo[0]);
-          split3_pair(f32x2{v.z, v.w}, hi[1], mid[1], lo[1]);
-          char *img = buf + (m >> 1) * 3 * kBwImg + off;
-          *reinterpret_cast<uint2 *>(img) = make_uint2(hi[0], hi[1]);
-          *reinterpret_cast<uint2 *>(img + kBwImg) = make_uint2(mid[0], mid[1]);
-          *reinterpret_cast<uint2 *>(img + 2 * kBwImg) = make_uint2(lo[0], lo[1]);
-        }
-        load(ii + 2, bk[j]);  // the bank is free: two chunks ahead
-        dw_signal(filled + b, 1, lane);
-      }
-    }
-  loaders_done:;
-  } else {
-    // -------------------------------- MFMA waves ----------------------------
-    const int m = wave - 8;
-    const int q = (lane >> 2) & 3, p = lane & 3;
-    auto frag_off = [&](int col0, int second) {
-      return img_off(8 * h + q + 4 * second, (col0 >> 3) + 2 * (g4 & 1) + (p >> 1)) + 8 * (p & 1);
-    };
-    const int ti = m >> 1, tj0 = 2 * (m & 1);
-    int offa[2], offb[2][2];
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      offa[r] = frag_off(32 * ti, r);
-      offb[0][r] = 3 * kBwImg + frag_off(32 * tj0, r);
-      offb[1][r] = 3 * kBwImg + frag_off(32 * (tj0 + 1), r);
-    }
-    auto read8 = [&](const char *base, const int (&o)[2]) {
-      const v4i16 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16_t *)(base + o[0]));
-      const v4i16 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16_t *)(base + o[1]));
-      const short y[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
-      return __builtin_bit_cast(bf16x8, y);
-    };
-    for (int i = 0; i < n_my; ++i) {
-      const int b = i % kDwRing, gen = i / kDwRing;
-      if (!dw_wait_ge(filled + b, 8 * (gen + 1), abort_word)) break;
-      const char *buf = lds + b * kDwBuf;
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const char *kb = buf + ks * 16 * 256;
-        bf16x8 fa[3], fb[2][3];
-#pragma unroll
-        for (int tt = 0; tt < 3; ++tt) {
-          fa[tt] = read8(kb + tt * kBwImg, offa);
-          fb[0][tt] = read8(kb + tt * kBwImg, offb[0]);
-          fb[1][tt] = read8(kb + tt * kBwImg, offb[1]);
-        }
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
-          accw[s2] = mfma_x6(fa[0], fa[1], fa[2], fb[s2][0], fb[s2][1], fb[s2][2], accw[s2]);
-      }
-      const int old = dw_signal(mdone + b, 1, lane);
-      if (old == 8 * gen + 7) dw_signal(freed + b, 1, lane);
-    }
-    float *slab = dw_partial + (int64_t)blockIdx.x * kBwF * kBwF;
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = 32 * ti + (r & 3) + 8 * (r >> 2) + 4 * h;
-        slab[row * kBwF + 32 * (tj0 + s2) + lc] = accw[s2][r];
-      }
-  }
-  if constexpr (HCS) {
-    // fold the 16 row groups (t >> 5) of each column in fixed order
-    __syncthreads();
-    float *red = reinterpret_cast<float *>(lds);
-    if (wave < 8) *reinterpret_cast<float4 *>(red + 4 * t) = make_float4(hc[0], hc[1], hc[2], hc[3]);
-    __syncthreads();
-    if (tid < kBwF) {
-      float c = 0.0f;
-#pragma unroll
-      for (int g = 0; g < 16; ++g) c = __fadd_rn(c, red[4 * (32 * g + (tid >> 2)) + (tid & 3)]);
-      colsum_partial[(int64_t)blockIdx.x * kBwF + tid] = c;
-    }
-  }
-}
-
-// ----------------------------------------------------------------------------
-// dW-only pass with no LDS (round 5, mgcn_set_option "dw_ws" 2): each wave
-// streams its rows of X (one 64-column half) and all of dH straight into
-// MFMA-layout registers -- lane (lc, h) of a 16-row k-step loads column lc
-// of rows 8 h .. 8 h + 7 (one dword per row; each instruction two 128-B row
-// segments) -- splits them into their bf16 terms in registers and
-// accumulates its 64 x 128 half of dW in eight 32x32 tiles (128
-// accumulators).  256-thread workgroups, one per CU, each over a contiguous
-// K range: waves 2 p + c (c: the column half) take the range's k-steps
-// p, p + 2, ...; the two pairs' tiles are added in LDS, one partial per
-// workgroup (folded in workgroup order).  D k-steps of raw loads in flight.
-constexpr int kDdThreads = 256;
-
-// NI = 2: waves 2 p + c take X's column half c over k-steps p, p + 2, ...
-// (128 accumulators); NI = 4: each wave the whole 128 x 128 over k-steps
-// w, w + 4, ... (256 accumulators, AGPRs: the VALU split of 64 loads per
-// k-step hides under 96 MFMAs instead of 48 loads under 48)
-template <bool HCS, int D, int NI>
-__global__ __launch_bounds__(kDdThreads, 1) void gemm_dw_direct_kernel(
-    const float *__restrict__ X, int64_t ldx, const float *__restrict__ dH, int64_t lddh,
-    int64_t M, int64_t rows_per_wg, float *__restrict__ dw_partial,
-    float *__restrict__ colsum_partial) {
-  constexpr int NP = NI;  // waves sharing a column range (k-step interleave): 2 or 4
-  __shared__ __attribute__((aligned(16))) float red[2 * NI * 4 * 16 * 64];
-  __shared__ float cred[4][kBwF];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lc = lane & 31, h = lane >> 5;
-  const int half = NI == 2 ? (wave & 1) : 0;
-  const int pair = NI == 2 ? (wave >> 1) : wave;
-  const int64_t wb = (int64_t)blockIdx.x * rows_per_wg;
-  int64_t we = wb + rows_per_wg;
-  if (we > M) we = M;
-  const int64_t nrows = we > wb ? we - wb : 0;
-  const auto rx = buf_rsrc(X + wb * ldx, (uint32_t)(nrows * ldx * 4));
-  const auto rh = buf_rsrc(dH + wb * lddh, (uint32_t)(nrows * lddh * 4));
-  const int n_steps = (int)((nrows + 15) / 16);
-  const int my_steps = n_steps > pair ? (n_steps - pair + NP - 1) / NP : 0;
-  const uint32_t xstep = (uint32_t)(16 * NP * ldx * 4), hstep = (uint32_t)(16 * NP * lddh * 4);
-  const uint32_t x0 = (uint32_t)(16 * pair * ldx * 4), h0 = (uint32_t)(16 * pair * lddh * 4);
-  const int va = 4 * (int)(8 * h * ldx + 64 * half + lc);
-  const int vb = 4 * (int)(8 * h * lddh + lc);
-
-  struct Raw {
-    float a[NI][8];
-    float b[4][8];
-  };
-  auto load = [&](int t, Raw &r) {  // k-step t of this wave (past the range: zeros)
-    const uint32_t so_x = x0 + (uint32_t)t * xstep, so_h = h0 + (uint32_t)t * hstep;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-#pragma unroll
-      for (int ib = 0; ib < NI; ++ib)
-        r.a[ib][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-            rx, va + 4 * (int)(j * ldx + 32 * ib), so_x, MGCN_NT_AUX));
-#pragma unroll
-      for (int nb = 0; nb < 4; ++nb)
-        r.b[nb][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-            rh, vb + 4 * (int)(j * lddh + 32 * nb), so_h, 0));
-    }
-  };
-  f32x16 acc[NI][4];
-#pragma unroll
-  for (int ib = 0; ib < NI; ++ib)
-#pragma unroll
-    for (int nb = 0; nb < 4; ++nb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[ib][nb][r] = 0.0f;
-  float hc[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // HCS (half 0): dH column sums, columns 32 nb + lc
-
-  Raw ring[D];
-#pragma unroll
-  for (int d = 0; d < D; ++d) load(d, ring[d]);
-  for (int t0 = 0; t0 < my_steps; t0 += D) {
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      const int t = t0 + d;
-      if (t >= my_steps) break;
-      Raw cur = ring[d];
-      load(t + D, ring[d]);
-      bf16x8 fa[NI][3], fb[4][3];
-#pragma unroll
-      for (int ib = 0; ib < NI; ++ib) split3_bf16(cur.a[ib], fa[ib][0], fa[ib][1], fa[ib][2]);
-#pragma unroll
-      for (int nb = 0; nb < 4; ++nb) {
-        split3_bf16(cur.b[nb], fb[nb][0], fb[nb][1], fb[nb][2]);
-        if constexpr (HCS) {
-          if (half == 0)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) hc[nb] = __fadd_rn(hc[nb], cur.b[nb][j]);
-        }
-      }
-#pragma unroll
-      for (int ib = 0; ib < NI; ++ib)
-#pragma unroll
-        for (int nb = 0; nb < 4; ++nb)
-          acc[ib][nb] = mfma_x6(fa[ib][0], fa[ib][1], fa[ib][2], fb[nb][0], fb[nb][1], fb[nb][2],
-                                acc[ib][nb]);
-    }
-  }
-  if constexpr (HCS) {
-    if (half == 0) {
-#pragma unroll
-      for (int nb = 0; nb < 4; ++nb) {
-        const float v = __fadd_rn(hc[nb], __shfl_xor(hc[nb], 32, 64));  // rows 8 h ..: both halves
-        if (h == 0) cred[pair][32 * nb + lc] = v;
-      }
-    }
-  }
-  // fold the waves sharing a column range through LDS ([slot][tile][r][lane]):
-  // NI = 2, pair 1 into pair 0; NI = 4, waves 2, 3 into 0, 1, then 1 into 0
-  auto put = [&](int slot) {
-#pragma unroll
-    for (int ib = 0; ib < NI; ++ib)
-#pragma unroll
-      for (int nb = 0; nb < 4; ++nb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) red[((slot * NI + ib) * 4 + nb) * 1024 + r * 64 + lane] = acc[ib][nb][r];
-  };
-  auto add = [&](int slot) {
-#pragma unroll
-    for (int ib = 0; ib < NI; ++ib)
-#pragma unroll
-      for (int nb = 0; nb < 4; ++nb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          acc[ib][nb][r] = __fadd_rn(acc[ib][nb][r], red[((slot * NI + ib) * 4 + nb) * 1024 + r * 64 + lane]);
-  };
-  bool writer;
-  if constexpr (NI == 2) {
-    if (pair == 1) put(half);
-    __syncthreads();
-    if (pair == 0) add(half);
-    writer = pair == 0;
-  } else {
-    if (wave >= 2) put(wave - 2);
-    __syncthreads();
-    if (wave < 2) add(wave);
-    __syncthreads();
-    if (wave == 1) put(0);
-    __syncthreads();
-    if (wave == 0) add(0);
-    writer = wave == 0;
-  }
-  if (writer) {
-    float *slab = dw_partial + (int64_t)blockIdx.x * kBwF * kBwF;
-#pragma unroll
-    for (int ib = 0; ib < NI; ++ib)
-#pragma unroll
-      for (int nb = 0; nb < 4; ++nb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = 32 * (NI == 2 ? 2 * half + ib : ib) + (r & 3) + 8 * (r >> 2) + 4 * h;
-          slab[row * kBwF + 32 * nb + lc] = acc[ib][nb][r];
-        }
-  }
-  if constexpr (HCS) {
-    __syncthreads();
-    if (threadIdx.x < kBwF) {
-      float c = 0.0f;
-#pragma unroll
-      for (int q = 0; q < NP; ++q) c = __fadd_rn(c, cred[q][threadIdx.x]);
-      colsum_partial[(int64_t)blockIdx.x * kBwF + threadIdx.x] = c;
-    }
-  }
-}
-
-template <bool HCS>
-int launch_dw_direct(const float *X, int64_t ldx, const float *dH, int64_t lddh, int64_t M,
-                     float *dwp, float *csp, int *grid_out, hipStream_t s) {
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-    cus = 256;
-  if (cus > kBwGrid) cus = kBwGrid;  // the workspace holds kBwGrid partials
-  int64_t rows = (M + cus - 1) / cus;
-  rows = (rows + 63) / 64 * 64;  // whole 16-row k-steps for every wave
-  const int grid = (int)((M + rows - 1) / rows);
-  *grid_out = grid;
-  if (g_dw_direct_ni == 2)
-    hipLaunchKernelGGL((gemm_dw_direct_kernel<HCS, 2, 2>), dim3(grid), dim3(kDdThreads), 0, s, X,
-                       ldx, dH, lddh, M, rows, dwp, csp);
-  else
-    hipLaunchKernelGGL((gemm_dw_direct_kernel<HCS, 1, 4>), dim3(grid), dim3(kDdThreads), 0, s, X,
-                       ldx, dH, lddh, M, rows, dwp, csp);
-  return check_launch("gemm_dw_direct_kernel");
-}
-
 }  // namespace
 }  // namespace mgcn
 
@@ -2514,20 +1976,8 @@ extern "C" int mgcn_gemm_bwd(int64_t M, int32_t F_in, int32_t F_out, const float
   const int64_t n_chunks = (M + kBwRows - 1) / kBwRows;
   const int grid = (int)(n_chunks < kBwGrid ? n_chunks : kBwGrid);
   int rc;
-  int fold_grid = grid;
-  if (dX == nullptr && g_dw_ws == 2 &&
-      (uint64_t)((M + 255) / 256 + 32) * (uint64_t)(ldx > lddh ? ldx : lddh) * 4u < (1ull << 32)) {
-    rc = hcs ? launch_dw_direct<true>(X, ldx, dH, lddh, M, dwp, csp, &fold_grid, s)
-             : launch_dw_direct<false>(X, ldx, dH, lddh, M, dwp, csp, &fold_grid, s);
-  } else if (dX == nullptr && g_dw_ws) {
-    if (hcs)
-      hipLaunchKernelGGL((gemm_dw_ws_kernel<true>), dim3(grid), dim3(1024), 0, s, X, ldx, dH, lddh,
-                         M, dwp, csp);
-    else
-      hipLaunchKernelGGL((gemm_dw_ws_kernel<false>), dim3(grid), dim3(1024), 0, s, X, ldx, dH,
-                         lddh, M, dwp, csp);
-    rc = check_launch("gemm_dw_ws_kernel");
-  } else if (dX == nullptr && hcs)
+  const int fold_grid = grid;
+  if (dX == nullptr && hcs)
     rc = launch_bwd<EPI_STORE, false, true>(grid, X, ldx, dH, lddh, W, ldw, M, dX, lddx,
                                             relu_mask, row_div, dwp, csp, s);
   else if (dX == nullptr)

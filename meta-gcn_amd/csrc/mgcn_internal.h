@@ -88,9 +88,6 @@ inline unsigned grid_for(int64_t work_items, int block) {
 // mgcn_set_option("gemm_tn_variant") -> gemm.hip
 int gemm_set_tn_variant(int value);
 int gemm_set_tn_staged(int value);  // mgcn_set_option("gemm_tn_staged")
-int gemm_set_dw_ws(int value);      // mgcn_set_option("dw_ws")
-int gemm_set_dw_direct_ni(int value);  // gemm.hip: "dw_direct_ni"
-int gemm_set_tn_wide2(int value);   // mgcn_set_option("gemm_tn_wide2")
 int gemm_set_precision(int value);
 int gemm_precision_is_x6();  // 1 under bf16x6 (the fused kernels need it)
 int xw_set_unroll(int value);  // fused.hip

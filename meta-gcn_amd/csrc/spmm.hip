@@ -476,10 +476,6 @@ int g_force_vec = 0;  // tuning knobs (mgcn_set_option)
 int g_unroll = 8;
 bool g_unroll_set = false;  // spmm_unroll given explicitly: every mode takes it
 int g_heavy_side = 1;  // heavy-row launch on a side stream (concurrent)
-// mgcn_set_option("heavy_mid_side"): heavy_rows() also puts the non-giant heavy
-// rows on the side stream (after the giant ones), so the caller's light-row
-// pass starts at once on its stream
-int g_heavy_mid_side = 0;
 
 template <int VEC, int G, int U, int MODE>
 int launch_one(const SpmmArgs &a, hipStream_t stream) {
@@ -705,14 +701,8 @@ int heavy_rows(int bwd, int64_t n_rows, int32_t F, const int64_t *rowptr, const 
       const int rc = bwd ? launch_heavy_v<BWD_SUM>(a, vec, true, side->stream)
                          : launch_heavy_v<FWD_SUM>(a, vec, true, side->stream);
       if (rc) return rc;
-      if (g_heavy_mid_side && n_heavy > n_giant) {
-        const int rc2 = bwd ? launch_heavy_v<BWD_SUM>(a, vec, false, side->stream)
-                            : launch_heavy_v<FWD_SUM>(a, vec, false, side->stream);
-        if (rc2) return rc2;
-      }
       MGCN_HIP_TRY(hipEventRecord(side->join, side->stream));
       *side_used = true;
-      if (g_heavy_mid_side) return MGCN_OK;  // (the mid heavy rows went with them)
     } else {
       const int rc = bwd ? launch_heavy_v<BWD_SUM>(a, vec, true, stream)
                          : launch_heavy_v<FWD_SUM>(a, vec, true, stream);
@@ -789,18 +779,6 @@ extern "C" int mgcn_set_option(const char *name, int value) {
     MGCN_REQUIRE(value >= 0 && value <= 2, "gemm_tn_variant must be 0, 1 or 2");
     return gemm_set_tn_variant(value);
   }
-  if (n == "gemm_tn_wide2") {
-    MGCN_REQUIRE(value == 0 || value == 1, "gemm_tn_wide2 must be 0 or 1");
-    return gemm_set_tn_wide2(value);
-  }
-  if (n == "dw_direct_ni") {
-    MGCN_REQUIRE(value == 2 || value == 4, "dw_direct_ni must be 2 or 4");
-    return gemm_set_dw_direct_ni(value);
-  }
-  if (n == "dw_ws") {
-    MGCN_REQUIRE(value >= 0 && value <= 2, "dw_ws must be 0, 1 or 2");
-    return gemm_set_dw_ws(value);
-  }
   if (n == "gemm_tn_staged") {
     MGCN_REQUIRE(value == 0 || value == 1, "gemm_tn_staged must be 0 or 1");
     return gemm_set_tn_staged(value);
@@ -810,8 +788,8 @@ extern "C" int mgcn_set_option(const char *name, int value) {
     return gemm_set_precision(value);
   }
   if (n == "spmm_xw_unroll") return xw_set_unroll(value);
-  if (n == "xw_ws" || n == "xw_ws_unroll" || n == "xw_ws_dbg" || n == "xw_ws_xm_unroll" || n == "xw_ws_full" || n == "xw_ws_max" || n == "xw_ws_full_unroll") return xw_set_ws(name, value);
-  if (n == "wide_pair" || n == "wide_unroll" || n == "wide_ws" || n == "wide_dbg" || n == "wide_mfma") return wide_set_option(name, value);
+  if (n == "xw_ws_dbg" || n == "xw_ws_full" || n == "xw_ws_max" || n == "xw_ws_full_unroll") return xw_set_ws(name, value);
+  if (n == "wide_pair" || n == "wide_ws" || n == "wide_dbg" || n == "wide_mfma") return wide_set_option(name, value);
   if (n == "residual_blocks") {
     MGCN_REQUIRE(value >= 64 && value <= 65536, "residual_blocks must be in [64, 65536]");
     g_rl_cap = value;
@@ -825,11 +803,6 @@ extern "C" int mgcn_set_option(const char *name, int value) {
   if (n == "heavy_side_fence") {
     MGCN_REQUIRE(value == 0 || value == 1, "heavy_side_fence must be 0 or 1");
     g_side_fence = value;
-    return MGCN_OK;
-  }
-  if (n == "heavy_mid_side") {
-    MGCN_REQUIRE(value == 0 || value == 1, "heavy_mid_side must be 0 or 1");
-    g_heavy_mid_side = value;
     return MGCN_OK;
   }
   if (n == "ws_spin_limit") {  // the warp-specialised kernels' hand-off bound (abort-path tests)

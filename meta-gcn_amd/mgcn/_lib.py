@@ -86,15 +86,8 @@ SIGNATURES = {
     "mgcn_spmm_xw_bwd_hcs": (_int, [_i64, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp,
                                     _i64, _vp, _i64, _int, _vp, _i64, _vp, _vp, _vp, _vp, _vp,
                                     _sz, _vp]),
-    "mgcn_spmm_xw_bwd_dwl_workspace_bytes": (_sz, [_i64]),
-    "mgcn_spmm_xw_bwd_dwl": (_int, [_i64, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp,
-                                    _i64, _vp, _vp, _vp, _int, _vp, _i64, _vp, _i64, _int, _vp,
-                                    _sz, _vp]),
     "mgcn_gemm_batched": (_int, [_i64, _i32, _i32, _i32, _vp, _i64, _i64, _i64, _vp, _i64, _i64,
                                  _i64, _vp, _i64, _i64, _i64, _int, _vp]),
-    "mgcn_spmm_max_xw_fwd_workspace_bytes": (_sz, []),
-    "mgcn_spmm_max_xw_fwd": (_int, [_i64, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _int, _vp, _i64,
-                                    _vp, _vp, _vp, _i64, _vp, _i64, _vp, _sz, _vp]),
     "mgcn_colsum_workspace_bytes": (_sz, [_i64, _i32]),
     "mgcn_relu_bwd_colsum": (_int, [_i64, _i32, _vp, _vp, _int, _vp, _vp, _vp, _vp, _sz, _vp]),
     "mgcn_residual_act": (_int, [_i64, _i32, _vp, _i64, _vp, _i64, _vp, _int, _vp, _i64, _vp]),

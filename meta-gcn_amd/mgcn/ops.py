@@ -40,12 +40,6 @@ _FUSE_XW = os.environ.get("MGCN_FUSE_XW", "1") != "0"
 # the dW pass) and the bottom layer (no gather at all) take the Z form.
 # MGCN_Z_MIDDLE=1 sends the middle layers through Z as well.
 _Z_MIDDLE = os.environ.get("MGCN_Z_MIDDLE", "0") != "0"
-# The lower layer's dW = Z^T dY fused into the adjoint that writes that dY
-# (mgcn_spmm_xw_bwd_dwl; every layer below a fused one keeps its Z): env
-# MGCN_DWL=1 / set_fused_dwl(True).  Off by default: measured at config 2 the
-# fused launch costs 1.17 ms against 0.87 + 0.22 ms for the dX-only adjoint
-# and the separate dW pass.
-_DWL = os.environ.get("MGCN_DWL", "0") != "0"
 # the top 128-wide layer of a stack (sum, no ReLU) takes the dW + dX adjoint
 # (the DWS kernel) instead of keeping Z for the dense Z^T dY pass: env
 # MGCN_TOP_FULL=0 turns it off.  Its bias gradient (dY's column sums) comes
@@ -78,28 +72,6 @@ def set_z_middle(enabled: bool) -> None:
     gather kernel (False, the default)."""
     global _Z_MIDDLE
     _Z_MIDDLE = bool(enabled)
-
-
-# Max layers followed by another 128 -> 128 layer write that layer's x @ W from
-# their own epilogue (mgcn_spmm_max_xw_fwd): MGCN_MAX_NEXT=1 / set_max_next(True).
-# Off by default: at config 4 the fused launch takes 1.19 ms against 0.95 +
-# 0.24 ms for the max SpMM and the GEMM (DESIGN.md §4), no step gain.
-_MAX_NEXT = os.environ.get("MGCN_MAX_NEXT", "0") != "0"
-
-
-def set_max_next(enabled: bool) -> None:
-    """Max layers write the next layer's x @ W from their epilogue (True;
-    mgcn_spmm_max_xw_fwd) or leave it to a GEMM launch (False, the default)."""
-    global _MAX_NEXT
-    _MAX_NEXT = bool(enabled)
-
-
-def set_fused_dwl(enabled: bool) -> None:
-    """Fuse the lower layer's dW = Z^T dY into the dX-only adjoint that
-    produces its dY (True; mgcn_spmm_xw_bwd_dwl) or run the separate dense dW
-    pass (False, the default: faster at config 2)."""
-    global _DWL
-    _DWL = bool(enabled)
 
 
 def set_kernel_timer(timer) -> None:
@@ -384,137 +356,6 @@ def spmm_xw_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tens
         _TIMER(tname, False)
     L.check(rc, "mgcn_spmm_xw_bwd")
     return dW, dX, colsum
-
-
-def spmm_max_xw_supported(view: CSRView, W: torch.Tensor, Wn: torch.Tensor,
-                          ld: int | None = None) -> bool:
-    """:func:`spmm_max_xw_fwd` takes a max layer (W) followed by Wn: both
-    128 x 128, bf16x6, no heavy rows, the gathered table within 32-bit
-    offsets."""
-    return (tuple(W.shape) == (128, 128) and tuple(Wn.shape) == (128, 128) and
-            spmm_xw_supported(view, 128, 128, L.REDUCE_SUM, ld))
-
-
-def spmm_max_xw_fwd(view: CSRView, w: torch.Tensor | None, H: torch.Tensor,
-                    bias: torch.Tensor | None, relu: bool, Wn: torch.Tensor, nnz: int,
-                    relu_mask: torch.Tensor | None = None):
-    """A max layer and the next layer's transform in one launch
-    (``mgcn_spmm_max_xw_fwd``): Y = relu(max_k H[col_k] w_k + b) -- bit for bit
-    :func:`spmm_fwd` (REDUCE_MAX) -- with its ReLU mask words and every
-    edge's winner bits ([nnz, 4], the ``mask_plan`` layout), and Hn = Y Wn
-    (the next layer's x @ weight_node, gcn_base_models.py:201).  Returns
-    (Y, winner bits, Hn)."""
-    lib = L.load()
-    H = _contig_f32(H, "H")
-    Wn = Wn.detach()
-    if Wn.dtype != torch.float32 or Wn.stride(1) != 1:
-        Wn = Wn.to(torch.float32).contiguous()
-    dev = L.require_device(H, view.rowptr, w, bias, Wn, relu_mask)
-    if H.size(0) != view.n_cols or H.size(1) != 128:
-        raise ValueError(f"spmm_max_xw_fwd: H {tuple(H.shape)} for {view.n_cols} sources, F = 128")
-    if bias is not None:
-        bias = bias.detach().to(torch.float32).contiguous()
-        if bias.numel() != 128:
-            raise ValueError(f"bias has {bias.numel()} entries, expected 128")
-    if relu_mask is not None and (relu_mask.shape != (view.n_rows, 4) or
-                                  relu_mask.dtype != torch.int32 or not relu):
-        raise ValueError(f"spmm_max_xw_fwd: relu_mask must be int32 [{view.n_rows}, 4] with relu")
-    Y = torch.empty(view.n_rows, 128, dtype=torch.float32, device=dev)
-    Hn = torch.empty(view.n_rows, 128, dtype=torch.float32, device=dev)
-    win = torch.empty(max(int(nnz), 1), 4, dtype=torch.int32, device=dev)
-    ws_bytes = int(lib.mgcn_spmm_max_xw_fwd_workspace_bytes())
-    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
-    if _TIMER is not None:
-        _TIMER("spmm_max_xw_fwd", True, view.n_rows, view.edges)
-    with L.device_guard(dev):
-        rc = lib.mgcn_spmm_max_xw_fwd(view.n_rows, view.n_cols, L.ptr(view.rowptr),
-                                      L.ptr(view.col), L.ptr(w), L.ptr(H), H.stride(0),
-                                      L.ptr(bias), int(bool(relu)), L.ptr(Y), Y.stride(0),
-                                      L.ptr(relu_mask), L.ptr(win), L.ptr(Wn), Wn.stride(0),
-                                      L.ptr(Hn), Hn.stride(0), L.ptr(ws), ws_bytes,
-                                      L.stream_of(dev))
-    if _TIMER is not None:
-        _TIMER("spmm_max_xw_fwd", False)
-    L.check(rc, "mgcn_spmm_max_xw_fwd")
-    return Y, win, Hn
-
-
-def spmm_xw_bwd_dwl_supported(F_in: int, F_out: int) -> bool:
-    """The dX-only adjoint with the lower layer's dW fused
-    (:func:`spmm_xw_bwd_dwl`): 128 x 128, bf16x6."""
-    return int(F_in) == 128 and int(F_out) == 128 and \
-        bool(L.load().mgcn_spmm_xw_bwd_full_supported(128, 128))
-
-
-def spmm_xw_bwd_dwl(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tensor | None,
-                    dY: torch.Tensor, W: torch.Tensor, Zl: torch.Tensor,
-                    relu_mask: torch.Tensor | None = None, row_div: torch.Tensor | None = None,
-                    dx_out: torch.Tensor | None = None, colsum_acc: torch.Tensor | None = None,
-                    dw_out: torch.Tensor | None = None, accumulate_dw: bool = False):
-    """Layer l's dX-only adjoint and layer l-1's weight gradient in one launch
-    (``mgcn_spmm_xw_bwd_dwl``): dX = relu'(lower) ((A^T dY [* row_scale])
-    W^T) [/ row_div] (bit for bit :func:`spmm_xw_bwd`'s dX-only form), the
-    lower layer's bias column sums (added into ``colsum_acc`` when given) and
-    dWl = Zl^T dX with Zl the lower layer's aggregate (:func:`spmm_xw_fwd`'s
-    Z) -- the reference's h^T (A^T dY_{l-1}) (gcn_base_models.py:201-241).
-    Returns (dX, colsum or None, dWl)."""
-    lib = L.load()
-    dY = _contig_f32(dY, "dY")
-    if dY.stride(0) % 4 or dY.data_ptr() % 16:
-        dY = dY.contiguous()
-    Zl = _contig_f32(Zl, "Zl")
-    if Zl.stride(0) % 4 or Zl.data_ptr() % 16:
-        Zl = Zl.contiguous()
-    W = W.detach()
-    if W.dtype != torch.float32 or W.stride(1) != 1:
-        W = W.to(torch.float32).contiguous()
-    dev = L.require_device(dY, W, Zl, view_t.rowptr, w_t, row_scale, relu_mask, row_div)
-    F_in, F_out = W.shape
-    M = view_t.n_rows
-    if not spmm_xw_bwd_dwl_supported(F_in, F_out):
-        raise ValueError(f"spmm_xw_bwd_dwl: unsupported W {tuple(W.shape)} (128 x 128, bf16x6)")
-    if dY.size(0) != view_t.n_cols or dY.size(1) != F_out or tuple(Zl.shape) != (M, F_in):
-        raise ValueError(f"spmm_xw_bwd_dwl: dY {tuple(dY.shape)}, Zl {tuple(Zl.shape)} do not fit "
-                         f"the graph ({M} sources, {view_t.n_cols} destinations)")
-    dX = dx_out if dx_out is not None else torch.empty(M, F_in, dtype=torch.float32, device=dev)
-    if (dX.dtype != torch.float32 or dX.dim() != 2 or tuple(dX.shape) != (M, F_in) or
-            dX.stride(1) != 1 or dX.stride(0) < F_in or dX.stride(0) % 4 or dX.data_ptr() % 16):
-        raise ValueError(f"spmm_xw_bwd_dwl: dx_out must be float32 [{M}, {F_in}], 16-byte rows")
-    dW = dw_out if dw_out is not None else torch.empty(F_in, F_in, dtype=torch.float32,
-                                                         device=dev)
-    if dW.dtype != torch.float32 or tuple(dW.shape) != (F_in, F_in) or dW.stride(1) != 1:
-        raise ValueError(f"spmm_xw_bwd_dwl: dw_out must be float32 [{F_in}, {F_in}]")
-    colsum = None
-    if relu_mask is not None:
-        if relu_mask.shape != (M, mask_words(F_in)) or relu_mask.dtype != torch.int32:
-            raise ValueError(f"spmm_xw_bwd_dwl: relu_mask must be int32 [{M}, {mask_words(F_in)}]")
-        relu_mask = relu_mask.contiguous()
-        if colsum_acc is not None:
-            if colsum_acc.dtype != torch.float32 or tuple(colsum_acc.shape) != (F_in,) or \
-                    not colsum_acc.is_contiguous():
-                raise ValueError(f"spmm_xw_bwd_dwl: colsum_acc must be a contiguous float32 [{F_in}]")
-            L.require_device(colsum_acc)
-            colsum = colsum_acc
-        else:
-            colsum = torch.empty(F_in, dtype=torch.float32, device=dev)
-    elif colsum_acc is not None or row_div is not None:
-        raise ValueError("spmm_xw_bwd_dwl: colsum_acc / row_div need relu_mask")
-    ws_bytes = int(lib.mgcn_spmm_xw_bwd_dwl_workspace_bytes(M))
-    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
-    if _TIMER is not None:
-        _TIMER("spmm_xw_bwd_dwl", True, view_t.n_rows, view_t.edges)
-    with L.device_guard(dev):
-        rc = lib.mgcn_spmm_xw_bwd_dwl(M, view_t.n_cols, L.ptr(view_t.rowptr), L.ptr(view_t.col),
-                                      L.ptr(w_t), L.ptr(row_scale), L.ptr(dY), dY.stride(0),
-                                      L.ptr(W), W.stride(0), L.ptr(dX), dX.stride(0),
-                                      L.ptr(relu_mask), L.ptr(row_div), L.ptr(colsum),
-                                      1 if colsum_acc is not None else 0, L.ptr(Zl), Zl.stride(0),
-                                      L.ptr(dW), dW.stride(0), 1 if accumulate_dw else 0,
-                                      L.ptr(ws), ws_bytes, L.stream_of(dev))
-    if _TIMER is not None:
-        _TIMER("spmm_xw_bwd_dwl", False)
-    L.check(rc, "mgcn_spmm_xw_bwd_dwl")
-    return dX, colsum, dW
 
 
 def spmm_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tensor | None,
@@ -1245,7 +1086,6 @@ class _GCNStack(torch.autograd.Function):
     def forward(ctx, x, plan, norm, reduce, relus, *params):
         Ws, bs = params[0::2], params[1::2]
         h = x
-        H_next = None  # the next layer's x @ W when a max layer's epilogue wrote it
         inputs, outs, args, rmasks, zs = [], [], [], [], []
         for i, (W, b, relu) in enumerate(zip(Ws, bs, relus)):
             z = None
@@ -1272,15 +1112,12 @@ class _GCNStack(torch.autograd.Function):
                 # middle layers keep the dW + dX gather kernel (_Z_MIDDLE)
                 below = i == 0 or (relus[i - 1] and rmasks[i - 1] is not None)
                 middle = 0 < i < len(Ws) - 1 and relus[i - 1]
-                dwl_next = (_DWL and nxt is not None and relu and
-                            spmm_xw_bwd_dwl_supported(*W.shape) and
-                            spmm_xw_bwd_dwl_supported(*nxt.shape))
                 top_full = (_TOP_FULL and i == len(Ws) - 1 and i > 0 and relus[i - 1] and
                             rmasks[i - 1] is not None and not relu and
                             reduce in (L.REDUCE_SUM, L.REDUCE_MEAN) and
                             plan.bwd.n_rows == plan.bwd.n_cols and xw_full_supported(*W.shape))
                 want_z = (bool(ctx.needs_input_grad[5 + 2 * i]) and below and not top_full and
-                          (_Z_MIDDLE or dwl_next or not middle or
+                          (_Z_MIDDLE or not middle or
                            not xw_full_supported(*W.shape)) and
                           dw_pass_supported(W.size(0), W.size(1)) and
                           spmm_xw_supported(plan.bwd, W.size(1), W.size(0), L.REDUCE_SUM))
@@ -1289,16 +1126,9 @@ class _GCNStack(torch.autograd.Function):
                 if want_z:
                     h, z = h
             else:
-                H = H_next if H_next is not None else _mm(h, W)
-                H_next = None
-                if (reduce == L.REDUCE_MAX and _MAX_NEXT and _FUSE_XW and nxt is not None and
-                        spmm_max_xw_supported(plan.fwd, W, nxt, H.stride(0))):
-                    # the next layer's x @ W from this layer's epilogue
-                    h, am, H_next = spmm_max_xw_fwd(plan.fwd, norm.w_fwd, H, b, relu, nxt,
-                                                    plan.nnz, relu_mask=rm)
-                else:
-                    h, am = spmm_fwd(plan.fwd, norm.w_fwd, H, reduce, b, relu, mask_plan=plan,
-                                     relu_mask=rm)
+                H = _mm(h, W)
+                h, am = spmm_fwd(plan.fwd, norm.w_fwd, H, reduce, b, relu, mask_plan=plan,
+                                 relu_mask=rm)
             outs.append(h)
             args.append(am)  # max: winner bits per edge (adjoint slot order)
             rmasks.append(rm)
@@ -1347,7 +1177,7 @@ class _GCNStack(torch.autograd.Function):
                    spmm_xw_supported(plan.bwd, Ws[top].size(0), Ws[top].size(1), L.REDUCE_SUM))
         # or from the bottom layer's dW = Z^T dY pass, which streams dZ beside
         # its own operands (mgcn_gemm_bwd_dw_cs): no separate pass over dZ
-        top_defer = (not top_z and not top_hcs and _TOP_CS_DEFER and not _DWL and top > 0 and
+        top_defer = (not top_z and not top_hcs and _TOP_CS_DEFER and top > 0 and
                      not relus[top] and rd is None and ctx.has_bias[top] and
                      ctx.needs_input_grad[5] and z_path(0) and
                      gemm_bwd_supported(*Ws[0].shape) and tuple(dZ.shape) == (zs[0].size(0), 128))
@@ -1368,18 +1198,10 @@ class _GCNStack(torch.autograd.Function):
 
         def adjoint_dx(l, dY):
             """Layer l's dX-only adjoint -> the lower layer's dY (with its ReLU
-            mask, bias gradient and mean divisor); the lower layer's dW from
-            the same launch when it takes the Z form (mgcn_spmm_xw_bwd_dwl)."""
+            mask, bias gradient and mean divisor)."""
             W = Ws[l]
-            if (_DWL and ctx.needs_input_grad[5 + 2 * (l - 1)] and z_path(l - 1) and
-                    spmm_xw_bwd_dwl_supported(*W.shape) and
-                    spmm_xw_bwd_dwl_supported(*Ws[l - 1].shape)):
-                dYn, db, gW[l - 1] = spmm_xw_bwd_dwl(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY,
-                                                     W, zs[l - 1], relu_mask=rmasks[l - 1],
-                                                     row_div=rd)
-            else:
-                _, dYn, db = spmm_xw_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, None, W,
-                                         relu_mask=rmasks[l - 1], row_div=rd)
+            _, dYn, db = spmm_xw_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, None, W,
+                                     relu_mask=rmasks[l - 1], row_div=rd)
             gb[l - 1] = db if ctx.has_bias[l - 1] else None
             return dYn
 
@@ -1409,7 +1231,7 @@ class _GCNStack(torch.autograd.Function):
                 hcs = bool(top_z and l == top and ctx.has_bias[top])
                 if gW[l] is None and top_S is not None and l == 0:
                     gW[l], gb[top] = dw_pass_cs(zs[l], dY, top_S)  # + the top bias gradient
-                elif gW[l] is None:  # (not already formed by the layer above's adjoint)
+                elif gW[l] is None:
                     gW[l], cs = dw_pass(zs[l], dY, W, dh_colsum=hcs)
                     if hcs:
                         gb[top] = cs

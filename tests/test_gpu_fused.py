@@ -543,80 +543,3 @@ def test_fused_gating_beyond_32bit_offsets(cuda):
         finally:
             ops.set_fused_layers(True)
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
-
-
-@pytest.mark.parametrize("N,E", [(20000, 200000), (4097, 40000), (33, 100), (1, 0)])
-@pytest.mark.parametrize("bias,relu", [(True, True), (False, False)])
-def test_max_layer_with_next_transform(cuda, N, E, bias, relu):
-    """mgcn_spmm_max_xw_fwd (round 5): Y, its ReLU mask words and every
-    edge's winner bits bit for bit mgcn_spmm_fwd(MAX) with a winner-bit
-    buffer; Hn = Y Wn within the fp64 |.|-bound (bf16x6 products)."""
-    from mgcn import _lib as L
-    from mgcn import ops
-    rng = np.random.default_rng(N + E + 3 * bias)
-    ei = _graph(rng, N, E)
-    plan, norm = _plan(cuda, ei, N, None)
-    g = torch.Generator(device=cuda).manual_seed(N)
-    H = torch.randn(N, 128, device=cuda, generator=g)
-    H[: N // 3] = torch.round(H[: N // 3])  # ties between edges (a later edge wins)
-    b = torch.randn(128, device=cuda, generator=g) * 0.1 if bias else None
-    Wn = torch.randn(128, 128, device=cuda, generator=g) * 0.1
-    assert ops.spmm_max_xw_supported(plan.fwd, Wn, Wn)
-    rm1 = torch.empty(N, 4, dtype=torch.int32, device=cuda) if relu else None
-    rm2 = torch.empty(N, 4, dtype=torch.int32, device=cuda) if relu else None
-    Y, win, Hn = ops.spmm_max_xw_fwd(plan.fwd, norm.w_fwd, H, b, relu, Wn, plan.nnz, relu_mask=rm1)
-    Yr, winr = ops.spmm_fwd(plan.fwd, norm.w_fwd, H, L.REDUCE_MAX, b, relu, mask_plan=plan,
-                            relu_mask=rm2)
-    assert torch.equal(Y, Yr)
-    assert torch.equal(win[:plan.nnz], winr[:plan.nnz])
-    if relu:
-        assert torch.equal(rm1, rm2)
-    ref = Y.double() @ Wn.double()
-    bound = Y.double().abs() @ Wn.double().abs()
-    assert ((Hn.double() - ref).abs() <= 1e-5 * bound + 1e-6).all()
-
-
-@pytest.mark.parametrize("eye", [True, False])
-def test_max_stack_with_fused_next_transform(cuda, eye):
-    """A 3-layer max stack (config 4's shape, smaller): the forward with each
-    max layer writing the next layer's x @ W (set_max_next(True)) against
-    GEMM + SpMM per layer (the default): W = I bit for bit, forward and
-    gradients (every bf16x6 product exact); random W: the forward within fp32
-    tolerance."""
-    from mgcn import ops
-    from mgcn.models import GCNLayer, GCNStack
-    torch.manual_seed(11)
-    rng = np.random.default_rng(29)
-    N = 6000
-    ei = _t(_graph(rng, N, 60000), cuda)
-    layers = [GCNLayer(128, 128, deg_norm=None, aggr="max", bias=True,
-                       non_linear="relu" if i < 2 else "none").to(cuda) for i in range(3)]
-    if eye:
-        with torch.no_grad():
-            for la in layers:
-                la.gcn.node_models[0].weight_node.copy_(torch.eye(128))
-    stack = GCNStack(layers)
-    x = torch.randn(N, 128, device=cuda, requires_grad=True)
-    dZ = torch.randn(N, 128, device=cuda)
-    res = []
-    for on in (True, False):
-        ops.set_max_next(on)
-        try:
-            x.grad = None
-            for p in stack.parameters():
-                p.grad = None
-            y = stack(x, ei)
-            y.backward(dZ)
-        finally:
-            ops.set_max_next(False)
-        res.append((y.detach(), x.grad.clone(), [p.grad.clone() for p in stack.parameters()]))
-    (ya, xa, ga), (yb, xb, gb) = res
-    if eye:
-        assert torch.equal(ya, yb) and torch.equal(xa, xb)
-        for a, b in zip(ga, gb):
-            torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-3)
-    else:
-        # max is continuous in H, so y stays within rounding; the argmax is
-        # not (an fp32-rounding difference in H flips near-ties), so the
-        # gradients of a random-W stack are compared only at W = I above
-        torch.testing.assert_close(ya, yb, rtol=1e-4, atol=1e-5)

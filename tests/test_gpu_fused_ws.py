@@ -1,20 +1,20 @@
 """GPU parity of the warp-specialised F = 128 adjoint (fused.hip,
-spmm_xw_bwd_ws_kernel): mgcn_spmm_xw_bwd's dX-only form (mgcn_set_option
-"xw_ws" 1; measured slower than the two-phase kernel at config 2, so off by
-default) and mgcn_spmm_xw_bwd_dwl -- the dX-only adjoint of
-layer l with layer l-1's dW = Zl^T dX in the same launch.
+spmm_xw_bwd_ws_kernel, DWS): mgcn_spmm_xw_bwd's dW + dX form (mgcn_set_option
+"xw_ws_full" 1, the default), its max adjoint and its dY column sums
+(mgcn_spmm_xw_bwd_hcs), against the two-phase kernel and the oracle; the
+dense dW passes (mgcn_gemm_bwd dW-only, mgcn_gemm_bwd_dw_cs).
 
 Reference: the adjoints of NodeModelAdditive's x @ W then gather -> * norm ->
-scatter_add (src/gcn_meta/models/gcn_base_models.py:201, 223-241); layer
-l-1's dW there is h^T (A^T dY_{l-1}) = (A h)^T dY_{l-1} = Zl^T dY_{l-1}.
+scatter_add (src/gcn_meta/models/gcn_base_models.py:201, 223-241).
 Bars:
-  * dX bit for bit the two-phase dX-only kernel's (xw_ws 0) and, at W = I,
-    the oracle adjoint's;
-  * column sums within fp32 summation-order tolerance;
-  * dWl within 4e-5 of the |.|-weighted fp64 Zl^T dX (two fp32 association
-    orders of one product), and equal to the separate dW pass's within that;
+  * dX bit for bit the two-phase kernel's and, at W = I, the oracle adjoint's;
+  * dW within the |.|-weighted fp64 bound of X^T dH (two fp32 association
+    orders of one product); column sums within fp32 summation-order tolerance;
   * empty / 1-row / ragged chunks, guard bands around every output;
-  * the GCN stack with the fused dW against the separate-pass stack.
+  * the GCN stack on DWS against the two-phase stack.
+(The dX-only warp-specialised form and DWL -- the lower layer's dW fused into
+the dX-only adjoint -- and the LDS-free / warp-specialised dW passes were
+measured slower and removed in round 6; their tests went with them.)
 """
 import numpy as np
 import pytest
@@ -47,216 +47,6 @@ def _plan(cuda, ei, N, deg_norm):
     from mgcn.graph import plan_for
     plan = plan_for(_t(ei, cuda), N)
     return plan, plan.norm(deg_norm)
-
-
-@pytest.fixture
-def xw_ws():
-    from mgcn import _lib as L
-    yield lambda v: L.set_option("xw_ws", v)
-    L.set_option("xw_ws", 0)
-
-
-@pytest.mark.parametrize("N,E,hub", GRAPHS)
-@pytest.mark.parametrize("deg_norm,epi", [("sm", "relu"), ("rw", "relu_div"), (None, "store")])
-def test_ws_dx_only_matches_two_phase_and_oracle(cuda, oracle, xw_ws, N, E, hub, deg_norm, epi):
-    from mgcn import ops
-    rng = np.random.default_rng(3 * N + E + len(epi))
-    ei = _graph(rng, N, E, hub)
-    plan, norm = _plan(cuda, ei, N, deg_norm)
-    dY = rng.standard_normal((N, F)).astype(np.float32)
-    lower = rng.standard_normal((N, F)).astype(np.float32)
-    rm = ops.make_relu_mask(_t(lower, cuda)) if epi != "store" else None
-    rd = plan.in_cnt if epi == "relu_div" else None
-    Wr = torch.randn(F, F, device=cuda, generator=torch.Generator(device=cuda).manual_seed(N)) * 0.1
-    out = {}
-    for form in (1, 0):
-        xw_ws(form)
-        for name, W in (("eye", torch.eye(F, device=cuda)), ("rand", Wr)):
-            out[form, name] = ops.spmm_xw_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd,
-                                              _t(dY, cuda), None, W, relu_mask=rm, row_div=rd)
-    for name in ("eye", "rand"):
-        assert torch.equal(out[1, name][1], out[0, name][1])
-        if rm is not None:
-            torch.testing.assert_close(out[1, name][2], out[0, name][2], rtol=1e-5, atol=1e-4)
-    # W = I: the oracle adjoint, bit for bit
-    _, wb, rs = oracle.edge_factors(ei, N, deg_norm)
-    dH, _ = oracle.aggr_bwd(ei, dY, wb, rs, "add")
-    ref = dH
-    if epi != "store":
-        ref = np.where(lower > 0, dH, 0).astype(np.float32)
-    if epi == "relu_div":
-        cnt = np.maximum(np.bincount(ei[1], minlength=N), 1).astype(np.float32)
-        ref = (ref / cnt[:, None]).astype(np.float32)
-    np.testing.assert_array_equal(out[1, "eye"][1].cpu().numpy(), ref)
-
-
-@pytest.mark.parametrize("N,E,hub", GRAPHS)
-@pytest.mark.parametrize("deg_norm,epi", [("sm", "relu"), ("rw", "relu_div"), (None, "store")])
-def test_dwl_matches_dx_only_and_dw_pass(cuda, xw_ws, N, E, hub, deg_norm, epi):
-    from mgcn import ops
-    rng = np.random.default_rng(5 * N + E + len(epi))
-    ei = _graph(rng, N, E, hub)
-    plan, norm = _plan(cuda, ei, N, deg_norm)
-    g = torch.Generator(device=cuda).manual_seed(N + 11)
-    dY = torch.randn(N, F, device=cuda, generator=g)
-    W = torch.randn(F, F, device=cuda, generator=g) * 0.1
-    Zl = torch.randn(N, F, device=cuda, generator=g)
-    rm = ops.make_relu_mask(torch.randn(N, F, device=cuda, generator=g)) if epi != "store" else None
-    rd = plan.in_cnt if epi == "relu_div" else None
-    dX, cs, dWl = ops.spmm_xw_bwd_dwl(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, W, Zl,
-                                      relu_mask=rm, row_div=rd)
-    for form in (1, 0):  # dX bit for bit both dX-only forms'
-        xw_ws(form)
-        _, dXr, csr = ops.spmm_xw_bwd(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, None, W,
-                                      relu_mask=rm, row_div=rd)
-        assert torch.equal(dX, dXr)
-        if rm is not None:
-            torch.testing.assert_close(cs, csr, rtol=1e-5, atol=1e-4)
-            if form == 1:
-                assert torch.equal(cs, csr)  # the same kernel's fold
-    ref = Zl.double().t() @ dX.double()
-    bound = Zl.double().abs().t() @ dX.double().abs()
-    assert ((dWl.double() - ref).abs() <= 4e-5 * bound + 1e-6).all()
-    dWp = ops.gemm_bwd(Zl, dX, W, want_dx=False)[0]  # the separate dense pass
-    assert ((dWl.double() - dWp.double()).abs() <= 8e-5 * bound + 1e-6).all()
-    # accumulate forms: dWl += ..., colsum += ...
-    acc_w = torch.ones(F, F, device=cuda)
-    acc_c = torch.ones(F, device=cuda) if rm is not None else None
-    ops.spmm_xw_bwd_dwl(plan.bwd, norm.w_bwd, norm.row_scale_bwd, dY, W, Zl, relu_mask=rm,
-                        row_div=rd, colsum_acc=acc_c, dw_out=acc_w, accumulate_dw=True)
-    torch.testing.assert_close(acc_w, dWl + 1, rtol=1e-6, atol=1e-5)
-    if rm is not None:
-        torch.testing.assert_close(acc_c, cs + 1, rtol=1e-6, atol=1e-5)
-
-
-SENT = 0x7FBADBAD
-BAND = 4096
-
-
-def _guarded(shape, dev, dtype=torch.float32):
-    n = int(np.prod(shape))
-    base = torch.full((BAND + n + BAND,), SENT, dtype=torch.int32, device=dev)
-    mid = base[BAND:BAND + n]
-    if dtype == torch.float32:
-        mid = mid.view(torch.float32)
-    return base, mid.view(*shape)
-
-
-def _intact(base):
-    torch.cuda.synchronize()
-    return bool((base[:BAND] == SENT).all()) and bool((base[base.numel() - BAND:] == SENT).all())
-
-
-def test_dwl_guard_bands_on_row_chunks(cuda):
-    """Row-range views (the sharded path's chunks) at 1, 15, 17, 31, 33, 190
-    rows and empty: dX / colsum / dWl / workspace bands untouched, dX rows
-    bit for bit the whole view's, dWl the chunk's own Zl^T dX."""
-    from mgcn import _lib as L
-    from mgcn import ops
-    N = 600
-    rng = np.random.default_rng(9)
-    ei = _graph(rng, N, 5000)
-    plan, norm = _plan(cuda, ei, N, "sm")
-    lib = L.load()
-    g = torch.Generator(device=cuda).manual_seed(5)
-    dY = torch.randn(N, F, device=cuda, generator=g)
-    W = torch.randn(F, F, device=cuda, generator=g) * 0.1
-    Zl = torch.randn(N, F, device=cuda, generator=g)
-    rm = ops.make_relu_mask(torch.randn(N, F, device=cuda, generator=g))
-    dXf, _, _ = ops.spmm_xw_bwd_dwl(plan.bwd, norm.w_bwd, None, dY, W, Zl, relu_mask=rm)
-    for a in (0, 5, 211):
-        for n in (1, 15, 17, 31, 33, 190, 0):
-            if a + n > N:
-                continue
-            v = plan.bwd.rows(a, a + n)
-            bx, dX = _guarded((max(n, 1), F), cuda)
-            bc, cs = _guarded((F,), cuda)
-            bw, dW = _guarded((F, F), cuda)
-            wsb = int(lib.mgcn_spmm_xw_bwd_dwl_workspace_bytes(n))
-            bws, ws = _guarded((wsb // 4,), cuda)
-            with L.device_guard(cuda):
-                rc = lib.mgcn_spmm_xw_bwd_dwl(
-                    n, v.n_cols, L.ptr(v.rowptr), L.ptr(v.col), L.ptr(norm.w_bwd), None,
-                    L.ptr(dY), F, L.ptr(W), F, L.ptr(dX), F, L.ptr(rm[a:]), None, L.ptr(cs), 0,
-                    L.ptr(Zl[a:]), F, L.ptr(dW), F, 0, L.ptr(ws), wsb, L.stream_of(cuda))
-            L.check(rc, "mgcn_spmm_xw_bwd_dwl")
-            for b in (bx, bc, bw, bws):
-                assert _intact(b), (a, n)
-            if n:
-                assert torch.equal(dX, dXf[a:a + n])
-                ref = Zl[a:a + n].double().t() @ dX.double()
-                bound = Zl[a:a + n].double().abs().t() @ dX.double().abs()
-                assert ((dW.double() - ref).abs() <= 4e-5 * bound + 1e-6).all()
-            else:
-                assert (dW == 0).all()
-
-
-@pytest.mark.parametrize("aggr,deg_norm", [("add", "sm"), ("mean", "rw")])
-def test_stack_fused_dw_vs_separate_pass(cuda, aggr, deg_norm):
-    """A 4-layer 128-wide GCN stack: the backward with every dW below the top
-    fused into the adjoint (set_fused_dwl(True)) against the separate Z^T dY
-    passes (the default): x.grad bitwise, every dW / db within tolerance;
-    both against the two-launch stack (the fused dW is off by default)."""
-    from mgcn import ops
-    from mgcn.models import GCNLayer, GCNStack
-    torch.manual_seed(3)
-    rng = np.random.default_rng(23)
-    N = 8000
-    ei = _t(_graph(rng, N, 80000), cuda)
-    stack = GCNStack([GCNLayer(F, F, deg_norm=deg_norm, aggr=aggr, bias=True,
-                               non_linear="relu" if i < 3 else "none").to(cuda) for i in range(4)])
-    x = torch.randn(N, F, device=cuda, requires_grad=True)
-    dZ = torch.randn(N, F, device=cuda)
-    res = []
-    for mode in ("dwl", "pass", "unfused"):
-        x.grad = None
-        for p in stack.parameters():
-            p.grad = None
-        ops.set_fused_dwl(mode == "dwl")
-        ops.set_fused_layers(mode != "unfused")
-        try:
-            y = stack(x, ei)
-            y.backward(dZ)
-        finally:
-            ops.set_fused_dwl(False)
-            ops.set_fused_layers(True)
-        res.append((y.detach(), x.grad.clone(), [p.grad.clone() for p in stack.parameters()]))
-    (ya, xa, ga), (yb, xb, gb), (yc, xc, gc) = res
-    assert torch.equal(ya, yb) and torch.equal(xa, xb)
-    for a, b in zip(ga, gb):
-        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-4)
-    torch.testing.assert_close(xa, xc, rtol=1e-4, atol=1e-5)
-    for a, c in zip(ga, gc):
-        torch.testing.assert_close(a, c, rtol=1e-4, atol=1e-3)
-
-
-@pytest.mark.parametrize("M", [1, 31, 33, 4097, 300000])
-@pytest.mark.parametrize("hcs", [False, True])
-def test_dw_pass_ws_bitwise_the_two_phase_kernel(cuda, M, hcs):
-    """mgcn_gemm_bwd's dW-only form on the warp-specialised kernel
-    (mgcn_set_option "dw_ws" 1; off by default, 0.234 vs 0.216 ms at config 2)
-    against gemm_bwd_kernel: the same
-    chunk-to-workgroup map, products and k-step order, so dW and dH's column
-    sums are bit for bit equal; both within the fp64 |.|-bound."""
-    from mgcn import _lib as L
-    from mgcn import ops
-    g = torch.Generator(device=cuda).manual_seed(M)
-    Z = torch.randn(M, F, device=cuda, generator=g)
-    dY = torch.randn(M, F, device=cuda, generator=g)
-    W = torch.randn(F, F, device=cuda, generator=g)
-    out = {}
-    try:
-        for form in (1, 0):
-            L.set_option("dw_ws", form)
-            out[form] = ops.gemm_bwd(Z, dY, W, want_dx=False, dh_colsum=hcs)
-    finally:
-        L.set_option("dw_ws", 0)
-    assert torch.equal(out[1][0], out[0][0])
-    if hcs:
-        assert torch.equal(out[1][2], out[0][2])
-    ref = Z.double().t() @ dY.double()
-    bound = Z.double().abs().t() @ dY.double().abs()
-    assert ((out[1][0].double() - ref).abs() <= 4e-5 * bound + 1e-6).all()
 
 
 @pytest.fixture
@@ -455,35 +245,6 @@ def test_stack_top_full_vs_z_form(cuda, monkeypatch, layers, hcs, defer, aggr, d
     assert torch.equal(ya, yb) and torch.equal(xa, xb)
     for a, b in zip(ga, gb):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-4)
-
-
-@pytest.mark.parametrize("M", [1, 31, 33, 4097, 300000])
-@pytest.mark.parametrize("hcs", [False, True])
-def test_dw_pass_direct(cuda, M, hcs):
-    """mgcn_gemm_bwd's dW-only form on the LDS-free kernel (mgcn_set_option
-    "dw_ws" 2: X and dH straight into MFMA-layout registers): dW within the
-    fp64 |.|-bound of Z^T dY and within twice it of the default kernel (a
-    different split-K); dH's column sums within fp32 summation tolerance."""
-    from mgcn import _lib as L
-    from mgcn import ops
-    g = torch.Generator(device=cuda).manual_seed(M + 7)
-    Z = torch.randn(M, F, device=cuda, generator=g)
-    dY = torch.randn(M, F, device=cuda, generator=g)
-    W = torch.randn(F, F, device=cuda, generator=g)
-    out = {}
-    try:
-        for form in (2, 0):
-            L.set_option("dw_ws", form)
-            out[form] = ops.gemm_bwd(Z, dY, W, want_dx=False, dh_colsum=hcs)
-    finally:
-        L.set_option("dw_ws", 0)
-    ref = Z.double().t() @ dY.double()
-    bound = Z.double().abs().t() @ dY.double().abs()
-    assert ((out[2][0].double() - ref).abs() <= 4e-5 * bound + 1e-6).all()
-    assert ((out[2][0].double() - out[0][0].double()).abs() <= 8e-5 * bound + 1e-6).all()
-    if hcs:
-        cb = dY.double().abs().sum(0)
-        assert ((out[2][2].double() - dY.double().sum(0)).abs() <= 1e-5 * cb + 1e-6).all()
 
 
 @pytest.mark.parametrize("N,E,hub", [(20000, 200000, 0), (3000, 20000, 700), (33, 100, 0)])
