@@ -189,6 +189,13 @@ def launch_bytes(name: str, rows: int, edges: int, F: int):
     if name.startswith("spmm_xw"):
         b = spmm_bytes(rows, edges, F)
         fl = 2.0 * rows * F * F
+        if name.endswith("_pk"):
+            # gathered from a packed table in place (mgcn.dist, round 6): per
+            # slot the row's F / 4-B header instead of its 4F B, plus its
+            # nonzero words at the nominal half density of a ReLU'd table
+            b -= edges * 4 * F
+            b += edges * (F / 4 + 2 * F)
+            name = name[:-3]
         if name == "spmm_xw_bwd":
             b += 4 * rows * F     # X rows read beside the gathered dY
             fl *= 2
@@ -207,13 +214,14 @@ def launch_bytes(name: str, rows: int, edges: int, F: int):
                 4.0 * rows * Fr * Fr)
     if name.startswith("pack_rows") or name == "unpack_rows":
         # zero-skipping exchange (mgcn.dist): a dense [rows, F] side plus the
-        # packed side at the ~half density of a ReLU'd table (4 B offset +
-        # F / 8 B of mask + ~2F B of values per row)
-        packed = 4 + F / 8 + 2 * F
+        # packed side at the ~half density of a ReLU'd table (F / 4 B of
+        # header pairs -- mask and position words -- + ~2F B of values per row)
         dense = 4 * F
-        if name == "pack_rows_count":
+        if name == "pack_rows_count":  # rows read; mask words + count written
             return rows * (dense + 4 + F / 8), 0.0
-        return rows * (dense + packed), 0.0
+        if name == "pack_rows_values":  # rows read; position words + values written
+            return rows * (dense + F / 8 + 2 * F), 0.0
+        return rows * (dense + F / 4 + 2 * F), 0.0
     if name == "input_layer_fwd":  # a, x read; Z written (the 1-wide SpMM is its own launch)
         return 8 * rows + 4 * F * rows, 0.0
     if name == "input_layer_bwd":  # dZ, Z, a, x read
@@ -229,6 +237,41 @@ def launch_bytes(name: str, rows: int, edges: int, F: int):
     if name == "relu_bwd_colsum":  # dZ read (+ Z read and dY written under ReLU): lower bound
         return 4 * F * rows, 0.0
     return 8 * F * rows, 2.0 * rows * F * F  # F x F transforms: read + write [rows, F]
+
+
+# The HIP kernel template behind each timed launch name: one template can
+# serve several launch forms (the forward with and without Z), and rocprofv3
+# reports per template, so the roofline's dominant kernel is picked per
+# template (launch-weighted over its forms).
+TEMPLATES = {"spmm_xw_fwd": "spmm_xw_fwd_kernel", "spmm_xw_fwd_z": "spmm_xw_fwd_kernel",
+             "spmm_xw_bwd": "spmm_xw_bwd_ws_kernel", "spmm_xw_bwd_dw": "spmm_xw_bwd_ws_kernel",
+             "spmm_xw_bwd_dx": "spmm_xw_bwd_kernel",
+             "spmm_xw_fwd_pk": "spmm_xw_wide_ws_kernel", "spmm_xw_fwd_z_pk": "spmm_xw_wide_ws_kernel",
+             "spmm_xw_bwd_dx_pk": "spmm_xw_wide_ws_kernel",
+             "gemm_bwd_dw_cs": "gemm_bwd_kernel", "gemm_bwd_dw": "gemm_bwd_kernel",
+             "gemm_bwd": "gemm_bwd_kernel"}
+
+
+def by_template(kern):
+    """{template: {launches, total_ms, avg_ms, bytes (per launch), gbs, forms}}
+    from the per-launch-name kernel table."""
+    out = {}
+    for name, k in kern.items():
+        t = TEMPLATES.get(name, name)
+        o = out.setdefault(t, {"launches": 0, "total_ms": 0.0, "bytes_total": 0.0, "forms": []})
+        o["launches"] += k["launches"]
+        o["total_ms"] += k["total_ms"]
+        o["forms"].append(name)
+        if k.get("bytes") is None or o["bytes_total"] is None:
+            o["bytes_total"] = None
+        else:
+            o["bytes_total"] += k["bytes"] * k["launches"]
+    for o in out.values():
+        o["avg_ms"] = o["total_ms"] / o["launches"]
+        b = o.pop("bytes_total")
+        o["bytes"] = None if b is None else b / o["launches"]
+        o["gbs"] = None if b is None else b / (o["total_ms"] * 1e-3) / 1e9
+    return out
 
 
 # ------------------------------------------------------------ main
@@ -470,19 +513,38 @@ def main():
                 continue
             kern[name] = dict(s_, bytes=bytes_ / s_["launches"], gbs=bytes_ / t / 1e9,
                               flop=flops / s_["launches"], tflops=flops / t / 1e12)
-        dom = max((k for k in kern if k.startswith("spmm")), key=lambda k: kern[k]["total_ms"])
-        a = kern[dom]["gbs"]
+        tmpl = by_template(kern)
+        dom = max((t for t in tmpl if t.startswith("spmm")), key=lambda t: tmpl[t]["total_ms"])
+        a = tmpl[dom]["gbs"]
         result["kernels"] = kern
+        result["kernel_templates"] = tmpl
         result["kernels_note"] = ("HIP events on the launch stream around every libmgcn launch, in a "
                                   "separate instrumented pass of min(K, 10) steps after the timed "
                                   "loop (per rank: rank 0's); bytes = algorithmic bytes per launch "
                                   "(bench.launch_bytes), gbs = their sum over the summed launch "
                                   "times; heavy-row launches on the side stream are not included "
                                   "(config 2 has none)")
-        traffic, src = pmc_traffic(dom, args, world)
-        result["roofline"] = {"bound": "hbm", "kernel": dom, "achieved": a, "peak": HBM_PEAK_GBS,
-                              "unit": "GB/s", "frac": a / HBM_PEAK_GBS, "traffic": traffic,
-                              "traffic_source": src}
+        # PMC traffic per launch of the template: its forms' committed
+        # measurements, weighted by their launches in this step
+        traffic, src, tot = 0.0, None, 0
+        for form in tmpl[dom]["forms"]:
+            t_, s_ = pmc_traffic(form, args, world)
+            if t_ is None:
+                traffic = None
+                break
+            traffic += t_ * kern[form]["launches"]
+            tot += kern[form]["launches"]
+            src = s_
+        if traffic is not None and tot:
+            traffic /= tot
+        result["roofline"] = {"bound": "hbm", "kernel": dom, "forms": tmpl[dom]["forms"],
+                              "achieved": a, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": a / HBM_PEAK_GBS, "traffic": traffic,
+                              "traffic_source": src,
+                              "note": "achieved = the template's algorithmic bytes per launch "
+                                      "(bench.launch_bytes, launch-weighted over its forms) / its "
+                                      "average HIP-event launch time; the dominant template by "
+                                      "GPU time, as rocprofv3 --stats reports kernels"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(ei_cpu, X, Ws[1], bs[1], n_edges)
     if rank == 0:

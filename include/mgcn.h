@@ -717,23 +717,71 @@ int mgcn_segment_mean(int64_t n_seg, int32_t F, const int64_t *ptr,
  * ReLU-masked gradients, about half +0.0 words; the reference is
  * single-device, so this replaces nothing of it -- it shrinks the exchange of
  * SURVEY.md §8(e)'s destination-range sharding).  A chunk of n rows of F
- * floats (F % 32 == 0) travels as one int32 buffer
- *   [offs: n][masks: n * F/32][vals: the rows' words that are not +0.0]
- * bit b of mask word w of a row <=> word 32 w + b is not +0.0 (bit-pattern
- * test: -0.0 / NaN travel as values); offs[i] = index in vals of row i's
- * first value.  mgcn_pack_rows_count writes the masks and per-row counts;
- * the caller forms offs (exclusive prefix sum of counts);
- * mgcn_pack_rows_values writes vals.  mgcn_unpack_rows expands n_seg such
- * segments (segment p at buf + p seg_words) into rows p n + i of T, bit for
- * bit the packed rows.
+ * floats (F % 32 == 0, W = F / 32) travels as one int32 buffer (ABI 21)
+ *   [hdr: n x W pairs (mask_w, pos_w)][vals: the rows' words that are not +0.0]
+ * bit b of mask_w of a row <=> word 32 w + b is not +0.0 (bit-pattern test:
+ * -0.0 / NaN travel as values); pos_w = index in vals of the row's first
+ * value at or after word 32 w (offs[i] + the popcounts of mask_0 .. w-1).
+ * mgcn_pack_rows_count writes the masks (hdr[2 (i W + w)]) and per-row
+ * counts; the caller forms offs (exclusive prefix sum of counts);
+ * mgcn_pack_rows_values writes vals and the positions (hdr[2 (i W + w) + 1]).
+ * mgcn_unpack_rows expands n_seg such segments (segment p at buf + p
+ * seg_words) into rows p n + i of T, bit for bit the packed rows; the fused
+ * 256-wide layer kernels also gather straight from them
+ * (mgcn_spmm_xw_fwd_packed / _bwd_packed).
  */
-int mgcn_pack_rows_count(int64_t n, int32_t F, const float *X, int64_t ldx, uint32_t *masks,
+int mgcn_pack_rows_count(int64_t n, int32_t F, const float *X, int64_t ldx, uint32_t *hdr,
                          int32_t *counts, void *stream);
 int mgcn_pack_rows_values(int64_t n, int32_t F, const float *X, int64_t ldx,
-                          const uint32_t *masks, const int32_t *offs, uint32_t *vals,
-                          void *stream);
+                          const int32_t *offs, uint32_t *hdr, uint32_t *vals, void *stream);
 int mgcn_unpack_rows(int64_t n_seg, int64_t n, int32_t F, const uint32_t *buf, int64_t seg_words,
                      float *T, int64_t ldt, void *stream);
+
+/*
+ * A packed exchange table gathered in place (ABI 21; the fused 256-wide
+ * layer kernels).  The zero-skipping exchange delivers a table of C row
+ * chunks x P ranks as C * P packed segments of `seg_rows` rows each (the
+ * layout above, segment s = c P + k at words + seg_base[s]); instead of
+ * expanding them into a dense [C P seg_rows, F] table (mgcn_unpack_rows: a
+ * write of the whole table and its re-read by the next layer), the gather
+ * reads each needed row from its segment: one 8-B header pair per lane, then
+ * the lane's nonzero words -- the bytes of the packed row only.  The view's
+ * column indices address packed rows as col = (s << row_bits) | i (row i of
+ * segment s; mgcn.dist builds these once per shard).  Results are bit for bit
+ * those of the dense table (every +0.0 the packing skipped is folded as 0.0).
+ */
+typedef struct mgcn_packed_table {
+  const uint32_t *words;   /* device: base the segment offsets count from */
+  int64_t n_words;         /* words readable at `words` (loads past it read 0) */
+  int32_t n_seg;           /* C * P segments, 1 .. 64 */
+  int32_t seg_rows;        /* rows per segment (the chunk rows) */
+  int32_t row_bits;        /* col = (s << row_bits) | i; seg_rows <= 2^row_bits */
+  int32_t F;               /* row width (256) */
+  int64_t seg_base[64];    /* word offset of segment s from `words` (host values,
+                              passed to the kernels by value; the segments may
+                              live in separate allocations of one device) */
+} mgcn_packed_table;
+
+/* mgcn_spmm_xw_fwd (F_in = F_out = 256, sum / mean) gathering X from a packed
+ * table: Y = epi((A X) W + b) (+ Z = A X, + ReLU mask words) -- bit for bit
+ * mgcn_spmm_xw_fwd on the unpacked table.  Scratch:
+ * mgcn_spmm_xw_fwd_workspace_bytes(256, 256). */
+int mgcn_spmm_xw_fwd_packed(int64_t n_rows, int32_t F_in, int32_t F_out, const int64_t *rowptr,
+                            const int32_t *col, const float *w, const mgcn_packed_table *X,
+                            const float *W, int64_t ldw, const float *bias, float *Y,
+                            int64_t ldy, int reduce, int relu, uint32_t *relu_mask, float *Z,
+                            int64_t ldz, void *workspace, size_t workspace_bytes, void *stream);
+
+/* mgcn_spmm_xw_bwd's dX-only form (F = 256) gathering dY from a packed table:
+ * dX = relu'(lower) ((A^T dY [* row_scale]) W^T) [/ row_div], colsum (+)=
+ * sum_rows dX -- bit for bit the dense-table call.  Scratch:
+ * mgcn_spmm_xw_bwd_workspace_bytes(n_rows, 256, 256). */
+int mgcn_spmm_xw_bwd_packed(int64_t n_rows, int32_t F_in, int32_t F_out, const int64_t *rowptr_t,
+                            const int32_t *col_t, const float *w_t, const float *row_scale,
+                            const mgcn_packed_table *dY, const float *W, int64_t ldw, float *dX,
+                            int64_t lddx, const uint32_t *relu_mask, const float *row_div,
+                            float *colsum, int accumulate, void *workspace,
+                            size_t workspace_bytes, void *stream);
 
 #ifdef __cplusplus
 }

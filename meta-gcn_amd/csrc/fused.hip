@@ -1765,3 +1765,91 @@ extern "C" int mgcn_debug_xw_prof(unsigned long long *host) {
 }
 #endif
 
+// ---------------------------------------------------------------- packed tables
+namespace {
+int check_packed(const mgcn_packed_table *t, const char *who) {
+  MGCN_REQUIRE(t != nullptr && t->words != nullptr, "%s: null packed table", who);
+  MGCN_REQUIRE(t->F == 256, "%s: packed tables of F = 256 only (got %d)", who, t->F);
+  MGCN_REQUIRE(t->n_seg >= 1 && t->n_seg <= 64, "%s: n_seg %d outside 1 .. 64", who, t->n_seg);
+  MGCN_REQUIRE(t->row_bits >= 0 && t->row_bits + 6 <= 31 && t->seg_rows >= 1 &&
+                   (int64_t)t->seg_rows <= ((int64_t)1 << t->row_bits),
+               "%s: seg_rows %d does not fit row_bits %d", who, t->seg_rows, t->row_bits);
+  // in-segment byte offsets stay below 2 GiB (the header plus a dense-size
+  // value area): the kernels' buffer ranges are capped there
+  MGCN_REQUIRE((uint64_t)t->seg_rows * (2 * 8 + 256) * 4u + 16u < (1ull << 31),
+               "%s: seg_rows %d too large for the 2-GiB in-segment offsets", who, t->seg_rows);
+  MGCN_REQUIRE(t->n_words >= 0, "%s: negative n_words", who);
+  return MGCN_OK;
+}
+}  // namespace
+
+extern "C" int mgcn_spmm_xw_fwd_packed(int64_t n_rows, int32_t F_in, int32_t F_out,
+                                       const int64_t *rowptr, const int32_t *col, const float *w,
+                                       const mgcn_packed_table *X, const float *W, int64_t ldw,
+                                       const float *bias, float *Y, int64_t ldy, int reduce,
+                                       int relu, uint32_t *relu_mask, float *Z, int64_t ldz,
+                                       void *workspace, size_t workspace_bytes, void *stream) {
+  clear_error();
+  if (int rc = take_device_error()) return rc;  // a previous launch failed on the device
+  MGCN_REQUIRE(n_rows >= 0, "mgcn_spmm_xw_fwd_packed: negative size");
+  MGCN_REQUIRE(F_in == 256 && F_out == 256 && mgcn_spmm_xw_supported(F_in, F_out, reduce),
+               "mgcn_spmm_xw_fwd_packed: 256 x 256, sum / mean, bf16x6 only");
+  MGCN_REQUIRE(relu_mask == nullptr || relu, "mgcn_spmm_xw_fwd_packed: relu_mask needs relu");
+  if (n_rows == 0) return MGCN_OK;
+  if (int rc = check_packed(X, "mgcn_spmm_xw_fwd_packed")) return rc;
+  MGCN_REQUIRE(rowptr && W && Y, "mgcn_spmm_xw_fwd_packed: null array");
+  MGCN_REQUIRE(ldw >= F_out && ldy >= F_out && ldy % 4 == 0 &&
+                   reinterpret_cast<uintptr_t>(Y) % 16 == 0 &&
+                   (uint64_t)16 * (uint64_t)(ldy > ldz ? ldy : ldz) * 4u < (1ull << 31),
+               "mgcn_spmm_xw_fwd_packed: Y must have 16-byte aligned rows");
+  MGCN_REQUIRE(relu_mask == nullptr || reinterpret_cast<uintptr_t>(relu_mask) % 16 == 0,
+               "mgcn_spmm_xw_fwd_packed: relu_mask not 16-byte aligned");
+  MGCN_REQUIRE(Z == nullptr || (ldz >= F_in && ldz % 4 == 0 && reinterpret_cast<uintptr_t>(Z) % 16 == 0),
+               "mgcn_spmm_xw_fwd_packed: Z must have 16-byte aligned rows (ldz >= F_in)");
+  const size_t need = mgcn_spmm_xw_fwd_workspace_bytes(F_in, F_out);
+  if (workspace == nullptr || workspace_bytes < need) {
+    set_error("mgcn_spmm_xw_fwd_packed: workspace %zu < %zu", workspace_bytes, need);
+    return MGCN_EWORKSPACE;
+  }
+  return xw_wide_fwd(n_rows, rowptr, col, w, nullptr, 0, W, ldw, bias, Y, ldy,
+                     reduce == MGCN_REDUCE_MEAN, relu != 0, relu_mask, Z, ldz, workspace,
+                     as_stream(stream), X);
+}
+
+extern "C" int mgcn_spmm_xw_bwd_packed(int64_t n_rows, int32_t F_in, int32_t F_out,
+                                       const int64_t *rowptr_t, const int32_t *col_t,
+                                       const float *w_t, const float *row_scale,
+                                       const mgcn_packed_table *dY, const float *W, int64_t ldw,
+                                       float *dX, int64_t lddx, const uint32_t *relu_mask,
+                                       const float *row_div, float *colsum, int accumulate,
+                                       void *workspace, size_t workspace_bytes, void *stream) {
+  clear_error();
+  if (int rc = take_device_error()) return rc;  // a previous launch failed on the device
+  MGCN_REQUIRE(n_rows >= 0, "mgcn_spmm_xw_bwd_packed: negative size");
+  MGCN_REQUIRE(F_in == 256 && F_out == 256 && gemm_precision_is_x6(),
+               "mgcn_spmm_xw_bwd_packed: 256 x 256, bf16x6 only");
+  MGCN_REQUIRE(row_div == nullptr || relu_mask != nullptr,
+               "mgcn_spmm_xw_bwd_packed: row_div needs relu_mask");
+  MGCN_REQUIRE(relu_mask == nullptr || colsum != nullptr,
+               "mgcn_spmm_xw_bwd_packed: relu_mask needs colsum");
+  hipStream_t s = as_stream(stream);
+  if (n_rows == 0) {  // an empty row range: no dX rows to write
+    if (colsum && !accumulate) MGCN_HIP_TRY(hipMemsetAsync(colsum, 0, sizeof(float) * F_in, s));
+    return MGCN_OK;
+  }
+  if (int rc = check_packed(dY, "mgcn_spmm_xw_bwd_packed")) return rc;
+  MGCN_REQUIRE(rowptr_t && W && dX, "mgcn_spmm_xw_bwd_packed: null array");
+  MGCN_REQUIRE(ldw >= F_out && lddx >= F_in && lddx % 4 == 0 &&
+                   reinterpret_cast<uintptr_t>(dX) % 16 == 0 &&
+                   (uint64_t)16 * (uint64_t)lddx * 4u < (1ull << 31),
+               "mgcn_spmm_xw_bwd_packed: bad W/dX (16-byte aligned dX rows)");
+  MGCN_REQUIRE(relu_mask == nullptr || reinterpret_cast<uintptr_t>(relu_mask) % 16 == 0,
+               "mgcn_spmm_xw_bwd_packed: relu_mask not 16-byte aligned");
+  const size_t need = mgcn_spmm_xw_bwd_workspace_bytes(n_rows, F_in, F_out);
+  if (workspace == nullptr || workspace_bytes < need) {
+    set_error("mgcn_spmm_xw_bwd_packed: workspace %zu < %zu", workspace_bytes, need);
+    return MGCN_EWORKSPACE;
+  }
+  return xw_wide_bwd_dx(n_rows, rowptr_t, col_t, w_t, row_scale, nullptr, 0, W, ldw, dX, lddx,
+                        relu_mask, row_div, colsum, accumulate, workspace, s, dY);
+}

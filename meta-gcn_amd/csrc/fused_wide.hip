@@ -182,6 +182,13 @@ struct WideArgs {
   int dbg;                     // wide_dbg (experiment builds only; masked by kDbgMask)
   uint32_t spin;               // warp-specialised hand-off spin bound (g_spin_limit)
   unsigned *err;               // device error word: kDevErrWide when a hand-off gave up
+  // packed table (mgcn_packed_table; the warp-specialised kernels, PK): X is
+  // then unused and col holds (segment << pk_rbits) | row
+  const uint32_t *pk;
+  int64_t pk_words;
+  int pk_nseg;
+  uint32_t pk_rbits, pk_head;
+  int64_t pk_base[64];         // segment word offsets (mgcn_packed_table.seg_base)
 };
 
 // a row's edge slots: [beg, beg + deg) (wave-uniform), and lane l's slot
@@ -321,6 +328,199 @@ __device__ __forceinline__ void wide_gather2(const float *__restrict__ X, int64_
           ab[1] = __fadd_rn(ab[1], __fmul_rn(xb[u].y, wb[u]));
           ab[2] = __fadd_rn(ab[2], __fmul_rn(xb[u].z, wb[u]));
           ab[3] = __fadd_rn(ab[3], __fmul_rn(xb[u].w, wb[u]));
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// In-place gather from a PACKED table (round 6; mgcn_packed_table, pack.hip's
+// layout).  Gathered row col = (s << rbits) | i is row i of packed segment s,
+// which starts at word base[s] of the buffer; the wave holds base[0 .. 63]
+// lane-resident (lane s: base[s], loaded once) and takes a row's base with
+// two v_readlane -- the row's whole address stays in SGPRs, as the dense
+// gather's does.  Lane l (words 4 l .. 4 l + 3 of the row) reads the pair
+// (mask_w, pos_w), w = l / 8, of the row's header (8 B), then 16 B of values
+// at pos_w + popc(mask_w below bit 4 (l % 8)) -- its own nonzero words first,
+// any excess belongs to the lanes above and is dropped -- and puts each word
+// back where its mask bit says, +0.0 elsewhere: exactly the dense row, so the
+// fold below is wide_gather2's, bit for bit.  Per row pair and U-slot batch:
+// the headers of batch k + 1 are issued under batch k's value loads.
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+struct PkView {
+  const uint32_t *words;
+  uint32_t rbits;   // col = (s << rbits) | i
+  uint32_t head;    // header words of a segment (seg_rows x 16)
+  uint32_t base_lo, base_hi;  // lane-resident: base[lane] (word offset of segment `lane`)
+  uint32_t bytes;             // lane-resident: readable bytes from that segment's start
+};
+
+// segment `lane`'s base and readable bytes (once per wave).  The range is
+// capped at 2 GiB: every in-segment offset is below that (the
+// mgcn_spmm_xw_*_packed check), so the 0xfffffff0 "no load" offset below
+// always falls outside it (a cap at 4 GiB would let it read the last bytes
+// before the cap -- unmapped memory when the buffers lie far apart)
+__device__ __forceinline__ void pk_view_init(PkView &pv, const uint32_t *words, int64_t n_words,
+                                             int n_seg, uint32_t rbits, uint32_t head,
+                                             int64_t base, int lane) {
+  pv.words = words;
+  pv.rbits = rbits;
+  pv.head = head;
+  pv.base_lo = (uint32_t)base;
+  pv.base_hi = (uint32_t)((uint64_t)base >> 32);
+  const int64_t avail = n_words - base;
+  pv.bytes = lane >= n_seg || avail <= 0 ? 0u
+             : avail >= (int64_t)0x1ffffffc ? 0x7ffffff0u : (uint32_t)avail * 4u;
+}
+
+// the range of packed row `col` (its segment) and the row's index in it; a
+// zero-byte range when !ok.  Everything here is wave-uniform (SGPRs).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t pk_rsrc(const PkView &pv, int col, bool ok,
+                                                          uint32_t &row) {
+  const uint32_t c = (uint32_t)col;
+  const int s = (int)(c >> pv.rbits);
+  row = c & ((1u << pv.rbits) - 1u);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)pv.base_lo, s);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)pv.base_hi, s);
+  const uint32_t bytes = (uint32_t)__builtin_amdgcn_readlane((int)pv.bytes, s);
+  const uint32_t *p = pv.words + (int64_t)(((uint64_t)hi << 32) | lo);
+  // (through readfirstlane, as buf_rsrc: provably uniform even where the
+  // compiler parks the parts in VGPRs -- else it wraps the load in a waterfall
+  // loop that waits for every load in flight)
+  return buf_rsrc(p, ok ? bytes : 0u);
+}
+
+__device__ __forceinline__ int64_t uniform64(int64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// the byte offset of the lane's header pair within a row header (w = lane / 8)
+__device__ __forceinline__ uint32_t pk_hoff(int lane) { return 8u * (uint32_t)(lane >> 3); }
+
+// the lane's four words of the row from its header pair and its values
+__device__ __forceinline__ float4 pk_expand(uint32_t nib, const u32x4 v) {
+  const uint32_t r2 = (nib & 1u) + ((nib >> 1) & 1u);  // values below word 2
+  const uint32_t r3 = r2 + ((nib >> 2) & 1u);          // ... below word 3
+  const uint32_t w0 = (nib & 1u) ? v[0] : 0u;
+  const uint32_t w1 = (nib & 2u) ? ((nib & 1u) ? v[1] : v[0]) : 0u;
+  const uint32_t w2 = (nib & 4u) ? (r2 == 0 ? v[0] : r2 == 1 ? v[1] : v[2]) : 0u;
+  const uint32_t w3 = (nib & 8u) ? (r3 == 0 ? v[0] : r3 == 1 ? v[1] : r3 == 2 ? v[2] : v[3]) : 0u;
+  return make_float4(__uint_as_float(w0), __uint_as_float(w1), __uint_as_float(w2),
+                     __uint_as_float(w3));
+}
+
+// the header pairs of U slots k0 .. of a row pair (slots past na / nb: a
+// zero-byte range, the pair reads 0)
+template <int U>
+__device__ __forceinline__ void pk_headers(const PkView &pv, int mca, int mcb, int k0, int na,
+                                           int nb, uint32_t hoff, u32x2 (&ha)[U],
+                                           u32x2 (&hb)[U]) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int k = (k0 + u) & 63;
+    uint32_t ia, ib;
+    const auto ra = pk_rsrc(pv, __builtin_amdgcn_readlane(mca, k), k0 + u < na, ia);
+    const auto rb = pk_rsrc(pv, __builtin_amdgcn_readlane(mcb, k), k0 + u < nb, ib);
+    ha[u] = __builtin_amdgcn_raw_buffer_load_b64(ra, 64u * ia + hoff, 0, 0);
+    hb[u] = __builtin_amdgcn_raw_buffer_load_b64(rb, 64u * ib + hoff, 0, 0);
+  }
+}
+
+// ha / hb hold, on entry, the header pairs of the first U slots of (ma, mb)
+// -- issued by the caller for the first pair, by the previous call for the
+// others -- and, on return, those of the next pair (na, nb), issued under this
+// pair's last value loads: a row pair then costs the dense gather's round
+// trips (one per batch), not one more for its first headers
+template <int U>
+__device__ __forceinline__ void wide_gather2_pk(const PkView &pv, const int32_t *__restrict__ col,
+                                                const float *__restrict__ w, const WRow &ma,
+                                                const WRow &mb, const WRow &na_, const WRow &nb_,
+                                                int lane, float (&aa)[4], float (&ab)[4],
+                                                u32x2 (&ha)[U], u32x2 (&hb)[U]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) aa[j] = ab[j] = 0.0f;
+  int mca = ma.mc, mcb = mb.mc;
+  float mwa = ma.mw, mwb = mb.mw;
+  // (row degrees are wave-uniform: in SGPRs, the batch branches are scalar)
+  const int64_t da = uniform64(ma.deg), db = uniform64(mb.deg);
+  const int64_t dm = da > db ? da : db;
+  const uint32_t hoff = pk_hoff(lane);
+  const uint32_t sh = 4u * (uint32_t)(lane & 7);  // the lane's nibble in mask_w
+  const uint32_t below = (1u << sh) - 1u;
+  const int64_t dna = uniform64(na_.deg), dnb = uniform64(nb_.deg);
+  const int nxa = (int)(dna < 64 ? dna : 64), nxb = (int)(dnb < 64 ? dnb : 64);
+  // (an empty pair still runs one all-masked batch: the next pair's headers
+  // are then issued from the one call site below -- two call sites let the
+  // compiler merge their operands into VGPR phis and wrap the loads in
+  // waterfall loops)
+  const int64_t dm1 = dm > 0 ? dm : 1;
+  for (int64_t e0 = 0; e0 < dm1; e0 += 64) {
+    const int na = (int)(da - e0 <= 0 ? 0 : da - e0 < 64 ? da - e0 : 64);  // wave-uniform
+    const int nb = (int)(db - e0 <= 0 ? 0 : db - e0 < 64 ? db - e0 : 64);
+    const int nm = na > nb ? na : nb;
+    const int nm1 = nm > 0 ? nm : 1;
+    if (e0 > 0) {  // rows longer than one metadata batch load the rest in place
+      mca = mcb = 0;
+      mwa = mwb = 1.0f;
+      if (e0 + lane < da) {
+        mca = col[ma.beg + e0 + lane];
+        if (w != nullptr) mwa = w[ma.beg + e0 + lane];
+      }
+      if (e0 + lane < db) {
+        mcb = col[mb.beg + e0 + lane];
+        if (w != nullptr) mwb = w[mb.beg + e0 + lane];
+      }
+      pk_headers<U>(pv, mca, mcb, 0, na, nb, hoff, ha, hb);
+    }
+    const bool last_window = e0 + 64 >= dm1;
+    for (int k0 = 0; k0 < nm1; k0 += U) {
+      u32x4 va[U], vb[U];
+      uint32_t nia[U], nib_b[U];
+      float wa[U], wb[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = (k0 + u) & 63;
+        wa[u] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mwa), k));
+        wb[u] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mwb), k));
+        uint32_t ia, ib;
+        const auto ra = pk_rsrc(pv, __builtin_amdgcn_readlane(mca, k), k0 + u < na, ia);
+        const auto rb = pk_rsrc(pv, __builtin_amdgcn_readlane(mcb, k), k0 + u < nb, ib);
+        nia[u] = (ha[u][0] >> sh) & 0xfu;
+        nib_b[u] = (hb[u][0] >> sh) & 0xfu;
+        const uint32_t qa = ha[u][1] + (uint32_t)__builtin_popcount(ha[u][0] & below);
+        const uint32_t qb = hb[u][1] + (uint32_t)__builtin_popcount(hb[u][0] & below);
+        // a lane with no nonzero word moves no bytes (offset past the range)
+        va[u] = __builtin_amdgcn_raw_buffer_load_b128(ra, nia[u] ? 4u * (pv.head + qa) : 0xfffffff0u, 0, 0);
+        vb[u] = __builtin_amdgcn_raw_buffer_load_b128(rb, nib_b[u] ? 4u * (pv.head + qb) : 0xfffffff0u, 0, 0);
+      }
+      // the next headers, under these values: this window's next batch, or
+      // (the last batch of the last window) the next pair's first -- one call
+      // site, its inputs selected
+      const bool more = k0 + U < nm;
+      if (more || last_window) {
+        const int sa = more ? mca : na_.mc, sb = more ? mcb : nb_.mc;
+        pk_headers<U>(pv, sa, sb, more ? k0 + U : 0, more ? na : nxa, more ? nb : nxb, hoff, ha,
+                      hb);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (k0 + u < na) {  // wave-uniform: strictly ascending edge order per row
+          const float4 x = pk_expand(nia[u], va[u]);
+          aa[0] = __fadd_rn(aa[0], __fmul_rn(x.x, wa[u]));
+          aa[1] = __fadd_rn(aa[1], __fmul_rn(x.y, wa[u]));
+          aa[2] = __fadd_rn(aa[2], __fmul_rn(x.z, wa[u]));
+          aa[3] = __fadd_rn(aa[3], __fmul_rn(x.w, wa[u]));
+        }
+        if (k0 + u < nb) {
+          const float4 x = pk_expand(nib_b[u], vb[u]);
+          ab[0] = __fadd_rn(ab[0], __fmul_rn(x.x, wb[u]));
+          ab[1] = __fadd_rn(ab[1], __fmul_rn(x.y, wb[u]));
+          ab[2] = __fadd_rn(ab[2], __fmul_rn(x.z, wb[u]));
+          ab[3] = __fadd_rn(ab[3], __fmul_rn(x.w, wb[u]));
         }
       }
     }
@@ -660,7 +860,7 @@ __device__ __forceinline__ int lds_signal(int *p, int v, int lane) {
   return __builtin_amdgcn_readfirstlane(old);
 }
 
-template <int U, bool BWD, int EPI, int NM>
+template <int U, bool BWD, int EPI, int NM, bool PK>
 __global__ __launch_bounds__(kSThreads) void spmm_xw_wide_ws_kernel(const WideArgs a) {
   // NM MFMA waves (4 or 8), 16 - NM gather waves; MFMA wave m owns the NT
   // n-tiles NT m .. NT m + NT - 1 (16 NT output columns)
@@ -695,6 +895,9 @@ __global__ __launch_bounds__(kSThreads) void spmm_xw_wide_ws_kernel(const WideAr
   if (wave < NG) {
     // ------------------------------- gather waves ---------------------------
     if (a.dbg & kDbgMask & 8) __builtin_amdgcn_s_setprio(2);
+    PkView pv{};
+    if constexpr (PK)
+      pk_view_init(pv, a.pk, a.pk_words, a.pk_nseg, a.pk_rbits, a.pk_head, a.pk_base[lane], lane);
     const int64_t n_pairs = 16 * n_my;
     auto pair_row = [&](int64_t p) { return chunk_of(p >> 4) * kSRows + 2 * (p & 15); };
     WRow cur, cur2, nxt, nxt2;
@@ -709,6 +912,14 @@ __global__ __launch_bounds__(kSThreads) void spmm_xw_wide_ws_kernel(const WideAr
       wrow_ptr(a.rowptr, rq, q < n_pairs && rq < a.n_rows, nxt);
       wrow_ptr(a.rowptr, rq + 1, q < n_pairs && rq + 1 < a.n_rows, nxt2);
     }
+    // PK: the header pairs of the current pair's first U slots (carried from
+    // pair to pair by wide_gather2_pk)
+    u32x2 pha[PK ? U : 1], phb[PK ? U : 1];
+    if constexpr (PK) {
+      const int64_t d0 = uniform64(cur.deg), d1 = uniform64(cur2.deg);
+      pk_headers<U>(pv, cur.mc, cur2.mc, 0, (int)(d0 < 64 ? d0 : 64), (int)(d1 < 64 ? d1 : 64),
+                    pk_hoff(lane), pha, phb);
+    }
     for (int64_t p = wave; p < n_pairs; p += NG) {
       wrow_first(a.col, a.w, lane, nxt);
       wrow_first(a.col, a.w, lane, nxt2);
@@ -721,7 +932,10 @@ __global__ __launch_bounds__(kSThreads) void spmm_xw_wide_ws_kernel(const WideAr
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[0][j] = acc[1][j] = 0.0f;
       } else {
-        wide_gather2<U>(a.X, a.ldx, a.col, a.w, cur, cur2, lane, acc[0], acc[1]);
+        if constexpr (PK)
+          wide_gather2_pk<U>(pv, a.col, a.w, cur, cur2, nxt, nxt2, lane, acc[0], acc[1], pha, phb);
+        else
+          wide_gather2<U>(a.X, a.ldx, a.col, a.w, cur, cur2, lane, acc[0], acc[1]);
       }
       const int64_t i = p >> 4;
       const int b = (int)(i % kSBufs);
@@ -946,21 +1160,27 @@ __global__ __launch_bounds__(kSThreads) void spmm_xw_wide_ws_kernel(const WideAr
   }
 }
 
-template <int U, int NM>
-int launch_wide_ws_un(const WideArgs &a, bool bwd, int epi, int grid, hipStream_t s) {
+template <int U, int NM, bool PK>
+int launch_wide_ws_unp(const WideArgs &a, bool bwd, int epi, int grid, hipStream_t s) {
   if (!bwd)
-    hipLaunchKernelGGL((spmm_xw_wide_ws_kernel<U, false, WEPI_STORE, NM>), dim3(grid),
+    hipLaunchKernelGGL((spmm_xw_wide_ws_kernel<U, false, WEPI_STORE, NM, PK>), dim3(grid),
                        dim3(kSThreads), 0, s, a);
   else if (epi == WEPI_RELU_DIV)
-    hipLaunchKernelGGL((spmm_xw_wide_ws_kernel<U, true, WEPI_RELU_DIV, NM>), dim3(grid),
+    hipLaunchKernelGGL((spmm_xw_wide_ws_kernel<U, true, WEPI_RELU_DIV, NM, PK>), dim3(grid),
                        dim3(kSThreads), 0, s, a);
   else if (epi == WEPI_RELU)
-    hipLaunchKernelGGL((spmm_xw_wide_ws_kernel<U, true, WEPI_RELU, NM>), dim3(grid),
+    hipLaunchKernelGGL((spmm_xw_wide_ws_kernel<U, true, WEPI_RELU, NM, PK>), dim3(grid),
                        dim3(kSThreads), 0, s, a);
   else
-    hipLaunchKernelGGL((spmm_xw_wide_ws_kernel<U, true, WEPI_STORE, NM>), dim3(grid),
+    hipLaunchKernelGGL((spmm_xw_wide_ws_kernel<U, true, WEPI_STORE, NM, PK>), dim3(grid),
                        dim3(kSThreads), 0, s, a);
   return check_launch("spmm_xw_wide_ws_kernel");
+}
+
+template <int U, int NM>
+int launch_wide_ws_un(const WideArgs &a, bool bwd, int epi, int grid, hipStream_t s) {
+  return a.pk != nullptr ? launch_wide_ws_unp<U, NM, true>(a, bwd, epi, grid, s)
+                         : launch_wide_ws_unp<U, NM, false>(a, bwd, epi, grid, s);
 }
 
 template <int U>
@@ -998,7 +1218,7 @@ int launch_wide_legacy(const WideArgs &a, bool bwd, int epi, int grid, hipStream
 
 // *grid: the workgroups launched (= the column-sum partials written)
 int launch_wide(const WideArgs &a, bool bwd, int epi, int *grid, hipStream_t s) {
-  if (g_wide_ws & (bwd ? 2 : 1)) {
+  if (a.pk != nullptr || (g_wide_ws & (bwd ? 2 : 1))) {  // (packed tables: this form only)
     const int64_t n_chunks = (a.n_rows + kSRows - 1) / kSRows;
     const int64_t cus = wide_grid() / 2;  // one workgroup per CU
     *grid = (int)(cus < n_chunks ? cus : n_chunks);
@@ -1023,6 +1243,20 @@ int launch_wimg(const float *W, int64_t ldw, bool trans, u32x4 *img, hipStream_t
 
 }  // namespace
 
+namespace {
+void set_packed(WideArgs &a, const mgcn_packed_table *pk) {
+  if (pk == nullptr) return;
+  a.X = nullptr;
+  a.ldx = 0;
+  a.pk = pk->words;
+  a.pk_words = pk->n_words;
+  for (int i = 0; i < 64; ++i) a.pk_base[i] = i < pk->n_seg ? pk->seg_base[i] : 0;
+  a.pk_nseg = pk->n_seg;
+  a.pk_rbits = (uint32_t)pk->row_bits;
+  a.pk_head = (uint32_t)pk->seg_rows * 2u * (kWF / 32);
+}
+}  // namespace
+
 size_t xw_wide_workspace_bytes(bool bwd) {
   return align_up((size_t)kWImgFrags * 16, 256) +
          (bwd ? align_up((size_t)wide_grid() * kWF * 4, 256) : 0);
@@ -1031,7 +1265,7 @@ size_t xw_wide_workspace_bytes(bool bwd) {
 int xw_wide_fwd(int64_t n_rows, const int64_t *rowptr, const int32_t *col, const float *w,
                 const float *X, int64_t ldx, const float *W, int64_t ldw, const float *bias,
                 float *Y, int64_t ldy, int mean, int relu, uint32_t *relu_mask, float *Z,
-                int64_t ldz, void *workspace, hipStream_t s) {
+                int64_t ldz, void *workspace, hipStream_t s, const mgcn_packed_table *pk) {
   u32x4 *img = static_cast<u32x4 *>(workspace);
   if (int rc = launch_wimg(W, ldw, false, img, s)) return rc;
   WideArgs a{};
@@ -1054,6 +1288,7 @@ int xw_wide_fwd(int64_t n_rows, const int64_t *rowptr, const int32_t *col, const
   a.spin = g_spin_limit;
   a.err = device_error_word();
   if (a.err == nullptr) return MGCN_EHIP;
+  set_packed(a, pk);
   int grid = 0;
   return launch_wide(a, false, WEPI_STORE, &grid, s);
 }
@@ -1062,7 +1297,7 @@ int xw_wide_bwd_dx(int64_t n_rows, const int64_t *rowptr_t, const int32_t *col_t
                    const float *w_t, const float *row_scale, const float *dY, int64_t lddy,
                    const float *W, int64_t ldw, float *dX, int64_t lddx,
                    const uint32_t *relu_mask, const float *row_div, float *colsum,
-                   int accumulate, void *workspace, hipStream_t s) {
+                   int accumulate, void *workspace, hipStream_t s, const mgcn_packed_table *pk) {
   u32x4 *img = static_cast<u32x4 *>(workspace);
   float *partial = reinterpret_cast<float *>(static_cast<char *>(workspace) +
                                              align_up((size_t)kWImgFrags * 16, 256));
@@ -1087,6 +1322,7 @@ int xw_wide_bwd_dx(int64_t n_rows, const int64_t *rowptr_t, const int32_t *col_t
   a.spin = g_spin_limit;
   a.err = device_error_word();
   if (a.err == nullptr) return MGCN_EHIP;
+  set_packed(a, pk);
   int grid = 0;
   int rc = launch_wide(a, true, epi, &grid, s);
   if (rc || epi == WEPI_STORE) return rc;

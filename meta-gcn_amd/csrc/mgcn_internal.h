@@ -189,12 +189,14 @@ size_t xw_wide_workspace_bytes(bool bwd);
 int xw_wide_fwd(int64_t n_rows, const int64_t *rowptr, const int32_t *col, const float *w,
                 const float *X, int64_t ldx, const float *W, int64_t ldw, const float *bias,
                 float *Y, int64_t ldy, int mean, int relu, uint32_t *relu_mask, float *Z,
-                int64_t ldz, void *workspace, hipStream_t s);
+                int64_t ldz, void *workspace, hipStream_t s,
+                const mgcn_packed_table *pk = nullptr);
 int xw_wide_bwd_dx(int64_t n_rows, const int64_t *rowptr_t, const int32_t *col_t,
                    const float *w_t, const float *row_scale, const float *dY, int64_t lddy,
                    const float *W, int64_t ldw, float *dX, int64_t lddx,
                    const uint32_t *relu_mask, const float *row_div, float *colsum,
-                   int accumulate, void *workspace, hipStream_t s);
+                   int accumulate, void *workspace, hipStream_t s,
+                   const mgcn_packed_table *pk = nullptr);
 int wide_set_option(const char *name, int value);  // "wide_pair" / "wide_unroll" / "wide_ws"
 
 }  // namespace mgcn

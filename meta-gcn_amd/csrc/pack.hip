@@ -1,14 +1,19 @@
 // Zero-skipping row packing for the sharded path's table exchange
 // (mgcn.dist): the tables the ranks all-gather between
 // layers are ReLU outputs (forward) or gradients masked by the same ReLU
-// (backward), about half exact zeros.  A chunk of rows travels as
+// (backward), about half exact zeros.  A chunk of n rows travels as
 //
-//   [offs: n int32][masks: n x F/32 uint32][vals: the nonzero words, row-major]
+//   [hdr: n x W pairs (mask_w, pos_w) uint32][vals: the nonzero words, row-major]
 //
-// bit b of mask word w of a row <=> word 32 w + b of the row is not +0.0 (a
-// BIT-PATTERN test: -0.0, NaN and denormals travel as values, so unpacking
-// restores every row bit for bit); offs[i] = the index in vals of row i's
-// first value (exclusive prefix sum of the rows' popcounts).
+// with W = F / 32.  Bit b of mask_w of a row <=> word 32 w + b of the row is
+// not +0.0 (a BIT-PATTERN test: -0.0, NaN and denormals travel as values, so
+// every row comes back bit for bit); pos_w = the index in vals of the row's
+// first value at or after word 32 w (the row's offset -- exclusive prefix sum
+// of the rows' popcounts -- plus the popcounts of its words below w).  The
+// pairs make the packed rows GATHERABLE in place (round 6): the lane that
+// holds words 4 j .. 4 j + 3 of a row reads one 8-B pair (w = j / 8) and
+// finds its values at pos_w + popc(mask_w below bit 4 (j % 8)) -- no scan over
+// the row (fused_wide.hip, spmm_xw_wide_ws_kernel<.., PK>).
 //
 // Layout of the work: a row is cut into segments of 256 words; a group of
 // G = min(64, F/4) lanes (a power of two) takes one segment, lane gl words
@@ -19,7 +24,7 @@
 // plus those of its own lane's lower words.  Mask word w of a segment is
 // lanes 8 w .. 8 w + 7's nibbles, interleaved out of the four ballots.
 // HBM-bound: pack reads the chunk once per kernel (4 F bytes per row) and
-// writes 4 + F/8 (+ 4 nnz); unpack reads 4 + F/8 + 4 nnz and writes 4 F.
+// writes F/4 (+ 4 nnz); unpack reads F/4 + 4 nnz and writes 4 F.
 
 #include "mgcn_internal.h"
 
@@ -81,7 +86,7 @@ template <int G>
 __global__ __launch_bounds__(64 * kPkWaves) void pack_count_kernel(int64_t n, int F,
                                                                    const float *__restrict__ X,
                                                                    int64_t ldx,
-                                                                   uint32_t *__restrict__ masks,
+                                                                   uint32_t *__restrict__ hdr,
                                                                    int32_t *__restrict__ counts) {
   const PkLane<G> p = pk_lane<G>();
   constexpr int RPW = 64 / G;  // rows per wave
@@ -103,7 +108,7 @@ __global__ __launch_bounds__(64 * kPkWaves) void pack_count_kernel(int64_t n, in
       seg_bits<G>(p, ok, v, nz, b);
       cnt += __popcll(b[0]) + __popcll(b[1]) + __popcll(b[2]) + __popcll(b[3]);
       const int w0 = f0 >> 5;
-      if (rok && p.gl < G / 8 && w0 + p.gl < words) masks[r * words + w0 + p.gl] = seg_word(b, p.gl);
+      if (rok && p.gl < G / 8 && w0 + p.gl < words) hdr[2 * (r * words + w0 + p.gl)] = seg_word(b, p.gl);
     }
     if (rok && p.gl == 0) counts[r] = cnt;
   }
@@ -112,10 +117,11 @@ __global__ __launch_bounds__(64 * kPkWaves) void pack_count_kernel(int64_t n, in
 template <int G>
 __global__ __launch_bounds__(64 * kPkWaves) void pack_values_kernel(
     int64_t n, int F, const float *__restrict__ X, int64_t ldx, const int32_t *__restrict__ offs,
-    uint32_t *__restrict__ vals) {
+    uint32_t *__restrict__ hdr, uint32_t *__restrict__ vals) {
   const PkLane<G> p = pk_lane<G>();
   constexpr int RPW = 64 / G;
   const int64_t stride = (int64_t)gridDim.x * kPkWaves * RPW;
+  const int words = F >> 5;
   for (int64_t r = ((int64_t)blockIdx.x * kPkWaves + (threadIdx.x >> 6)) * RPW + p.grp; r < n + p.grp;
        r += stride) {
     const bool rok = r < n;
@@ -131,6 +137,8 @@ __global__ __launch_bounds__(64 * kPkWaves) void pack_values_kernel(
       const uint64_t lo = p.below >> (p.grp * G);
       int64_t q = pos + __popcll(b[0] & lo) + __popcll(b[1] & lo) + __popcll(b[2] & lo) +
                   __popcll(b[3] & lo);
+      // the first lane of each mask word's 8 writes the word's value position
+      if (ok && (p.gl & 7) == 0) hdr[2 * (r * words + (f >> 5)) + 1] = (uint32_t)q;
       if (nz[0]) vals[q++] = v.x;
       if (nz[1]) vals[q++] = v.y;
       if (nz[2]) vals[q++] = v.z;
@@ -162,8 +170,8 @@ __global__ __launch_bounds__(64 * kPkWaves) void unpack_kernel(int64_t n_seg, in
     const int64_t sg = rok ? kk / n : 0, i = rok ? kk - sg * n : 0;
     const uint32_t *seg = buf + sg * seg_words;
     const int f = 4 * p.gl;
-    pos = rok ? reinterpret_cast<const int32_t *>(seg)[i] : 0;
-    nib = (rok && f < F) ? (seg[n + i * words + (f >> 5)] >> (f & 31)) & 0xfu : 0u;
+    pos = rok ? (int64_t)seg[2 * i * words + 1] : 0;  // pos_0: the row's offset
+    nib = (rok && f < F) ? (seg[2 * (i * words + (f >> 5))] >> (f & 31)) & 0xfu : 0u;
   };
   int64_t k = ((int64_t)blockIdx.x * kPkWaves + (threadIdx.x >> 6)) * RPW + p.grp;
   int64_t pos_n;
@@ -176,14 +184,14 @@ __global__ __launch_bounds__(64 * kPkWaves) void unpack_kernel(int64_t n_seg, in
     header(k + stride, pos_n, nib_n);  // the next row's header, under this row's values
     const int64_t sg = rok ? k / n : 0, i = rok ? k - sg * n : 0;
     const uint32_t *seg = buf + sg * seg_words;
-    const uint32_t *mk = seg + n + i * words;
-    const uint32_t *vals = seg + n + n * words;
+    const uint32_t *hd = seg + 2 * i * words;
+    const uint32_t *vals = seg + 2 * n * words;
     uint32_t *t = reinterpret_cast<uint32_t *>(T + (rok ? k : 0) * ldt);
     for (int f0 = 0; f0 < F; f0 += 4 * G) {
       const int f = f0 + 4 * p.gl;
       const bool ok = rok && f < F;
       // this lane's nibble of its mask word: word f >> 5, bits (f & 31) .. + 3
-      const uint32_t nib = f0 == 0 ? nib0 : ok ? (mk[f >> 5] >> (f & 31)) & 0xfu : 0u;
+      const uint32_t nib = f0 == 0 ? nib0 : ok ? (hd[2 * (f >> 5)] >> (f & 31)) & 0xfu : 0u;
       bool nz[4] = {(nib & 1u) != 0, (nib & 2u) != 0, (nib & 4u) != 0, (nib & 8u) != 0};
       uint64_t b[4];
 #pragma unroll
@@ -226,32 +234,32 @@ using namespace mgcn;
   }
 
 extern "C" int mgcn_pack_rows_count(int64_t n, int32_t F, const float *X, int64_t ldx,
-                                    uint32_t *masks, int32_t *counts, void *stream) {
+                                    uint32_t *hdr, int32_t *counts, void *stream) {
   clear_error();
   MGCN_REQUIRE(n >= 0 && F > 0 && F % 32 == 0 && ldx >= F,
                "mgcn_pack_rows_count: need n >= 0, F a multiple of 32, ldx >= F");
   if (n == 0) return MGCN_OK;
-  MGCN_REQUIRE(X && masks && counts, "mgcn_pack_rows_count: null array");
+  MGCN_REQUIRE(X && hdr && counts, "mgcn_pack_rows_count: null array");
   MGCN_REQUIRE(pk_aligned(X, ldx), "mgcn_pack_rows_count: rows must be 16-byte aligned");
   const int G = pk_group(F);
   PK_DISPATCH(G, pack_count_kernel, dim3(pk_grid(n, G)), dim3(64 * kPkWaves), 0,
-              as_stream(stream), n, (int)F, X, ldx, masks, counts);
+              as_stream(stream), n, (int)F, X, ldx, hdr, counts);
   return check_launch("pack_count_kernel");
 }
 
 extern "C" int mgcn_pack_rows_values(int64_t n, int32_t F, const float *X, int64_t ldx,
-                                     const uint32_t *masks, const int32_t *offs, uint32_t *vals,
+                                     const int32_t *offs, uint32_t *hdr, uint32_t *vals,
                                      void *stream) {
   clear_error();
   MGCN_REQUIRE(n >= 0 && F > 0 && F % 32 == 0 && ldx >= F,
                "mgcn_pack_rows_values: need n >= 0, F a multiple of 32, ldx >= F");
   if (n == 0) return MGCN_OK;
-  MGCN_REQUIRE(X && masks && offs && vals, "mgcn_pack_rows_values: null array");
+  MGCN_REQUIRE(X && hdr && offs && vals, "mgcn_pack_rows_values: null array");
   MGCN_REQUIRE(pk_aligned(X, ldx), "mgcn_pack_rows_values: rows must be 16-byte aligned");
   // the masks are recomputed from the rows (the same bits pack_count wrote)
   const int G = pk_group(F);
   PK_DISPATCH(G, pack_values_kernel, dim3(pk_grid(n, G)), dim3(64 * kPkWaves), 0,
-              as_stream(stream), n, (int)F, X, ldx, offs, vals);
+              as_stream(stream), n, (int)F, X, ldx, offs, hdr, vals);
   return check_launch("pack_values_kernel");
 }
 
@@ -263,7 +271,7 @@ extern "C" int mgcn_unpack_rows(int64_t n_seg, int64_t n, int32_t F, const uint3
   if (n_seg == 0 || n == 0) return MGCN_OK;
   MGCN_REQUIRE(buf && T, "mgcn_unpack_rows: null array");
   MGCN_REQUIRE(pk_aligned(T, ldt), "mgcn_unpack_rows: T rows must be 16-byte aligned");
-  MGCN_REQUIRE(seg_words >= n * (1 + F / 32), "mgcn_unpack_rows: segment of %lld words < header",
+  MGCN_REQUIRE(seg_words >= n * 2 * (F / 32), "mgcn_unpack_rows: segment of %lld words < header",
                (long long)seg_words);
   const int G = pk_group(F);
   PK_DISPATCH(G, unpack_kernel, dim3(pk_grid(n_seg * n, G)), dim3(64 * kPkWaves), 0,

@@ -114,11 +114,25 @@ SIGNATURES = {
     "mgcn_pack_rows_count": (_int, [_i64, _i32, _vp, _i64, _vp, _vp, _vp]),
     "mgcn_pack_rows_values": (_int, [_i64, _i32, _vp, _i64, _vp, _vp, _vp, _vp]),
     "mgcn_unpack_rows": (_int, [_i64, _i64, _i32, _vp, _i64, _vp, _i64, _vp]),
+    "mgcn_spmm_xw_fwd_packed": (_int, [_i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp,
+                                       _i64, _int, _int, _vp, _vp, _i64, _vp, _sz, _vp]),
+    "mgcn_spmm_xw_bwd_packed": (_int, [_i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp,
+                                       _i64, _vp, _vp, _vp, _int, _vp, _sz, _vp]),
     "mgcn_residual_layer_bwd_workspace_bytes": (_sz, [_i64, _i32]),
     "mgcn_residual_layer_bwd": (_int, [_i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp,
                                        _int, _int, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp,
                                        _vp, _i64, _i64, _vp, _sz, _vp]),
 }
+
+class PackedTableC(ctypes.Structure):
+    """include/mgcn.h mgcn_packed_table."""
+    _fields_ = [("words", ctypes.c_void_p), ("n_words", ctypes.c_int64),
+                ("n_seg", ctypes.c_int32), ("seg_rows", ctypes.c_int32),
+                ("row_bits", ctypes.c_int32), ("F", ctypes.c_int32),
+                ("seg_base", ctypes.c_int64 * 64)]
+
+
+byref = ctypes.byref
 
 _lock = threading.Lock()
 _lib = None

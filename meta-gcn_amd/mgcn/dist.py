@@ -107,13 +107,18 @@ class HipBackend:
         from .ops import mask_words
         return mask_words(F)
 
-    def pack_count(self, rows, masks, counts):
+    def pack_count(self, rows, hdr, counts):
         from .ops import pack_rows_count
-        pack_rows_count(rows, masks, counts)
+        pack_rows_count(rows, hdr, counts)
 
-    def pack_values(self, rows, masks, offs, vals):
+    def pack_values(self, rows, offs, hdr, vals):
         from .ops import pack_rows_values
-        pack_rows_values(rows, masks, offs, vals)
+        pack_rows_values(rows, offs, hdr, vals)
+
+    def packed_gather_ok(self, F):
+        """The fused layer kernels of width F gather packed tables in place
+        (mgcn_spmm_xw_fwd_packed / _bwd_packed: F = 256)."""
+        return F == 256
 
     def unpack(self, buf, n_seg, n, seg_words, out):
         from .ops import unpack_rows
@@ -188,6 +193,31 @@ class Shard:
     # sharded step timed on one GPU (scripts/config5_rank.py)
     emulated: bool = False
     _tables: dict = None
+    _pk_views: tuple = None
+
+    def packed_views(self):
+        """(fwd, bwd, row_bits): the two views with their columns as packed
+        positions (segment << row_bits) | row -- the addresses of the
+        in-place gather from a :class:`mgcn.ops.PackedTable` (built once)."""
+        if self._pk_views is None:
+            from .ops import packed_cols, packed_row_bits
+            rb = packed_row_bits(self.chunk_rows)
+            views = []
+            for v in (self.fwd, self.bwd):
+                views.append(CSRView(rowptr=v.rowptr, col=packed_cols(v.col, self.chunk_rows, rb),
+                                     eid=v.eid, n_rows=v.n_rows, n_cols=v.n_cols,
+                                     n_edges=v.n_edges))
+            self._pk_views = (views[0], views[1], rb)
+        return self._pk_views
+
+    def view_for(self, table, which: str, a: int, e: int, n_edges: int):
+        """Rows [a, e) of the fwd / bwd view addressing `table` (dense or packed)."""
+        if isinstance(table, torch.Tensor):
+            v = self.fwd if which == "fwd" else self.bwd
+        else:
+            f, b, _ = self.packed_views()
+            v = f if which == "fwd" else b
+        return v.rows(a, e, n_edges)
 
     @property
     def rows(self) -> int:
@@ -302,7 +332,7 @@ def _size_stream(dev):
 
 
 def _wait(works):
-    for w in works:
+    for w in works or ():
         if w is not None:
             w.wait()
 
@@ -316,51 +346,84 @@ STATS = {"dense_words": 0, "sent_words": 0}
 
 def set_pack_exchange(enabled) -> None:
     """Zero-skipping (packed) exchange of the ReLU'd tables of the sharded
-    stack: True / False, or "auto" (the default): packed up to
-    PACK_AUTO_MAX_WORLD ranks.  Packing halves the words on xGMI but adds an
-    unpack pass that writes the received (P - 1)/P of every table locally;
-    the link time a table saves shrinks as 1/P while that pass grows, and on
-    the measured config-5 rank the two cross between P = 4
-    (packed 315 vs dense 335 ms predicted) and P = 8 (193 vs 167 ms) at the
-    ideal 153 GB/s per link."""
+    stack: True / False, or "auto" (the default).  Packing about halves the
+    words on xGMI.  Where the next layer's fused kernel gathers packed tables
+    in place (F = 256, round 6: no unpack pass) "auto" always packs;
+    elsewhere the received segments are expanded into the dense table first
+    (mgcn_unpack_rows), a pass that writes the received (P - 1)/P of every
+    table, and "auto" packs only up to PACK_AUTO_MAX_WORLD ranks (the link
+    time a table saves shrinks as 1/P while that pass grows)."""
     global PACK_EXCHANGE
     PACK_EXCHANGE = enabled if enabled == "auto" else bool(enabled)
 
 
-def _pack_on(shard: Shard) -> bool:
+# mgcn.dist.set_pack_inplace: gather packed tables in place where the kernels
+# can (True, the default) or always expand them (False: the round-5 path, A/B)
+PACK_INPLACE = os.environ.get("MGCN_PACK_INPLACE", "1") != "0"
+
+
+def set_pack_inplace(enabled: bool) -> None:
+    global PACK_INPLACE
+    PACK_INPLACE = bool(enabled)
+
+
+def _inplace_ok(shard: Shard, backend, F: int) -> bool:
+    return PACK_INPLACE and getattr(backend, "packed_gather_ok", lambda f: False)(F) and \
+        shard.chunks * shard.world <= 64
+
+
+def _pack_on(shard: Shard, backend=None, F: int = 0) -> bool:
     if PACK_EXCHANGE == "auto":
-        return shard.world <= PACK_AUTO_MAX_WORLD
+        return shard.world <= PACK_AUTO_MAX_WORLD or (backend is not None and
+                                                      _inplace_ok(shard, backend, F))
     return bool(PACK_EXCHANGE)
 
 
 class _ChunkExchange:
     """All-gathers the row chunks of one [rows, F] fp32 tensor into an
     exchange table, chunk by chunk as the caller produces them.  ``packed``:
-    each chunk is packed (offsets, nonzero masks, nonzero words; libmgcn
-    mgcn_pack_rows_*), the ranks all-gather their packed sizes, send buffers
-    of the largest size and unpack every rank's segment into the table --
-    bit for bit the dense exchange; a chunk whose largest packed form is not
-    smaller than the dense chunk goes dense.  The packed path needs each
-    chunk's sizes on the host: :meth:`start` issues a chunk's pack and size
-    exchange, :meth:`finish` (called one chunk later, so the GPU has the next
-    chunk's compute queued while the host waits) its payload.  Emulated rank:
-    the rank's own segment is copied (dense) or packed and unpacked at all P
-    positions (the receive-side work of a real rank, with its own data; no
+    each chunk is packed (pack.hip's layout: per-row header pairs (mask_w,
+    pos_w), then the nonzero words; libmgcn mgcn_pack_rows_*), the ranks
+    all-gather their packed sizes, then send buffers of the largest size.
+    The received segments are then either gathered IN PLACE by the next
+    kernel (``inplace``: the result is a :class:`mgcn.ops.PackedTable` over
+    the chunks' receive buffers, no dense table is ever written) or expanded
+    into the dense table (mgcn_unpack_rows; a chunk whose largest packed form
+    is not smaller than the dense chunk then goes dense) -- bit for bit the
+    dense exchange either way.  The packed path needs each chunk's sizes on
+    the host: :meth:`start` issues a chunk's pack and size exchange,
+    :meth:`finish` (called one chunk later, so the GPU has the next chunk's
+    compute queued while the host waits on an event) its payload.  Emulated
+    rank: the rank's own segment stands in for all P (copied into the P
+    positions of the receive buffer, or packed and unpacked at all P
+    positions: the receive-side work of a real rank, with its own data; no
     collective runs)."""
 
-    def __init__(self, shard: Shard, local_pad: torch.Tensor, table: torch.Tensor, group,
-                 backend, packed: bool):
-        self.sh, self.local, self.table, self.group, self.be = shard, local_pad, table, group, backend
+    def __init__(self, shard: Shard, local_pad: torch.Tensor, table, group, backend,
+                 packed: bool, inplace: bool = False):
+        """``table``: the dense table, or a callable that allocates it (only
+        called when some chunk goes dense)."""
+        self.sh, self.local, self.group, self.be = shard, local_pad, group, backend
+        self._table = table
         F = local_pad.size(1)
-        # (the packed form's row offsets are int32, pack.hip: a chunk of 2^31
-        # words or more goes dense)
+        # (the packed form's value positions are int32, pack.hip: a chunk of
+        # 2^31 words or more goes dense)
         self.packed = bool(packed) and local_pad.dtype == torch.float32 and F % 32 == 0 and \
             hasattr(backend, "pack_count") and (_collective(shard.world) or shard.emulated) and \
             shard.chunk_rows * F < 2 ** 31
+        self.inplace = self.packed and bool(inplace)
         self.words = F // 32
         self.pending = []
         self.works = []
         self.stats = STATS
+        self.recv = []      # inplace: the chunks' receive buffers
+        self.seg = []       # inplace: words per segment of each chunk
+
+    @property
+    def table(self):
+        if callable(self._table):
+            self._table = self._table()
+        return self._table
 
     def start(self, c: int) -> None:
         sh = self.sh
@@ -370,10 +433,11 @@ class _ChunkExchange:
         cr = sh.chunk_rows
         rows = self.local[c * cr:(c + 1) * cr]
         dev = rows.device
-        head = cr * (1 + self.words)
-        send = torch.empty(head + cr * rows.size(1), dtype=torch.int32, device=dev)
+        head = 2 * cr * self.words
+        # (+4 words: a lane's 16-B value read may run 3 words past the values)
+        send = torch.empty(head + cr * rows.size(1) + 4, dtype=torch.int32, device=dev)
         counts = torch.empty(cr, dtype=torch.int32, device=dev)
-        self.be.pack_count(rows, send[cr:head].view(cr, self.words), counts)
+        self.be.pack_count(rows, send[:head].view(cr, 2 * self.words), counts)
         total = counts.sum(dtype=torch.int64).view(1)
         P = sh.world
         if sh.emulated or not _collective(P):
@@ -416,18 +480,34 @@ class _ChunkExchange:
             if work is not None:
                 work.wait()
             cap = int(totals.max())
-        head = cr * (1 + self.words)
+        head = 2 * cr * self.words
         seg = head + cap
         self.stats["dense_words"] += cr * F * P
-        if seg >= cr * F:  # nothing to gain: dense
+        if seg >= cr * F and not self.inplace:  # nothing to gain: dense
             self.stats["sent_words"] += cr * F * P
             self.works.append(_gather_chunk(sh, c, self.local, self.table, self.group))
             return
         self.stats["sent_words"] += seg * P
-        offs = send[:cr]
-        torch.cumsum(counts, 0, dtype=torch.int32, out=offs)
+        offs = torch.cumsum(counts, 0, dtype=torch.int32)
         offs.sub_(counts)
-        self.be.pack_values(rows, send[cr:head].view(cr, self.words), offs, send[head:head + cap])
+        self.be.pack_values(rows, offs, send[:head].view(cr, 2 * self.words), send[head:head + cap])
+        if self.inplace:
+            if sh.emulated:
+                # the rank's own segment stands in for all P (its P positions
+                # alias it): no collective and no copy -- the receive-side
+                # write of a real rank is the exchange's, which
+                # scripts/config5_rank.py accounts for separately
+                self.recv.append(send)
+                self.seg.append(0)
+                return
+            # P segments back to back (+4 words: a lane's 16-B value read may
+            # run 3 words past the last segment's values)
+            recv = torch.empty(P * seg + 4, dtype=torch.int32, device=rows.device)
+            recv[P * seg:].zero_()
+            _gather_into(recv[:P * seg], send[:seg], P, self.group, False)
+            self.recv.append(recv)
+            self.seg.append(seg)
+            return
         blk = self.table[c * P * cr:(c + 1) * P * cr]
         if sh.emulated:  # a real rank's receive-side work: P segments unpacked
             for p in range(P):
@@ -441,6 +521,24 @@ class _ChunkExchange:
         self.finish()
         _wait(self.works)
         self.works = []
+
+    def result(self):
+        """The exchanged table: the dense table, or (inplace) the
+        PackedTable over the chunks' receive buffers (segment c P + k = rank
+        k's part of row chunk c, the exchange layout's order)."""
+        self.wait()
+        if not self.inplace:
+            return self.table
+        from .ops import PackedTable
+        from .ops import packed_row_bits
+        P = self.sh.world
+        seg_buf, seg_off = [], []
+        for c, sg in enumerate(self.seg):
+            for k in range(P):
+                seg_buf.append(c)
+                seg_off.append(k * sg)  # (emulated rank: sg = 0, all P alias its own)
+        return PackedTable(self.recv, seg_buf, seg_off, self.sh.chunk_rows,
+                           packed_row_bits(self.sh.chunk_rows), self.local.size(1))
 
 
 def gather_table(shard: Shard, local: torch.Tensor, group=None, slot: str = "g") -> torch.Tensor:
@@ -628,26 +726,29 @@ class _ShardedStack(torch.autograd.Function):
             if relus[i] and not last:
                 rm = torch.empty(sh.pad_rows, 4 * ((F_out + 127) // 128), dtype=torch.int32,
                                  device=dev)
-            nxt = None if last else new_table(sh, F_out, torch.float32, dev, "t%d" % (i & 1))
-            # the layer's output rows (ReLU'd below the top) travel packed
-            xch = None if nxt is None else _ChunkExchange(sh, out, nxt, group, be,
-                                                          _pack_on(sh) and relus[i])
+            # the layer's output rows (ReLU'd below the top) travel packed;
+            # the next layer gathers them in place where its kernel can
+            xch = None
+            if not last:
+                pk = relus[i] and _pack_on(sh, be, F_out)
+                slot = "t%d" % (i & 1)
+                xch = _ChunkExchange(sh, out, lambda F=F_out, s_=slot: new_table(
+                    sh, F, torch.float32, dev, s_), group, be, pk,
+                    inplace=pk and _inplace_ok(sh, be, F_out))
             for c in range(C):
                 a, e = sh.chunk(c)
                 if e > a:
-                    be.spmm_xw_fwd(sh.fwd.rows(a, e, sh.chunk_edges_fwd[c]), sh.w_fwd, tab, W,
-                                   reduce, b, relus[i], relu_mask=None if rm is None else rm[a:e],
-                                   want_z=want_z, out=out[a:e],
-                                   z_out=None if z is None else z[a:e])
+                    be.spmm_xw_fwd(sh.view_for(tab, "fwd", a, e, sh.chunk_edges_fwd[c]), sh.w_fwd,
+                                   tab, W, reduce, b, relus[i],
+                                   relu_mask=None if rm is None else rm[a:e], want_z=want_z,
+                                   out=out[a:e], z_out=None if z is None else z[a:e])
                 if xch is not None:
                     xch.start(c)
                     xch.finish(keep=1)
-            if xch is not None:
-                xch.wait()
             outs.append(out)
             zs.append(z)
             rms.append(rm)
-            tab = nxt
+            tab = None if xch is None else xch.result()
         ctx.shard, ctx.reduce, ctx.relus, ctx.backend, ctx.group = sh, reduce, relus, be, group
         ctx.n = n
         ctx.x_is_table = x_is_table
@@ -699,15 +800,22 @@ class _ShardedStack(torch.autograd.Function):
                     gb[top] = cs
             if not wants_dx(l):
                 break
-            _wait(works)
+            if isinstance(works, _ChunkExchange):
+                tab = works.result()  # (dense, or the packed table gathered in place)
+            else:
+                _wait(works)
             dX = torch.empty(sh.pad_rows, W.size(0), dtype=torch.float32, device=dev)
-            ntab = xch = None
+            xch = None
             if l > 0 and wants_dx(l - 1):
-                ntab = new_table(sh, W.size(0), torch.float32, dev, "t%d" % ((l - 1) & 1))
                 if sh.pad_rows > rows:
                     dX[rows:].zero_()  # padding rows travel too (packed: as zeros)
                 # masked by the lower layer's ReLU: travels packed
-                xch = _ChunkExchange(sh, dX, ntab, group, be, _pack_on(sh) and relus[l - 1])
+                Fx = W.size(0)
+                pk = relus[l - 1] and _pack_on(sh, be, Fx)
+                slot = "t%d" % ((l - 1) & 1)
+                xch = _ChunkExchange(sh, dX, lambda F=Fx, s_=slot: new_table(
+                    sh, F, torch.float32, dev, s_), group, be, pk,
+                    inplace=pk and _inplace_ok(sh, be, Fx))
             works = []
             # the lower layer's bias gradient: every chunk's column sums are
             # added into one device vector by the adjoint launches themselves
@@ -719,7 +827,7 @@ class _ShardedStack(torch.autograd.Function):
                 a, e = sh.chunk(c)
                 if e > a:
                     be.spmm_xw_bwd_dx(
-                        sh.bwd.rows(a, e, sh.chunk_edges_bwd[c]), sh.w_bwd,
+                        sh.view_for(tab, "bwd", a, e, sh.chunk_edges_bwd[c]), sh.w_bwd,
                         None if sh.row_scale is None else sh.row_scale[a:e], tab, W,
                         relu_mask=rms[l - 1][a:e] if l > 0 else None,
                         row_div=rd[a:e] if (l > 0 and rd is not None) else None, out=dX[a:e],
@@ -727,12 +835,13 @@ class _ShardedStack(torch.autograd.Function):
                 if xch is not None:
                     xch.start(c)
                     xch.finish(keep=1)
-            if xch is not None:
-                works = [xch]  # its last chunk is finished at the wait, after the next dW
+            # (the exchange's last chunk is finished at the next layer's
+            # result(), after its dW)
+            works = xch
             if l > 0:
                 if ctx.has_bias[l - 1]:
                     gb[l - 1] = csum
-                dY, tab = dX, ntab
+                dY, tab = dX, None
             else:
                 dx = dX[:rows]
         grads = []

@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import os
 from collections import Counter
+from dataclasses import dataclass
 
 import torch
 
@@ -189,17 +190,25 @@ def spmm_xw_fwd(view: CSRView, w: torch.Tensor | None, X: torch.Tensor, W: torch
     ``want_z`` returns (Y, Z): Z = the aggregated rows before W (for mean
     before the division), from which the backward forms dW = Z^T dY.
     ``out`` / ``z_out``: [n_rows, F] row-major buffers (16-byte aligned rows)
-    to write Y / Z into instead of new tensors."""
+    to write Y / Z into instead of new tensors.  ``X`` may be a
+    :class:`PackedTable` (256-wide layers; the view's columns then are packed
+    positions): the rows are gathered from the packed exchange buffers in
+    place (``mgcn_spmm_xw_fwd_packed``), bit for bit the dense table's result."""
     lib = L.load()
-    X = _contig_f32(X, "X")
-    if X.stride(0) % 4 or X.data_ptr() % 16:
-        X = X.contiguous()
+    packed = isinstance(X, PackedTable)
+    if not packed:
+        X = _contig_f32(X, "X")
+        if X.stride(0) % 4 or X.data_ptr() % 16:
+            X = X.contiguous()
     W = W.detach()
-    dev = L.require_device(X, W, view.rowptr, w, bias, relu_mask)
-    if X.size(0) != view.n_cols:
-        raise ValueError(f"X has {X.size(0)} rows, graph has {view.n_cols} source nodes")
+    dev = L.require_device(X.words if packed else X, W, view.rowptr, w, bias, relu_mask)
     F_in, F_out = W.shape
-    if X.size(1) != F_in:
+    if packed:
+        if X.F != F_in:
+            raise ValueError(f"spmm_xw_fwd: packed table of F = {X.F}, W is [{F_in}, {F_out}]")
+    elif X.size(0) != view.n_cols:
+        raise ValueError(f"X has {X.size(0)} rows, graph has {view.n_cols} source nodes")
+    elif X.size(1) != F_in:
         raise ValueError(f"spmm_xw_fwd: X is [{X.size(0)}, {X.size(1)}], W is [{F_in}, {F_out}]")
     if W.dtype != torch.float32 or W.stride(1) != 1:
         W = W.to(torch.float32).contiguous()
@@ -230,19 +239,28 @@ def spmm_xw_fwd(view: CSRView, w: torch.Tensor | None, X: torch.Tensor, W: torch
                              f"16-byte aligned rows")
     ws_bytes = int(lib.mgcn_spmm_xw_fwd_workspace_bytes(F_in, F_out))
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev) if ws_bytes else None
-    tname = "spmm_xw_fwd_z" if want_z else "spmm_xw_fwd"
+    tname = ("spmm_xw_fwd_z" if want_z else "spmm_xw_fwd") + ("_pk" if packed else "")
     if _TIMER is not None:
         _TIMER(tname, True, view.n_rows, view.edges)
     with L.device_guard(dev):
-        rc = lib.mgcn_spmm_xw_fwd(view.n_rows, view.n_cols, F_in, F_out, L.ptr(view.rowptr),
-                                  L.ptr(view.col), L.ptr(w), L.ptr(X), X.stride(0), L.ptr(W),
-                                  W.stride(0), L.ptr(bias), L.ptr(Y), Y.stride(0), reduce,
-                                  int(bool(relu)), L.ptr(relu_mask), L.ptr(Z),
-                                  Z.stride(0) if Z is not None else 0, L.ptr(ws), ws_bytes,
-                                  L.stream_of(dev))
+        if packed:
+            pk = X.c_struct()
+            rc = lib.mgcn_spmm_xw_fwd_packed(view.n_rows, F_in, F_out, L.ptr(view.rowptr),
+                                             L.ptr(view.col), L.ptr(w), L.byref(pk), L.ptr(W),
+                                             W.stride(0), L.ptr(bias), L.ptr(Y), Y.stride(0),
+                                             reduce, int(bool(relu)), L.ptr(relu_mask), L.ptr(Z),
+                                             Z.stride(0) if Z is not None else 0, L.ptr(ws),
+                                             ws_bytes, L.stream_of(dev))
+        else:
+            rc = lib.mgcn_spmm_xw_fwd(view.n_rows, view.n_cols, F_in, F_out, L.ptr(view.rowptr),
+                                      L.ptr(view.col), L.ptr(w), L.ptr(X), X.stride(0), L.ptr(W),
+                                      W.stride(0), L.ptr(bias), L.ptr(Y), Y.stride(0), reduce,
+                                      int(bool(relu)), L.ptr(relu_mask), L.ptr(Z),
+                                      Z.stride(0) if Z is not None else 0, L.ptr(ws), ws_bytes,
+                                      L.stream_of(dev))
     if _TIMER is not None:
         _TIMER(tname, False)
-    L.check(rc, "mgcn_spmm_xw_fwd")
+    L.check(rc, "mgcn_spmm_xw_fwd_packed" if packed else "mgcn_spmm_xw_fwd")
     return (Y, Z) if want_z else Y
 
 
@@ -261,8 +279,12 @@ def spmm_xw_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tens
     float32 [F_out] tensor; the dW + dX form of a whole square graph, no max)
     receives the column sums of dY itself -- the layer's own bias gradient --
     from the same launch (``mgcn_spmm_xw_bwd_hcs``).  Returns
-    (dW, dX or None, colsum or None)."""
+    (dW, dX or None, colsum or None).  ``dY`` may be a :class:`PackedTable`
+    (256-wide, dX-only form X = None; ``mgcn_spmm_xw_bwd_packed``)."""
     lib = L.load()
+    if isinstance(dY, PackedTable):
+        return _spmm_xw_bwd_packed(view_t, w_t, row_scale, dY, X, W, want_dx, relu_mask, row_div,
+                                   win_mask, dx_out, colsum_acc, dy_colsum_out)
     dY = _contig_f32(dY, "dY")
     if dY.stride(0) % 4 or dY.data_ptr() % 16:
         dY = dY.contiguous()
@@ -356,6 +378,52 @@ def spmm_xw_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tens
         _TIMER(tname, False)
     L.check(rc, "mgcn_spmm_xw_bwd")
     return dW, dX, colsum
+
+
+def _spmm_xw_bwd_packed(view_t, w_t, row_scale, dY, X, W, want_dx, relu_mask, row_div,
+                        win_mask, dx_out, colsum_acc, dy_colsum_out):
+    """:func:`spmm_xw_bwd`'s dX-only form gathering dY from a PackedTable."""
+    lib = L.load()
+    if X is not None or not want_dx or win_mask is not None or dy_colsum_out is not None:
+        raise ValueError("spmm_xw_bwd: a packed dY takes the dX-only form (X = None, no max)")
+    W = W.detach()
+    if W.dtype != torch.float32 or W.stride(1) != 1 or W.stride(0) % 4 or W.data_ptr() % 16:
+        W = W.to(torch.float32).contiguous()
+    dev = L.require_device(dY.words, W, view_t.rowptr, w_t, row_scale, relu_mask, row_div)
+    F_in, F_out = W.shape
+    M = view_t.n_rows
+    if dY.F != F_out:
+        raise ValueError(f"spmm_xw_bwd: packed dY of F = {dY.F}, W is [{F_in}, {F_out}]")
+    dX = dx_out if dx_out is not None else torch.empty(M, F_in, dtype=torch.float32, device=dev)
+    if (dX.dtype != torch.float32 or dX.dim() != 2 or tuple(dX.shape) != (M, F_in) or
+            dX.stride(1) != 1 or dX.stride(0) % 4 or dX.data_ptr() % 16):
+        raise ValueError(f"spmm_xw_bwd: dx_out must be float32 [{M}, {F_in}], 16-byte rows")
+    colsum = None
+    if relu_mask is not None:
+        mw = mask_words(F_in)
+        if relu_mask.shape != (M, mw) or relu_mask.dtype != torch.int32:
+            raise ValueError(f"spmm_xw_bwd: relu_mask must be int32 [{M}, {mw}]")
+        relu_mask = relu_mask.contiguous()
+        colsum = colsum_acc if colsum_acc is not None else torch.empty(F_in, dtype=torch.float32,
+                                                                         device=dev)
+    elif colsum_acc is not None:
+        raise ValueError("spmm_xw_bwd: colsum_acc needs relu_mask")
+    ws_bytes = int(lib.mgcn_spmm_xw_bwd_workspace_bytes(M, F_in, F_out))
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    if _TIMER is not None:
+        _TIMER("spmm_xw_bwd_dx_pk", True, view_t.n_rows, view_t.edges)
+    pk = dY.c_struct()
+    with L.device_guard(dev):
+        rc = lib.mgcn_spmm_xw_bwd_packed(M, F_in, F_out, L.ptr(view_t.rowptr), L.ptr(view_t.col),
+                                         L.ptr(w_t), L.ptr(row_scale), L.byref(pk), L.ptr(W),
+                                         W.stride(0), L.ptr(dX), dX.stride(0), L.ptr(relu_mask),
+                                         L.ptr(row_div), L.ptr(colsum),
+                                         1 if colsum_acc is not None else 0, L.ptr(ws), ws_bytes,
+                                         L.stream_of(dev))
+    if _TIMER is not None:
+        _TIMER("spmm_xw_bwd_dx_pk", False)
+    L.check(rc, "mgcn_spmm_xw_bwd_packed")
+    return None, dX, colsum
 
 
 def spmm_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tensor | None,
@@ -1797,44 +1865,105 @@ class _SegmentMean(torch.autograd.Function):
 
 
 # ------------------------------------------------- packed table exchange
-def pack_rows_count(rows: torch.Tensor, masks: torch.Tensor, counts: torch.Tensor) -> None:
-    """masks[i] = the not-+0.0 bits of rows[i] (F / 32 words), counts[i] =
-    their number (``mgcn_pack_rows_count``; mgcn.dist's packed exchange)."""
+def pack_rows_count(rows: torch.Tensor, hdr: torch.Tensor, counts: torch.Tensor) -> None:
+    """hdr[i, 2 w] = mask word w of rows[i] (its not-+0.0 bits), counts[i] =
+    their number (``mgcn_pack_rows_count``; mgcn.dist's packed exchange).
+    ``hdr`` is the [n, 2 F/32] int32 header of the packed chunk."""
     lib = L.load()
     rows = _contig_f32(rows, "rows")
     n, F = rows.shape
-    dev = L.require_device(rows, masks, counts)
-    if masks.shape != (n, F // 32) or masks.dtype != torch.int32 or not masks.is_contiguous() \
+    dev = L.require_device(rows, hdr, counts)
+    if hdr.shape != (n, 2 * (F // 32)) or hdr.dtype != torch.int32 or not hdr.is_contiguous() \
             or counts.shape != (n,) or counts.dtype != torch.int32:
-        raise ValueError("pack_rows_count: masks int32 [n, F/32], counts int32 [n]")
+        raise ValueError("pack_rows_count: hdr int32 [n, 2 F/32] contiguous, counts int32 [n]")
     if _TIMER is not None:
         _TIMER("pack_rows_count", True, n)
     with L.device_guard(dev):
-        rc = lib.mgcn_pack_rows_count(n, F, L.ptr(rows), rows.stride(0), L.ptr(masks),
+        rc = lib.mgcn_pack_rows_count(n, F, L.ptr(rows), rows.stride(0), L.ptr(hdr),
                                       L.ptr(counts), L.stream_of(dev))
     if _TIMER is not None:
         _TIMER("pack_rows_count", False)
     L.check(rc, "mgcn_pack_rows_count")
 
 
-def pack_rows_values(rows: torch.Tensor, masks: torch.Tensor, offs: torch.Tensor,
+def pack_rows_values(rows: torch.Tensor, offs: torch.Tensor, hdr: torch.Tensor,
                      vals: torch.Tensor) -> None:
-    """vals[offs[i] ...] = the not-+0.0 words of rows[i] in order
-    (``mgcn_pack_rows_values``)."""
+    """vals[offs[i] ...] = the not-+0.0 words of rows[i] in order, and the
+    header's value positions hdr[i, 2 w + 1] (``mgcn_pack_rows_values``)."""
     lib = L.load()
     rows = _contig_f32(rows, "rows")
     n, F = rows.shape
-    dev = L.require_device(rows, masks, offs, vals)
-    if offs.shape != (n,) or offs.dtype != torch.int32 or vals.dtype != torch.int32:
-        raise ValueError("pack_rows_values: offs int32 [n], vals int32")
+    dev = L.require_device(rows, offs, hdr, vals)
+    if offs.shape != (n,) or offs.dtype != torch.int32 or vals.dtype != torch.int32 or \
+            hdr.shape != (n, 2 * (F // 32)) or hdr.dtype != torch.int32 or not hdr.is_contiguous():
+        raise ValueError("pack_rows_values: offs int32 [n], hdr int32 [n, 2 F/32], vals int32")
     if _TIMER is not None:
         _TIMER("pack_rows_values", True, n)
     with L.device_guard(dev):
-        rc = lib.mgcn_pack_rows_values(n, F, L.ptr(rows), rows.stride(0), L.ptr(masks),
-                                       L.ptr(offs), L.ptr(vals), L.stream_of(dev))
+        rc = lib.mgcn_pack_rows_values(n, F, L.ptr(rows), rows.stride(0), L.ptr(offs),
+                                       L.ptr(hdr), L.ptr(vals), L.stream_of(dev))
     if _TIMER is not None:
         _TIMER("pack_rows_values", False)
     L.check(rc, "mgcn_pack_rows_values")
+
+
+@dataclass
+class PackedTable:
+    """An exchange table as the zero-skipping exchange delivered it
+    (``mgcn_packed_table``): C x P packed segments of ``seg_rows`` rows each
+    (pack.hip's layout), segment s at word ``seg_off[s]`` of buffer
+    ``bufs[seg_buf[s]]`` (one receive buffer per row chunk, or one for all).
+    The fused 256-wide layer kernels gather from it in place
+    (:func:`spmm_xw_fwd` / :func:`spmm_xw_bwd` with a PackedTable for X / dY,
+    over a view whose columns are packed positions (s << row_bits) | i:
+    :func:`packed_cols`)."""
+    bufs: list               # int32 tensors holding the segments (kept alive here)
+    seg_buf: list            # segment s -> index into bufs
+    seg_off: list            # segment s -> word offset in that buffer
+    seg_rows: int
+    row_bits: int
+    F: int
+
+    @property
+    def n_seg(self) -> int:
+        return len(self.seg_off)
+
+    @property
+    def words(self) -> torch.Tensor:
+        return self.bufs[0]
+
+    def c_struct(self):
+        """The C descriptor: every segment's offset counted from the lowest
+        buffer address (one device address space)."""
+        if self.n_seg > 64:
+            raise ValueError(f"PackedTable: {self.n_seg} segments (at most 64)")
+        ptrs = [b.data_ptr() for b in self.bufs]
+        anchor = min(ptrs)
+        if any((p - anchor) % 4 for p in ptrs):
+            raise ValueError("PackedTable: buffers must be 4-byte aligned")
+        rel = [(p - anchor) // 4 for p in ptrs]
+        t = L.PackedTableC()
+        t.words = anchor
+        t.n_words = max(r + b.numel() for r, b in zip(rel, self.bufs))
+        t.n_seg = self.n_seg
+        t.seg_rows = int(self.seg_rows)
+        t.row_bits = int(self.row_bits)
+        t.F = int(self.F)
+        for s_, (bi, off) in enumerate(zip(self.seg_buf, self.seg_off)):
+            t.seg_base[s_] = rel[bi] + int(off)
+        return t
+
+
+def packed_row_bits(seg_rows: int) -> int:
+    return max(int(seg_rows - 1).bit_length(), 0)
+
+
+def packed_cols(col: torch.Tensor, seg_rows: int, row_bits: int) -> torch.Tensor:
+    """Table positions t (row t % seg_rows of segment t // seg_rows) ->
+    packed positions (s << row_bits) | i, int32."""
+    t = col.to(torch.int64)
+    s_ = torch.div(t, seg_rows, rounding_mode="floor")
+    return ((s_ << row_bits) | (t - s_ * seg_rows)).to(torch.int32)
 
 
 def unpack_rows(buf: torch.Tensor, n_seg: int, n: int, seg_words: int, out: torch.Tensor) -> None:

@@ -32,6 +32,7 @@ import torch  # noqa: E402
 from bench import KernelTimer, launch_bytes  # noqa: E402
 
 XGMI_LINK_GBS = 153.0  # per link and direction
+HBM_WRITE_TBS = 5.0    # streaming write rate charged for the received words (upper-bound term)
 
 
 def _global_ids(t, sh):
@@ -147,6 +148,8 @@ def main():
     step = model.step_fn(None, None, X_table=Xt, dY_local=dYl)
 
     def run(packed):
+        sh._tables = None  # the other run's persistent dense tables
+        torch.cuda.empty_cache()
         mdist.set_pack_exchange(packed)
         for _ in range(args.warmup):
             step()
@@ -161,8 +164,10 @@ def main():
         return ms, (st["sent_words"] / st["dense_words"] if st["dense_words"] else 1.0)
 
     # the step with every table kept dense (the rank-local compute alone), then
-    # with the zero-skipping exchange (adds the pack and, for every table, the
-    # unpack of all P segments: a real rank's receive-side work)
+    # with the zero-skipping exchange: the pack of every ReLU'd table, the
+    # receive-side write of all P segments of it (a real rank's RCCL receive),
+    # and the next layer gathering the packed segments in place (round 6; no
+    # unpack pass -- MGCN_PACK_INPLACE=0 restores the round-5 unpack)
     ms_dense, _ = run(False)
     packed = model.fused and not args.dense_exchange
     ms, ratio = run(True) if packed else (ms_dense, 1.0)
@@ -182,28 +187,32 @@ def main():
     kernel_ms = sum(k["total_ms"] for k in kern.values())
     check = sample_check(model, Xt, odeg, args.check_rows, F) if args.check_rows else None
     del odeg
-    # predicted curve.  Local work of a rank at P: the compute scales with its
-    # rows (8 / P of rank 0's here); the pack / unpack work with the share of
-    # each table received, (P - 1) / P (measured here at P = 8: 7/8).  Each
-    # exchanged table is an all-gather of [N, F] fp32, a rank receiving
-    # (P - 1) / P of it over P - 1 xGMI links; packed tables at `ratio` of
-    # their words.
+    # predicted curve.  Local work of a rank at P: the measured step (its
+    # compute, the pack, the in-place packed gathers) scales with its rows
+    # (8 / P of rank 0's here).  Each exchanged table is an all-gather of
+    # [N, F] fp32, a rank receiving (P - 1) / P of it over P - 1 xGMI links;
+    # packed tables at `ratio` of their words.  The received words are written
+    # into the rank's HBM by the exchange; the emulated rank aliases its own
+    # segment instead, so `local_ms_recv` adds that write at HBM_WRITE_TBS as
+    # if it did not overlap the compute (an upper bound).
     tables = (2 * (L - 1)) if model.fused else (2 * L)
     # the fused stack packs the ReLU'd forward tables (L - 1) and the
     # ReLU-masked backward ones (L - 2); the top layer's dY travels dense
     packed_tables = (2 * L - 3) if packed else 0
     eff_tables = tables - packed_tables + packed_tables * ratio
-    xwork = max(ms - ms_dense, 0.0)
     curve = {}
     for p in (1, 2, 4, 8):
         compute = ms_dense * args.world / p
-        local = compute + (xwork * ((p - 1) / p) / ((args.world - 1) / args.world) if p > 1 else 0.0)
+        local = (ms if packed_tables else ms_dense) * args.world / p if p > 1 else compute
+        recv = 0.0 if p == 1 else eff_tables * 4.0 * N * F * (p - 1) / p / (HBM_WRITE_TBS * 1e12) * 1e3
         xch = 0.0 if p == 1 else eff_tables * (4.0 * N * F * (p - 1) / p) / (
             (p - 1) * XGMI_LINK_GBS * 1e9) * 1e3
         xch_dense = 0.0 if p == 1 else tables * (4.0 * N * F * (p - 1) / p) / (
             (p - 1) * XGMI_LINK_GBS * 1e9) * 1e3
         step_ms = max(local, xch)
         curve[str(p)] = {"compute_ms": compute, "local_ms": local, "exchange_ms": xch,
+                         "local_ms_recv": local + recv,
+                         "step_ms_overlapped_recv": max(local + recv, xch),
                          "exchange_ms_dense": xch_dense,
                          "step_ms_overlapped": step_ms,
                          "step_ms_overlapped_dense": max(compute, xch_dense),
@@ -212,7 +221,8 @@ def main():
     out = {"workload": f"config5 rank {args.rank} of {args.world}: N={N}, E={2 * P} (+{N} loops), "
                        f"F={F}, {L}-layer GCN (sm, add, bias, ReLU) fwd+bwd, exchange tables "
                        "resident (no RCCL; ms_per_step includes the zero-skipping exchange's "
-                       "pack and the unpack of all P segments of every packed table)",
+                       "pack and the receive-side write of all P segments of every packed "
+                       "table, gathered in place by the next layer)",
            "path": ("fused layer kernels (_ShardedStack)" if model.fused else
                     "per layer: x @ W (mgcn_gemm_nn) + SpMM; adjoint SpMM + dW (mgcn_gemm_tn) + "
                     "dX (mgcn_gemm_nn)"),
@@ -226,6 +236,7 @@ def main():
            "packed_exchange_ratio": ratio if packed_tables else None,
            "dense_equivalent_tables_per_step": eff_tables,
            "xgmi_link_gbs": XGMI_LINK_GBS, "predicted_curve": curve,
+           "pack_inplace": mdist.PACK_INPLACE,
            "peak_mem_gb": torch.cuda.max_memory_allocated() / 1e9,
            "sampled_check": check}
     print(json.dumps(out), flush=True)

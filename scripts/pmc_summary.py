@@ -22,7 +22,8 @@ from bench import spmm_bytes  # noqa: E402
 N, NNZ, F = 1_000_000, 11_000_000, 128
 KERNELS = {"fwd": "spmm_xw_fwd_kernel", "fwd_z": "spmm_xw_fwd_kernel",
            "bwd": "spmm_xw_bwd_ws_kernel", "bwd_dw": "spmm_xw_bwd_ws_kernel",
-           "bwd_dx": "spmm_xw_bwd_kernel", "gemm_dw": "gemm_bwd_kernel"}
+           "bwd_dx": "spmm_xw_bwd_kernel", "gemm_dw": "gemm_bwd_kernel",
+           "gemm_dw_cs": "gemm_bwd_kernel"}
 
 
 def per_kernel(d, counter):
@@ -74,7 +75,7 @@ def main():
             streamed = 4.0 * N * F  # X rows, read once
         name = {"fwd": "spmm_xw_fwd", "fwd_z": "spmm_xw_fwd_z", "bwd": "spmm_xw_bwd",
                 "bwd_dw": "spmm_xw_bwd_dw", "bwd_dx": "spmm_xw_bwd_dx",
-                "gemm_dw": "gemm_bwd_dw"}[kind]
+                "gemm_dw": "gemm_bwd_dw", "gemm_dw_cs": "gemm_bwd_dw_cs"}[kind]
         if kind == "bwd":
             alg += 4 * N * F
         elif kind == "fwd_z":
@@ -83,6 +84,9 @@ def main():
             alg += 16 * N
         elif kind == "gemm_dw":  # a dense pass: X and dY streamed, 128 x 128 partials written
             alg = 8 * N * F
+            streamed = float(alg)
+        elif kind == "gemm_dw_cs":  # ... plus a third [N, F] stream for its column sums
+            alg = 12 * N * F
             streamed = float(alg)
         # the streamed part reported at 1 / copy_factor, the rest at 1 / gather_factor
         read = streamed + gather_factor * max(fk - streamed / copy_factor, 0.0)

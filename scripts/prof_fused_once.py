@@ -1,6 +1,6 @@
 """Run one fused layer kernel a few times on the config-2 graph for
 rocprofv3 PMC passes:
-    python scripts/prof_fused_once.py {fwd,fwd_z,bwd,bwd_dw,bwd_dx,gemm_dw,spmm} [reps]"""
+    python scripts/prof_fused_once.py {fwd,fwd_z,bwd,bwd_dw,bwd_dx,gemm_dw,gemm_dw_cs,spmm} [reps]"""
 import os
 import sys
 
@@ -26,6 +26,7 @@ W = torch.randn(F, F, device=dev, generator=g) * 0.1
 b = torch.randn(F, device=dev, generator=g) * 0.1
 dY = torch.randn(n, F, device=dev, generator=g)
 rm = ops.make_relu_mask(torch.randn(n, F, device=dev, generator=g))
+rmS = torch.randn(n, F, device=dev, generator=g)
 fn = {"fwd": lambda: ops.spmm_xw_fwd(plan.fwd, norm.w_fwd, X, W, L.REDUCE_SUM, b, True,
                                      relu_mask=rm),
       "bwd": lambda: ops.spmm_xw_bwd(plan.bwd, norm.w_bwd, None, dY, X, W, relu_mask=rm),
@@ -34,6 +35,9 @@ fn = {"fwd": lambda: ops.spmm_xw_fwd(plan.fwd, norm.w_fwd, X, W, L.REDUCE_SUM, b
                                        relu_mask=rm, want_z=True),
       "bwd_dx": lambda: ops.spmm_xw_bwd(plan.bwd, norm.w_bwd, None, dY, None, W, relu_mask=rm),
       "gemm_dw": lambda: ops.gemm_bwd(X, dY, W, want_dx=False, dh_colsum=True),
+      # the bottom layer's dW = Z^T dY + the top layer's bias gradient (column
+      # sums of a third stream, mgcn_gemm_bwd_dw_cs) -- the bench step's form
+      "gemm_dw_cs": lambda: ops.dw_pass_cs(X, dY, rmS),
       "spmm": lambda: ops.spmm_bwd(plan.bwd, norm.w_bwd, None, dY, L.REDUCE_SUM)}[kind]
 for _ in range(reps):
     fn()

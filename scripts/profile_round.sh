@@ -17,7 +17,7 @@ timeout -k 10 300 python -u bench.py > $O/bench_default.json 2> $O/bench_default
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench -- \
   python3 $R/bench.py --no-cpu-baseline > $O/bench_under_rocprof.json 2> $O/bench_under_rocprof.err
-for k in fwd fwd_z bwd bwd_dw bwd_dx gemm_dw; do
+for k in fwd fwd_z bwd bwd_dw bwd_dx gemm_dw gemm_dw_cs; do
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 90 rocprofv3 --pmc $c --output-format csv -d $O/pmc_${k}_$c -o pmc -- \
       python3 $R/scripts/prof_fused_once.py $k 3 > /dev/null 2>&1

@@ -145,7 +145,7 @@ class CpuBackend:
 
     # ------------------------------------------------ packed table exchange
     # (libmgcn mgcn_pack_rows_count / _values, mgcn_unpack_rows: the same
-    # buffer layout [offs: n][masks: n x F/32][vals], bit-pattern test)
+    # buffer layout [hdr: n x W pairs (mask_w, pos_w)][vals], bit-pattern test)
     @staticmethod
     def _bits_to_words(bits):
         n, F = bits.shape
@@ -158,27 +158,53 @@ class CpuBackend:
         w = words.to(torch.int64) & 0xFFFFFFFF
         return ((w.unsqueeze(-1) >> torch.arange(32, dtype=torch.int64)) & 1).bool().view(-1, F)
 
-    def pack_count(self, rows, masks, counts):
+    def pack_count(self, rows, hdr, counts):
         bits = rows.contiguous().view(torch.int32) != 0
-        masks.copy_(self._bits_to_words(bits))
+        hdr[:, 0::2] = self._bits_to_words(bits)
         counts.copy_(bits.sum(1).to(torch.int32))
 
-    def pack_values(self, rows, masks, offs, vals):
+    def pack_values(self, rows, offs, hdr, vals):
+        F = rows.size(1)
         v = rows.contiguous().view(torch.int32)
-        bits = self._words_to_bits(masks, rows.size(1))
+        bits = self._words_to_bits(hdr[:, 0::2].contiguous(), F)
         nz = v[bits]
         vals[:nz.numel()] = nz
+        per_word = bits.view(-1, F // 32, 32).sum(-1).to(torch.int64)
+        below = torch.cumsum(per_word, 1) - per_word
+        hdr[:, 1::2] = (offs.to(torch.int64).view(-1, 1) + below).to(torch.int32)
 
     def unpack(self, buf, n_seg, n, seg_words, out):
         F = out.size(1)
         words = F // 32
         for p in range(n_seg):
             seg = buf[p * seg_words:(p + 1) * seg_words]
-            bits = self._words_to_bits(seg[n:n + n * words].view(n, words), F)
-            o = torch.zeros(n, F, dtype=torch.int32)
-            k = int(bits.sum())
-            o[bits] = seg[n + n * words:n + n * words + k]
-            out[p * n:(p + 1) * n] = o.view(torch.float32)
+            out[p * n:(p + 1) * n] = self._unpack_seg(seg, n, F)
+
+    def _unpack_seg(self, seg, n, F):
+        words = F // 32
+        hdr = seg[:2 * n * words].view(n, 2 * words)
+        bits = self._words_to_bits(hdr[:, 0::2].contiguous(), F)
+        o = torch.zeros(n, F, dtype=torch.int32)
+        k = int(bits.sum())
+        o[bits] = seg[2 * n * words:2 * n * words + k]
+        return o.view(torch.float32)
+
+    def packed_gather_ok(self, F):
+        return True  # (the double takes packed tables at any width)
+
+    def _dense_table(self, tab, view):
+        """A PackedTable expanded (the double's stand-in for the in-place
+        gather) and the view's packed columns mapped back to table rows."""
+        rows = []
+        for s_ in range(tab.n_seg):
+            buf = tab.bufs[tab.seg_buf[s_]]
+            rows.append(self._unpack_seg(buf[tab.seg_off[s_]:], tab.seg_rows, tab.F))
+        dense = torch.cat(rows)
+        c = view.col.to(torch.int64)
+        t = (c >> tab.row_bits) * tab.seg_rows + (c & ((1 << tab.row_bits) - 1))
+        v = CSRView(rowptr=view.rowptr, col=t.to(torch.int32), eid=view.eid, n_rows=view.n_rows,
+                    n_cols=dense.size(0), n_edges=view.n_edges)
+        return dense, v
 
     def relu_bwd_colsum(self, dZ, Z, relu, want_db, row_div=None):
         dY = torch.where(Z > 0, dZ, torch.zeros_like(dZ)) if relu else dZ
@@ -193,6 +219,8 @@ class CpuBackend:
     # ------------------------------------------------------------ fused layer
     def spmm_xw_fwd(self, view, w, X, W, reduce, bias=None, relu=False, relu_mask=None,
                     want_z=False, out=None, z_out=None):
+        if not isinstance(X, torch.Tensor):  # a PackedTable
+            X, view = self._dense_table(X, view)
         rows, _, x = self._aggregate(view, w, X)
         Z = torch.zeros(view.n_rows, X.size(1)).index_add_(0, rows, x)
         A = Z
@@ -215,6 +243,8 @@ class CpuBackend:
 
     def spmm_xw_bwd_dx(self, view_t, w_t, row_scale, dY, W, relu_mask=None, row_div=None,
                        out=None, colsum=None):
+        if not isinstance(dY, torch.Tensor):  # a PackedTable
+            dY, view_t = self._dense_table(dY, view_t)
         dH = self.spmm_bwd(view_t, w_t, row_scale, dY, L.REDUCE_SUM)
         dX = _mm(dH, W.detach().t())
         cs = None

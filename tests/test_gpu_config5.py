@@ -67,6 +67,31 @@ def _mask_bits(rm, F):
     return ((rm.long()[:, word] >> bit) & 1).bool()
 
 
+def _packed_rows(tab, s_, i_):
+    """Rows i_ of segments s_ of a PackedTable, decoded from the buffers in
+    torch (pack.hip layout: row i's header pairs (mask_w, pos_w) at words
+    2 W i .. of its segment, its values at head + pos_0 ..)."""
+    F, W = tab.F, tab.F // 32
+    head = 2 * W * tab.seg_rows
+    out = torch.zeros(s_.numel(), F, dtype=torch.int32, device=s_.device)
+    seg_buf = torch.tensor(tab.seg_buf, device=s_.device)
+    seg_off = torch.tensor(tab.seg_off, dtype=torch.int64, device=s_.device)
+    for bi, buf in enumerate(tab.bufs):
+        sel = torch.nonzero(seg_buf[s_] == bi).view(-1)
+        if sel.numel() == 0:
+            continue
+        base = seg_off[s_[sel]]
+        h = base.view(-1, 1) + 2 * W * i_[sel].view(-1, 1) + torch.arange(2 * W, device=s_.device)
+        hdr = buf[h].to(torch.int64) & 0xFFFFFFFF
+        bits = ((hdr[:, 0::2].unsqueeze(-1) >> torch.arange(32, device=s_.device)) & 1).bool()
+        bits = bits.view(-1, F)
+        rank = torch.cumsum(bits.long(), 1) - 1
+        idx = base.view(-1, 1) + head + hdr[:, 1:2] + rank
+        vals = buf[torch.where(bits, idx, torch.zeros_like(idx))]
+        out[sel] = torch.where(bits, vals, torch.zeros_like(vals))
+    return out.view(torch.float32)
+
+
 class _Checks:
     def __init__(self):
         self.worst = {}
@@ -101,10 +126,16 @@ def _checking_backend(dinv, rng):
             deg = rp[1:] - rp[:-1]
             row_of = torch.repeat_interleave(torch.arange(e - o, device=cols.device), deg)
             me = sh.lo + a + o + row_of
-            other = _global_ids(cols, sh)
+            if isinstance(tab, torch.Tensor):
+                other = _global_ids(cols, sh)
+                g = tab[cols].to(torch.float64)
+            else:  # a packed table gathered in place: rows decoded from the segments
+                s_ = cols >> tab.row_bits
+                i_ = cols & ((1 << tab.row_bits) - 1)
+                other = _global_ids(s_ * tab.seg_rows + i_, sh)
+                g = _packed_rows(tab, s_, i_).to(torch.float64)
             w64 = dinv[me] * dinv[other]
-            g = tab[cols].to(torch.float64)
-            agg = torch.zeros(e - o, tab.size(1), dtype=torch.float64, device=g.device)
+            agg = torch.zeros(e - o, g.size(1), dtype=torch.float64, device=g.device)
             agg.index_add_(0, row_of, g * w64[:, None])
             absg = torch.zeros_like(agg).index_add_(0, row_of, g.abs() * w64.abs()[:, None])
             return agg, absg
@@ -222,6 +253,8 @@ def test_config5_rank_fp64(cuda, config5, rank):
     step = model.step_fn(None, None, X_table=Xt, dY_local=dYl)
     try:
         for packed in (False, True):
+            sh._tables = None  # (the dense run's persistent tables: freed before the packed run)
+            torch.cuda.empty_cache()
             mdist.set_pack_exchange(packed)
             be.checks = _Checks()
             mdist.STATS.update(dense_words=0, sent_words=0)

@@ -49,6 +49,24 @@ def _plan(cuda, ei, N, deg_norm):
     return plan, plan.norm(deg_norm)
 
 
+SENT = 0x7FBADBAD
+BAND = 4096
+
+
+def _guarded(shape, dev, dtype=torch.float32):
+    n = int(np.prod(shape))
+    base = torch.full((BAND + n + BAND,), SENT, dtype=torch.int32, device=dev)
+    mid = base[BAND:BAND + n]
+    if dtype == torch.float32:
+        mid = mid.view(torch.float32)
+    return base, mid.view(*shape)
+
+
+def _intact(base):
+    torch.cuda.synchronize()
+    return bool((base[:BAND] == SENT).all()) and bool((base[base.numel() - BAND:] == SENT).all())
+
+
 @pytest.fixture
 def xw_ws_full():
     from mgcn import _lib as L

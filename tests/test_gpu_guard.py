@@ -250,16 +250,21 @@ def test_pack_unpack_bands(cuda, F):
     for n in [1, 15, 17, 31, 33, 190]:
         rows = torch.relu(torch.randn(n, F, device=cuda, generator=g))
         words = F // 32
-        masks = Guarded((n, words), torch.int32, cuda)
         counts = Guarded((n,), torch.int32, cuda)
-        ops.pack_rows_count(rows, masks.t, counts.t)
+        # the count pass writes only the header's mask words: its guard bands
+        # and the interleaved position words must stay as they are
+        hdr = Guarded((n, 2 * words), torch.int32, cuda)
+        hdr.t.fill_(-1)
+        ops.pack_rows_count(rows, hdr.t, counts.t)
+        assert (hdr.t[:, 1::2] == -1).all()
         total = int(counts.t.sum())
         offs = torch.cumsum(counts.t, 0, dtype=torch.int32) - counts.t
-        seg = n * (1 + words) + total
+        seg = 2 * n * words + total
         send = Guarded((seg,), torch.int32, cuda)
-        send.t[:n] = offs
-        send.t[n:n + n * words] = masks.t.view(-1)
-        ops.pack_rows_values(rows, masks.t, offs, send.t[n * (1 + words):])
+        send.t[:2 * n * words] = hdr.t.view(-1)
+        ops.pack_rows_values(rows, offs, send.t[:2 * n * words].view(n, 2 * words),
+                             send.t[2 * n * words:])
+        masks = hdr
         P = 3
         recv = torch.cat([send.t] * P)
         out = Guarded((P * n, F), torch.float32, cuda)

@@ -34,15 +34,14 @@ def _pack_gpu(x, cuda):
     n, F = x.shape
     w = F // 32
     xs = x.to(cuda)
-    head = n * (1 + w)
+    head = 2 * n * w
     send = torch.empty(head + n * F, dtype=torch.int32, device=cuda)
     counts = torch.empty(n, dtype=torch.int32, device=cuda)
-    ops.pack_rows_count(xs, send[n:head].view(n, w), counts)
+    hdr = send[:head].view(n, 2 * w)
+    ops.pack_rows_count(xs, hdr, counts)
     total = int(counts.sum())
-    offs = send[:n]
-    torch.cumsum(counts, 0, dtype=torch.int32, out=offs)
-    offs.sub_(counts)
-    ops.pack_rows_values(xs, send[n:head].view(n, w), offs, send[head:head + total])
+    offs = torch.cumsum(counts, 0, dtype=torch.int32) - counts
+    ops.pack_rows_values(xs, offs, hdr, send[head:head + total])
     return send[:head + total].cpu(), counts.cpu()
 
 
@@ -51,13 +50,14 @@ def _pack_cpu(x):
     be = CpuBackend()
     n, F = x.shape
     w = F // 32
-    head = n * (1 + w)
+    head = 2 * n * w
     send = torch.empty(head + n * F, dtype=torch.int32)
     counts = torch.empty(n, dtype=torch.int32)
-    be.pack_count(x, send[n:head].view(n, w), counts)
+    hdr = send[:head].view(n, 2 * w)
+    be.pack_count(x, hdr, counts)
     total = int(counts.sum())
-    send[:n] = torch.cumsum(counts, 0, dtype=torch.int32) - counts
-    be.pack_values(x, send[n:head].view(n, w), send[:n], send[head:head + total])
+    offs = torch.cumsum(counts, 0, dtype=torch.int32) - counts
+    be.pack_values(x, offs, hdr, send[head:head + total])
     return send[:head + total], counts
 
 
@@ -91,10 +91,130 @@ def test_pack_rows_with_a_leading_dimension(cuda):
     x = big[:, :F]
     w = F // 32
     counts = torch.empty(n, dtype=torch.int32, device=cuda)
-    masks = torch.empty(n, w, dtype=torch.int32, device=cuda)
-    ops.pack_rows_count(x, masks, counts)
-    ref_m = torch.empty(n, w, dtype=torch.int32)
+    hdr = torch.empty(n, 2 * w, dtype=torch.int32, device=cuda)
+    ops.pack_rows_count(x, hdr, counts)
+    ref_h = torch.empty(n, 2 * w, dtype=torch.int32)
     ref_c = torch.empty(n, dtype=torch.int32)
     from cpu_backend import CpuBackend
-    CpuBackend().pack_count(x.cpu().contiguous(), ref_m, ref_c)
-    assert torch.equal(masks.cpu(), ref_m) and torch.equal(counts.cpu(), ref_c)
+    CpuBackend().pack_count(x.cpu().contiguous(), ref_h, ref_c)
+    assert torch.equal(hdr.cpu()[:, 0::2], ref_h[:, 0::2]) and torch.equal(counts.cpu(), ref_c)
+
+
+# ------------------------------------------------- in-place packed gather
+def _packed_table(T, cr, cuda, n_bufs=2):
+    """T [S cr, F] (S segments of cr rows) packed segment by segment into
+    n_bufs separate device buffers: a PackedTable over them."""
+    from mgcn import ops
+    S = T.size(0) // cr
+    segs = [_pack_gpu(T[s * cr:(s + 1) * cr], cuda)[0] for s in range(S)]
+    per = -(-S // n_bufs)
+    bufs, seg_buf, seg_off = [], [], []
+    for b in range(n_bufs):
+        part = segs[b * per:(b + 1) * per]
+        if not part:
+            break
+        off = 0
+        words = []
+        for p in part:
+            seg_buf.append(len(bufs))
+            seg_off.append(off)
+            words.append(p)
+            off += p.numel()
+        words.append(torch.zeros(4, dtype=torch.int32))  # the 16-B value reads' slack
+        bufs.append(torch.cat(words).to(cuda))
+    return ops.PackedTable(bufs, seg_buf, seg_off, cr, ops.packed_row_bits(cr), T.size(1))
+
+
+def _graph_view(rng, n_rows, T_rows, E, cuda, heavy=0):
+    from mgcn.graph import CSRView
+    dst = np.concatenate([rng.integers(0, n_rows, E), np.zeros(heavy, np.int64)])
+    src = np.concatenate([rng.integers(0, T_rows, E), rng.integers(0, T_rows, heavy)])
+    order = np.argsort(dst, kind="stable")
+    rowptr = np.zeros(n_rows + 1, np.int64)
+    rowptr[1:] = np.cumsum(np.bincount(dst, minlength=n_rows))
+    col = src[order].astype(np.int32)
+    w = rng.uniform(0.1, 1.0, len(col)).astype(np.float32)
+    v = CSRView(rowptr=torch.from_numpy(rowptr).to(cuda), col=torch.from_numpy(col).to(cuda),
+                eid=torch.from_numpy(order.astype(np.int32)).to(cuda), n_rows=n_rows,
+                n_cols=T_rows)
+    return v, torch.from_numpy(w).to(cuda)
+
+
+def _mask256(Z):
+    """[rows, 8] ReLU mask words of a 256-wide layer (fused_wide.hip layout:
+    feature f at word 4 (f >> 7) + (f & 3), bit (f & 127) >> 2)."""
+    f = torch.arange(256, device=Z.device)
+    word = 4 * (f >> 7) + (f & 3)
+    bit = (f & 127) >> 2
+    m = torch.zeros(Z.size(0), 8, dtype=torch.int64, device=Z.device)
+    m.index_add_(1, word, (Z > 0).long() << bit)
+    return torch.where(m >= 2 ** 31, m - 2 ** 32, m).to(torch.int32)
+
+
+def _pk_view(v, cr, rb):
+    from mgcn import ops
+    from mgcn.graph import CSRView
+    return CSRView(rowptr=v.rowptr, col=ops.packed_cols(v.col, cr, rb), eid=v.eid,
+                   n_rows=v.n_rows, n_cols=v.n_cols)
+
+
+@pytest.mark.parametrize("n_rows,cr,S,E,heavy", [(5000, 700, 6, 60000, 0), (33, 1000, 3, 300, 150),
+                                                 (4097, 4097, 2, 50000, 0)])
+@pytest.mark.parametrize("mean", [False, True])
+def test_packed_gather_forward_bitwise_the_dense_table(cuda, n_rows, cr, S, E, heavy, mean):
+    """mgcn_spmm_xw_fwd_packed == mgcn_spmm_xw_fwd on the unpacked table: Y,
+    Z and the ReLU mask words bit for bit (ragged segments, rows past 64
+    slots, empty rows, -0.0 values, two receive buffers)."""
+    from mgcn import _lib as L
+    from mgcn import ops
+    F = 256
+    rng = np.random.default_rng(n_rows + S)
+    T = torch.relu(torch.randn(S * cr, F, generator=torch.Generator().manual_seed(S)))
+    T[::7, ::5] = -0.0
+    tab = _packed_table(T, cr, cuda)
+    v, w = _graph_view(rng, n_rows, S * cr, E, cuda, heavy)
+    vp = _pk_view(v, cr, tab.row_bits)
+    g = torch.Generator(device=cuda).manual_seed(1)
+    W = torch.randn(F, F, device=cuda, generator=g) * 0.1
+    b = torch.randn(F, device=cuda, generator=g)
+    red = L.REDUCE_MEAN if mean else L.REDUCE_SUM
+    outs = []
+    for view, X in ((v, T.to(cuda)), (vp, tab)):
+        rm = torch.empty(n_rows, 8, dtype=torch.int32, device=cuda)
+        y, z = ops.spmm_xw_fwd(view, w, X, W, red, b, True, relu_mask=rm, want_z=True)
+        outs.append((y, z, rm))
+    for a, b_ in zip(*outs):
+        assert torch.equal(a.view(torch.int32), b_.view(torch.int32))
+
+
+@pytest.mark.parametrize("n_rows,cr,S,E", [(5000, 700, 6, 60000), (33, 1000, 3, 300)])
+@pytest.mark.parametrize("epi", ["store", "relu", "relu_div"])
+def test_packed_gather_adjoint_bitwise_the_dense_table(cuda, n_rows, cr, S, E, epi):
+    """mgcn_spmm_xw_bwd_packed == the dX-only mgcn_spmm_xw_bwd on the unpacked
+    table: dX bit for bit, the accumulated column sums too."""
+    from mgcn import ops
+    F = 256
+    rng = np.random.default_rng(7 * n_rows + S)
+    T = torch.randn(S * cr, F, generator=torch.Generator().manual_seed(S + 1))
+    T = torch.where(torch.rand(S * cr, F, generator=torch.Generator().manual_seed(2)) < 0.5,
+                    torch.zeros(()), T)
+    tab = _packed_table(T, cr, cuda, n_bufs=3)
+    v, w = _graph_view(rng, n_rows, S * cr, E, cuda)
+    vp = _pk_view(v, cr, tab.row_bits)
+    g = torch.Generator(device=cuda).manual_seed(3)
+    W = torch.randn(F, F, device=cuda, generator=g) * 0.1
+    rs = torch.rand(n_rows, device=cuda, generator=g)
+    rm = rd = None
+    if epi != "store":
+        rm = _mask256(torch.randn(n_rows, F, device=cuda, generator=g))
+    if epi == "relu_div":
+        rd = torch.randint(1, 9, (n_rows,), device=cuda, generator=g).float()
+    outs = []
+    for view, X in ((v, T.to(cuda)), (vp, tab)):
+        cs = torch.full((F,), 0.5, device=cuda) if rm is not None else None
+        _, dX, c = ops.spmm_xw_bwd(view, w, rs, X, None, W, relu_mask=rm, row_div=rd,
+                                   colsum_acc=cs)
+        outs.append((dX, c))
+    assert torch.equal(outs[0][0].view(torch.int32), outs[1][0].view(torch.int32))
+    if rm is not None:
+        assert torch.equal(outs[0][1], outs[1][1])
