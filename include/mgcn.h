@@ -738,8 +738,8 @@ int mgcn_unpack_rows(int64_t n_seg, int64_t n, int32_t F, const uint32_t *buf, i
                      float *T, int64_t ldt, void *stream);
 
 /*
- * A packed exchange table gathered in place (ABI 21; the fused 256-wide
- * layer kernels).  The zero-skipping exchange delivers a table of C row
+ * A packed exchange table gathered in place (ABI 21; the fused 128- and
+ * 256-wide layer kernels).  The zero-skipping exchange delivers a table of C row
  * chunks x P ranks as C * P packed segments of `seg_rows` rows each (the
  * layout above, segment s = c P + k at words + seg_base[s]); instead of
  * expanding them into a dense [C P seg_rows, F] table (mgcn_unpack_rows: a
@@ -749,6 +749,11 @@ int mgcn_unpack_rows(int64_t n_seg, int64_t n, int32_t F, const uint32_t *buf, i
  * column indices address packed rows as col = (s << row_bits) | i (row i of
  * segment s; mgcn.dist builds these once per shard).  Results are bit for bit
  * those of the dense table (every +0.0 the packing skipped is folded as 0.0).
+ * F = 128: the kernels read the whole table through ONE 32-bit range (the two
+ * rows a wave gathers at once are addressed per lane), so every seg_base lies
+ * in 0 .. n_words and n_words * 4 <= 2 GiB - 16 B (one receive buffer;
+ * MGCN_EINVAL otherwise).  F = 256 (a wave per row, its address in SGPRs):
+ * segments anywhere in one device's address space.
  */
 typedef struct mgcn_packed_table {
   const uint32_t *words;   /* device: base the segment offsets count from */
@@ -756,26 +761,26 @@ typedef struct mgcn_packed_table {
   int32_t n_seg;           /* C * P segments, 1 .. 64 */
   int32_t seg_rows;        /* rows per segment (the chunk rows) */
   int32_t row_bits;        /* col = (s << row_bits) | i; seg_rows <= 2^row_bits */
-  int32_t F;               /* row width (256) */
+  int32_t F;               /* row width (128 or 256) */
   int64_t seg_base[64];    /* word offset of segment s from `words` (host values,
                               passed to the kernels by value; the segments may
                               live in separate allocations of one device) */
 } mgcn_packed_table;
 
-/* mgcn_spmm_xw_fwd (F_in = F_out = 256, sum / mean) gathering X from a packed
- * table: Y = epi((A X) W + b) (+ Z = A X, + ReLU mask words) -- bit for bit
- * mgcn_spmm_xw_fwd on the unpacked table.  Scratch:
- * mgcn_spmm_xw_fwd_workspace_bytes(256, 256). */
+/* mgcn_spmm_xw_fwd (F_in = F_out = 128 or 256, sum / mean) gathering X from a
+ * packed table: Y = epi((A X) W + b) (+ Z = A X, + ReLU mask words) -- bit for
+ * bit mgcn_spmm_xw_fwd on the unpacked table.  Scratch:
+ * mgcn_spmm_xw_fwd_workspace_bytes(F, F). */
 int mgcn_spmm_xw_fwd_packed(int64_t n_rows, int32_t F_in, int32_t F_out, const int64_t *rowptr,
                             const int32_t *col, const float *w, const mgcn_packed_table *X,
                             const float *W, int64_t ldw, const float *bias, float *Y,
                             int64_t ldy, int reduce, int relu, uint32_t *relu_mask, float *Z,
                             int64_t ldz, void *workspace, size_t workspace_bytes, void *stream);
 
-/* mgcn_spmm_xw_bwd's dX-only form (F = 256) gathering dY from a packed table:
- * dX = relu'(lower) ((A^T dY [* row_scale]) W^T) [/ row_div], colsum (+)=
- * sum_rows dX -- bit for bit the dense-table call.  Scratch:
- * mgcn_spmm_xw_bwd_workspace_bytes(n_rows, 256, 256). */
+/* mgcn_spmm_xw_bwd's dX-only form (F = 128 or 256) gathering dY from a packed
+ * table: dX = relu'(lower) ((A^T dY [* row_scale]) W^T) [/ row_div], colsum
+ * (+)= sum_rows dX -- bit for bit the dense-table call.  Scratch:
+ * mgcn_spmm_xw_bwd_workspace_bytes(n_rows, F, F). */
 int mgcn_spmm_xw_bwd_packed(int64_t n_rows, int32_t F_in, int32_t F_out, const int64_t *rowptr_t,
                             const int32_t *col_t, const float *w_t, const float *row_scale,
                             const mgcn_packed_table *dY, const float *W, int64_t ldw, float *dX,

@@ -190,6 +190,7 @@ struct RowMeta {
   int mc;
   float mw;
   int ms;  // max adjoint (meta_first_m): fwd slot of the lane's edge
+  int mv;  // packed table (meta_first_pk): word offset of the lane's edge's segment values
 };
 
 __device__ __forceinline__ void meta_rowptr(const int64_t *__restrict__ rowptr, int64_t row,
@@ -262,6 +263,125 @@ __device__ __forceinline__ void gather_row_meta(const __amdgpu_buffer_rsrc_t rx,
           acc[1] = __fadd_rn(acc[1], __fmul_rn(xv[u].y, wk[u]));
           acc[2] = __fadd_rn(acc[2], __fmul_rn(xv[u].z, wk[u]));
           acc[3] = __fadd_rn(acc[3], __fmul_rn(xv[u].w, wk[u]));
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// In-place gather from a PACKED table at F = 128 (round 6; pack.hip's layout;
+// fused_wide.hip's wide_gather2_pk is the 256-wide form).  The two lane groups
+// of a wave walk different rows, so a row's address is per lane: the table is
+// read through ONE buffer resource (every segment at a word offset below
+// 2^29, the mgcn_spmm_xw_*_packed check), and the metadata loads turn a
+// slot's packed col (s << rbits) | i into the word offsets of its row header
+// (base[s] + 8 i) and of its segment's values (base[s] + head) -- base[]
+// lane-resident, one ds_bpermute per 32 slots, not per slot.  Lane gl reads
+// the header pair w = gl / 8 (8 B), then 16 B of values at pos_w +
+// popc(mask_w below bit 4 (gl % 8)), expanded by pk_expand: the dense row's
+// bits, so the fold is gather_row_meta's, bit for bit.  The headers of batch
+// k + 1 (after a row's last batch: the next row's first) load under batch k's
+// values, so a row costs the dense gather's round trips.
+struct Pk128 {
+  __amdgpu_buffer_rsrc_t r;  // the whole table
+  uint32_t rbits, head;      // col = (s << rbits) | i; head = seg_rows * 8 words
+  uint32_t base;             // lane-resident: base[lane], word offset of segment `lane`
+};
+
+// packed col -> (header word offset, value-area word offset); all lanes
+// active (ds_bpermute), masked slots carry col 0
+__device__ __forceinline__ void pk128_meta(const Pk128 &pk, int c, int &mh, int &mv) {
+  const uint32_t s = (uint32_t)c >> pk.rbits;
+  const uint32_t i = (uint32_t)c & ((1u << pk.rbits) - 1u);
+  const uint32_t b = (uint32_t)__shfl((int)pk.base, (int)(s & 63u), 64);
+  mh = (int)(b + 8u * i);
+  mv = (int)(b + pk.head);
+}
+
+__device__ __forceinline__ void meta_first_pk(const Pk128 &pk, const int32_t *__restrict__ col,
+                                              const float *__restrict__ w, int gl, RowMeta &m) {
+  meta_first(col, w, gl, m);
+  pk128_meta(pk, m.mc, m.mc, m.mv);
+}
+
+// the header pairs of slots k0 .. k0 + U - 1 of the group's row (slots past
+// n: the "no load" offset, the pair reads 0 and its values are never read)
+template <int U>
+__device__ __forceinline__ void pk128_headers(const Pk128 &pk, int mh, int grp, int k0, int n,
+                                              uint32_t hoff, u32x2 (&h)[U]) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int k = k0 + u;
+    const uint32_t hk = (uint32_t)bcast_g(mh, grp, k & 31);
+    h[u] = __builtin_amdgcn_raw_buffer_load_b64(pk.r, k < n ? 4u * hk + hoff : 0xfffffff0u, 0, 0);
+  }
+}
+
+// gather_row_meta from a packed table: hh holds, on entry, the header pairs
+// of the row's first U slots and, on return, those of row nx's
+template <int U>
+__device__ __forceinline__ void gather_row_meta_pk(const Pk128 &pk, const int32_t *__restrict__ col,
+                                                   const float *__restrict__ w, const RowMeta &m,
+                                                   const RowMeta &nx, int gl, int grp,
+                                                   float (&acc)[4], u32x2 (&hh)[U]) {
+  const int64_t beg = m.beg, deg = m.deg;
+  const int64_t odeg = __shfl_xor(deg, 32, 64);
+  const int64_t maxdeg = deg > odeg ? deg : odeg;
+  // (two empty rows still run one all-masked batch: the next rows' headers
+  // are issued from the one call site below)
+  const int64_t maxdeg1 = maxdeg > 0 ? maxdeg : 1;
+  acc[0] = acc[1] = acc[2] = acc[3] = 0.0f;
+  int mh = m.mc, mv = m.mv;
+  float mw = m.mw;
+  const uint32_t hoff = 8u * (uint32_t)(gl >> 3);
+  const uint32_t sh = 4u * (uint32_t)(gl & 7);  // the lane's nibble in mask_w
+  const uint32_t below = (1u << sh) - 1u;
+  const int nn = nx.deg < 32 ? nx.deg : 32;
+  for (int64_t e0 = 0; e0 < maxdeg1; e0 += 32) {
+    const int64_t rem = deg - e0;
+    const int nb = rem <= 0 ? 0 : (rem < 32 ? (int)rem : 32);
+    const int64_t remw = maxdeg1 - e0;
+    const int nbmax = remw < 32 ? (int)remw : 32;  // wave-uniform
+    if (e0 > 0) {  // rows longer than one metadata batch load the rest in place
+      const int64_t my = e0 + gl;
+      int c = 0;
+      mw = 1.0f;
+      if (my < deg) {
+        c = col[beg + my];
+        if (w != nullptr) mw = w[beg + my];
+      }
+      pk128_meta(pk, c, mh, mv);
+      pk128_headers<U>(pk, mh, grp, 0, nb, hoff, hh);
+    }
+    const bool last_window = e0 + 32 >= maxdeg1;
+    for (int k0 = 0; k0 < nbmax; k0 += U) {
+      u32x4 v[U];
+      uint32_t nib[U];
+      float wk[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = k0 + u;
+        wk[u] = bcast_g(mw, grp, k & 31);
+        const uint32_t vk = (uint32_t)bcast_g(mv, grp, k & 31);
+        nib[u] = (hh[u][0] >> sh) & 0xfu;
+        const uint32_t q = hh[u][1] + (uint32_t)__builtin_popcount(hh[u][0] & below);
+        // a lane with no nonzero word moves no bytes (offset past the range)
+        v[u] = __builtin_amdgcn_raw_buffer_load_b128(pk.r, nib[u] ? 4u * (vk + q) : 0xfffffff0u, 0, 0);
+      }
+      // the next headers, under these values: this window's next batch, or
+      // (the last batch of the last window) row nx's first -- one call site
+      const bool more = k0 + U < nbmax;
+      if (more || last_window)
+        pk128_headers<U>(pk, more ? mh : nx.mc, grp, more ? k0 + U : 0, more ? nb : nn, hoff, hh);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (k0 + u < nb) {  // strictly ascending edge order (gather_row_meta)
+          const float4 x = pk_expand(nib[u], v[u]);
+          acc[0] = __fadd_rn(acc[0], __fmul_rn(x.x, wk[u]));
+          acc[1] = __fadd_rn(acc[1], __fmul_rn(x.y, wk[u]));
+          acc[2] = __fadd_rn(acc[2], __fmul_rn(x.z, wk[u]));
+          acc[3] = __fadd_rn(acc[3], __fmul_rn(x.w, wk[u]));
         }
       }
     }
@@ -437,9 +557,13 @@ struct XwArgs {
   int64_t ldz;
   int mean;
   int relu;
+  // packed table (PK kernels; mgcn_spmm_xw_fwd_packed): X unused
+  const uint32_t *pk;
+  uint32_t pk_bytes, pk_rbits, pk_head;
+  uint32_t pk_base[64];
 };
 
-template <int U>
+template <int U, bool PK = false>
 __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_fwd_kernel(const XwArgs a) {
   __shared__ __attribute__((aligned(16))) char lds[kXfLds];
   const int tid = threadIdx.x;
@@ -450,8 +574,16 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_fwd_kernel(c
   const int64_t n_chunks = (a.n_rows + kXwRows - 1) / kXwRows;
   const bool has_b = a.bias != nullptr;
   // gathers through one buffer resource over X: 32-bit offsets, 1 VGPR each
-  const auto rx = buf_rsrc(a.X, (uint32_t)(a.n_cols * a.ldx * 4));
+  const auto rx = buf_rsrc(PK ? nullptr : a.X, PK ? 0u : (uint32_t)(a.n_cols * a.ldx * 4));
   const uint32_t ldx_b = (uint32_t)a.ldx * 4u;
+  Pk128 pk{};
+  u32x2 hh[PK ? U : 1];
+  if constexpr (PK) {
+    pk.r = buf_rsrc(a.pk, a.pk_bytes);
+    pk.rbits = a.pk_rbits;
+    pk.head = a.pk_head;
+    pk.base = a.pk_base[lane];
+  }
 
   // W fragments of this wave's 16 output columns: B[k][n] = W[k][n], lane
   // (g4, l16) holds k = 32 ks + 8 g4 + j of column n = 16 wave + l16
@@ -499,7 +631,12 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_fwd_kernel(c
                    a.n_rows};
   RowMeta cur, nxt;
   meta_rowptr(a.rowptr, seq.row(0), seq.row(0) < a.n_rows, cur);
-  meta_first(a.col, a.w, gl, cur);
+  if constexpr (PK) {
+    meta_first_pk(pk, a.col, a.w, gl, cur);
+    pk128_headers<U>(pk, cur.mc, grp, 0, cur.deg < 32 ? cur.deg : 32, 8u * (uint32_t)(gl >> 3), hh);
+  } else {
+    meta_first(a.col, a.w, gl, cur);
+  }
   meta_rowptr(a.rowptr, seq.row(1), seq.row(1) < a.n_rows, nxt);
   int it = 0;
   for (int64_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x, ++it) {
@@ -511,12 +648,18 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_fwd_kernel(c
     for (int p = 0; p < 2; ++p) {
       const int lr = 16 * p + 2 * wave + grp;
       const int64_t k = 2 * it + p;
-      meta_first(a.col, a.w, gl, nxt);
+      if constexpr (PK)
+        meta_first_pk(pk, a.col, a.w, gl, nxt);
+      else
+        meta_first(a.col, a.w, gl, nxt);
       RowMeta nn;
       const int64_t r2 = seq.row(k + 2);
       meta_rowptr(a.rowptr, r2, r2 < a.n_rows && k + 2 < 2 * n_my, nn);
       float acc[4];
-      gather_row_meta<U>(rx, ldx_b, a.col, a.w, cur, gl, grp, acc);
+      if constexpr (PK)
+        gather_row_meta_pk<U>(pk, a.col, a.w, cur, nxt, gl, grp, acc, hh);
+      else
+        gather_row_meta<U>(rx, ldx_b, a.col, a.w, cur, gl, grp, acc);
       if (a.Z != nullptr) {
         // the aggregate the backward's dW = Z^T dY reads (whole 512-B rows;
         // rows past the end fall outside the chunk's buffer range)
@@ -604,6 +747,10 @@ struct XbArgs {
   float *colsum_partial;  // [grid][128]
   const uint32_t *win_mask;  // max adjoint: winner bits per fwd slot ([nnz][4])
   const int32_t *slot_map;   // max adjoint: fwd slot of every bwd slot
+  // packed dY (dX-only PK kernel; mgcn_spmm_xw_bwd_packed): dY unused
+  const uint32_t *pk;
+  uint32_t pk_bytes, pk_rbits, pk_head;
+  uint32_t pk_base[64];
 };
 
 #ifdef MGCN_XW_PROFILE
@@ -620,8 +767,9 @@ __device__ unsigned long long g_xprof[2][64][6];
 // DW = false: dX only (X == NULL) -- the caller forms dW = Z^T dY from the
 // forward's aggregate (mgcn_gemm_bwd, dW-only), so the chunk's X rows, their
 // images and the dW MFMAs drop out.
-template <int U, bool DX, int EPI, bool MAXM, bool DW = true>
+template <int U, bool DX, int EPI, bool MAXM, bool DW = true, bool PK = false>
 __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(const XbArgs a) {
+  static_assert(!PK || (!DW && !MAXM), "the packed gather serves the dX-only adjoint");
   __shared__ __attribute__((aligned(16))) char lds[kXbLds];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -630,8 +778,16 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
   const int h = lane >> 5, lc = lane & 31;
   const int l16 = lane & 15, g4 = lane >> 4;
   const int64_t n_chunks = (a.n_rows + kXwRows - 1) / kXwRows;
-  const auto rdy = buf_rsrc(a.dY, (uint32_t)(a.n_cols * a.lddy * 4));
+  const auto rdy = buf_rsrc(PK ? nullptr : a.dY, PK ? 0u : (uint32_t)(a.n_cols * a.lddy * 4));
   const uint32_t ldy_b = (uint32_t)a.lddy * 4u;
+  Pk128 pk{};
+  u32x2 hh[PK ? U : 1];
+  if constexpr (PK) {
+    pk.r = buf_rsrc(a.pk, a.pk_bytes);
+    pk.rbits = a.pk_rbits;
+    pk.head = a.pk_head;
+    pk.base = a.pk_base[lane];
+  }
   float *stage = reinterpret_cast<float *>(lds + kXbStageOff);
   const float *wp = a.W + (int64_t)(16 * wave + l16) * a.ldw + 8 * g4;  // B[k][n] = W[n][k]
 
@@ -728,7 +884,12 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
   RowMeta cur{}, nxt{};
   if constexpr (!DW && !MAXM) {
     meta_rowptr(a.rowptr, seq.row(0), seq.row(0) < a.n_rows, cur);
-    meta_first(a.col, a.w, gl, cur);
+    if constexpr (PK) {
+      meta_first_pk(pk, a.col, a.w, gl, cur);
+      pk128_headers<U>(pk, cur.mc, grp, 0, cur.deg < 32 ? cur.deg : 32, 8u * (uint32_t)(gl >> 3), hh);
+    } else {
+      meta_first(a.col, a.w, gl, cur);
+    }
     meta_rowptr(a.rowptr, seq.row(1), seq.row(1) < a.n_rows, nxt);
   }
   int it = 0;
@@ -771,11 +932,17 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
       float acc[4];
       if constexpr (!DW && !MAXM) {
         const int64_t k = 2 * it + p;
-        meta_first(a.col, a.w, gl, nxt);
+        if constexpr (PK)
+          meta_first_pk(pk, a.col, a.w, gl, nxt);
+        else
+          meta_first(a.col, a.w, gl, nxt);
         RowMeta nn;
         const int64_t rk2 = seq.row(k + 2);
         meta_rowptr(a.rowptr, rk2, rk2 < a.n_rows && k + 2 < 2 * n_my, nn);
-        gather_row_meta<U>(rdy, ldy_b, a.col, a.w, cur, gl, grp, acc);
+        if constexpr (PK)
+          gather_row_meta_pk<U>(pk, a.col, a.w, cur, nxt, gl, grp, acc, hh);
+        else
+          gather_row_meta<U>(rdy, ldy_b, a.col, a.w, cur, gl, grp, acc);
         cur = nxt;
         nxt = nn;
       } else {
@@ -896,6 +1063,9 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
 }
 
 int g_xw_unroll = 5;  // forward gathers in flight per row (5: config 2 5.06 -> 5.005 ms/step; 6 spills)
+// packed-table forms: slots in flight per row (experiment builds sweep them)
+int g_xw_pk_unroll = 4;
+int g_xw_pk_bwd_unroll = 3;
 
 int xw_grid() {
   int dev = 0, cus = 256;
@@ -905,28 +1075,28 @@ int xw_grid() {
   return kXwPerCU * cus;
 }
 
-template <int U>
+template <int U, bool PK = false>
 int launch_xw(const XwArgs &a, hipStream_t s) {
   const int64_t n_chunks = (a.n_rows + kXwRows - 1) / kXwRows;
   int64_t grid = xw_grid();
   if (grid > n_chunks) grid = n_chunks;
-  hipLaunchKernelGGL((spmm_xw_fwd_kernel<U>), dim3((unsigned)grid), dim3(kXwThreads), 0, s, a);
+  hipLaunchKernelGGL((spmm_xw_fwd_kernel<U, PK>), dim3((unsigned)grid), dim3(kXwThreads), 0, s, a);
   return check_launch("spmm_xw_fwd_kernel");
 }
 
-template <int U, bool DX, int EPI, bool MAXM, bool DW = true>
+template <int U, bool DX, int EPI, bool MAXM, bool DW = true, bool PK = false>
 int launch_xb(const XbArgs &a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((spmm_xw_bwd_kernel<U, DX, EPI, MAXM, DW>), dim3((unsigned)grid),
+  hipLaunchKernelGGL((spmm_xw_bwd_kernel<U, DX, EPI, MAXM, DW, PK>), dim3((unsigned)grid),
                      dim3(kXwThreads), 0, s, a);
   return check_launch("spmm_xw_bwd_kernel");
 }
 
 // dX only (no X, no dW), sum adjoint
-template <int U>
+template <int U, bool PK = false>
 int launch_xb_dx(const XbArgs &a, int epi, int grid, hipStream_t s) {
-  if (epi == EPI_RELU_DIV) return launch_xb<U, true, EPI_RELU_DIV, false, false>(a, grid, s);
-  if (epi == EPI_RELU) return launch_xb<U, true, EPI_RELU, false, false>(a, grid, s);
-  return launch_xb<U, true, EPI_STORE, false, false>(a, grid, s);
+  if (epi == EPI_RELU_DIV) return launch_xb<U, true, EPI_RELU_DIV, false, false, PK>(a, grid, s);
+  if (epi == EPI_RELU) return launch_xb<U, true, EPI_RELU, false, false, PK>(a, grid, s);
+  return launch_xb<U, true, EPI_STORE, false, false, PK>(a, grid, s);
 }
 
 template <int U, bool MAXM>
@@ -1466,6 +1636,14 @@ int xw_set_ws(const char *name, int value) {
     set_error("%s: unsupported value %d", name, value);
     return (int)MGCN_EINVAL;
   };
+  if (n == "xw_pk_unroll" || n == "xw_pk_bwd_unroll") {  // (experiment builds: the sweep)
+    if (!MGCN_EXPERIMENT) {
+      set_error("%s: experiment builds only (make exp -> libmgcn_exp.so)", name);
+      return MGCN_EINVAL;
+    }
+    return n == "xw_pk_unroll" ? unroll(g_xw_pk_unroll, {3, 4, 5, 6})
+                               : unroll(g_xw_pk_bwd_unroll, {2, 3, 4});
+  }
   if (n == "xw_ws_max") return flag(g_xw_ws_max);
   if (n == "xw_ws_full") return flag(g_xw_ws_full);
   if (n == "xw_ws_dbg") {  // (timing experiments: results WRONG when set)
@@ -1767,19 +1945,39 @@ extern "C" int mgcn_debug_xw_prof(unsigned long long *host) {
 
 // ---------------------------------------------------------------- packed tables
 namespace {
-int check_packed(const mgcn_packed_table *t, const char *who) {
+int check_packed(const mgcn_packed_table *t, int32_t F, const char *who) {
   MGCN_REQUIRE(t != nullptr && t->words != nullptr, "%s: null packed table", who);
-  MGCN_REQUIRE(t->F == 256, "%s: packed tables of F = 256 only (got %d)", who, t->F);
+  MGCN_REQUIRE(t->F == F, "%s: packed table of F = %d for a layer of F = %d", who, t->F, F);
   MGCN_REQUIRE(t->n_seg >= 1 && t->n_seg <= 64, "%s: n_seg %d outside 1 .. 64", who, t->n_seg);
   MGCN_REQUIRE(t->row_bits >= 0 && t->row_bits + 6 <= 31 && t->seg_rows >= 1 &&
                    (int64_t)t->seg_rows <= ((int64_t)1 << t->row_bits),
                "%s: seg_rows %d does not fit row_bits %d", who, t->seg_rows, t->row_bits);
   // in-segment byte offsets stay below 2 GiB (the header plus a dense-size
   // value area): the kernels' buffer ranges are capped there
-  MGCN_REQUIRE((uint64_t)t->seg_rows * (2 * 8 + 256) * 4u + 16u < (1ull << 31),
+  MGCN_REQUIRE((uint64_t)t->seg_rows * (2 * (F / 32) + F) * 4u + 16u < (1ull << 31),
                "%s: seg_rows %d too large for the 2-GiB in-segment offsets", who, t->seg_rows);
   MGCN_REQUIRE(t->n_words >= 0, "%s: negative n_words", who);
+  if (F == kXwF) {
+    // F = 128: one buffer resource over the whole table (32-bit offsets)
+    MGCN_REQUIRE((uint64_t)t->n_words * 4u <= 0x7ffffff0ull,
+                 "%s: an F = 128 packed table spans at most 2 GiB - 16 B (got %lld words)", who,
+                 (long long)t->n_words);
+    for (int s = 0; s < t->n_seg; ++s)
+      MGCN_REQUIRE(t->seg_base[s] >= 0 && t->seg_base[s] <= t->n_words,
+                   "%s: segment %d at word %lld outside the table's %lld words", who, s,
+                   (long long)t->seg_base[s], (long long)t->n_words);
+  }
   return MGCN_OK;
+}
+
+// the F = 128 kernels' view of a checked packed table
+template <class Args>
+void fill_pk128(Args &a, const mgcn_packed_table *t) {
+  a.pk = t->words;
+  a.pk_bytes = (uint32_t)(t->n_words * 4);
+  a.pk_rbits = (uint32_t)t->row_bits;
+  a.pk_head = (uint32_t)t->seg_rows * 8u;
+  for (int s = 0; s < 64; ++s) a.pk_base[s] = s < t->n_seg ? (uint32_t)t->seg_base[s] : 0u;
 }
 }  // namespace
 
@@ -1792,12 +1990,46 @@ extern "C" int mgcn_spmm_xw_fwd_packed(int64_t n_rows, int32_t F_in, int32_t F_o
   clear_error();
   if (int rc = take_device_error()) return rc;  // a previous launch failed on the device
   MGCN_REQUIRE(n_rows >= 0, "mgcn_spmm_xw_fwd_packed: negative size");
-  MGCN_REQUIRE(F_in == 256 && F_out == 256 && mgcn_spmm_xw_supported(F_in, F_out, reduce),
-               "mgcn_spmm_xw_fwd_packed: 256 x 256, sum / mean, bf16x6 only");
+  MGCN_REQUIRE(mgcn_spmm_xw_supported(F_in, F_out, reduce),
+               "mgcn_spmm_xw_fwd_packed: 128 x 128 or 256 x 256, sum / mean, bf16x6 only");
   MGCN_REQUIRE(relu_mask == nullptr || relu, "mgcn_spmm_xw_fwd_packed: relu_mask needs relu");
   if (n_rows == 0) return MGCN_OK;
-  if (int rc = check_packed(X, "mgcn_spmm_xw_fwd_packed")) return rc;
+  if (int rc = check_packed(X, F_in, "mgcn_spmm_xw_fwd_packed")) return rc;
   MGCN_REQUIRE(rowptr && W && Y, "mgcn_spmm_xw_fwd_packed: null array");
+  if (F_in == kXwF) {
+    MGCN_REQUIRE(ldw >= F_out && ldy >= F_out && (uint64_t)kXwRows * (uint64_t)ldy * 4u < (1ull << 31),
+                 "mgcn_spmm_xw_fwd_packed: bad ldw / ldy");
+    MGCN_REQUIRE(bias == nullptr || reinterpret_cast<uintptr_t>(bias) % 4 == 0,
+                 "mgcn_spmm_xw_fwd_packed: bias not 4-byte aligned");
+    MGCN_REQUIRE(relu_mask == nullptr || reinterpret_cast<uintptr_t>(relu_mask) % 16 == 0,
+                 "mgcn_spmm_xw_fwd_packed: relu_mask not 16-byte aligned");
+    MGCN_REQUIRE(Z == nullptr || (ldz >= F_in && ldz % 4 == 0 && reinterpret_cast<uintptr_t>(Z) % 16 == 0 &&
+                                  (uint64_t)kXwRows * (uint64_t)ldz * 4u < (1ull << 31)),
+                 "mgcn_spmm_xw_fwd_packed: Z must have 16-byte aligned rows (ldz >= F_in)");
+    XwArgs a{};
+    a.n_rows = n_rows;
+    a.rowptr = rowptr;
+    a.col = col;
+    a.w = w;
+    a.W = W;
+    a.ldw = ldw;
+    a.bias = bias;
+    a.Y = Y;
+    a.ldy = ldy;
+    a.relu_mask = relu_mask;
+    a.Z = Z;
+    a.ldz = ldz;
+    a.mean = reduce == MGCN_REDUCE_MEAN;
+    a.relu = relu != 0;
+    fill_pk128(a, X);
+    hipStream_t s = as_stream(stream);
+    // (the product build instantiates U = 4 only)
+    constexpr bool X = MGCN_EXPERIMENT;
+    if (X && g_xw_pk_unroll == 3) return launch_xw<X ? 3 : 4, true>(a, s);
+    if (X && g_xw_pk_unroll == 5) return launch_xw<X ? 5 : 4, true>(a, s);
+    if (X && g_xw_pk_unroll == 6) return launch_xw<X ? 6 : 4, true>(a, s);
+    return launch_xw<4, true>(a, s);
+  }
   MGCN_REQUIRE(ldw >= F_out && ldy >= F_out && ldy % 4 == 0 &&
                    reinterpret_cast<uintptr_t>(Y) % 16 == 0 &&
                    (uint64_t)16 * (uint64_t)(ldy > ldz ? ldy : ldz) * 4u < (1ull << 31),
@@ -1826,8 +2058,8 @@ extern "C" int mgcn_spmm_xw_bwd_packed(int64_t n_rows, int32_t F_in, int32_t F_o
   clear_error();
   if (int rc = take_device_error()) return rc;  // a previous launch failed on the device
   MGCN_REQUIRE(n_rows >= 0, "mgcn_spmm_xw_bwd_packed: negative size");
-  MGCN_REQUIRE(F_in == 256 && F_out == 256 && gemm_precision_is_x6(),
-               "mgcn_spmm_xw_bwd_packed: 256 x 256, bf16x6 only");
+  MGCN_REQUIRE(mgcn_spmm_xw_supported(F_in, F_out, MGCN_REDUCE_SUM),
+               "mgcn_spmm_xw_bwd_packed: 128 x 128 or 256 x 256, bf16x6 only");
   MGCN_REQUIRE(row_div == nullptr || relu_mask != nullptr,
                "mgcn_spmm_xw_bwd_packed: row_div needs relu_mask");
   MGCN_REQUIRE(relu_mask == nullptr || colsum != nullptr,
@@ -1837,8 +2069,51 @@ extern "C" int mgcn_spmm_xw_bwd_packed(int64_t n_rows, int32_t F_in, int32_t F_o
     if (colsum && !accumulate) MGCN_HIP_TRY(hipMemsetAsync(colsum, 0, sizeof(float) * F_in, s));
     return MGCN_OK;
   }
-  if (int rc = check_packed(dY, "mgcn_spmm_xw_bwd_packed")) return rc;
+  if (int rc = check_packed(dY, F_out, "mgcn_spmm_xw_bwd_packed")) return rc;
   MGCN_REQUIRE(rowptr_t && W && dX, "mgcn_spmm_xw_bwd_packed: null array");
+  if (F_in == kXwF) {
+    MGCN_REQUIRE(ldw >= F_out && lddx >= F_in && (uint64_t)kXwRows * (uint64_t)lddx * 4u < (1ull << 31),
+                 "mgcn_spmm_xw_bwd_packed: bad W/dX");
+    MGCN_REQUIRE(ldw % 4 == 0 && reinterpret_cast<uintptr_t>(W) % 16 == 0,
+                 "mgcn_spmm_xw_bwd_packed: W must have 16-byte aligned rows");
+    MGCN_REQUIRE(relu_mask == nullptr || reinterpret_cast<uintptr_t>(relu_mask) % 16 == 0,
+                 "mgcn_spmm_xw_bwd_packed: relu_mask not 16-byte aligned");
+    const size_t need = mgcn_spmm_xw_bwd_workspace_bytes(n_rows, F_in, F_out);
+    if (workspace == nullptr || workspace_bytes < need) {
+      set_error("mgcn_spmm_xw_bwd_packed: workspace %zu < %zu", workspace_bytes, need);
+      return MGCN_EWORKSPACE;
+    }
+    const int epi = relu_mask == nullptr ? EPI_STORE : row_div != nullptr ? EPI_RELU_DIV : EPI_RELU;
+    const int64_t n_chunks = (n_rows + kXwRows - 1) / kXwRows;
+    int grid = xw_grid();
+    if (grid > n_chunks) grid = (int)n_chunks;
+    XbArgs a{};
+    a.n_rows = n_rows;
+    a.rowptr = rowptr_t;
+    a.col = col_t;
+    a.w = w_t;
+    a.row_scale = row_scale;
+    a.W = W;
+    a.ldw = ldw;
+    a.dX = dX;
+    a.lddx = lddx;
+    a.relu_mask = relu_mask;
+    a.row_div = row_div;
+    a.dw_partial = static_cast<float *>(workspace);
+    a.colsum_partial = reinterpret_cast<float *>(static_cast<char *>(workspace) +
+                                                 align_up((size_t)xw_grid() * kXwF * kXwF * 4, 256));
+    fill_pk128(a, dY);
+    constexpr bool X = MGCN_EXPERIMENT;  // (the product build instantiates U = 3 only)
+    int rc;
+    if (X && g_xw_pk_bwd_unroll == 2)
+      rc = launch_xb_dx<X ? 2 : 3, true>(a, epi, grid, s);
+    else if (X && g_xw_pk_bwd_unroll == 4)
+      rc = launch_xb_dx<X ? 4 : 3, true>(a, epi, grid, s);
+    else
+      rc = launch_xb_dx<3, true>(a, epi, grid, s);
+    if (rc || epi == EPI_STORE) return rc;
+    return launch_fold(a.colsum_partial, grid, kXwF, kXwF, colsum, kXwF, accumulate, s);
+  }
   MGCN_REQUIRE(ldw >= F_out && lddx >= F_in && lddx % 4 == 0 &&
                    reinterpret_cast<uintptr_t>(dX) % 16 == 0 &&
                    (uint64_t)16 * (uint64_t)lddx * 4u < (1ull << 31),

@@ -347,8 +347,6 @@ __device__ __forceinline__ void wide_gather2(const float *__restrict__ X, int64_
 // back where its mask bit says, +0.0 elsewhere: exactly the dense row, so the
 // fold below is wide_gather2's, bit for bit.  Per row pair and U-slot batch:
 // the headers of batch k + 1 are issued under batch k's value loads.
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-
 struct PkView {
   const uint32_t *words;
   uint32_t rbits;   // col = (s << rbits) | i
@@ -400,18 +398,6 @@ __device__ __forceinline__ int64_t uniform64(int64_t v) {
 
 // the byte offset of the lane's header pair within a row header (w = lane / 8)
 __device__ __forceinline__ uint32_t pk_hoff(int lane) { return 8u * (uint32_t)(lane >> 3); }
-
-// the lane's four words of the row from its header pair and its values
-__device__ __forceinline__ float4 pk_expand(uint32_t nib, const u32x4 v) {
-  const uint32_t r2 = (nib & 1u) + ((nib >> 1) & 1u);  // values below word 2
-  const uint32_t r3 = r2 + ((nib >> 2) & 1u);          // ... below word 3
-  const uint32_t w0 = (nib & 1u) ? v[0] : 0u;
-  const uint32_t w1 = (nib & 2u) ? ((nib & 1u) ? v[1] : v[0]) : 0u;
-  const uint32_t w2 = (nib & 4u) ? (r2 == 0 ? v[0] : r2 == 1 ? v[1] : v[2]) : 0u;
-  const uint32_t w3 = (nib & 8u) ? (r3 == 0 ? v[0] : r3 == 1 ? v[1] : r3 == 2 ? v[2] : v[3]) : 0u;
-  return make_float4(__uint_as_float(w0), __uint_as_float(w1), __uint_as_float(w2),
-                     __uint_as_float(w3));
-}
 
 // the header pairs of U slots k0 .. of a row pair (slots past na / nb: a
 // zero-byte range, the pair reads 0)

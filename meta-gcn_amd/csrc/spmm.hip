@@ -788,7 +788,9 @@ extern "C" int mgcn_set_option(const char *name, int value) {
     return gemm_set_precision(value);
   }
   if (n == "spmm_xw_unroll") return xw_set_unroll(value);
-  if (n == "xw_ws_dbg" || n == "xw_ws_full" || n == "xw_ws_max" || n == "xw_ws_full_unroll") return xw_set_ws(name, value);
+  if (n == "xw_ws_dbg" || n == "xw_ws_full" || n == "xw_ws_max" || n == "xw_ws_full_unroll" ||
+      n == "xw_pk_unroll" || n == "xw_pk_bwd_unroll")
+    return xw_set_ws(name, value);
   if (n == "wide_pair" || n == "wide_ws" || n == "wide_dbg" || n == "wide_mfma") return wide_set_option(name, value);
   if (n == "residual_blocks") {
     MGCN_REQUIRE(value >= 64 && value <= 65536, "residual_blocks must be in [64, 65536]");

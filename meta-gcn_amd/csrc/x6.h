@@ -22,6 +22,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16 lds_v4i16_t;
 
@@ -104,6 +105,21 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *base, uin
   void *p = reinterpret_cast<void *>(((uint64_t)hi << 32) | lo);
   return __builtin_amdgcn_make_buffer_rsrc(p, 0, (int)__builtin_amdgcn_readfirstlane(bytes),
                                            0x00020000);
+}
+
+// Packed-table rows (pack.hip's layout): the lane's four words of a row from
+// the 4-bit slice `nib` of its header mask word and the 16 B read at its value
+// position (its own nonzero words first): each word back where its mask bit
+// says, +0.0 elsewhere -- exactly the dense row's bits
+__device__ __forceinline__ float4 pk_expand(uint32_t nib, const u32x4 v) {
+  const uint32_t r2 = (nib & 1u) + ((nib >> 1) & 1u);  // values below word 2
+  const uint32_t r3 = r2 + ((nib >> 2) & 1u);          // ... below word 3
+  const uint32_t w0 = (nib & 1u) ? v[0] : 0u;
+  const uint32_t w1 = (nib & 2u) ? ((nib & 1u) ? v[1] : v[0]) : 0u;
+  const uint32_t w2 = (nib & 4u) ? (r2 == 0 ? v[0] : r2 == 1 ? v[1] : v[2]) : 0u;
+  const uint32_t w3 = (nib & 8u) ? (r3 == 0 ? v[0] : r3 == 1 ? v[1] : r3 == 2 ? v[2] : v[3]) : 0u;
+  return make_float4(__uint_as_float(w0), __uint_as_float(w1), __uint_as_float(w2),
+                     __uint_as_float(w3));
 }
 
 }  // namespace x6

@@ -117,8 +117,8 @@ class HipBackend:
 
     def packed_gather_ok(self, F):
         """The fused layer kernels of width F gather packed tables in place
-        (mgcn_spmm_xw_fwd_packed / _bwd_packed: F = 256)."""
-        return F == 256
+        (mgcn_spmm_xw_fwd_packed / _bwd_packed: F = 128 and 256)."""
+        return F in (128, 256)
 
     def unpack(self, buf, n_seg, n, seg_words, out):
         from .ops import unpack_rows
@@ -367,9 +367,20 @@ def set_pack_inplace(enabled: bool) -> None:
     PACK_INPLACE = bool(enabled)
 
 
+def _single_recv_words(shard: Shard, F: int) -> int:
+    """Words of the one receive buffer an F = 128 in-place table lives in:
+    every row chunk's P segments at dense capacity (header + cr F words)."""
+    cr = shard.chunk_rows
+    return shard.chunks * shard.world * (2 * cr * (F // 32) + cr * F) + 4
+
+
 def _inplace_ok(shard: Shard, backend, F: int) -> bool:
+    """In place: at most 64 segments; at F = 128 (whose kernels address the
+    whole table through one 32-bit range) a table whose single receive buffer
+    spans at most 2 GiB - 16 B."""
     return PACK_INPLACE and getattr(backend, "packed_gather_ok", lambda f: False)(F) and \
-        shard.chunks * shard.world <= 64
+        shard.chunks * shard.world <= 64 and \
+        (F != 128 or _single_recv_words(shard, F) * 4 <= 0x7ffffff0)
 
 
 def _pack_on(shard: Shard, backend=None, F: int = 0) -> bool:
@@ -418,6 +429,12 @@ class _ChunkExchange:
         self.stats = STATS
         self.recv = []      # inplace: the chunks' receive buffers
         self.seg = []       # inplace: words per segment of each chunk
+        # inplace at F = 128: ONE receive buffer for every chunk (the kernels
+        # address the table through one range), chunk c's segments from word
+        # c P (header + cr F) on; self.base[c] = that word
+        self.single = self.inplace and F == 128
+        self.big = None
+        self.base = []
 
     @property
     def table(self):
@@ -491,6 +508,21 @@ class _ChunkExchange:
         offs = torch.cumsum(counts, 0, dtype=torch.int32)
         offs.sub_(counts)
         self.be.pack_values(rows, offs, send[:head].view(cr, 2 * self.words), send[head:head + cap])
+        if self.single:
+            dcap = head + cr * F
+            if self.big is None:
+                self.big = torch.empty(_single_recv_words(sh, F), dtype=torch.int32,
+                                       device=rows.device)
+                self.big[-4:].zero_()
+            base = c * P * dcap
+            if sh.emulated:  # the rank's own segment at chunk c's place, aliased P times
+                self.big[base:base + seg].copy_(send[:seg])
+                self.seg.append(0)
+            else:
+                _gather_into(self.big[base:base + P * seg], send[:seg], P, self.group, False)
+                self.seg.append(seg)
+            self.base.append(base)
+            return
         if self.inplace:
             if sh.emulated:
                 # the rank's own segment stands in for all P (its P positions
@@ -535,9 +567,11 @@ class _ChunkExchange:
         seg_buf, seg_off = [], []
         for c, sg in enumerate(self.seg):
             for k in range(P):
-                seg_buf.append(c)
-                seg_off.append(k * sg)  # (emulated rank: sg = 0, all P alias its own)
-        return PackedTable(self.recv, seg_buf, seg_off, self.sh.chunk_rows,
+                # (emulated rank: sg = 0, all P alias its own)
+                seg_buf.append(0 if self.single else c)
+                seg_off.append((self.base[c] if self.single else 0) + k * sg)
+        return PackedTable([self.big] if self.single else self.recv, seg_buf, seg_off,
+                           self.sh.chunk_rows,
                            packed_row_bits(self.sh.chunk_rows), self.local.size(1))
 
 

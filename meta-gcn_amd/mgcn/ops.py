@@ -191,8 +191,8 @@ def spmm_xw_fwd(view: CSRView, w: torch.Tensor | None, X: torch.Tensor, W: torch
     before the division), from which the backward forms dW = Z^T dY.
     ``out`` / ``z_out``: [n_rows, F] row-major buffers (16-byte aligned rows)
     to write Y / Z into instead of new tensors.  ``X`` may be a
-    :class:`PackedTable` (256-wide layers; the view's columns then are packed
-    positions): the rows are gathered from the packed exchange buffers in
+    :class:`PackedTable` (128- or 256-wide layers; the view's columns then
+    are packed positions): the rows are gathered from the packed exchange buffers in
     place (``mgcn_spmm_xw_fwd_packed``), bit for bit the dense table's result."""
     lib = L.load()
     packed = isinstance(X, PackedTable)
@@ -280,7 +280,7 @@ def spmm_xw_bwd(view_t: CSRView, w_t: torch.Tensor | None, row_scale: torch.Tens
     receives the column sums of dY itself -- the layer's own bias gradient --
     from the same launch (``mgcn_spmm_xw_bwd_hcs``).  Returns
     (dW, dX or None, colsum or None).  ``dY`` may be a :class:`PackedTable`
-    (256-wide, dX-only form X = None; ``mgcn_spmm_xw_bwd_packed``)."""
+    (128- or 256-wide, dX-only form X = None; ``mgcn_spmm_xw_bwd_packed``)."""
     lib = L.load()
     if isinstance(dY, PackedTable):
         return _spmm_xw_bwd_packed(view_t, w_t, row_scale, dY, X, W, want_dx, relu_mask, row_div,
@@ -1913,10 +1913,12 @@ class PackedTable:
     (``mgcn_packed_table``): C x P packed segments of ``seg_rows`` rows each
     (pack.hip's layout), segment s at word ``seg_off[s]`` of buffer
     ``bufs[seg_buf[s]]`` (one receive buffer per row chunk, or one for all).
-    The fused 256-wide layer kernels gather from it in place
+    The fused 128- and 256-wide layer kernels gather from it in place
     (:func:`spmm_xw_fwd` / :func:`spmm_xw_bwd` with a PackedTable for X / dY,
     over a view whose columns are packed positions (s << row_bits) | i:
-    :func:`packed_cols`)."""
+    :func:`packed_cols`).  At F = 128 every segment must lie within 2 GiB of
+    the lowest buffer (the kernels read the table through one range: in
+    practice, one buffer)."""
     bufs: list               # int32 tensors holding the segments (kept alive here)
     seg_buf: list            # segment s -> index into bufs
     seg_off: list            # segment s -> word offset in that buffer

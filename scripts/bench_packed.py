@@ -1,12 +1,15 @@
-"""The 256-wide fused layer kernels gathering a dense table vs the same table
-packed (mgcn_spmm_xw_fwd / _bwd vs mgcn_spmm_xw_fwd_packed / _bwd_packed), at
-a config-5 rank's shape: 6.24M destination rows of ~11 slots over a table of
-C * P segments of cr rows (default 4 x 8 x 1.56M = 50M rows, F = 256), half
-the table's words +0.0 (a ReLU'd layer).  `--alias` points all P segments of
-a chunk at one physical segment (the emulated rank's stand-in).  Prints one
-JSON line of per-launch times (HIP events, median of --reps).
+"""The fused layer kernels gathering a dense table vs the same table packed
+(mgcn_spmm_xw_fwd / _bwd vs mgcn_spmm_xw_fwd_packed / _bwd_packed).  Default:
+a config-5 rank's shape, 6.24M destination rows of ~11 slots over a table of
+C * P segments of cr rows (4 x 8 x 1.56M = 50M rows, F = 256); `--config2`:
+config 2's shape at F = 128 (1M rows of 11 slots over a 1M-row table in 8
+segments, one receive buffer).  Half the table's words are +0.0 (a ReLU'd
+layer).  `--alias` points that many consecutive segments at one physical
+segment (the emulated rank's stand-in).  Prints one JSON line of per-launch
+times (HIP events, median of --reps).
 
     python scripts/bench_packed.py [--rows 6240000 --cr 1561000 --segs 32 --reps 5]
+    python scripts/bench_packed.py --config2
 """
 import argparse
 import json
@@ -27,12 +30,16 @@ def main():
     ap.add_argument("--deg", type=int, default=11)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--alias", type=int, default=8, help="segments sharing one physical segment")
+    ap.add_argument("--config2", action="store_true", help="config 2's shape at F = 128")
     args = ap.parse_args()
+    F = 256
+    if args.config2:
+        F = 128
+        args.rows, args.cr, args.segs, args.alias = 1_000_000, 125_000, 8, 1
     from mgcn import _lib as L
     from mgcn import ops
     from mgcn.graph import CSRView
     dev = torch.device("cuda:0")
-    F = 256
     g = torch.Generator(device=dev).manual_seed(0)
     T_rows = args.segs * args.cr
     n = args.rows
@@ -89,9 +96,17 @@ def main():
         for k in range(args.alias):
             seg_buf.append(p)
             seg_off.append(0)
+    if F == 128:  # one receive buffer (the F = 128 kernels' single range)
+        offs_ = [0]
+        for b_ in bufs:
+            offs_.append(offs_[-1] + b_.numel())
+        one = torch.cat(bufs)
+        seg_off = [offs_[p] for p in seg_buf]
+        seg_buf = [0] * len(seg_buf)
+        bufs = [one]
     tab = ops.PackedTable(bufs, seg_buf, seg_off, args.cr, rb, F)
     res["packed_over_dense"] = packed_words / (n_phys * args.cr * F)
-    rm = torch.empty(n, 8, dtype=torch.int32, device=dev)
+    rm = torch.empty(n, ops.mask_words(F), dtype=torch.int32, device=dev)
     Y = torch.empty(n, F, device=dev)
     Z = torch.empty(n, F, device=dev)
     res["fwd_dense_ms"] = timeit(lambda: ops.spmm_xw_fwd(view, w, dense, W, L.REDUCE_SUM, b, True,

@@ -113,11 +113,13 @@ def test_sharded_matches_single_process(world, aggr, F, fused, chunks):
                 np.testing.assert_allclose(g, g1, rtol=1e-5, atol=1e-5 * max(1, np.abs(g1).max()))
 
 
-@pytest.mark.parametrize("world,aggr,F,chunks", [(2, "add", 32, 4), (4, "mean", 64, 3)])
+@pytest.mark.parametrize("world,aggr,F,chunks", [(2, "add", 32, 4), (4, "mean", 64, 3),
+                                                  (2, "add", 128, 3)])
 def test_packed_exchange_is_bitwise_the_dense_one(world, aggr, F, chunks):
     """The zero-skipping exchange (ReLU'd forward tables, ReLU-masked
     backward tables) against the dense exchange of the same sharded stack:
-    every output, dX row and gradient bit for bit, with fewer words sent."""
+    every output, dX row and gradient bit for bit, with fewer words sent
+    (F = 128: the in-place table in ONE receive buffer, dist._single_recv_words)."""
     packed = _launch(world, aggr, F, True, chunks, pack=True)
     dense = _launch(world, aggr, F, True, chunks, pack=False)
     for rp, rd in zip(packed, dense):

@@ -158,20 +158,28 @@ def _pk_view(v, cr, rb):
                    n_rows=v.n_rows, n_cols=v.n_cols)
 
 
+def _relu_mask(Z):
+    """The lower layer's ReLU mask words of Z (> 0) in the fused kernels'
+    layout for Z's width."""
+    from mgcn import ops
+    return _mask256(Z) if Z.size(1) == 256 else ops.make_relu_mask(Z)
+
+
 @pytest.mark.parametrize("n_rows,cr,S,E,heavy", [(5000, 700, 6, 60000, 0), (33, 1000, 3, 300, 150),
                                                  (4097, 4097, 2, 50000, 0)])
 @pytest.mark.parametrize("mean", [False, True])
-def test_packed_gather_forward_bitwise_the_dense_table(cuda, n_rows, cr, S, E, heavy, mean):
+@pytest.mark.parametrize("F", [128, 256])
+def test_packed_gather_forward_bitwise_the_dense_table(cuda, n_rows, cr, S, E, heavy, mean, F):
     """mgcn_spmm_xw_fwd_packed == mgcn_spmm_xw_fwd on the unpacked table: Y,
-    Z and the ReLU mask words bit for bit (ragged segments, rows past 64
-    slots, empty rows, -0.0 values, two receive buffers)."""
+    Z and the ReLU mask words bit for bit (ragged segments, rows past 32 / 64
+    slots, empty rows, -0.0 values; at F = 256 two receive buffers, at
+    F = 128 one -- its kernels read the table through one 2-GiB range)."""
     from mgcn import _lib as L
     from mgcn import ops
-    F = 256
     rng = np.random.default_rng(n_rows + S)
     T = torch.relu(torch.randn(S * cr, F, generator=torch.Generator().manual_seed(S)))
     T[::7, ::5] = -0.0
-    tab = _packed_table(T, cr, cuda)
+    tab = _packed_table(T, cr, cuda, n_bufs=2 if F == 256 else 1)
     v, w = _graph_view(rng, n_rows, S * cr, E, cuda, heavy)
     vp = _pk_view(v, cr, tab.row_bits)
     g = torch.Generator(device=cuda).manual_seed(1)
@@ -180,7 +188,7 @@ def test_packed_gather_forward_bitwise_the_dense_table(cuda, n_rows, cr, S, E, h
     red = L.REDUCE_MEAN if mean else L.REDUCE_SUM
     outs = []
     for view, X in ((v, T.to(cuda)), (vp, tab)):
-        rm = torch.empty(n_rows, 8, dtype=torch.int32, device=cuda)
+        rm = torch.empty(n_rows, ops.mask_words(F), dtype=torch.int32, device=cuda)
         y, z = ops.spmm_xw_fwd(view, w, X, W, red, b, True, relu_mask=rm, want_z=True)
         outs.append((y, z, rm))
     for a, b_ in zip(*outs):
@@ -189,16 +197,16 @@ def test_packed_gather_forward_bitwise_the_dense_table(cuda, n_rows, cr, S, E, h
 
 @pytest.mark.parametrize("n_rows,cr,S,E", [(5000, 700, 6, 60000), (33, 1000, 3, 300)])
 @pytest.mark.parametrize("epi", ["store", "relu", "relu_div"])
-def test_packed_gather_adjoint_bitwise_the_dense_table(cuda, n_rows, cr, S, E, epi):
+@pytest.mark.parametrize("F", [128, 256])
+def test_packed_gather_adjoint_bitwise_the_dense_table(cuda, n_rows, cr, S, E, epi, F):
     """mgcn_spmm_xw_bwd_packed == the dX-only mgcn_spmm_xw_bwd on the unpacked
     table: dX bit for bit, the accumulated column sums too."""
     from mgcn import ops
-    F = 256
     rng = np.random.default_rng(7 * n_rows + S)
     T = torch.randn(S * cr, F, generator=torch.Generator().manual_seed(S + 1))
     T = torch.where(torch.rand(S * cr, F, generator=torch.Generator().manual_seed(2)) < 0.5,
                     torch.zeros(()), T)
-    tab = _packed_table(T, cr, cuda, n_bufs=3)
+    tab = _packed_table(T, cr, cuda, n_bufs=3 if F == 256 else 1)
     v, w = _graph_view(rng, n_rows, S * cr, E, cuda)
     vp = _pk_view(v, cr, tab.row_bits)
     g = torch.Generator(device=cuda).manual_seed(3)
@@ -206,7 +214,7 @@ def test_packed_gather_adjoint_bitwise_the_dense_table(cuda, n_rows, cr, S, E, e
     rs = torch.rand(n_rows, device=cuda, generator=g)
     rm = rd = None
     if epi != "store":
-        rm = _mask256(torch.randn(n_rows, F, device=cuda, generator=g))
+        rm = _relu_mask(torch.randn(n_rows, F, device=cuda, generator=g))
     if epi == "relu_div":
         rd = torch.randint(1, 9, (n_rows,), device=cuda, generator=g).float()
     outs = []
@@ -218,3 +226,25 @@ def test_packed_gather_adjoint_bitwise_the_dense_table(cuda, n_rows, cr, S, E, e
     assert torch.equal(outs[0][0].view(torch.int32), outs[1][0].view(torch.int32))
     if rm is not None:
         assert torch.equal(outs[0][1], outs[1][1])
+
+
+def test_packed_table_of_f128_must_fit_one_range(cuda):
+    """An F = 128 packed table spanning more than 2 GiB (segments in buffers
+    far apart) is refused with an error, never read."""
+    from mgcn import _lib as L
+    from mgcn import ops
+    cr, F = 64, 128
+    T = torch.relu(torch.randn(2 * cr, F, generator=torch.Generator().manual_seed(5)))
+    tab = _packed_table(T, cr, cuda, n_bufs=1)
+    W = torch.randn(F, F, device=cuda) * 0.1
+    v, w = _graph_view(np.random.default_rng(1), 10, 2 * cr, 50, cuda)
+    vp = _pk_view(v, cr, tab.row_bits)
+    c = tab.c_struct()
+    c.seg_base[1] = (1 << 29) + 8  # a second segment past the 2-GiB range
+    c.n_words = (1 << 29) + 16
+    lib = L.load()
+    Y = torch.empty(10, F, device=cuda)
+    rc = lib.mgcn_spmm_xw_fwd_packed(10, F, F, L.ptr(vp.rowptr), L.ptr(vp.col), L.ptr(w),
+                                     L.byref(c), L.ptr(W), F, None, L.ptr(Y), F, L.REDUCE_SUM, 0,
+                                     None, None, 0, None, 0, L.stream_of(cuda))
+    assert rc == L.EINVAL and b"2 GiB" in lib.mgcn_last_error()
