@@ -1063,8 +1063,11 @@ __global__ __launch_bounds__(kXwThreads, 2 * kXwPerCU) void spmm_xw_bwd_kernel(c
 }
 
 int g_xw_unroll = 5;  // forward gathers in flight per row (5: config 2 5.06 -> 5.005 ms/step; 6 spills)
-// packed-table forms: slots in flight per row (experiment builds sweep them)
-int g_xw_pk_unroll = 4;
+// packed-table forms: slots in flight per row (experiment builds sweep them;
+// config 2's shape, profiles/r06/packed_unroll_sweep.json: forward 1.20 / 1.27
+// / 1.39 / 1.41 ms at U = 3 / 4 / 5 / 6 -- the extra registers spill more as U
+// grows --, adjoint 1.07 / 1.05 / 1.08 ms at 2 / 3 / 4)
+int g_xw_pk_unroll = 3;
 int g_xw_pk_bwd_unroll = 3;
 
 int xw_grid() {
@@ -2023,12 +2026,12 @@ extern "C" int mgcn_spmm_xw_fwd_packed(int64_t n_rows, int32_t F_in, int32_t F_o
     a.relu = relu != 0;
     fill_pk128(a, X);
     hipStream_t s = as_stream(stream);
-    // (the product build instantiates U = 4 only)
+    // (the product build instantiates U = 3 only)
     constexpr bool X = MGCN_EXPERIMENT;
-    if (X && g_xw_pk_unroll == 3) return launch_xw<X ? 3 : 4, true>(a, s);
-    if (X && g_xw_pk_unroll == 5) return launch_xw<X ? 5 : 4, true>(a, s);
-    if (X && g_xw_pk_unroll == 6) return launch_xw<X ? 6 : 4, true>(a, s);
-    return launch_xw<4, true>(a, s);
+    if (X && g_xw_pk_unroll == 4) return launch_xw<X ? 4 : 3, true>(a, s);
+    if (X && g_xw_pk_unroll == 5) return launch_xw<X ? 5 : 3, true>(a, s);
+    if (X && g_xw_pk_unroll == 6) return launch_xw<X ? 6 : 3, true>(a, s);
+    return launch_xw<3, true>(a, s);
   }
   MGCN_REQUIRE(ldw >= F_out && ldy >= F_out && ldy % 4 == 0 &&
                    reinterpret_cast<uintptr_t>(Y) % 16 == 0 &&
