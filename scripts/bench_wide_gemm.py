@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--feat", type=int, default=256)
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="mgcn_set_option before the run (A/B)")
+    ap.add_argument("--tn-only", action="store_true", help="time only mgcn_gemm_tn")
     args = ap.parse_args()
     from mgcn import ops
     from mgcn import _lib as L
@@ -58,7 +59,13 @@ def main():
     print(json.dumps({"op": "gemm_tn Z^T dY", "K": M, "M": F, "N": F, "ms": ms,
                       "gbs": 8.0 * M * F / ms / 1e6,
                       "tflops_equiv": 2.0 * M * F * F / ms / 1e9,
-                      "err": norm_err(C, Z.t(), dY)}), flush=True)
+                      "err": norm_err(C, Z.t(), dY),
+                      # bit digest of C: A/B builds of one product compare bit for bit
+                      "digest": int(C.view(torch.int32).to(torch.int64).mul_(
+                          torch.arange(1, C.numel() + 1, device=dev).view_as(C)).sum())}),
+          flush=True)
+    if args.tn_only:
+        return
     s = 200_000
     for name, fn, chk in [
             ("gemm_nn X W", lambda: ops.gemm_nn(Z, W),
