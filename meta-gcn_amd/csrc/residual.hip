@@ -12,10 +12,11 @@
 // per layer at 15-40 us each.  Here the aggregation and both 32 x 32
 // products happen in one pass over the rows:
 //
-// forward   one 8-lane group per destination row gathers the rows of X over
-//           its in-edges (edge order, separately rounded products and sums:
-//           the SpMM's arithmetic), so (A X) is on chip; the group stages it
-//           and its own row of X in a 16-row LDS tile of the wave, whose
+// forward   an 8-lane group gathers the rows of X over the in-edges of two
+//           destination rows at once (tile rows g and 8 + g; each row in its
+//           edge order, separately rounded products and sums: the SpMM's
+//           arithmetic), so (A X) is on chip; the group stages them and their
+//           own rows of X in a 16-row LDS tile of the wave, whose
 //           (A X) W and X Wr^T run on v_mfma_f32_16x16x4_f32 (exact f32
 //           products; W / Wr^T operands staged once per workgroup), then the
 //           bias, ReLU, join and ReLU; writes Z as whole rows and two 32-bit
@@ -47,6 +48,12 @@
 
 namespace mgcn {
 namespace {
+
+// light-row tiles: U slots of each of a lane group's two rows per round
+// (round 6: both 8-row steps of a tile aggregated together at U = 4, config 3
+// 2.48 -> 2.41 ms/step, against one step after the other at U = 8)
+constexpr int kRlU = 4;
+
 
 constexpr int kRF = 32;             // features (in = out)
 constexpr int kRG = 8;              // lanes per row: 4 floats each
@@ -174,21 +181,43 @@ void residual_layer_kernel(const RlArgs a) {
   const bool fmask = BWD && a.mmask != nullptr;
   float msa[4] = {0.f, 0.f, 0.f, 0.f}, mss[4] = {0.f, 0.f, 0.f, 0.f};  // fmask column sums
   const int64_t n_tiles = (a.n_items + kTileRows - 1) / kTileRows;
+  // a tile's row ids (tile rows grp, 8 + grp; -1 past the launch's rows)
+  auto tile_ids = [&](int64_t wv, int (&r)[2]) {
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const int64_t item = wv * kTileRows + 8 * st + grp;
+      r[st] = item >= a.n_items ? -1 : a.items != nullptr ? a.items[item] : (int)item;
+    }
+  };
+  auto tile_meta = [&](const int (&r)[2], int64_t (&b)[2], int (&d)[2]) {
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      b[st] = r[st] >= 0 ? a.rowptr[r[st]] : 0;
+      d[st] = r[st] >= 0 ? (int)(a.rowptr[r[st] + 1] - b[st]) : 0;
+    }
+  };
   for (int64_t wv = (int64_t)rblk * kRWaves + wib; wv < n_tiles;
        wv += (int64_t)row_blocks * kRWaves) {
-    // ---- two row steps of 8 rows: aggregate, stage with the own rows ----
-#pragma unroll 1
-    for (int st = 0; st < 2; ++st) {
-      const int tr = 8 * st + grp;
-      const int64_t item = wv * kTileRows + tr;
-      const bool ok = item < a.n_items;
-      const int64_t row = !ok ? 0 : a.items != nullptr ? (int64_t)a.items[item] : item;
-      float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    // ---- the tile's 16 rows, two per lane group (tile rows grp, 8 + grp),
+    // aggregated together: one dependent chain (schedule id -> row pointers
+    // -> slots -> gathered rows) per tile instead of one per 8-row step, and
+    // U slots of EACH row in flight per round; each row folds in its own
+    // edge order (the SpMM's sums, bit for bit) ----
+    {
+      int rid[2], deg[2];
+      int64_t beg[2];
+      tile_ids(wv, rid);
+      tile_meta(rid, beg, deg);
+      int64_t row[2];
+      bool ok[2];
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        ok[st] = rid[st] >= 0;
+        row[st] = ok[st] ? rid[st] : 0;
+      }
+      float acc[2][4] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
       if (a.gather) {
-        // a row's degree fits 32 bits (col is int32); its slots are addressed from beg
-        const int64_t beg = ok ? a.rowptr[row] : 0;
-        const int deg = ok ? (int)(a.rowptr[row + 1] - beg) : 0;
-        int maxdeg = deg;
+        int maxdeg = deg[0] > deg[1] ? deg[0] : deg[1];
 #pragma unroll
         for (int off = kRG; off < 64; off <<= 1) {
           const int o = __shfl_xor(maxdeg, off, 64);
@@ -196,62 +225,81 @@ void residual_layer_kernel(const RlArgs a) {
         }
         for (int e0 = 0; e0 < maxdeg; e0 += kRG) {
           const int my = e0 + gl;
-          int mc = 0;
-          float mw = 1.0f;
-          if (my < deg) {
-            mc = a.col[beg + my];
-            if (has_w) mw = a.w[beg + my];
+          int mc[2] = {0, 0};
+          float mw[2] = {1.0f, 1.0f};
+          int nb[2];
+#pragma unroll
+          for (int st = 0; st < 2; ++st) {
+            if (my < deg[st]) {
+              mc[st] = a.col[beg[st] + my];
+              if (has_w) mw[st] = a.w[beg[st] + my];
+            }
+            const int rem = deg[st] - e0;
+            nb[st] = rem <= 0 ? 0 : (rem < kRG ? rem : kRG);
           }
-          const int rem = deg - e0;
-          const int nb = rem <= 0 ? 0 : (rem < kRG ? rem : kRG);
           const int remw = maxdeg - e0;
           const int nbmax = remw < kRG ? remw : kRG;  // wave-uniform
           for (int k0 = 0; k0 < nbmax; k0 += U) {
-            float4 xv[U];
-            float wk[U];
-            bool okk[U];
+            float4 xv[2][U];
+            float wk[2][U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-              const int k = (k0 + u) & (kRG - 1);
-              const int ck = __shfl(mc, gbase + k, 64);
-              wk[u] = __shfl(mw, gbase + k, 64);
-              okk[u] = k0 + u < nb;
-              xv[u] = okk[u] ? ld4(a.T + (int64_t)ck * a.ldt + f0) : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-            // fold strictly in edge order (the SpMM's sums, bit for bit)
+            for (int u = 0; u < U; ++u)
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-              if (okk[u]) {
-                acc[0] = __fadd_rn(acc[0], __fmul_rn(xv[u].x, wk[u]));
-                acc[1] = __fadd_rn(acc[1], __fmul_rn(xv[u].y, wk[u]));
-                acc[2] = __fadd_rn(acc[2], __fmul_rn(xv[u].z, wk[u]));
-                acc[3] = __fadd_rn(acc[3], __fmul_rn(xv[u].w, wk[u]));
+              for (int st = 0; st < 2; ++st) {
+                const int k = (k0 + u) & (kRG - 1);
+                const int ck = __shfl(mc[st], gbase + k, 64);
+                wk[st][u] = __shfl(mw[st], gbase + k, 64);
+                xv[st][u] = k0 + u < nb[st] ? ld4(a.T + (int64_t)ck * a.ldt + f0)
+                                            : make_float4(0.f, 0.f, 0.f, 0.f);
               }
-            }
+#pragma unroll
+            for (int st = 0; st < 2; ++st)
+#pragma unroll
+              for (int u = 0; u < U; ++u) {
+                if (k0 + u < nb[st]) {
+                  acc[st][0] = __fadd_rn(acc[st][0], __fmul_rn(xv[st][u].x, wk[st][u]));
+                  acc[st][1] = __fadd_rn(acc[st][1], __fmul_rn(xv[st][u].y, wk[st][u]));
+                  acc[st][2] = __fadd_rn(acc[st][2], __fmul_rn(xv[st][u].z, wk[st][u]));
+                  acc[st][3] = __fadd_rn(acc[st][3], __fmul_rn(xv[st][u].w, wk[st][u]));
+                }
+              }
           }
         }
-        if (!BWD && a.mean) {
-          const float c = (float)(deg > 1 ? deg : 1);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc[j] = __fdiv_rn(acc[j], c);
-        }
-        if (BWD && a.row_scale != nullptr && ok) {
-          const float sc = a.row_scale[row];
+        for (int st = 0; st < 2; ++st) {
+          if (!BWD && a.mean) {
+            const float c = (float)(deg[st] > 1 ? deg[st] : 1);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc[j] = __fmul_rn(acc[j], sc);
+            for (int j = 0; j < 4; ++j) acc[st][j] = __fdiv_rn(acc[st][j], c);
+          }
+          if (BWD && a.row_scale != nullptr && ok[st]) {
+            const float sc = a.row_scale[row[st]];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[st][j] = __fmul_rn(acc[st][j], sc);
+          }
+          // backward: dH goes out for the weight GEMM
+          if (BWD && ok[st])
+            st4(a.agg + row[st] * a.ldagg + f0,
+                make_float4(acc[st][0], acc[st][1], acc[st][2], acc[st][3]));
         }
-        // backward: dH goes out for the weight GEMM
-        if (BWD && ok) st4(a.agg + row * a.ldagg + f0, make_float4(acc[0], acc[1], acc[2], acc[3]));
-      } else if (ok) {
-        const float4 v = ld4(a.agg + row * a.ldagg + f0);
-        acc[0] = v.x, acc[1] = v.y, acc[2] = v.z, acc[3] = v.w;
+      } else {
+#pragma unroll
+        for (int st = 0; st < 2; ++st)
+          if (ok[st]) {
+            const float4 v = ld4(a.agg + row[st] * a.ldagg + f0);
+            acc[st][0] = v.x, acc[st][1] = v.y, acc[st][2] = v.z, acc[st][3] = v.w;
+          }
       }
-      // the own operand is loaded here, not held across the gathers
+      // the own operands are loaded here, not held across the gathers
       // (registers set the occupancy)
-      const float4 ov = ok ? ld4(a.own + row * a.ldo + f0) : make_float4(0.f, 0.f, 0.f, 0.f);
-      st4(&T[tr][f0], make_float4(acc[0], acc[1], acc[2], acc[3]));
-      st4(&T[tr][kRF + f0], ov);
-      if (gl == 0) tile_row[wib][tr] = ok ? row : -1;
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const int tr = 8 * st + grp;
+        const float4 ov = ok[st] ? ld4(a.own + row[st] * a.ldo + f0) : make_float4(0.f, 0.f, 0.f, 0.f);
+        st4(&T[tr][f0], make_float4(acc[st][0], acc[st][1], acc[st][2], acc[st][3]));
+        st4(&T[tr][kRF + f0], ov);
+        if (gl == 0) tile_row[wib][tr] = ok[st] ? row[st] : -1;
+      }
     }
     __builtin_amdgcn_wave_barrier();
 
@@ -464,7 +512,7 @@ int launch_rl(const RlArgs &a, hipStream_t s) {
   }
   const int64_t blocks = rl_blocks(a.n_items, BWD && a.mmask != nullptr) + a.gemm.blocks +
                          a.side[0].blocks + a.side[1].blocks;
-  hipLaunchKernelGGL((residual_layer_kernel<8, BWD>), dim3((unsigned)blocks), dim3(kRBlock), 0, s, a);
+  hipLaunchKernelGGL((residual_layer_kernel<kRlU, BWD>), dim3((unsigned)blocks), dim3(kRBlock), 0, s, a);
   return check_launch("residual_layer_kernel");
 }
 
