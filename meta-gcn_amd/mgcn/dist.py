@@ -194,6 +194,10 @@ class Shard:
     emulated: bool = False
     _tables: dict = None
     _pk_views: tuple = None
+    # packed exchange: the largest packed value count over the ranks of each
+    # (exchange, row chunk) at its last exchange (identical on every rank:
+    # it comes from the all-gathered sizes) -- the next exchange's capacity
+    cap_hint: dict = None
 
     def packed_views(self):
         """(fwd, bwd, row_bits): the two views with their columns as packed
@@ -367,6 +371,31 @@ def set_pack_inplace(enabled: bool) -> None:
     PACK_INPLACE = bool(enabled)
 
 
+# Speculative capacity (round 6).  An all-gather moves equal sizes, so a
+# packed chunk is sent at the largest packed size over the ranks; the first
+# exchange of a table learns that size on the host (one event wait per chunk,
+# one chunk behind).  Every later exchange of the same (layer, direction,
+# chunk) sends at the size the last one saw plus SPEC_SLACK, issuing the
+# payload right behind the pack with no host wait; the all-gathered sizes are
+# checked once per table, when the next layer asks for it (one host sync per
+# table instead of one per chunk), and a chunk whose size outgrew its
+# capacity on some rank is all-gathered again at its true size before anything
+# reads it -- the same bits either way.  set_spec_exchange(False): round 5's
+# per-chunk form always.
+SPEC_EXCHANGE = os.environ.get("MGCN_SPEC_EXCHANGE", "1") != "0"
+SPEC_SLACK = 0.02  # capacity = last size x (1 + SLACK) + 64 words (tests set it below 0)
+
+
+def set_spec_exchange(enabled: bool) -> None:
+    global SPEC_EXCHANGE
+    SPEC_EXCHANGE = bool(enabled)
+
+
+def _spec_cap(true_words: int, limit: int) -> int:
+    c = int(true_words * (1.0 + SPEC_SLACK)) + (64 if SPEC_SLACK >= 0 else 0)
+    return max(0, min(c, limit))
+
+
 def _single_recv_words(shard: Shard, F: int) -> int:
     """Words of the one receive buffer an F = 128 in-place table lives in:
     every row chunk's P segments at dense capacity (header + cr F words)."""
@@ -411,9 +440,12 @@ class _ChunkExchange:
     collective runs)."""
 
     def __init__(self, shard: Shard, local_pad: torch.Tensor, table, group, backend,
-                 packed: bool, inplace: bool = False):
+                 packed: bool, inplace: bool = False, key=None):
         """``table``: the dense table, or a callable that allocates it (only
-        called when some chunk goes dense)."""
+        called when some chunk goes dense).  ``key``: this exchange's place in
+        the step (layer, direction), under which the shard keeps each chunk's
+        packed size for the next step's speculative capacity (None: never
+        speculate)."""
         self.sh, self.local, self.group, self.be = shard, local_pad, group, backend
         self._table = table
         F = local_pad.size(1)
@@ -435,6 +467,10 @@ class _ChunkExchange:
         self.single = self.inplace and F == 128
         self.big = None
         self.base = []
+        self.key = key
+        self.spec = []      # speculative chunks: (c, rows, send, counts, totals, work, cap, how)
+        if shard.cap_hint is None:
+            shard.cap_hint = {}
 
     @property
     def table(self):
@@ -462,6 +498,17 @@ class _ChunkExchange:
         else:
             totals = torch.empty(P, dtype=torch.int64, device=dev)
             work = _gather_into(totals, total, P, self.group, True)
+        # (in place only: a truncated segment is then read by nothing before
+        # result() has re-sent it; the expanding path would unpack it at once)
+        hint = sh.cap_hint.get((self.key, c)) if (
+            SPEC_EXCHANGE and self.inplace and self.key is not None and not sh.emulated) else None
+        if hint is not None:
+            # speculative: the payload goes right behind the pack at the
+            # capacity the last exchange saw; result() checks the sizes
+            self._payload(c, rows, send, counts, hint)
+            self.spec.append((c, rows, send, counts, totals, work, hint))
+            self.stats["spec_chunks"] = self.stats.get("spec_chunks", 0) + 1
+            return
         # the sizes reach the host through a side stream that waits only for
         # the size exchange: finish() then waits for THAT (an event), not for
         # everything queued on the compute stream after it (`.item()` on the
@@ -488,8 +535,6 @@ class _ChunkExchange:
             self._finish_one(*self.pending.pop(0))
 
     def _finish_one(self, c, rows, send, counts, totals, work, host, ev):
-        sh = self.sh
-        cr, P, F = sh.chunk_rows, sh.world, rows.size(1)
         if ev is not None:
             ev.synchronize()  # the size exchange (and its copy) only
             cap = int(host.max())
@@ -497,17 +542,32 @@ class _ChunkExchange:
             if work is not None:
                 work.wait()
             cap = int(totals.max())
+        if self.key is not None:
+            self.sh.cap_hint[(self.key, c)] = _spec_cap(cap, self.sh.chunk_rows * rows.size(1))
+        self._payload(c, rows, send, counts, cap)
+
+    def _payload(self, c, rows, send, counts, cap, again=False):
+        """Pack chunk c's values and issue its payload at ``cap`` value words
+        per rank (``again``: a speculative chunk re-sent at its true size;
+        its values are packed already)."""
+        sh = self.sh
+        cr, P, F = sh.chunk_rows, sh.world, rows.size(1)
         head = 2 * cr * self.words
         seg = head + cap
-        self.stats["dense_words"] += cr * F * P
+        if not again:
+            self.stats["dense_words"] += cr * F * P
         if seg >= cr * F and not self.inplace:  # nothing to gain: dense
             self.stats["sent_words"] += cr * F * P
             self.works.append(_gather_chunk(sh, c, self.local, self.table, self.group))
             return
         self.stats["sent_words"] += seg * P
-        offs = torch.cumsum(counts, 0, dtype=torch.int32)
-        offs.sub_(counts)
-        self.be.pack_values(rows, offs, send[:head].view(cr, 2 * self.words), send[head:head + cap])
+        if not again:
+            offs = torch.cumsum(counts, 0, dtype=torch.int32)
+            offs.sub_(counts)
+            # every value (the send buffer holds a dense chunk's worth); the
+            # first `cap` words travel
+            self.be.pack_values(rows, offs, send[:head].view(cr, 2 * self.words),
+                                send[head:head + cr * F])
         if self.single:
             dcap = head + cr * F
             if self.big is None:
@@ -517,11 +577,10 @@ class _ChunkExchange:
             base = c * P * dcap
             if sh.emulated:  # the rank's own segment at chunk c's place, aliased P times
                 self.big[base:base + seg].copy_(send[:seg])
-                self.seg.append(0)
+                self._put(c, again, seg=0, base=base)
             else:
                 _gather_into(self.big[base:base + P * seg], send[:seg], P, self.group, False)
-                self.seg.append(seg)
-            self.base.append(base)
+                self._put(c, again, seg=seg, base=base)
             return
         if self.inplace:
             if sh.emulated:
@@ -529,16 +588,14 @@ class _ChunkExchange:
                 # alias it): no collective and no copy -- the receive-side
                 # write of a real rank is the exchange's, which
                 # scripts/config5_rank.py accounts for separately
-                self.recv.append(send)
-                self.seg.append(0)
+                self._put(c, again, seg=0, recv=send)
                 return
             # P segments back to back (+4 words: a lane's 16-B value read may
             # run 3 words past the last segment's values)
             recv = torch.empty(P * seg + 4, dtype=torch.int32, device=rows.device)
             recv[P * seg:].zero_()
             _gather_into(recv[:P * seg], send[:seg], P, self.group, False)
-            self.recv.append(recv)
-            self.seg.append(seg)
+            self._put(c, again, seg=seg, recv=recv)
             return
         blk = self.table[c * P * cr:(c + 1) * P * cr]
         if sh.emulated:  # a real rank's receive-side work: P segments unpacked
@@ -549,8 +606,43 @@ class _ChunkExchange:
         _gather_into(recv, send[:seg], P, self.group, False)
         self.be.unpack(recv, P, cr, seg, blk)
 
+    def _put(self, c, again, seg, base=None, recv=None):
+        """Record chunk c's in-place segments (chunks are started in order;
+        ``again`` replaces chunk c's record)."""
+        if again:
+            self.seg[c] = seg
+            if recv is not None:
+                self.recv[c] = recv
+            return
+        assert len(self.seg) == c, "chunks are exchanged in order"
+        self.seg.append(seg)
+        if base is not None:
+            self.base.append(base)
+        if recv is not None:
+            self.recv.append(recv)
+
+    def _check_spec(self) -> None:
+        """One host sync for every speculative chunk of this exchange: their
+        all-gathered sizes; a chunk that outgrew its capacity on some rank is
+        sent again at its true size (every rank decides alike: the sizes are
+        all-gathered); the hints follow the sizes."""
+        if not self.spec:
+            return
+        for *_, work, _cap in self.spec:
+            if work is not None:
+                work.wait()
+        sizes = torch.stack([t.view(-1).max() for *_, t, _w, _cap in self.spec]).cpu()
+        lim = self.sh.chunk_rows * self.local.size(1)
+        for (c, rows, send, counts, totals, work, cap), true in zip(self.spec, sizes.tolist()):
+            self.sh.cap_hint[(self.key, c)] = _spec_cap(int(true), lim)
+            if true > cap:
+                self.stats["spec_resent"] = self.stats.get("spec_resent", 0) + 1
+                self._payload(c, rows, send, counts, int(true), again=True)
+        self.spec = []
+
     def wait(self) -> None:
         self.finish()
+        self._check_spec()
         _wait(self.works)
         self.works = []
 
@@ -768,7 +860,7 @@ class _ShardedStack(torch.autograd.Function):
                 slot = "t%d" % (i & 1)
                 xch = _ChunkExchange(sh, out, lambda F=F_out, s_=slot: new_table(
                     sh, F, torch.float32, dev, s_), group, be, pk,
-                    inplace=pk and _inplace_ok(sh, be, F_out))
+                    inplace=pk and _inplace_ok(sh, be, F_out), key=("fwd", i, F_out))
             for c in range(C):
                 a, e = sh.chunk(c)
                 if e > a:
@@ -849,7 +941,7 @@ class _ShardedStack(torch.autograd.Function):
                 slot = "t%d" % ((l - 1) & 1)
                 xch = _ChunkExchange(sh, dX, lambda F=Fx, s_=slot: new_table(
                     sh, F, torch.float32, dev, s_), group, be, pk,
-                    inplace=pk and _inplace_ok(sh, be, Fx))
+                    inplace=pk and _inplace_ok(sh, be, Fx), key=("bwd", l, Fx))
             works = []
             # the lower layer's bias gradient: every chunk's column sums are
             # added into one device vector by the adjoint launches themselves

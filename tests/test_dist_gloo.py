@@ -36,7 +36,8 @@ def _problem(N=300, pairs=1500, F=16, L=3, seed=0):
     return ei, N, X, Ws, bs, dY
 
 
-def _run(rank, world, port, aggr, out_q, F=16, fused=True, chunks=4, pack=True, force=False):
+def _run(rank, world, port, aggr, out_q, F=16, fused=True, chunks=4, pack=True, force=False,
+         slack=None):
     sys.path[:0] = [os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "meta-gcn_amd"),
                     HERE]
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -49,6 +50,8 @@ def _run(rank, world, port, aggr, out_q, F=16, fused=True, chunks=4, pack=True, 
         from mgcn.dist import ShardedGCN
         mdist.set_pack_exchange(pack)
         mdist.set_force_collectives(force)
+        if slack is not None:
+            mdist.SPEC_SLACK = slack
         ei, N, X, Ws, bs, dY = _problem(F=F)
         m = ShardedGCN(ei, N, Ws, bs, device=torch.device("cpu"), aggr=aggr,
                        backend=CpuBackend(), fused=fused, chunks=chunks)
@@ -74,12 +77,12 @@ def _run(rank, world, port, aggr, out_q, F=16, fused=True, chunks=4, pack=True, 
         dist.destroy_process_group()
 
 
-def _launch(world, aggr, F=16, fused=True, chunks=4, pack=True, force=False):
+def _launch(world, aggr, F=16, fused=True, chunks=4, pack=True, force=False, slack=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_run, args=(r, world, port, aggr, q, F, fused, chunks, pack,
-                                            force))
+                                            force, slack))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -130,7 +133,27 @@ def test_packed_exchange_is_bitwise_the_dense_one(world, aggr, F, chunks):
                 np.testing.assert_array_equal(g, g1)
         st = rp["stats"]
         assert 0 < st["sent_words"] < 0.8 * st["dense_words"], st
+        # the second pass sent every in-place chunk at the sizes the first learnt
+        assert st.get("spec_chunks", 0) > 0 and st.get("spec_resent", 0) == 0, st
         assert rd["stats"]["dense_words"] == 0
+
+
+@pytest.mark.parametrize("world,F,chunks", [(2, 128, 3), (2, 256, 2)])
+def test_speculative_exchange_resends_chunks_that_outgrow_their_capacity(world, F, chunks):
+    """The second pass of every worker sends each in-place packed chunk at
+    the capacity the first pass learnt (dist.SPEC_EXCHANGE); with the slack
+    set to -50 % every such chunk outgrows it, and result() must send it
+    again at its true size before the next layer reads it: the same bits as
+    the dense exchange, with resends counted."""
+    packed = _launch(world, "add", F, True, chunks, pack=True, slack=-0.5)
+    dense = _launch(world, "add", F, True, chunks, pack=False)
+    for rp, rd in zip(packed, dense):
+        for key in ("out", "dX", "out_table"):
+            np.testing.assert_array_equal(rp[key], rd[key])
+        for key in ("grads", "grads_table"):
+            for g, g1 in zip(rp[key], rd[key]):
+                np.testing.assert_array_equal(g, g1)
+        assert rp["stats"].get("spec_resent", 0) > 0, rp["stats"]
 
 
 @pytest.mark.parametrize("aggr", ["add", "mean"])

@@ -5,7 +5,8 @@ collectives over gloo.  Here a ONE-rank `nccl` (= RCCL on ROCm) process group
 with mgcn.dist.set_force_collectives(True) makes the sharded stack issue every
 collective a rank of a multi-GPU group issues -- the chunked
 all_gather_into_tensor(async_op=True) of each layer's rows (dense), the packed
-exchange's size gather and payload gather (packed), the all_gather of the
+exchange's size gather and payload gather (packed; later steps at the learnt
+speculative capacity, and re-sent when it is too small), the all_gather of the
 inverse degrees at setup, the bucketed all_reduce of the gradients, and
 DataParallel's all_sum / broadcast / has-grad-flagged all_reduce -- on RCCL's
 stream, over HIP tensors.  The results must equal, bit for bit, the same
@@ -65,14 +66,28 @@ def _child(backend, force, port, q):
                 mdist.set_pack_exchange(pack)
                 m = mdist.ShardedGCN(ei, N, Ws, bs, device=dev, aggr=aggr, chunks=3)
                 assert m.fused
-                Xl = m.local_rows(X).requires_grad_(True)
-                out = m.forward(Xl)
-                out.backward(m.local_rows(dY))
-                mdist.allreduce_grads(m.params())
-                torch.cuda.synchronize()
                 key = f"{F}-{aggr}-{'packed' if pack else 'dense'}"
-                res[key] = [out.detach().cpu().numpy(), Xl.grad.cpu().numpy()] + \
-                    [p.grad.cpu().numpy() for p in m.params()]
+                # packed: step 2 sends every chunk at the sizes step 1 learnt
+                # (speculative capacity) and learns half of them (slack -50 %),
+                # step 3 sends at those (every chunk re-sent at its true
+                # size): each step the same bits
+                for step, slack in enumerate((0.02, -0.5, -0.5) if pack else (0.02,)):
+                    mdist.SPEC_SLACK = slack
+                    for p in m.params():
+                        p.grad = None
+                    Xl = m.local_rows(X).requires_grad_(True)
+                    out = m.forward(Xl)
+                    out.backward(m.local_rows(dY))
+                    mdist.allreduce_grads(m.params())
+                    torch.cuda.synchronize()
+                    got = [out.detach().cpu().numpy(), Xl.grad.cpu().numpy()] + \
+                        [p.grad.cpu().numpy() for p in m.params()]
+                    if step == 0:
+                        res[key] = got
+                    else:
+                        res[f"{key}-step{step}-same"] = all(
+                            np.array_equal(a, b) for a, b in zip(got, res[key]))
+                mdist.SPEC_SLACK = 0.02
         res["packed_words"] = dict(mdist.STATS)
         # DataParallel: all_sum, broadcast, the flagged gradient all-reduce
         lin = torch.nn.Linear(8, 4).to(dev)
@@ -105,8 +120,14 @@ def test_rccl_one_rank_forced_collectives_match_world_one(cuda):
     assert rc["backend"] == "nccl"
     # the packed exchange really ran (sizes gathered, payload sent packed)
     assert 0 < rc["packed_words"]["sent_words"] < rc["packed_words"]["dense_words"]
+    # the speculative-capacity steps: used, the too-small one re-sent, same bits
+    assert rc["packed_words"].get("spec_chunks", 0) > 0, rc["packed_words"]
+    assert rc["packed_words"].get("spec_resent", 0) > 0, rc["packed_words"]
     for key in ref:
         if key in ("backend", "packed_words", "dp"):
+            continue
+        if key.endswith("-same"):
+            assert rc[key] and ref[key], key
             continue
         for a, b in zip(rc[key], ref[key]):
             np.testing.assert_array_equal(a, b, err_msg=key)
