@@ -37,7 +37,7 @@ def _problem(N=3000, pairs=15000, F=32, L=3, seed=0):
     return ei, N, X, Ws, bs, dY
 
 
-def _run(rank, world, port, aggr, out_q, F=32, chunks=4):
+def _run(rank, world, port, aggr, out_q, F=32, chunks=4, identity=False):
     sys.path[:0] = [os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "meta-gcn_amd")]
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -53,6 +53,8 @@ def _run(rank, world, port, aggr, out_q, F=32, chunks=4):
         torch.cuda.set_device(dev)
         from mgcn.dist import ShardedGCN, allreduce_grads
         ei, N, X, Ws, bs, dY = _problem(F=F)
+        if identity:  # W = I: the layer products are exact, the oracle's sums bit for bit
+            Ws = [torch.eye(F) for _ in Ws]
         m = ShardedGCN(ei, N, Ws, bs, device=dev, aggr=aggr, chunks=chunks)
         Xl = m.local_rows(X).requires_grad_(True)
         out = m.forward(Xl)
@@ -76,11 +78,11 @@ def _run(rank, world, port, aggr, out_q, F=32, chunks=4):
         dist.destroy_process_group()
 
 
-def _launch(world, aggr, F=32, chunks=4):
+def _launch(world, aggr, F=32, chunks=4, identity=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_run, args=(r, world, port, aggr, q, F, chunks))
+    procs = [ctx.Process(target=_run, args=(r, world, port, aggr, q, F, chunks, identity))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -116,6 +118,38 @@ def test_sharded_gpu_matches_one_rank(cuda, world, aggr, F, chunks):
         for key in ("grads", "grads_table"):  # re-associated partial sums
             for g, g1 in zip(r[key], single[key]):
                 np.testing.assert_allclose(g, g1, rtol=1e-5, atol=1e-5 * np.abs(g1).max())
+
+
+@pytest.mark.parametrize("world,aggr,F,chunks", [(2, "add", 128, 3), (4, "mean", 128, 4),
+                                                  (2, "add", 256, 2), (2, "max", 32, 3)])
+def test_sharded_gpu_identity_weights_match_the_oracle(cuda, oracle, world, aggr, F, chunks):
+    """The sharded step on the GPU against the ORACLE, not against itself:
+    with W = I every layer product is exact, so each rank's output rows and
+    dX rows must equal, bit for bit, the oracle chain (oracle/mgcn_oracle.c,
+    the reference's scatter_add / scatter_mean / scatter_max path,
+    gcn_base_models.py:199-243) over the whole graph -- the exchanged tables
+    (packed and gathered in place at F = 128 / 256; the second pass at the
+    speculative capacity the first learnt), the chunked all-gathers and the
+    row-range views included.  Both input forms: local rows (with dX) and the
+    replicated table (bench.py's)."""
+    shards = _launch(world, aggr, F, chunks, identity=True)
+    ei, N, X, Ws, bs, dY = _problem(F=F)
+    ein = ei.numpy()
+    wf, wb, rs = oracle.edge_factors(ein, N, "sm")
+    h, outs, ams = X.numpy(), [], []
+    for i in range(3):
+        h, am = oracle.aggr_fwd(ein, h, wf, aggr, bs[i].numpy(), relu=i < 2)
+        outs.append(h)
+        ams.append(am)
+    g = dY.numpy()
+    for l in (2, 1, 0):
+        g, _ = oracle.aggr_bwd(ein, g, wb, rs, aggr, outs[l], relu=l < 2, argmax=ams[l])
+    assert shards[0]["lo"] == 0 and shards[-1]["hi"] == N
+    for r in shards:
+        lo, hi = r["lo"], r["hi"]
+        np.testing.assert_array_equal(r["out"], outs[2][lo:hi])
+        np.testing.assert_array_equal(r["out_table"], outs[2][lo:hi])
+        np.testing.assert_array_equal(r["dX"], g[lo:hi])
 
 
 def test_sharded_fused_matches_single_gpu_stack(cuda):
