@@ -61,7 +61,11 @@ def _pack_cpu(x):
     return send[:head + total], counts
 
 
-@pytest.mark.parametrize("n,F", [(1, 32), (37, 32), (1000, 128), (4097, 256), (64, 96)])
+@pytest.mark.parametrize("n,F", [(1, 32), (37, 32), (1000, 128), (4097, 256), (64, 96),
+                                 (130, 512),
+                                 # past one grid-stride trip of the capped grid (the
+                                 # pack kernels take 4 rows per wave and trip)
+                                 (300_001, 256), (270_007, 128)])
 def test_pack_layout_matches_cpu_double_and_round_trips(cuda, n, F):
     from mgcn import ops
     x = _rows(n, F, seed=n + F)
