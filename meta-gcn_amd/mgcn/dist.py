@@ -499,9 +499,10 @@ class _ChunkExchange:
             totals = torch.empty(P, dtype=torch.int64, device=dev)
             work = _gather_into(totals, total, P, self.group, True)
         # (in place only: a truncated segment is then read by nothing before
-        # result() has re-sent it; the expanding path would unpack it at once)
+        # result() has re-sent it; the expanding path would unpack it at once.
+        # An emulated rank takes it too: it times a real rank's later steps)
         hint = sh.cap_hint.get((self.key, c)) if (
-            SPEC_EXCHANGE and self.inplace and self.key is not None and not sh.emulated) else None
+            SPEC_EXCHANGE and self.inplace and self.key is not None) else None
         if hint is not None:
             # speculative: the payload goes right behind the pack at the
             # capacity the last exchange saw; result() checks the sizes
