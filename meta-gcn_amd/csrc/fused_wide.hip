@@ -1175,13 +1175,23 @@ int launch_wide_ws_u(const WideArgs &a, bool bwd, int epi, int grid, hipStream_t
                           : launch_wide_ws_un<U, 4>(a, bwd, epi, grid, s);
 }
 
-int wide_grid() {
+int wide_cus() {
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     cus = 256;
-  return 2 * cus;
+  return cus;
 }
+int wide_grid() { return 2 * wide_cus(); }  // the two-phase kernels: two workgroups per CU
+// The warp-specialised kernels hold one workgroup per CU at a time (their LDS),
+// over a grid of kWideWsGridMult x CUs: the hardware hands the next workgroup
+// to whichever CU frees first, so a CU slowed by work beside it -- a rank's
+// RCCL workgroups during the exchange -- takes fewer chunks instead of
+// holding the whole launch back (round 6, config-5 rank beside a 64-workgroup
+// stand-in for the receive writes: 183.8 -> 154.9 ms/step, 4 / 16 / 32 x:
+// 162.5 / 155.7 / 156.7; alone 119.4 vs 120.1 ms, profiles/r06/recv_load_ab.json)
+constexpr int kWideWsGridMult = 8;
+int wide_ws_grid() { return kWideWsGridMult * wide_cus(); }
 
 template <int U, bool PAIR>
 int launch_wide_p(const WideArgs &a, bool bwd, int epi, int grid, hipStream_t s) {
@@ -1206,8 +1216,8 @@ int launch_wide_legacy(const WideArgs &a, bool bwd, int epi, int grid, hipStream
 int launch_wide(const WideArgs &a, bool bwd, int epi, int *grid, hipStream_t s) {
   if (a.pk != nullptr || (g_wide_ws & (bwd ? 2 : 1))) {  // (packed tables: this form only)
     const int64_t n_chunks = (a.n_rows + kSRows - 1) / kSRows;
-    const int64_t cus = wide_grid() / 2;  // one workgroup per CU
-    *grid = (int)(cus < n_chunks ? cus : n_chunks);
+    const int64_t g = wide_ws_grid();  // one workgroup per CU resident at a time
+    *grid = (int)(g < n_chunks ? g : n_chunks);
     return launch_wide_ws_u<kWideU>(a, bwd, epi, *grid, s);
   }
   const int64_t n_chunks = (a.n_rows + kWRows - 1) / kWRows;
@@ -1245,7 +1255,9 @@ void set_packed(WideArgs &a, const mgcn_packed_table *pk) {
 
 size_t xw_wide_workspace_bytes(bool bwd) {
   return align_up((size_t)kWImgFrags * 16, 256) +
-         (bwd ? align_up((size_t)wide_grid() * kWF * 4, 256) : 0);
+         (bwd ? align_up((size_t)(wide_ws_grid() > wide_grid() ? wide_ws_grid() : wide_grid()) *
+                             kWF * 4, 256)
+              : 0);
 }
 
 int xw_wide_fwd(int64_t n_rows, const int64_t *rowptr, const int32_t *col, const float *w,

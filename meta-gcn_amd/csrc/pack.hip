@@ -278,3 +278,36 @@ extern "C" int mgcn_unpack_rows(int64_t n_seg, int64_t n, int32_t F, const uint3
               as_stream(stream), n_seg, n, (int)F, buf, seg_words, T, ldt);
   return check_launch("unpack_kernel");
 }
+
+#if MGCN_EXPERIMENT
+// Experiment build only (libmgcn_exp.so; not in mgcn.h): a stand-in for the
+// HBM writes of a rank's RCCL receive, for scripts/config5_rank.py
+// --recv-load-wgs.  `workgroups` 256-thread workgroups (a collective's
+// footprint: RCCL runs its all-gather in a few dozen workgroups) write
+// `total_bytes` of zeros with 16-B nt stores, wrapping over [buf, buf +
+// buf_bytes): the received words landing in HBM while the rank computes.
+// A bounded grid-stride loop (no flag, no spin).
+namespace {
+typedef unsigned int wl_u32x4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void hbm_write_load_kernel(wl_u32x4 *__restrict__ buf, int64_t n16,
+                                                             int64_t total16) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const wl_u32x4 z = {0u, 0u, 0u, 0u};
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total16; i += stride)
+    __builtin_nontemporal_store(z, buf + (i % n16));
+}
+}  // namespace
+
+extern "C" int mgcn_exp_hbm_write_load(void *buf, int64_t buf_bytes, int64_t total_bytes,
+                                       int32_t workgroups, void *stream) {
+  clear_error();
+  MGCN_REQUIRE(buf != nullptr && buf_bytes >= 16 && total_bytes >= 0 && workgroups > 0 &&
+                   reinterpret_cast<uintptr_t>(buf) % 16 == 0,
+               "mgcn_exp_hbm_write_load: bad arguments");
+  if (total_bytes == 0) return MGCN_OK;
+  hipLaunchKernelGGL(hbm_write_load_kernel, dim3((unsigned)workgroups), dim3(256), 0,
+                     as_stream(stream), static_cast<wl_u32x4 *>(buf), buf_bytes / 16,
+                     total_bytes / 16);
+  return check_launch("hbm_write_load_kernel");
+}
+#endif

@@ -20,6 +20,7 @@ the xGMI link rate.
 Prints one JSON line.
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -44,6 +45,71 @@ def _global_ids(t, sh):
     i = c * cr + (t - c * P * cr - k * cr)
     b = torch.tensor(sh.bounds, dtype=torch.int64, device=t.device)
     return b[k] + i
+
+
+def receive_load(step, args, N, F, L, fused, packed, ratio, dev):
+    """The packed step timed beside a stand-in for the writes a real rank's
+    RCCL receive makes into its HBM while it computes: per step, the received
+    (P - 1) / P of every exchanged table (packed ones at `ratio`) written by
+    `--recv-load-wgs` workgroups on a side stream (libmgcn_exp.so's
+    mgcn_exp_hbm_write_load; a collective runs in a few dozen workgroups).
+    Returns the main stream's ms per step under that load, the side stream's,
+    and the load's time alone."""
+    from mgcn import _lib as L_
+    from mgcn import dist as mdist
+    lib = L_.load()
+    fn = getattr(lib, "mgcn_exp_hbm_write_load", None)
+    if fn is None:
+        sys.exit("--recv-load-wgs needs MGCN_LIB=<libmgcn_exp.so> (make -C meta-gcn_amd/csrc exp)")
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
+                   ctypes.c_void_p]
+    fn.restype = ctypes.c_int
+    P = args.world
+    tables = (2 * (L - 1)) if fused else (2 * L)
+    packed_tables = (2 * L - 3) if packed else 0
+    eff = tables - packed_tables + packed_tables * ratio
+    per_step = int(eff * 4.0 * N * F * (P - 1) / P) // 16 * 16
+    buf = torch.empty(4 << 30, dtype=torch.uint8, device=dev)
+    side = torch.cuda.Stream(device=dev)
+    mdist.set_pack_exchange(True)
+
+    def load(n_steps):
+        with torch.cuda.stream(side):
+            L_.check(fn(buf.data_ptr(), buf.numel(), per_step * n_steps, args.recv_load_wgs,
+                        side.cuda_stream), "mgcn_exp_hbm_write_load")
+
+    # the load alone
+    torch.cuda.synchronize()
+    a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a0.record(side)
+    load(args.steps)
+    a1.record(side)
+    torch.cuda.synchronize()
+    alone = a0.elapsed_time(a1) / args.steps
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    main = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    side.wait_stream(main)
+    e0.record(main)
+    s0.record(side)
+    load(args.steps)  # the whole timed region's receive writes, from its start
+    s1.record(side)
+    for _ in range(args.steps):
+        step()
+    e1.record(main)
+    torch.cuda.synchronize()
+    del buf
+    return {"workgroups": args.recv_load_wgs, "bytes_per_step": per_step,
+            "alone_ms_per_step": alone, "alone_TBs": per_step / (alone * 1e-3) / 1e12,
+            "ms_per_step_under_load": e0.elapsed_time(e1) / args.steps,
+            "side_ms_per_step_under_load": s0.elapsed_time(s1) / args.steps,
+            "note": "main stream: the packed rank step (P segments aliased, as in ms_per_step); "
+                    "side stream: the step's received bytes written by a workgroup-limited "
+                    "kernel (16-B nt stores), a stand-in for RCCL's receive into HBM; the "
+                    "xGMI transfer itself is not modelled here"}
 
 
 def sample_check(model, Xt, odeg, n_rows, F, tol=1e-5):
@@ -113,6 +179,11 @@ def main():
                     help="no zero-skipping: the ReLU'd tables travel dense")
     ap.add_argument("--check-rows", type=int, default=1024,
                     help="rows per window of the sampled fp64 check (0: no check)")
+    ap.add_argument("--recv-load-wgs", type=int, default=0,
+                    help="also time the packed step beside a stand-in for a real rank's RCCL "
+                         "receive: this many workgroups writing the step's received bytes into "
+                         "HBM on a side stream (needs MGCN_LIB=<libmgcn_exp.so>: "
+                         "mgcn_exp_hbm_write_load)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
@@ -171,6 +242,9 @@ def main():
     ms_dense, _ = run(False)
     packed = model.fused and not args.dense_exchange
     ms, ratio = run(True) if packed else (ms_dense, 1.0)
+    recv_load = None
+    if args.recv_load_wgs > 0:
+        recv_load = receive_load(step, args, N, F, L, model.fused, packed, ratio, dev)
     timer = KernelTimer()
     ops.set_kernel_timer(timer)
     step()
@@ -239,6 +313,13 @@ def main():
            "pack_inplace": mdist.PACK_INPLACE,
            "peak_mem_gb": torch.cuda.max_memory_allocated() / 1e9,
            "sampled_check": check}
+    if recv_load is not None:
+        # P = world with the local step measured beside the receive writes
+        p = args.world
+        x8 = curve[str(p)]["exchange_ms"]
+        recv_load["step_ms_p%d" % p] = max(recv_load["ms_per_step_under_load"], x8)
+        recv_load["speedup_1_to_%d" % p] = curve["1"]["compute_ms"] / recv_load["step_ms_p%d" % p]
+        out["recv_load"] = recv_load
     print(json.dumps(out), flush=True)
     if check is not None and not check["ok"]:
         sys.exit("config5_rank: sampled rows outside the fp64 bound")
