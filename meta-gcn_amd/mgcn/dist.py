@@ -352,11 +352,13 @@ def set_pack_exchange(enabled) -> None:
     """Zero-skipping (packed) exchange of the ReLU'd tables of the sharded
     stack: True / False, or "auto" (the default).  Packing about halves the
     words on xGMI.  Where the next layer's fused kernel gathers packed tables
-    in place (F = 256, round 6: no unpack pass) "auto" always packs;
-    elsewhere the received segments are expanded into the dense table first
-    (mgcn_unpack_rows), a pass that writes the received (P - 1)/P of every
-    table, and "auto" packs only up to PACK_AUTO_MAX_WORLD ranks (the link
-    time a table saves shrinks as 1/P while that pass grows)."""
+    in place (F = 128 / 256, round 6: no unpack pass) "auto" packs row chunks
+    of at least PACK_AUTO_MIN_CHUNK_BYTES (smaller ones cost more in launches
+    than they save on the links); elsewhere the received segments are
+    expanded into the dense table first (mgcn_unpack_rows), a pass that
+    writes the received (P - 1)/P of every table, and "auto" packs only up to
+    PACK_AUTO_MAX_WORLD ranks (the link time a table saves shrinks as 1/P
+    while that pass grows)."""
     global PACK_EXCHANGE
     PACK_EXCHANGE = enabled if enabled == "auto" else bool(enabled)
 
@@ -412,10 +414,20 @@ def _inplace_ok(shard: Shard, backend, F: int) -> bool:
         (F != 128 or _single_recv_words(shard, F) * 4 <= 0x7ffffff0)
 
 
+# "auto" packs an in-place table only when its row chunks are at least this
+# big: a packed chunk costs a fixed ~70 us of launches and host work (pack,
+# sizes, payload), which small chunks do not earn back on the links (round 6,
+# scripts/config5_rank.py at config 2's shape, one rank of P = 8, 16-MB
+# chunks: 1.96 ms/step packed vs 1.14 dense, against 1.16 vs 1.67 ms of
+# exchange; config 5's 1.6-GB chunks: 120 vs 108 ms against 110 vs 167)
+PACK_AUTO_MIN_CHUNK_BYTES = 32 << 20
+
+
 def _pack_on(shard: Shard, backend=None, F: int = 0) -> bool:
     if PACK_EXCHANGE == "auto":
-        return shard.world <= PACK_AUTO_MAX_WORLD or (backend is not None and
-                                                      _inplace_ok(shard, backend, F))
+        if backend is not None and _inplace_ok(shard, backend, F):
+            return shard.chunk_rows * F * 4 >= PACK_AUTO_MIN_CHUNK_BYTES
+        return shard.world <= PACK_AUTO_MAX_WORLD
     return bool(PACK_EXCHANGE)
 
 

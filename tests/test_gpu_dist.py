@@ -51,7 +51,12 @@ def _run(rank, world, port, aggr, out_q, F=32, chunks=4, identity=False):
     try:
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
+        from mgcn import dist as mdist
         from mgcn.dist import ShardedGCN, allreduce_grads
+        # packed wherever the tables are ReLU'd ("auto" would keep these small
+        # chunks dense, dist.PACK_AUTO_MIN_CHUNK_BYTES): bit for bit the dense
+        # exchange, which world 1 takes
+        mdist.set_pack_exchange(True)
         ei, N, X, Ws, bs, dY = _problem(F=F)
         if identity:  # W = I: the layer products are exact, the oracle's sums bit for bit
             Ws = [torch.eye(F) for _ in Ws]
