@@ -298,6 +298,33 @@ __global__ __launch_bounds__(256) void hbm_write_load_kernel(wl_u32x4 *__restric
 }
 }  // namespace
 
+// the same with reads: copy [buf, buf + buf_bytes / 2) to the other half,
+// wrapping -- `total_bytes` written AND read (a rank's all-gather both reads
+// its own segment for every peer and receives theirs)
+namespace {
+__global__ __launch_bounds__(256) void hbm_copy_load_kernel(wl_u32x4 *__restrict__ buf, int64_t half16,
+                                                            int64_t total16) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total16; i += stride) {
+    const int64_t j = i % half16;
+    __builtin_nontemporal_store(__builtin_nontemporal_load(buf + j), buf + half16 + j);
+  }
+}
+}  // namespace
+
+extern "C" int mgcn_exp_hbm_copy_load(void *buf, int64_t buf_bytes, int64_t total_bytes,
+                                      int32_t workgroups, void *stream) {
+  clear_error();
+  MGCN_REQUIRE(buf != nullptr && buf_bytes >= 32 && total_bytes >= 0 && workgroups > 0 &&
+                   reinterpret_cast<uintptr_t>(buf) % 16 == 0,
+               "mgcn_exp_hbm_copy_load: bad arguments");
+  if (total_bytes == 0) return MGCN_OK;
+  hipLaunchKernelGGL(hbm_copy_load_kernel, dim3((unsigned)workgroups), dim3(256), 0,
+                     as_stream(stream), static_cast<wl_u32x4 *>(buf), buf_bytes / 32,
+                     total_bytes / 16);
+  return check_launch("hbm_copy_load_kernel");
+}
+
 extern "C" int mgcn_exp_hbm_write_load(void *buf, int64_t buf_bytes, int64_t total_bytes,
                                        int32_t workgroups, void *stream) {
   clear_error();

@@ -58,7 +58,7 @@ def receive_load(step, args, N, F, L, fused, packed, ratio, dev):
     from mgcn import _lib as L_
     from mgcn import dist as mdist
     lib = L_.load()
-    fn = getattr(lib, "mgcn_exp_hbm_write_load", None)
+    fn = getattr(lib, "mgcn_exp_hbm_%s_load" % args.recv_load_kind, None)
     if fn is None:
         sys.exit("--recv-load-wgs needs MGCN_LIB=<libmgcn_exp.so> (make -C meta-gcn_amd/csrc exp)")
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
@@ -101,8 +101,23 @@ def receive_load(step, args, N, F, L, fused, packed, ratio, dev):
         step()
     e1.record(main)
     torch.cuda.synchronize()
+    # per-kernel times of one more step beside the load (HIP events)
+    from mgcn import ops
+    timer = KernelTimer()
+    side.wait_stream(main)
+    load(2)  # (twice the step's bytes: the load surely spans the whole step)
+    ops.set_kernel_timer(timer)
+    step()
+    torch.cuda.synchronize()
+    ops.set_kernel_timer(None)
+    kern = {}
+    for name, k in timer.summary().items():
+        k.pop("sizes")
+        kern[name] = {kk: round(v, 4) if isinstance(v, float) else v for kk, v in k.items()}
     del buf
-    return {"workgroups": args.recv_load_wgs, "bytes_per_step": per_step,
+    return {"workgroups": args.recv_load_wgs, "kind": args.recv_load_kind,
+            "bytes_per_step": per_step,
+            "kernels_under_load": kern,
             "alone_ms_per_step": alone, "alone_TBs": per_step / (alone * 1e-3) / 1e12,
             "ms_per_step_under_load": e0.elapsed_time(e1) / args.steps,
             "side_ms_per_step_under_load": s0.elapsed_time(s1) / args.steps,
@@ -179,6 +194,9 @@ def main():
                     help="no zero-skipping: the ReLU'd tables travel dense")
     ap.add_argument("--check-rows", type=int, default=1024,
                     help="rows per window of the sampled fp64 check (0: no check)")
+    ap.add_argument("--recv-load-kind", choices=["write", "copy"], default="write",
+                    help="the stand-in writes the received bytes (write) or also reads as many "
+                         "(copy: a rank's all-gather reads its own segment for every peer)")
     ap.add_argument("--recv-load-wgs", type=int, default=0,
                     help="also time the packed step beside a stand-in for a real rank's RCCL "
                          "receive: this many workgroups writing the step's received bytes into "
