@@ -480,7 +480,8 @@ class _ChunkExchange:
         self.big = None
         self.base = []
         self.key = key
-        self.spec = []      # speculative chunks: (c, rows, send, counts, totals, work, cap, how)
+        self.spec = []      # speculative chunks: (c, rows, send, counts, totals, work, cap)
+        self.spec_ev = []   # ... and (GPU) where each one's sizes are done
         if shard.cap_hint is None:
             shard.cap_hint = {}
 
@@ -517,7 +518,14 @@ class _ChunkExchange:
             SPEC_EXCHANGE and self.inplace and self.key is not None) else None
         if hint is not None:
             # speculative: the payload goes right behind the pack at the
-            # capacity the last exchange saw; result() checks the sizes
+            # capacity the last exchange saw; result() checks the sizes.  (An
+            # event marks where this chunk's sizes are done on the compute
+            # stream: result() waits for those, not for the payloads queued
+            # behind them.)
+            if dev.type == "cuda":
+                ev_sz = torch.cuda.Event()
+                ev_sz.record()
+                self.spec_ev.append(ev_sz)
             self._payload(c, rows, send, counts, hint)
             self.spec.append((c, rows, send, counts, totals, work, hint))
             self.stats["spec_chunks"] = self.stats.get("spec_chunks", 0) + 1
@@ -641,10 +649,33 @@ class _ChunkExchange:
         all-gathered); the hints follow the sizes."""
         if not self.spec:
             return
-        for *_, work, _cap in self.spec:
-            if work is not None:
-                work.wait()
-        sizes = torch.stack([t.view(-1).max() for *_, t, _w, _cap in self.spec]).cpu()
+        tots = [t for *_, t, _w, _cap in self.spec]
+        if self.spec_ev:
+            # the sizes reach the host through the side stream, which waits
+            # for them alone: the compute stream keeps running the payloads
+            # (and whatever else is queued) while the host waits
+            dev = tots[0].device
+            side = _size_stream(dev)
+            with torch.cuda.stream(side):
+                for ev_sz in self.spec_ev:
+                    side.wait_event(ev_sz)
+                for *_, work, _cap in self.spec:
+                    if work is not None:
+                        work.wait()
+                dsz = torch.stack([t.view(-1).max() for t in tots])
+                host = torch.empty(dsz.numel(), dtype=dsz.dtype, pin_memory=True)
+                host.copy_(dsz, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(side)
+            for t in tots:
+                t.record_stream(side)
+            ev.synchronize()
+            sizes = host
+        else:
+            for *_, work, _cap in self.spec:
+                if work is not None:
+                    work.wait()
+            sizes = torch.stack([t.view(-1).max() for t in tots]).cpu()
         lim = self.sh.chunk_rows * self.local.size(1)
         for (c, rows, send, counts, totals, work, cap), true in zip(self.spec, sizes.tolist()):
             self.sh.cap_hint[(self.key, c)] = _spec_cap(int(true), lim)
@@ -652,6 +683,7 @@ class _ChunkExchange:
                 self.stats["spec_resent"] = self.stats.get("spec_resent", 0) + 1
                 self._payload(c, rows, send, counts, int(true), again=True)
         self.spec = []
+        self.spec_ev = []
 
     def wait(self) -> None:
         self.finish()
