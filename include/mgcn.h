@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define MGCN_ABI_VERSION 21
+#define MGCN_ABI_VERSION 22
 
 /* return codes */
 #define MGCN_OK 0
@@ -736,6 +736,22 @@ int mgcn_pack_rows_values(int64_t n, int32_t F, const float *X, int64_t ldx,
                           const int32_t *offs, uint32_t *hdr, uint32_t *vals, void *stream);
 int mgcn_unpack_rows(int64_t n_seg, int64_t n, int32_t F, const uint32_t *buf, int64_t seg_words,
                      float *T, int64_t ldt, void *stream);
+
+/*
+ * The same packed chunk in ONE pass (ABI 22; F in {32, 64, 128, 256}): hdr
+ * (masks and positions), vals and *total (device int64: the number of
+ * values) from a single read of the rows -- a workgroup holds its tile of
+ * rows in registers and takes its offset from its predecessors' published
+ * counts (decoupled look-back), so neither the count pass's read nor the
+ * host-side scan of the counts is needed.  Bit for bit the two-pass output.
+ * workspace: mgcn_pack_rows_workspace_bytes(n, F) bytes, 16-byte aligned
+ * (cleared by the call on `stream`).  A look-back that waits past the spin
+ * bound reports MGCN_EDEVICE (see mgcn_check_device).
+ */
+size_t mgcn_pack_rows_workspace_bytes(int64_t n, int32_t F);
+int mgcn_pack_rows(int64_t n, int32_t F, const float *X, int64_t ldx, uint32_t *hdr,
+                   uint32_t *vals, int64_t *total, void *workspace, size_t workspace_bytes,
+                   void *stream);
 
 /*
  * A packed exchange table gathered in place (ABI 21; the fused 128- and

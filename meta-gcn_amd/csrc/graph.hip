@@ -73,6 +73,7 @@ const char *device_error_what(unsigned code) {
   switch (code) {
     case kDevErrDws: return "spmm_xw_bwd_ws_kernel (128-wide adjoint)";
     case kDevErrWide: return "spmm_xw_wide_ws_kernel (256-wide layer)";
+    case kDevErrPack: return "pack_rows_kernel (single-pass pack)";
     default: return "unknown kernel";
   }
 }
@@ -82,7 +83,7 @@ int take_device_error() {
   const unsigned code = *g_dev_err_host;
   if (code == 0) return MGCN_OK;
   *g_dev_err_host = 0u;
-  set_error("device: %s stopped at a warp-specialised hand-off that exceeded its spin bound; "
+  set_error("device: %s stopped at a hand-off that exceeded its spin bound; "
             "the outputs of that launch are invalid (code %u)",
             device_error_what(code), code);
   return MGCN_EDEVICE;

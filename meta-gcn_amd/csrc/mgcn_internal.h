@@ -36,6 +36,7 @@ extern uint32_t g_spin_limit;                       // kSpinLimitDefault unless 
 // it after a stream sync.
 constexpr unsigned kDevErrDws = 1;   // spmm_xw_bwd_ws_kernel: hand-off spin bound exceeded
 constexpr unsigned kDevErrWide = 2;  // spmm_xw_wide_ws_kernel: hand-off spin bound exceeded
+constexpr unsigned kDevErrPack = 3;  // pack_rows_kernel: look-back spin bound exceeded
 unsigned *device_error_word();       // device pointer (nullptr + set_error on failure)
 int take_device_error();
 

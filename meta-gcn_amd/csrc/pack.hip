@@ -212,6 +212,145 @@ __global__ __launch_bounds__(64 * kPkWaves) void unpack_kernel(int64_t n_seg, in
   }
 }
 
+// Single-pass pack (round 6): counts, offsets and values in ONE read of the
+// chunk.  A workgroup takes a tile of rows -- a ticket (atomicAdd) orders the
+// tiles by start, so every tile's predecessors are resident or done -- and
+// holds them in registers (kPrIters 16-B loads per lane); it publishes its
+// nonzero count, looks back over its predecessors' published counts for its
+// offset (decoupled look-back: a predecessor's aggregate, or its inclusive
+// prefix, which ends the walk), publishes its own inclusive prefix and writes
+// the header pairs and values from the registers.  The two-pass form reads
+// every row twice (count, then values) and scans the counts between them.
+// Rows of one 256-word segment only (F = 4 G: 32, 64, 128, 256).
+// Status word of a tile: (flag << 62) | value, flag 1 = aggregate, 2 =
+// inclusive prefix; 0 = not yet published.  Relaxed agent-scope atomics: the
+// word carries its own data.  A walk that waits past the spin bound stores
+// kDevErrPack and takes 0 for the missing part (every wave still finishes).
+#ifndef MGCN_PR_ITERS
+#define MGCN_PR_ITERS 16
+#endif
+constexpr int kPrIters = MGCN_PR_ITERS;
+constexpr uint64_t kPrAgg = 1ull << 62, kPrInc = 2ull << 62, kPrVal = (1ull << 62) - 1;
+
+template <int G>
+constexpr int pr_tile_rows() { return kPrIters * (64 / G) * kPkWaves; }
+
+template <int G>
+__global__ __launch_bounds__(64 * kPkWaves) void pack_rows_kernel(
+    int64_t n, const float *__restrict__ X, int64_t ldx, uint32_t *__restrict__ hdr,
+    uint32_t *__restrict__ vals, int64_t *__restrict__ total, uint64_t *__restrict__ status,
+    unsigned *__restrict__ ticket, int64_t n_tiles, uint32_t spin_limit, unsigned *err) {
+  const PkLane<G> p = pk_lane<G>();
+  constexpr int RPW = 64 / G;
+  constexpr int RW = kPrIters * RPW;  // rows per wave
+  constexpr int RT = RW * kPkWaves;   // rows per tile
+  constexpr int WORDS = G / 8;        // mask words per row (F = 4 G)
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  __shared__ int64_t s_tile, s_prefix;
+  __shared__ int64_t s_wsum[kPkWaves];
+  if (threadIdx.x == 0) s_tile = (int64_t)atomicAdd(ticket, 1u);
+  __syncthreads();
+  const int64_t tile = s_tile;
+  const int64_t r0 = tile * RT + (int64_t)wave * RW + p.grp;
+
+  // the tile's rows into registers; per row, this lane's row offset in the wave
+  uint4 v[kPrIters];
+#pragma unroll
+  for (int i = 0; i < kPrIters; ++i) {
+    const int64_t r = r0 + (int64_t)i * RPW;
+    v[i] = r < n ? *reinterpret_cast<const uint4 *>(X + r * ldx + 4 * p.gl)
+                 : make_uint4(0u, 0u, 0u, 0u);
+  }
+  const uint64_t groups_below = (1ull << (p.grp * G)) - 1ull;  // lanes of the lower groups
+  int64_t wsum = 0;  // wave-uniform: values of the wave's rows so far
+  int32_t roff[kPrIters];
+#pragma unroll
+  for (int i = 0; i < kPrIters; ++i) {
+    const uint64_t b0 = __ballot(v[i].x != 0u), b1 = __ballot(v[i].y != 0u);
+    const uint64_t b2 = __ballot(v[i].z != 0u), b3 = __ballot(v[i].w != 0u);
+    roff[i] = (int32_t)(wsum + __popcll(b0 & groups_below) + __popcll(b1 & groups_below) +
+                        __popcll(b2 & groups_below) + __popcll(b3 & groups_below));
+    wsum += __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
+  }
+  if (lane == 0) s_wsum[wave] = wsum;
+  __syncthreads();
+  int64_t agg = 0, woff = 0;
+#pragma unroll
+  for (int w = 0; w < kPkWaves; ++w) {
+    woff += w < wave ? s_wsum[w] : 0;
+    agg += s_wsum[w];
+  }
+
+  if (wave == 0) {
+    int64_t excl = 0;
+    if (tile == 0) {
+      if (lane == 0) __hip_atomic_store(status, kPrInc | (uint64_t)agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      if (lane == 0)
+        __hip_atomic_store(status + tile, kPrAgg | (uint64_t)agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int64_t look = tile - 1;
+      uint32_t spins = 0;
+      for (;;) {
+        // lane l reads tile look - l (before tile 0: an inclusive 0)
+        const int64_t q = look - lane;
+        const uint64_t st = q >= 0 ? __hip_atomic_load(status + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                   : kPrInc;
+        const uint64_t inc = __ballot((st >> 62) == 2u);
+        const uint64_t none = __ballot((st >> 62) == 0u);
+        const int first = inc != 0 ? __builtin_ctzll(inc) : 64;  // nearest inclusive prefix
+        const uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1ull);
+        if (none & need) {  // a tile on the way has not published yet
+          if (++spins > spin_limit) {
+            report_device_error(err, kDevErrPack);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        int64_t part = lane <= first ? (int64_t)(st & kPrVal) : 0;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) part += __shfl_xor(part, off, 64);
+        excl += part;
+        if (first < 64) break;
+        look -= 64;
+      }
+      if (lane == 0)
+        __hip_atomic_store(status + tile, kPrInc | (uint64_t)(excl + agg), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0) {
+      s_prefix = excl;
+      if (tile == n_tiles - 1) *total = excl + agg;
+    }
+  }
+  __syncthreads();
+
+  // header pairs and values from the registers
+  const int64_t base = s_prefix + woff;
+  const uint64_t lo = p.below >> (p.grp * G);
+#pragma unroll
+  for (int i = 0; i < kPrIters; ++i) {
+    const int64_t r = r0 + (int64_t)i * RPW;
+    const bool ok = r < n;
+    bool nz[4];
+    uint64_t b[4];
+    seg_bits<G>(p, ok, v[i], nz, b);
+    const int64_t rowpos = base + roff[i];
+    if (ok && p.gl < WORDS) {
+      const uint64_t under = (1ull << (8 * p.gl)) - 1ull;  // the lanes of words below gl
+      const int64_t pw = rowpos + __popcll(b[0] & under) + __popcll(b[1] & under) +
+                         __popcll(b[2] & under) + __popcll(b[3] & under);
+      *reinterpret_cast<uint2 *>(hdr + 2 * (r * WORDS + p.gl)) = make_uint2(seg_word(b, p.gl), (uint32_t)pw);
+    }
+    int64_t q = rowpos + __popcll(b[0] & lo) + __popcll(b[1] & lo) + __popcll(b[2] & lo) + __popcll(b[3] & lo);
+    if (nz[0]) vals[q++] = v[i].x;
+    if (nz[1]) vals[q++] = v[i].y;
+    if (nz[2]) vals[q++] = v[i].z;
+    if (nz[3]) vals[q++] = v[i].w;
+  }
+}
+
 int pk_group(int F) { return F >= 256 ? 64 : F >= 128 ? 32 : F >= 64 ? 16 : 8; }
 
 unsigned pk_grid(int64_t rows, int G) {
@@ -261,6 +400,47 @@ extern "C" int mgcn_pack_rows_values(int64_t n, int32_t F, const float *X, int64
   PK_DISPATCH(G, pack_values_kernel, dim3(pk_grid(n, G)), dim3(64 * kPkWaves), 0,
               as_stream(stream), n, (int)F, X, ldx, offs, hdr, vals);
   return check_launch("pack_values_kernel");
+}
+
+extern "C" size_t mgcn_pack_rows_workspace_bytes(int64_t n, int32_t F) {
+  if (n <= 0 || (F != 32 && F != 64 && F != 128 && F != 256)) return 0;
+  const int G = pk_group(F);
+  const int64_t rt = G == 64 ? pr_tile_rows<64>() : G == 32 ? pr_tile_rows<32>()
+                     : G == 16 ? pr_tile_rows<16>() : pr_tile_rows<8>();
+  return (size_t)(16 + 8 * ((n + rt - 1) / rt));
+}
+
+extern "C" int mgcn_pack_rows(int64_t n, int32_t F, const float *X, int64_t ldx, uint32_t *hdr,
+                              uint32_t *vals, int64_t *total, void *workspace,
+                              size_t workspace_bytes, void *stream) {
+  clear_error();
+  if (int rc = take_device_error()) return rc;  // a previous launch failed on the device
+  MGCN_REQUIRE(n >= 0 && (F == 32 || F == 64 || F == 128 || F == 256) && ldx >= F,
+               "mgcn_pack_rows: need n >= 0, F in {32, 64, 128, 256}, ldx >= F");
+  MGCN_REQUIRE(total != nullptr, "mgcn_pack_rows: null total");
+  hipStream_t s = as_stream(stream);
+  if (n == 0) {
+    MGCN_HIP_TRY(hipMemsetAsync(total, 0, sizeof(int64_t), s));
+    return MGCN_OK;
+  }
+  MGCN_REQUIRE(X && hdr && vals && workspace, "mgcn_pack_rows: null array");
+  MGCN_REQUIRE(pk_aligned(X, ldx), "mgcn_pack_rows: rows must be 16-byte aligned");
+  MGCN_REQUIRE((uintptr_t)hdr % 8 == 0 && (uintptr_t)workspace % 16 == 0,
+               "mgcn_pack_rows: hdr must be 8-byte and workspace 16-byte aligned");
+  const size_t need = mgcn_pack_rows_workspace_bytes(n, F);
+  MGCN_REQUIRE(workspace_bytes >= need, "mgcn_pack_rows: workspace of %zu bytes < %zu",
+               workspace_bytes, need);
+  unsigned *err = device_error_word();
+  if (err == nullptr) return MGCN_EHIP;
+  const int64_t n_tiles = (int64_t)(need - 16) / 8;
+  MGCN_REQUIRE(n_tiles < (1ll << 31), "mgcn_pack_rows: too many rows");
+  // the ticket and the tiles' status words start at 0 every launch
+  MGCN_HIP_TRY(hipMemsetAsync(workspace, 0, need, s));
+  unsigned *ticket = static_cast<unsigned *>(workspace);
+  uint64_t *status = reinterpret_cast<uint64_t *>(static_cast<char *>(workspace) + 16);
+  PK_DISPATCH(pk_group(F), pack_rows_kernel, dim3((unsigned)n_tiles), dim3(64 * kPkWaves), 0, s,
+              n, X, ldx, hdr, vals, total, status, ticket, n_tiles, g_spin_limit, err);
+  return check_launch("pack_rows_kernel");
 }
 
 extern "C" int mgcn_unpack_rows(int64_t n_seg, int64_t n, int32_t F, const uint32_t *buf,

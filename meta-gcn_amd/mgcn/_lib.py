@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmgcn.so")
 
 # constants mirrored from include/mgcn.h
-ABI_VERSION = 21
+ABI_VERSION = 22
 OK, EINVAL, EINDEX, EHIP, EWORKSPACE, EDEVICE = 0, 1, 2, 3, 4, 5
 REDUCE_SUM, REDUCE_MEAN, REDUCE_MAX = 0, 1, 2
 NORM_NONE, NORM_SM, NORM_RW = 0, 1, 2
@@ -114,6 +114,8 @@ SIGNATURES = {
     "mgcn_pack_rows_count": (_int, [_i64, _i32, _vp, _i64, _vp, _vp, _vp]),
     "mgcn_pack_rows_values": (_int, [_i64, _i32, _vp, _i64, _vp, _vp, _vp, _vp]),
     "mgcn_unpack_rows": (_int, [_i64, _i64, _i32, _vp, _i64, _vp, _i64, _vp]),
+    "mgcn_pack_rows_workspace_bytes": (_sz, [_i64, _i32]),
+    "mgcn_pack_rows": (_int, [_i64, _i32, _vp, _i64, _vp, _vp, _vp, _vp, _sz, _vp]),
     "mgcn_spmm_xw_fwd_packed": (_int, [_i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp,
                                        _i64, _int, _int, _vp, _vp, _i64, _vp, _sz, _vp]),
     "mgcn_spmm_xw_bwd_packed": (_int, [_i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp,

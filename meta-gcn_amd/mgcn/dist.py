@@ -115,6 +115,14 @@ class HipBackend:
         from .ops import pack_rows_values
         pack_rows_values(rows, offs, hdr, vals)
 
+    def pack_rows(self, rows, hdr, vals, total):
+        from .ops import pack_rows
+        pack_rows(rows, hdr, vals, total)
+
+    def pack_rows_ok(self, F):
+        from .ops import PACK_ROWS_WIDTHS
+        return F in PACK_ROWS_WIDTHS
+
     def packed_gather_ok(self, F):
         """The fused layer kernels of width F gather packed tables in place
         (mgcn_spmm_xw_fwd_packed / _bwd_packed: F = 128 and 256)."""
@@ -393,6 +401,18 @@ def set_spec_exchange(enabled: bool) -> None:
     SPEC_EXCHANGE = bool(enabled)
 
 
+# Single-pass pack (round 6): where the backend has it (mgcn_pack_rows, F in
+# 32 / 64 / 128 / 256) a chunk is packed in one read of its rows, its value
+# count left on the device -- no count pass, no scan of the counts, the pack
+# done before the sizes are exchanged.  set_fused_pack(False): the two passes.
+FUSED_PACK = os.environ.get("MGCN_FUSED_PACK", "1") != "0"
+
+
+def set_fused_pack(enabled: bool) -> None:
+    global FUSED_PACK
+    FUSED_PACK = bool(enabled)
+
+
 def _spec_cap(true_words: int, limit: int) -> int:
     c = int(true_words * (1.0 + SPEC_SLACK)) + (64 if SPEC_SLACK >= 0 else 0)
     return max(0, min(c, limit))
@@ -502,9 +522,18 @@ class _ChunkExchange:
         head = 2 * cr * self.words
         # (+4 words: a lane's 16-B value read may run 3 words past the values)
         send = torch.empty(head + cr * rows.size(1) + 4, dtype=torch.int32, device=dev)
-        counts = torch.empty(cr, dtype=torch.int32, device=dev)
-        self.be.pack_count(rows, send[:head].view(cr, 2 * self.words), counts)
-        total = counts.sum(dtype=torch.int64).view(1)
+        F = rows.size(1)
+        if FUSED_PACK and hasattr(self.be, "pack_rows") and self.be.pack_rows_ok(F):
+            # packed here, once: counts None tells _payload the values are in
+            counts = None
+            self.stats["pack_one_pass"] = self.stats.get("pack_one_pass", 0) + 1
+            total = torch.empty(1, dtype=torch.int64, device=dev)
+            self.be.pack_rows(rows, send[:head].view(cr, 2 * self.words),
+                              send[head:head + cr * F], total)
+        else:
+            counts = torch.empty(cr, dtype=torch.int32, device=dev)
+            self.be.pack_count(rows, send[:head].view(cr, 2 * self.words), counts)
+            total = counts.sum(dtype=torch.int64).view(1)
         P = sh.world
         if sh.emulated or not _collective(P):
             totals, work = total, None
@@ -582,7 +611,7 @@ class _ChunkExchange:
             self.works.append(_gather_chunk(sh, c, self.local, self.table, self.group))
             return
         self.stats["sent_words"] += seg * P
-        if not again:
+        if not again and counts is not None:
             offs = torch.cumsum(counts, 0, dtype=torch.int32)
             offs.sub_(counts)
             # every value (the send buffer holds a dense chunk's worth); the

@@ -1968,6 +1968,35 @@ def packed_cols(col: torch.Tensor, seg_rows: int, row_bits: int) -> torch.Tensor
     return ((s_ << row_bits) | (t - s_ * seg_rows)).to(torch.int32)
 
 
+PACK_ROWS_WIDTHS = (32, 64, 128, 256)  # mgcn_pack_rows: one 256-word segment per row
+
+
+def pack_rows(rows: torch.Tensor, hdr: torch.Tensor, vals: torch.Tensor,
+              total: torch.Tensor) -> None:
+    """The packed chunk in one pass (``mgcn_pack_rows``): hdr as
+    pack_rows_count + pack_rows_values write it, vals, and total[0] = the
+    number of values (device int64) -- no counts, no scan."""
+    lib = L.load()
+    rows = _contig_f32(rows, "rows")
+    n, F = rows.shape
+    dev = L.require_device(rows, hdr, vals, total)
+    if F not in PACK_ROWS_WIDTHS or hdr.shape != (n, 2 * (F // 32)) or hdr.dtype != torch.int32 \
+            or not hdr.is_contiguous() or vals.dtype != torch.int32 or total.dtype != torch.int64 \
+            or total.numel() < 1:
+        raise ValueError("pack_rows: F in (32, 64, 128, 256), hdr int32 [n, 2 F/32] contiguous, "
+                         "vals int32, total int64")
+    ws_bytes = int(lib.mgcn_pack_rows_workspace_bytes(n, F))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev) if ws_bytes else None
+    if _TIMER is not None:
+        _TIMER("pack_rows", True, n)
+    with L.device_guard(dev):
+        rc = lib.mgcn_pack_rows(n, F, L.ptr(rows), rows.stride(0), L.ptr(hdr), L.ptr(vals),
+                                L.ptr(total), L.ptr(ws), ws_bytes, L.stream_of(dev))
+    if _TIMER is not None:
+        _TIMER("pack_rows", False)
+    L.check(rc, "mgcn_pack_rows")
+
+
 def unpack_rows(buf: torch.Tensor, n_seg: int, n: int, seg_words: int, out: torch.Tensor) -> None:
     """out[p n + i] = row i of packed segment p of ``buf`` (``mgcn_unpack_rows``)."""
     lib = L.load()

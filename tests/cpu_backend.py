@@ -173,6 +173,16 @@ class CpuBackend:
         below = torch.cumsum(per_word, 1) - per_word
         hdr[:, 1::2] = (offs.to(torch.int64).view(-1, 1) + below).to(torch.int32)
 
+    def pack_rows(self, rows, hdr, vals, total):
+        counts = torch.empty(rows.size(0), dtype=torch.int32)
+        self.pack_count(rows, hdr, counts)
+        offs = torch.cumsum(counts, 0, dtype=torch.int32) - counts
+        self.pack_values(rows, offs, hdr, vals)
+        total[0] = int(counts.sum())
+
+    def pack_rows_ok(self, F):
+        return F in (32, 64, 128, 256)
+
     def unpack(self, buf, n_seg, n, seg_words, out):
         F = out.size(1)
         words = F // 32

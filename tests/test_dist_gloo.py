@@ -37,7 +37,7 @@ def _problem(N=300, pairs=1500, F=16, L=3, seed=0):
 
 
 def _run(rank, world, port, aggr, out_q, F=16, fused=True, chunks=4, pack=True, force=False,
-         slack=None):
+         slack=None, one_pass=True):
     sys.path[:0] = [os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "meta-gcn_amd"),
                     HERE]
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -50,6 +50,7 @@ def _run(rank, world, port, aggr, out_q, F=16, fused=True, chunks=4, pack=True, 
         from mgcn.dist import ShardedGCN
         mdist.set_pack_exchange(pack)
         mdist.set_force_collectives(force)
+        mdist.set_fused_pack(one_pass)
         if slack is not None:
             mdist.SPEC_SLACK = slack
         ei, N, X, Ws, bs, dY = _problem(F=F)
@@ -77,12 +78,13 @@ def _run(rank, world, port, aggr, out_q, F=16, fused=True, chunks=4, pack=True, 
         dist.destroy_process_group()
 
 
-def _launch(world, aggr, F=16, fused=True, chunks=4, pack=True, force=False, slack=None):
+def _launch(world, aggr, F=16, fused=True, chunks=4, pack=True, force=False, slack=None,
+            one_pass=True):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_run, args=(r, world, port, aggr, q, F, fused, chunks, pack,
-                                            force, slack))
+                                            force, slack, one_pass))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -116,14 +118,18 @@ def test_sharded_matches_single_process(world, aggr, F, fused, chunks):
                 np.testing.assert_allclose(g, g1, rtol=1e-5, atol=1e-5 * max(1, np.abs(g1).max()))
 
 
-@pytest.mark.parametrize("world,aggr,F,chunks", [(2, "add", 32, 4), (4, "mean", 64, 3),
-                                                  (2, "add", 128, 3)])
-def test_packed_exchange_is_bitwise_the_dense_one(world, aggr, F, chunks):
+@pytest.mark.parametrize("world,aggr,F,chunks,one_pass", [
+    (2, "add", 32, 4, True), (4, "mean", 64, 3, True), (2, "add", 128, 3, True),
+    (2, "add", 128, 3, False), (2, "mean", 96, 2, True)])
+def test_packed_exchange_is_bitwise_the_dense_one(world, aggr, F, chunks, one_pass):
     """The zero-skipping exchange (ReLU'd forward tables, ReLU-masked
     backward tables) against the dense exchange of the same sharded stack:
     every output, dX row and gradient bit for bit, with fewer words sent
-    (F = 128: the in-place table in ONE receive buffer, dist._single_recv_words)."""
-    packed = _launch(world, aggr, F, True, chunks, pack=True)
+    (F = 128: the in-place table in ONE receive buffer, dist._single_recv_words).
+    Chunks packed in one pass (mgcn_pack_rows' double) or in two (count,
+    scan, values: set_fused_pack(False), and F = 96, which the one pass does
+    not take)."""
+    packed = _launch(world, aggr, F, True, chunks, pack=True, one_pass=one_pass)
     dense = _launch(world, aggr, F, True, chunks, pack=False)
     for rp, rd in zip(packed, dense):
         for key in ("out", "dX", "out_table"):
@@ -135,6 +141,8 @@ def test_packed_exchange_is_bitwise_the_dense_one(world, aggr, F, chunks):
         assert 0 < st["sent_words"] < 0.8 * st["dense_words"], st
         # the second pass sent every in-place chunk at the sizes the first learnt
         assert st.get("spec_chunks", 0) > 0 and st.get("spec_resent", 0) == 0, st
+        assert (st.get("pack_one_pass", 0) > 0) == (one_pass and F % 32 == 0 and F // 32 in
+                                                    (1, 2, 4, 8)), st
         assert rd["stats"]["dense_words"] == 0
 
 

@@ -104,6 +104,60 @@ def test_pack_rows_with_a_leading_dimension(cuda):
     assert torch.equal(hdr.cpu()[:, 0::2], ref_h[:, 0::2]) and torch.equal(counts.cpu(), ref_c)
 
 
+def _pack_gpu_one_pass(xs, cuda):
+    from mgcn import ops
+    n, F = xs.shape
+    head = 2 * n * (F // 32)
+    send = torch.full((head + n * F,), -7, dtype=torch.int32, device=cuda)
+    total = torch.full((1,), -1, dtype=torch.int64, device=cuda)
+    ops.pack_rows(xs, send[:head].view(n, 2 * (F // 32)), send[head:], total)
+    t = int(total.item())
+    return send[:head + t], t
+
+
+@pytest.mark.parametrize("n,F", [(1, 32), (37, 32), (515, 64), (1000, 128), (4097, 256),
+                                 (300_001, 256), (270_007, 128), (100_003, 32)])
+def test_single_pass_pack_is_the_two_pass_pack(cuda, n, F):
+    """mgcn_pack_rows (one read, decoupled look-back over tiles) writes the
+    buffer mgcn_pack_rows_count + _values write, word for word, and its
+    device total is the values' number (thousands of tiles at the larger
+    sizes: look-back windows past 64 predecessors)."""
+    x = _rows(n, F, seed=n * 3 + F)
+    got, t = _pack_gpu_one_pass(x.to(cuda), cuda)
+    ref, cnt = _pack_gpu(x, cuda)
+    assert t == int(cnt.sum())
+    np.testing.assert_array_equal(got.cpu().numpy(), ref.numpy())
+    if n <= 5000:
+        np.testing.assert_array_equal(got.cpu().numpy(), _pack_cpu(x)[0].numpy())
+
+
+def test_single_pass_pack_at_a_rank_chunk_with_a_leading_dimension(cuda):
+    """A config-5-sized chunk (1.56M rows x 256, ~1.6 GB; ReLU'd, about half
+    zeros) taken from a wider buffer (ld > F), against the two-pass pack on
+    the device; empty input writes total = 0."""
+    from mgcn import ops
+    n, F = 1_560_000, 256
+    g = torch.Generator(device=cuda).manual_seed(11)
+    big = torch.relu(torch.randn(n, F + 32, device=cuda, generator=g))
+    x = big[:, :F]
+    got, t = _pack_gpu_one_pass(x, cuda)
+    head = 2 * n * (F // 32)
+    send = torch.empty(head + n * F, dtype=torch.int32, device=cuda)
+    counts = torch.empty(n, dtype=torch.int32, device=cuda)
+    hdr = send[:head].view(n, 2 * (F // 32))
+    ops.pack_rows_count(x, hdr, counts)
+    offs = torch.cumsum(counts, 0, dtype=torch.int32) - counts
+    ops.pack_rows_values(x, offs, hdr, send[head:])
+    assert t == int(counts.sum())
+    assert torch.equal(got, send[:head + t])
+    del big, send, got
+    total = torch.full((1,), -1, dtype=torch.int64, device=cuda)
+    e = torch.empty(0, F, device=cuda)
+    ops.pack_rows(e, torch.empty(0, 16, dtype=torch.int32, device=cuda),
+                  torch.empty(0, dtype=torch.int32, device=cuda), total)
+    assert int(total.item()) == 0
+
+
 # ------------------------------------------------- in-place packed gather
 def _packed_table(T, cr, cuda, n_bufs=2):
     """T [S cr, F] (S segments of cr rows) packed segment by segment into

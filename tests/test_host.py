@@ -33,7 +33,7 @@ def test_library_exports_every_header_symbol():
 def test_abi_version_and_option_errors():
     import mgcn
     lib = mgcn.load()
-    assert lib.mgcn_abi_version() == mgcn._lib.ABI_VERSION == 21
+    assert lib.mgcn_abi_version() == mgcn._lib.ABI_VERSION == 22
     assert lib.mgcn_set_option(b"no_such_option", 1) == 1
     assert b"unknown option" in lib.mgcn_last_error()
     # the switches that change results (timing experiments) and the spin bound
