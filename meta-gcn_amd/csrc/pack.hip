@@ -221,11 +221,19 @@ __global__ __launch_bounds__(64 * kPkWaves) void unpack_kernel(int64_t n_seg, in
 // prefix, which ends the walk), publishes its own inclusive prefix and writes
 // the header pairs and values from the registers.  The two-pass form reads
 // every row twice (count, then values) and scans the counts between them.
+// Values leave through a 1-KB LDS row per wave: an iteration's values are one
+// contiguous run, stored by consecutive lanes (0.69 vs 0.81 ms for a config-5
+// chunk with each lane storing its own words; 8 / 24 / 32 iterations per
+// lane: 0.77 (with staging) / 0.73 / 0.70 -- scripts/bench_pack.py,
+// profiles/r06/pack_one_pass.json).  Against the two passes: 0.69 vs 1.07 ms.
 // Rows of one 256-word segment only (F = 4 G: 32, 64, 128, 256).
 // Status word of a tile: (flag << 62) | value, flag 1 = aggregate, 2 =
 // inclusive prefix; 0 = not yet published.  Relaxed agent-scope atomics: the
 // word carries its own data.  A walk that waits past the spin bound stores
 // kDevErrPack and takes 0 for the missing part (every wave still finishes).
+#ifndef MGCN_PR_LDS
+#define MGCN_PR_LDS 1
+#endif
 #ifndef MGCN_PR_ITERS
 #define MGCN_PR_ITERS 16
 #endif
@@ -249,6 +257,9 @@ __global__ __launch_bounds__(64 * kPkWaves) void pack_rows_kernel(
   const int lane = threadIdx.x & 63;
   __shared__ int64_t s_tile, s_prefix;
   __shared__ int64_t s_wsum[kPkWaves];
+#if MGCN_PR_LDS
+  __shared__ uint32_t s_stage[kPkWaves][256];
+#endif
   if (threadIdx.x == 0) s_tile = (int64_t)atomicAdd(ticket, 1u);
   __syncthreads();
   const int64_t tile = s_tile;
@@ -344,10 +355,30 @@ __global__ __launch_bounds__(64 * kPkWaves) void pack_rows_kernel(
       *reinterpret_cast<uint2 *>(hdr + 2 * (r * WORDS + p.gl)) = make_uint2(seg_word(b, p.gl), (uint32_t)pw);
     }
     int64_t q = rowpos + __popcll(b[0] & lo) + __popcll(b[1] & lo) + __popcll(b[2] & lo) + __popcll(b[3] & lo);
+#if MGCN_PR_LDS
+    // the iteration's values are one contiguous run [ib, ib + ic): staged in
+    // the wave's LDS row, then stored by consecutive lanes (a wave's LDS
+    // operations execute in order: no barrier between the writes and reads)
+    const int64_t ib = base + __builtin_amdgcn_readfirstlane(roff[i]);
+    const int ic = __popcll(__ballot(nz[0])) + __popcll(__ballot(nz[1])) + __popcll(__ballot(nz[2])) +
+                   __popcll(__ballot(nz[3]));
+    uint32_t *st = s_stage[wave];
+    int l = (int)(q - ib);
+    if (nz[0]) st[l++] = v[i].x;
+    if (nz[1]) st[l++] = v[i].y;
+    if (nz[2]) st[l++] = v[i].z;
+    if (nz[3]) st[l++] = v[i].w;
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (lane + 64 * k < ic) vals[ib + lane + 64 * k] = st[lane + 64 * k];
+    __builtin_amdgcn_wave_barrier();
+#else
     if (nz[0]) vals[q++] = v[i].x;
     if (nz[1]) vals[q++] = v[i].y;
     if (nz[2]) vals[q++] = v[i].z;
     if (nz[3]) vals[q++] = v[i].w;
+#endif
   }
 }
 

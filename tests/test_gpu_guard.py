@@ -272,3 +272,36 @@ def test_pack_unpack_bands(cuda, F):
         for gd in (masks, counts, send, out):
             assert gd.intact(), (F, n)
         assert torch.equal(out.t, rows.repeat(P, 1))
+
+
+@pytest.mark.parametrize("F", [32, 128, 256])
+def test_single_pass_pack_bands(cuda, F):
+    """mgcn_pack_rows: header, values (sized to exactly the nonzero words),
+    the device total and the look-back workspace between sentinel bands,
+    at row counts inside one tile and across tiles; the packed buffer is the
+    two-pass one."""
+    from mgcn import _lib as L
+    from mgcn import ops
+    lib = L.load()
+    g = torch.Generator(device=cuda).manual_seed(F + 1)
+    for n in [1, 15, 17, 31, 33, 190, 1000, 4099]:
+        rows = torch.relu(torch.randn(n, F, device=cuda, generator=g))
+        words = F // 32
+        nv = int((rows.view(torch.int32) != 0).sum())
+        hdr = Guarded((n, 2 * words), torch.int32, cuda)
+        vals = Guarded((nv,), torch.int32, cuda)
+        tot = Guarded((2,), torch.int32, cuda)
+        wsb = _ws(lib, "mgcn_pack_rows_workspace_bytes", n, F)
+        ws = Guarded((wsb,), torch.uint8, cuda)
+        rc = lib.mgcn_pack_rows(n, F, L.ptr(rows), F, L.ptr(hdr.t), L.ptr(vals.t), L.ptr(tot.t),
+                                L.ptr(ws.t), wsb, L.stream_of(cuda))
+        L.check(rc, "mgcn_pack_rows")
+        for gd in (hdr, vals, tot, ws):
+            assert gd.intact(), (F, n)
+        assert int(tot.t.view(torch.int64)[0]) == nv
+        counts = torch.empty(n, dtype=torch.int32, device=cuda)
+        h2 = torch.empty(n, 2 * words, dtype=torch.int32, device=cuda)
+        ops.pack_rows_count(rows, h2, counts)
+        v2 = torch.empty(nv, dtype=torch.int32, device=cuda)
+        ops.pack_rows_values(rows, torch.cumsum(counts, 0, dtype=torch.int32) - counts, h2, v2)
+        assert torch.equal(hdr.t, h2) and torch.equal(vals.t, v2)
