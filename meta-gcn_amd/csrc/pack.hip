@@ -230,7 +230,9 @@ __global__ __launch_bounds__(64 * kPkWaves) void unpack_kernel(int64_t n_seg, in
 // Status word of a tile: (flag << 62) | value, flag 1 = aggregate, 2 =
 // inclusive prefix; 0 = not yet published.  Relaxed agent-scope atomics: the
 // word carries its own data.  A walk that waits past the spin bound stores
-// kDevErrPack and takes 0 for the missing part (every wave still finishes).
+// kDevErrPack and takes 0 for the missing part (every wave still finishes;
+// the offsets then only come out too SMALL, so every store stays inside the
+// chunk's buffers).
 #ifndef MGCN_PR_LDS
 #define MGCN_PR_LDS 1
 #endif
@@ -425,6 +427,8 @@ extern "C" int mgcn_pack_rows_values(int64_t n, int32_t F, const float *X, int64
                "mgcn_pack_rows_values: need n >= 0, F a multiple of 32, ldx >= F");
   if (n == 0) return MGCN_OK;
   MGCN_REQUIRE(X && hdr && offs && vals, "mgcn_pack_rows_values: null array");
+  MGCN_REQUIRE(n <= (int64_t)(UINT32_MAX / (uint32_t)F),
+               "mgcn_pack_rows_values: n F must fit the header's 32-bit value positions");
   MGCN_REQUIRE(pk_aligned(X, ldx), "mgcn_pack_rows_values: rows must be 16-byte aligned");
   // the masks are recomputed from the rows (the same bits pack_count wrote)
   const int G = pk_group(F);
@@ -449,6 +453,8 @@ extern "C" int mgcn_pack_rows(int64_t n, int32_t F, const float *X, int64_t ldx,
   MGCN_REQUIRE(n >= 0 && (F == 32 || F == 64 || F == 128 || F == 256) && ldx >= F,
                "mgcn_pack_rows: need n >= 0, F in {32, 64, 128, 256}, ldx >= F");
   MGCN_REQUIRE(total != nullptr, "mgcn_pack_rows: null total");
+  MGCN_REQUIRE(n <= (int64_t)(UINT32_MAX / (uint32_t)F),
+               "mgcn_pack_rows: n F must fit the header's 32-bit value positions");
   hipStream_t s = as_stream(stream);
   if (n == 0) {
     MGCN_HIP_TRY(hipMemsetAsync(total, 0, sizeof(int64_t), s));
