@@ -32,6 +32,7 @@ namespace mgcn {
 namespace {
 
 constexpr int kPkWaves = 4;
+typedef unsigned int wl_u32x4 __attribute__((ext_vector_type(4)));
 
 // word w (w < G / 8) of a segment from the group's four ballots (bit gl of
 // b[j] <=> word 4 gl + j is nonzero): bit 4 i + j <- bit 8 w + i of b[j]
@@ -225,7 +226,8 @@ __global__ __launch_bounds__(64 * kPkWaves) void unpack_kernel(int64_t n_seg, in
 // contiguous run, stored by consecutive lanes (0.69 vs 0.81 ms for a config-5
 // chunk with each lane storing its own words; 8 / 24 / 32 iterations per
 // lane: 0.77 (with staging) / 0.73 / 0.70 -- scripts/bench_pack.py,
-// profiles/r06/pack_one_pass.json).  Against the two passes: 0.69 vs 1.07 ms.
+// profiles/r06/pack_one_pass.json).  The rows are read with the nt policy
+// (read once: 0.669 vs 0.691 ms).  Against the two passes: 0.67 vs 1.07 ms.
 // Rows of one 256-word segment only (F = 4 G: 32, 64, 128, 256).
 // Status word of a tile: (flag << 62) | value, flag 1 = aggregate, 2 =
 // inclusive prefix; 0 = not yet published.  Relaxed agent-scope atomics: the
@@ -233,6 +235,9 @@ __global__ __launch_bounds__(64 * kPkWaves) void unpack_kernel(int64_t n_seg, in
 // kDevErrPack and takes 0 for the missing part (every wave still finishes;
 // the offsets then only come out too SMALL, so every store stays inside the
 // chunk's buffers).
+#ifndef MGCN_PR_NTLOAD
+#define MGCN_PR_NTLOAD 1
+#endif
 #ifndef MGCN_PR_LDS
 #define MGCN_PR_LDS 1
 #endif
@@ -272,8 +277,17 @@ __global__ __launch_bounds__(64 * kPkWaves) void pack_rows_kernel(
 #pragma unroll
   for (int i = 0; i < kPrIters; ++i) {
     const int64_t r = r0 + (int64_t)i * RPW;
+#if MGCN_PR_NTLOAD
+    if (r < n) {
+      const wl_u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const wl_u32x4 *>(X + r * ldx + 4 * p.gl));
+      v[i] = make_uint4(t.x, t.y, t.z, t.w);
+    } else {
+      v[i] = make_uint4(0u, 0u, 0u, 0u);
+    }
+#else
     v[i] = r < n ? *reinterpret_cast<const uint4 *>(X + r * ldx + 4 * p.gl)
                  : make_uint4(0u, 0u, 0u, 0u);
+#endif
   }
   const uint64_t groups_below = (1ull << (p.grp * G)) - 1ull;  // lanes of the lower groups
   int64_t wsum = 0;  // wave-uniform: values of the wave's rows so far
@@ -505,7 +519,6 @@ extern "C" int mgcn_unpack_rows(int64_t n_seg, int64_t n, int32_t F, const uint3
 // buf_bytes): the received words landing in HBM while the rank computes.
 // A bounded grid-stride loop (no flag, no spin).
 namespace {
-typedef unsigned int wl_u32x4 __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256) void hbm_write_load_kernel(wl_u32x4 *__restrict__ buf, int64_t n16,
                                                              int64_t total16) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
