@@ -406,6 +406,10 @@ def set_spec_exchange(enabled: bool) -> None:
 # count left on the device -- no count pass, no scan of the counts, the pack
 # done before the sizes are exchanged.  set_fused_pack(False): the two passes.
 FUSED_PACK = os.environ.get("MGCN_FUSED_PACK", "1") != "0"
+# ... for chunks of at least this many bytes: a small chunk has fewer tiles
+# than the GPU has CUs and its look-back costs more than the second read
+# (config 2 at P = 8, 31k x 128 rows: 27 vs 22 us; 125k x 128: 57 vs 74 us)
+FUSED_PACK_MIN_BYTES = 32 << 20
 
 
 def set_fused_pack(enabled: bool) -> None:
@@ -523,7 +527,8 @@ class _ChunkExchange:
         # (+4 words: a lane's 16-B value read may run 3 words past the values)
         send = torch.empty(head + cr * rows.size(1) + 4, dtype=torch.int32, device=dev)
         F = rows.size(1)
-        if FUSED_PACK and hasattr(self.be, "pack_rows") and self.be.pack_rows_ok(F):
+        if FUSED_PACK and hasattr(self.be, "pack_rows") and self.be.pack_rows_ok(F) and \
+                cr * F * 4 >= FUSED_PACK_MIN_BYTES:
             # packed here, once: counts None tells _payload the values are in
             counts = None
             self.stats["pack_one_pass"] = self.stats.get("pack_one_pass", 0) + 1

@@ -51,6 +51,7 @@ def _run(rank, world, port, aggr, out_q, F=16, fused=True, chunks=4, pack=True, 
         mdist.set_pack_exchange(pack)
         mdist.set_force_collectives(force)
         mdist.set_fused_pack(one_pass)
+        mdist.FUSED_PACK_MIN_BYTES = 0  # the tests' chunks are small
         if slack is not None:
             mdist.SPEC_SLACK = slack
         ei, N, X, Ws, bs, dY = _problem(F=F)

@@ -62,6 +62,9 @@ def _child(backend, force, port, q):
         res = {"backend": dist.get_backend()}
         for F, aggr in ((128, "add"), (128, "mean"), (256, "add")):
             ei, N, X, Ws, bs, dY = _problem(F=F, seed=F)
+            # F = 256: chunks packed in one pass (mgcn_pack_rows, below its
+            # size threshold here); F = 128: the two passes
+            mdist.FUSED_PACK_MIN_BYTES = 0 if F == 256 else 32 << 20
             for pack in (False, True):
                 mdist.set_pack_exchange(pack)
                 m = mdist.ShardedGCN(ei, N, Ws, bs, device=dev, aggr=aggr, chunks=3)
@@ -123,6 +126,7 @@ def test_rccl_one_rank_forced_collectives_match_world_one(cuda):
     # the speculative-capacity steps: used, the too-small one re-sent, same bits
     assert rc["packed_words"].get("spec_chunks", 0) > 0, rc["packed_words"]
     assert rc["packed_words"].get("spec_resent", 0) > 0, rc["packed_words"]
+    assert rc["packed_words"].get("pack_one_pass", 0) > 0, rc["packed_words"]
     for key in ref:
         if key in ("backend", "packed_words", "dp"):
             continue
